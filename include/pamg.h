@@ -1,0 +1,168 @@
+/*
+ * pamg.h — C-ABI of the MI355X-native AMG V-cycle solve path (libpamg.so).
+ *
+ * Drop-in boundary. The reference (tirtho109/parallel_AMG) contains only
+ * README.md:1-2 ("Apply AMG algorithm parallelly using PartitionedArrays.jl") — there is no
+ * reference FFI to mirror line by line. Each entry point below replaces the PartitionedArrays
+ * operation named in its comment (the surface an AMG solver written against
+ * PartitionedArrays calls, README.md:2); INTEGRATION.md shows the Julia `ccall` binding and
+ * the Python ctypes binding (parallel_amg_amd/_lib.py) a maintainer would use.
+ *
+ * Conventions
+ *  - Every function returns int: PAMG_OK (0) or a negative PAMG_E_* code; the message of the
+ *    last failure on the calling thread is pamg_last_error().
+ *  - Handles are opaque and owned by the library; free them with the matching _destroy.
+ *  - Host arrays are copied; the caller keeps ownership and may free them after the call.
+ *  - Device calls are enqueued on the context's compute stream and are complete on return
+ *    unless the name ends in _async (then pamg_ctx_sync() completes them).
+ *  - One host thread per context; one context per GPU; one GPU per process (the
+ *    PartitionedArrays "one part per MPI rank" shape; ranks exchange ghosts over RCCL).
+ *  - Numerics: SPEC.md (fp64 values, int32 device indices, fixed summation order).
+ */
+#ifndef PAMG_H
+#define PAMG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PAMG_OK 0
+#define PAMG_E_ARG (-1)      /* bad argument / shape mismatch */
+#define PAMG_E_HIP (-2)      /* HIP runtime error */
+#define PAMG_E_RCCL (-3)     /* RCCL error */
+#define PAMG_E_OVERFLOW (-4) /* index does not fit the device int32 layout */
+#define PAMG_E_SETUP (-5)    /* setup failed (missing diagonal, non-SPD coarse matrix, ...) */
+#define PAMG_E_STATE (-6)    /* call not valid in the current state (e.g. no communicator) */
+#define PAMG_E_NOMEM (-7)    /* host or device allocation failed */
+
+typedef struct pamg_ctx pamg_ctx;   /* one GPU, its streams and (optionally) an RCCL comm */
+typedef struct pamg_plan pamg_plan; /* ghost layout + neighbour exchange lists (a PRange) */
+typedef struct pamg_vec pamg_vec;   /* device PVector: own values then ghost slots */
+typedef struct pamg_mat pamg_mat;   /* device PSparseMatrix part: own rows, local columns */
+typedef struct pamg_hier pamg_hier; /* device AMG hierarchy (V-cycle) */
+typedef struct pamg_hcsr pamg_hcsr; /* host CSR produced by the setup routines */
+
+const char* pamg_version(void);
+const char* pamg_last_error(void);
+
+/* ------------------------------------------------------------------ context */
+/* Replaces the PartitionedArrays backend objects (with_mpi / with_debug). */
+int pamg_ctx_create(int device, pamg_ctx** out);
+int pamg_ctx_destroy(pamg_ctx* ctx);
+int pamg_ctx_sync(pamg_ctx* ctx);
+/* RCCL communicator for multi-part runs: rank 0 calls pamg_comm_unique_id, the 128 bytes are
+ * broadcast by the host layer (MPI / torch.distributed), then every rank calls pamg_comm_init. */
+int pamg_comm_unique_id(unsigned char id[128]);
+int pamg_comm_init(pamg_ctx* ctx, int nranks, int rank, const unsigned char id[128]);
+int pamg_comm_rank(const pamg_ctx* ctx, int* rank, int* nranks);
+
+/* ------------------------------------------------------------------ exchange plan */
+/* Replaces PRange / ExchangeGraph: ghosts [n_own, n_own+n_ghost) grouped by neighbour in
+ * nbr order (recv_counts), and per neighbour the own indices sent to it (send_idx,
+ * concatenated in nbr order, send_counts). */
+int pamg_plan_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, int n_nbr,
+                     const int32_t* nbr_rank, const int64_t* recv_counts,
+                     const int64_t* send_counts, const int64_t* send_idx, pamg_plan** out);
+int pamg_plan_destroy(pamg_plan* plan);
+
+/* ------------------------------------------------------------------ vectors (PVector) */
+int pamg_vec_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, pamg_vec** out);
+int pamg_vec_destroy(pamg_vec* v);
+int pamg_vec_size(const pamg_vec* v, int64_t* n_own, int64_t* n_ghost);
+int pamg_vec_upload(pamg_ctx* ctx, pamg_vec* v, const double* own);     /* own_values(v) .= */
+int pamg_vec_download(pamg_ctx* ctx, const pamg_vec* v, double* own);
+int pamg_vec_device_ptr(pamg_vec* v, double** dptr);                    /* zero-copy interop */
+int pamg_vec_fill(pamg_ctx* ctx, pamg_vec* v, double value);            /* fill!(v, a) */
+int pamg_vec_copy(pamg_ctx* ctx, const pamg_vec* src, pamg_vec* dst);   /* copy!(dst, src) */
+int pamg_vec_axpby(pamg_ctx* ctx, double a, const pamg_vec* x, double b, pamg_vec* y); /* y=a x+b y */
+int pamg_vec_dot(pamg_ctx* ctx, const pamg_vec* x, const pamg_vec* y, double* out);    /* dot */
+int pamg_vec_nrm2(pamg_ctx* ctx, const pamg_vec* x, double* out);                      /* norm */
+/* consistent!(x) |> wait : owners' values into the ghost slots described by plan. */
+int pamg_exchange(pamg_ctx* ctx, const pamg_plan* plan, pamg_vec* x);
+
+/* ------------------------------------------------------------------ matrices (PSparseMatrix) */
+/* One part's own rows; columns already local (own 0..n_own-1 of the column space, then the
+ * plan's ghosts), each row in ascending GLOBAL column order (SPEC §S1). col is int32 or int64
+ * (col_is_64); index_base 0 or 1 (Julia). col_plan may be NULL for a single part. */
+int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols_local, const int64_t* rowptr,
+                    const void* col, int col_is_64, const double* val, int index_base,
+                    const pamg_plan* col_plan, pamg_mat** out);
+int pamg_mat_destroy(pamg_mat* A);
+int pamg_mat_info(const pamg_mat* A, int64_t* nrows, int64_t* ncols_local, int64_t* nnz);
+
+/* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
+int pamg_spmv(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, pamg_vec* y);
+/* r = b - A x ; if nrm2 != NULL, *nrm2 = ||r|| over all parts. */
+int pamg_residual(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec* b,
+                  pamg_vec* r, double* nrm2);
+/* nsweeps weighted-Jacobi sweeps on x (tmp is the ping-pong buffer; result in x). */
+int pamg_jacobi(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec* b,
+                pamg_vec* tmp, double omega, int nsweeps);
+
+/* ------------------------------------------------------------------ hierarchy / V-cycle */
+/* Levels 0..nlevels-1; P[l], R[l] for l < nlevels-1 (NULL entries otherwise). The coarsest
+ * level is solved with Ainv (column-major, n_coarse x n_coarse, SPEC §S5); coarse_offsets
+ * (nranks+1 entries, NULL for one part) gives each rank's rows of the coarsest level.
+ * The hierarchy references (does not own) the matrices: keep them alive. */
+int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* const* P,
+                     pamg_mat* const* R, const double* omega, int64_t n_coarse,
+                     const double* ainv_colmajor, const int64_t* coarse_offsets,
+                     pamg_hier** out);
+int pamg_hier_destroy(pamg_hier* H);
+/* 1 = replay the V-cycle as a captured hipGraph (default 1 on one part), 0 = eager launches. */
+int pamg_hier_set_graph(pamg_hier* H, int enable);
+/* x <- V(x) ncycles times (SPEC §S6); res_hist (ncycles, may be NULL) gets ||b - A x||. */
+int pamg_vcycle(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles,
+                double* res_hist);
+int pamg_vcycle_async(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles);
+/* Kernel timing of the last pamg_vcycle/_async (events on the compute stream): per level,
+ * milliseconds spent in [jacobi_pre, residual, restrict, prolong, jacobi_post, coarse]. */
+int pamg_hier_profile(pamg_hier* H, int enable);
+int pamg_hier_profile_read(pamg_hier* H, double* ms_per_level_op /* nlevels*6 */);
+
+/* Micro-benchmark hook: `reps` back-to-back y = A x launches (no exchange), returning the
+ * average kernel time in ms measured with HIP events on the launch stream. */
+int pamg_bench_spmv(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, pamg_vec* y, int reps,
+                    double* avg_ms);
+
+/* ------------------------------------------------------------------ host setup (SPEC §S4) */
+/* Host CSR: int64 rowptr, int32 columns (global ids), fp64 values. */
+int pamg_hcsr_create(int64_t nrows, int64_t ncols, int64_t nnz, pamg_hcsr** out);
+int pamg_hcsr_destroy(pamg_hcsr* M);
+int pamg_hcsr_info(const pamg_hcsr* M, int64_t* nrows, int64_t* ncols, int64_t* nnz);
+int pamg_hcsr_data(pamg_hcsr* M, int64_t** rowptr, int32_t** col, double** val);
+/* Rows [r0, r1) of the SPEC §S2 grid operator; kind 0 poisson2d, 1 poisson3d, 2 aniso3d. */
+int pamg_gen_grid(int kind, int64_t nx, int64_t ny, int64_t nz, double eps, int64_t r0,
+                  int64_t r1, pamg_hcsr** out);
+int pamg_gen_xstar(int64_t i0, int64_t n, uint64_t seed, double* out);
+/* Gershgorin bound over own rows; A's rows are global rows row0.. (diagonal at col row0+i). */
+int pamg_setup_gershgorin(const pamg_hcsr* A, int64_t row0, double* rho);
+/* Decoupled standard aggregation (SPEC §S4.2-3): agg[i] local aggregate id or -1. */
+int pamg_setup_aggregate(const pamg_hcsr* A, int64_t row0, double theta, int32_t* agg,
+                         int64_t* n_agg);
+/* Tentative prolongator rows: T[i, coarse0 + agg[i]] = 1/sqrt(|agg|). */
+int pamg_setup_tentative(int64_t n, const int32_t* agg, int64_t n_agg, int64_t coarse0,
+                         int64_t ncols_global, pamg_hcsr** out);
+/* C = X * Y (SPEC §S4.5). Y's rows are the own rows [y0, y0+Yown.nrows) plus the ghost rows
+ * Yghost whose global row ids are ghost_ids (ascending, n_ghost). Yghost may be NULL. */
+int pamg_setup_spgemm(const pamg_hcsr* X, int64_t y0, const pamg_hcsr* Yown,
+                      const int64_t* ghost_ids, int64_t n_ghost, const pamg_hcsr* Yghost,
+                      pamg_hcsr** out);
+/* In place: AT -> P = T - (omega / a_ii) * AT (SPEC §S4.6); A rows are global rows row0.. */
+int pamg_setup_smooth(const pamg_hcsr* A, int64_t row0, const pamg_hcsr* T, pamg_hcsr* AT,
+                      double omega);
+/* Transpose of the local rows of P (global rows row0..) restricted to columns [c0, c1):
+ * rows = coarse ids c0..c1-1, columns = global fine ids, ascending (SPEC §S4.7). */
+int pamg_setup_transpose(const pamg_hcsr* P, int64_t row0, int64_t c0, int64_t c1,
+                         pamg_hcsr** out);
+/* Row-wise concatenation of k CSR pieces with equal row counts (part order = column order). */
+int pamg_setup_hstack_rows(int k, const pamg_hcsr* const* pieces, pamg_hcsr** out);
+/* Dense Cholesky inverse of a full (single-piece) matrix, column-major out (SPEC §S5). */
+int pamg_setup_cholinv(const pamg_hcsr* A, double* ainv_colmajor);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PAMG_H */

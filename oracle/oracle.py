@@ -1,0 +1,199 @@
+"""ctypes front end of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may import
+this module; the product (``parallel_amg_amd``) never does. It restates SPEC.md (§S1-§S7);
+the C source is ``oracle/pamg_oracle.c``. Parity with the Julia reference is unpinned
+(the reference, /root/reference/README.md:1-2, holds no code) — see DESIGN.md §Oracle.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libpamg_oracle.so")
+SEED = 20240807
+KINDS = {"poisson2d": 0, "poisson3d": 1, "aniso3d": 2}
+
+_i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        i64, dbl, vp = C.c_int64, C.c_double, C.c_void_p
+        L.orc_xstar.argtypes = [i64, i64, C.c_uint64, _f64p]
+        L.orc_gen_rows.restype = i64
+        L.orc_gen_rows.argtypes = [C.c_int, i64, i64, i64, dbl, i64, i64, vp, vp, vp]
+        for f in ("orc_spmv",):
+            getattr(L, f).argtypes = [i64, _i64p, _i64p, _f64p, _f64p, _f64p]
+        L.orc_residual.argtypes = [i64, _i64p, _i64p, _f64p, _f64p, _f64p, _f64p]
+        L.orc_jacobi.argtypes = [i64, _i64p, _i64p, _f64p, _f64p, _f64p, dbl, _f64p]
+        L.orc_setup.restype = vp
+        L.orc_setup.argtypes = [i64, _i64p, _i64p, _f64p, C.c_int, _i64p, dbl, C.c_int, i64]
+        L.orc_free.argtypes = [vp]
+        L.orc_status.argtypes = [vp]
+        L.orc_nlev.argtypes = [vp]
+        L.orc_omega.restype = dbl
+        L.orc_omega.argtypes = [vp, C.c_int]
+        L.orc_rho.restype = dbl
+        L.orc_rho.argtypes = [vp, C.c_int]
+        L.orc_csr_info.argtypes = [vp, C.c_int, C.c_int, _i64p]
+        L.orc_csr_get.argtypes = [vp, C.c_int, C.c_int, _i64p, _i64p, _f64p]
+        L.orc_agg_get.argtypes = [vp, C.c_int, _i64p]
+        L.orc_offs_get.argtypes = [vp, C.c_int, _i64p]
+        L.orc_ainv_get.argtypes = [vp, _f64p]
+        L.orc_solve.argtypes = [vp, _f64p, _f64p, C.c_int, vp]
+        _lib = L
+    return _lib
+
+
+@dataclass
+class CSR:
+    """Host CSR with int64 indices (SPEC §S1)."""
+    rowptr: np.ndarray
+    col: np.ndarray
+    val: np.ndarray
+    ncols: int
+
+    @property
+    def nrows(self):
+        return len(self.rowptr) - 1
+
+    @property
+    def nnz(self):
+        return int(self.rowptr[-1])
+
+    def to_scipy(self):
+        import scipy.sparse as sp
+        return sp.csr_matrix((self.val, self.col, self.rowptr), shape=(self.nrows, self.ncols))
+
+
+def grid_shape(kind: str, n: int):
+    return (n, n, 1) if kind == "poisson2d" else (n, n, n)
+
+
+def generate(kind: str, nx: int, ny: int, nz: int, eps: float = 1e-3, r0: int = 0, r1=None) -> CSR:
+    """Rows [r0, r1) of the SPEC §S2 grid operator (global column ids)."""
+    L = lib()
+    n = nx * ny * nz
+    r1 = n if r1 is None else r1
+    k = KINDS[kind]
+    nnz = L.orc_gen_rows(k, nx, ny, nz, eps, r0, r1, None, None, None)
+    rp = np.empty(r1 - r0 + 1, np.int64)
+    col = np.empty(nnz, np.int64)
+    val = np.empty(nnz, np.float64)
+    L.orc_gen_rows(k, nx, ny, nz, eps, r0, r1, rp.ctypes.data, col.ctypes.data, val.ctypes.data)
+    return CSR(rp, col, val, n)
+
+
+def xstar(n: int, i0: int = 0, seed: int = SEED) -> np.ndarray:
+    out = np.empty(n, np.float64)
+    lib().orc_xstar(i0, n, seed, out)
+    return out
+
+
+def spmv(A: CSR, x: np.ndarray) -> np.ndarray:
+    y = np.empty(A.nrows, np.float64)
+    lib().orc_spmv(A.nrows, A.rowptr, A.col, A.val, np.ascontiguousarray(x, np.float64), y)
+    return y
+
+
+def residual(A: CSR, x, b):
+    r = np.empty(A.nrows, np.float64)
+    lib().orc_residual(A.nrows, A.rowptr, A.col, A.val, np.ascontiguousarray(x, np.float64),
+                       np.ascontiguousarray(b, np.float64), r)
+    return r
+
+
+def jacobi(A: CSR, x, b, omega: float):
+    xn = np.empty(A.nrows, np.float64)
+    lib().orc_jacobi(A.nrows, A.rowptr, A.col, A.val, np.ascontiguousarray(x, np.float64),
+                     np.ascontiguousarray(b, np.float64), omega, xn)
+    return xn
+
+
+def uniform_offsets(n: int, nparts: int) -> np.ndarray:
+    """SPEC §S7: part p owns [floor(p n / P), floor((p+1) n / P))."""
+    return np.array([(p * n) // nparts for p in range(nparts + 1)], np.int64)
+
+
+@dataclass
+class Hierarchy:
+    A: list = field(default_factory=list)
+    P: list = field(default_factory=list)
+    R: list = field(default_factory=list)
+    agg: list = field(default_factory=list)
+    offsets: list = field(default_factory=list)
+    omega: list = field(default_factory=list)
+    rho: list = field(default_factory=list)
+    ainv: np.ndarray = None
+    _h: int = 0
+
+    @property
+    def nlevels(self):
+        return len(self.A)
+
+    def solve(self, b, ncycles, x0=None, res_hist=False):
+        x = np.zeros(len(b)) if x0 is None else np.array(x0, np.float64, copy=True)
+        hist = np.zeros(ncycles) if res_hist else None
+        lib().orc_solve(self._h, x, np.ascontiguousarray(b, np.float64), ncycles,
+                        hist.ctypes.data if res_hist else None)
+        return (x, hist) if res_hist else x
+
+    def __del__(self):
+        if self._h and _lib is not None:
+            _lib.orc_free(self._h)
+            self._h = 0
+
+
+def setup(A: CSR, nparts: int = 1, theta: float = 0.02, max_levels: int = 20,
+          max_coarse: int = 1000) -> Hierarchy:
+    """SPEC §S4-§S5 smoothed-aggregation setup (global view, decoupled by parts)."""
+    L = lib()
+    offs = uniform_offsets(A.nrows, nparts)
+    h = L.orc_setup(A.nrows, A.rowptr, A.col, A.val, nparts, offs, theta, max_levels, max_coarse)
+    H = Hierarchy(_h=h)
+    if L.orc_status(h) != 0:
+        raise RuntimeError("oracle setup: coarse Cholesky failed")
+    nlev = L.orc_nlev(h)
+    info = np.zeros(3, np.int64)
+
+    def get(l, which):
+        L.orc_csr_info(h, l, which, info)
+        nr, nc, nnz = (int(v) for v in info)
+        rp = np.empty(nr + 1, np.int64); col = np.empty(nnz, np.int64); val = np.empty(nnz)
+        L.orc_csr_get(h, l, which, rp, col, val)
+        return CSR(rp, col, val, nc)
+
+    for l in range(nlev):
+        H.A.append(get(l, 0))
+        H.omega.append(L.orc_omega(h, l))
+        H.rho.append(L.orc_rho(h, l))
+        o = np.empty(nparts + 1, np.int64)
+        L.orc_offs_get(h, l, o)
+        H.offsets.append(o)
+        if l < nlev - 1:
+            H.P.append(get(l, 1))
+            H.R.append(get(l, 2))
+            a = np.empty(H.A[l].nrows, np.int64)
+            L.orc_agg_get(h, l, a)
+            H.agg.append(a)
+    nL = H.A[-1].nrows
+    H.ainv = np.empty(nL * nL)
+    L.orc_ainv_get(h, H.ainv)
+    H.ainv = H.ainv.reshape(nL, nL).T.copy()  # stored column-major -> row-major matrix
+    return H

@@ -1,0 +1,124 @@
+"""ctypes binding of libpamg.so (include/pamg.h) — the Python side of the C-ABI boundary.
+
+The library is built in-tree (``parallel_amg_amd/libpamg.so``) by ``build.build()``; there
+is deliberately NO fallback: if the shared library is missing or a symbol is absent, every
+entry point raises, so a test can never pass on a silent CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpamg.so")
+
+PAMG_OK = 0
+ERRORS = {-1: "PAMG_E_ARG", -2: "PAMG_E_HIP", -3: "PAMG_E_RCCL", -4: "PAMG_E_OVERFLOW",
+          -5: "PAMG_E_SETUP", -6: "PAMG_E_STATE", -7: "PAMG_E_NOMEM"}
+
+
+class PamgError(RuntimeError):
+    def __init__(self, code, fn, msg):
+        super().__init__(f"{fn} -> {ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+vp = C.c_void_p
+i32, i64, dbl = C.c_int, C.c_int64, C.c_double
+pvp = C.POINTER(C.c_void_p)
+pi64 = C.POINTER(C.c_int64)
+pdbl = C.POINTER(C.c_double)
+pi32 = C.POINTER(C.c_int32)
+
+# name -> argtypes (all return int status unless listed in _RESTYPE)
+SIGNATURES = {
+    "pamg_version": [],
+    "pamg_last_error": [],
+    "pamg_ctx_create": [i32, pvp],
+    "pamg_ctx_destroy": [vp],
+    "pamg_ctx_sync": [vp],
+    "pamg_comm_unique_id": [C.c_char_p],
+    "pamg_comm_init": [vp, i32, i32, C.c_char_p],
+    "pamg_comm_rank": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
+    "pamg_plan_create": [vp, i64, i64, i32, vp, vp, vp, vp, pvp],
+    "pamg_plan_destroy": [vp],
+    "pamg_vec_create": [vp, i64, i64, pvp],
+    "pamg_vec_destroy": [vp],
+    "pamg_vec_size": [vp, pi64, pi64],
+    "pamg_vec_upload": [vp, vp, vp],
+    "pamg_vec_download": [vp, vp, vp],
+    "pamg_vec_device_ptr": [vp, pvp],
+    "pamg_vec_fill": [vp, vp, dbl],
+    "pamg_vec_copy": [vp, vp, vp],
+    "pamg_vec_axpby": [vp, dbl, vp, dbl, vp],
+    "pamg_vec_dot": [vp, vp, vp, pdbl],
+    "pamg_vec_nrm2": [vp, vp, pdbl],
+    "pamg_exchange": [vp, vp, vp],
+    "pamg_mat_upload": [vp, i64, i64, vp, vp, i32, vp, i32, vp, pvp],
+    "pamg_mat_destroy": [vp],
+    "pamg_mat_info": [vp, pi64, pi64, pi64],
+    "pamg_spmv": [vp, vp, vp, vp],
+    "pamg_residual": [vp, vp, vp, vp, vp, pdbl],
+    "pamg_jacobi": [vp, vp, vp, vp, vp, dbl, i32],
+    "pamg_hier_create": [vp, i32, vp, vp, vp, vp, i64, vp, vp, pvp],
+    "pamg_hier_destroy": [vp],
+    "pamg_hier_set_graph": [vp, i32],
+    "pamg_vcycle": [vp, vp, vp, vp, i32, vp],
+    "pamg_vcycle_async": [vp, vp, vp, vp, i32],
+    "pamg_hier_profile": [vp, i32],
+    "pamg_hier_profile_read": [vp, vp],
+    "pamg_bench_spmv": [vp, vp, vp, vp, i32, pdbl],
+    "pamg_hcsr_create": [i64, i64, i64, pvp],
+    "pamg_hcsr_destroy": [vp],
+    "pamg_hcsr_info": [vp, pi64, pi64, pi64],
+    "pamg_hcsr_data": [vp, C.POINTER(pi64), C.POINTER(pi32), C.POINTER(pdbl)],
+    "pamg_gen_grid": [i32, i64, i64, i64, dbl, i64, i64, pvp],
+    "pamg_gen_xstar": [i64, i64, C.c_uint64, vp],
+    "pamg_setup_gershgorin": [vp, i64, pdbl],
+    "pamg_setup_aggregate": [vp, i64, dbl, vp, pi64],
+    "pamg_setup_tentative": [i64, vp, i64, i64, i64, pvp],
+    "pamg_setup_spgemm": [vp, i64, vp, vp, i64, vp, pvp],
+    "pamg_setup_smooth": [vp, i64, vp, vp, dbl],
+    "pamg_setup_transpose": [vp, i64, i64, i64, pvp],
+    "pamg_setup_hstack_rows": [i32, vp, pvp],
+    "pamg_setup_cholinv": [vp, vp],
+}
+_RESTYPE = {"pamg_version": C.c_char_p, "pamg_last_error": C.c_char_p}
+
+_lib = None
+
+
+def lib():
+    """Load libpamg.so (raises if it has not been built — no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(or `make -C parallel_amg_amd/csrc`). There is no CPU fallback.")
+        L = C.CDLL(LIB_PATH)
+        for name, args in SIGNATURES.items():
+            f = getattr(L, name)  # AttributeError if the ABI lost a symbol
+            f.argtypes = args
+            f.restype = _RESTYPE.get(name, C.c_int)
+        _lib = L
+    return _lib
+
+
+def call(name, *args):
+    """Call a status-returning entry point; raise PamgError with pamg_last_error on failure."""
+    L = lib()
+    rc = getattr(L, name)(*args)
+    if rc != PAMG_OK:
+        msg = L.pamg_last_error().decode(errors="replace")
+        raise PamgError(rc, name, msg)
+    return rc
+
+
+def last_error() -> str:
+    return lib().pamg_last_error().decode(errors="replace")
+
+
+def ptr(a):
+    """Raw data pointer of a numpy array (None for empty arrays)."""
+    return C.c_void_p(a.ctypes.data) if a is not None and a.size else None

@@ -1,0 +1,278 @@
+// kernels.hip — gfx950 (CDNA4) kernels of the AMG V-cycle solve path.
+//
+// Every row-sum kernel implements SPEC.md §S3 exactly: products p = a*x rounded, summed
+// left to right in storage order from +0.0, never fused (built with -ffp-contract=off), so
+// results are bit-identical to the CPU oracle and run-to-run deterministic.
+//
+// CSR row kernel (k_rows_tile): the path is HBM-bound sparse work (12 B/nnz of matrix
+// stream + vectors, ~0.17 flop/B), so there is no MFMA here. One 256-thread workgroup takes
+// a tile of <= 256 consecutive rows / <= 2048 nonzeros:
+//   phase 0  the tile's row pointers -> LDS;
+//   phase 1  the tile's columns/values are streamed with 16-byte loads (int4 / 2x double2
+//            per lane, fully coalesced, 1 KiB per wave-instruction), each lane gathers its
+//            four x[col] and writes the four products to LDS (the "LDS-staged partial
+//            sums"); for Jacobi the lane that holds a row's diagonal stores it in LDS;
+//   phase 2  one lane per row adds its products from LDS in storage order and applies the
+//            epilogue (SpMV / residual / Jacobi / prolongate-add), coalesced stores.
+// Rows longer than the tile budget go to k_rows_long (one workgroup per row, chunked).
+#include "pamg_device.h"
+
+namespace pamg {
+namespace {
+
+template <int OP>
+__device__ __forceinline__ void epilogue(int r, double s, const double* __restrict__ x,
+                                         const double* __restrict__ b, double* __restrict__ y,
+                                         double omega, double d) {
+    if constexpr (OP == OP_SPMV) {
+        y[r] = s;
+    } else if constexpr (OP == OP_RESID) {
+        y[r] = b[r] - s;
+    } else if constexpr (OP == OP_JACOBI) {
+        const double u = b[r] - s;
+        const double v = omega * u;
+        const double w = v / d;
+        y[r] = x[r] + w;
+    } else {
+        y[r] = y[r] + s;
+    }
+}
+
+template <int OP>
+__global__ __launch_bounds__(kBlock) void k_rows_tile(
+    const int2* __restrict__ tiles, const int* __restrict__ rowptr, const int* __restrict__ col,
+    const double* __restrict__ val, const double* __restrict__ x, const double* __restrict__ b,
+    double* __restrict__ y, double omega) {
+    __shared__ __attribute__((aligned(16))) double lprod[kTileNnz + 8];
+    __shared__ int lrp[kTileRows + 1];
+    __shared__ double ldiag[OP == OP_JACOBI ? kTileRows : 1];
+
+    const int tid = threadIdx.x;
+    const int2 t = tiles[blockIdx.x];
+    const int r0 = t.x, nr = t.y - t.x;
+    for (int i = tid; i <= nr; i += kBlock) lrp[i] = rowptr[r0 + i];
+    __syncthreads();
+    const int z0 = lrp[0], z1 = lrp[nr];
+    const int za = z0 & ~3;  // 16-byte aligned start of the column stream
+
+    for (int g = za + 4 * tid; g < z1; g += 4 * kBlock) {
+        const int4 c4 = *reinterpret_cast<const int4*>(col + g);
+        const double2 va = *reinterpret_cast<const double2*>(val + g);
+        const double2 vb = *reinterpret_cast<const double2*>(val + g + 2);
+        const int cc[4] = {c4.x, c4.y, c4.z, c4.w};
+        const double vv[4] = {va.x, va.y, vb.x, vb.y};
+        double p[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int k = g + e;
+            const bool ok = (k >= z0) & (k < z1);
+            p[e] = ok ? vv[e] * x[cc[e]] : 0.0;
+            if constexpr (OP == OP_JACOBI) {
+                const int rl = cc[e] - r0;  // own column id == local row id of its diagonal
+                if (ok && rl >= 0 && rl < nr && k >= lrp[rl] && k < lrp[rl + 1]) ldiag[rl] = vv[e];
+            }
+        }
+        *reinterpret_cast<double2*>(&lprod[g - za]) = make_double2(p[0], p[1]);
+        *reinterpret_cast<double2*>(&lprod[g - za + 2]) = make_double2(p[2], p[3]);
+    }
+    __syncthreads();
+    if (tid < nr) {
+        const int r = r0 + tid;
+        const int kb = lrp[tid] - za, ke = lrp[tid + 1] - za;
+        double s = 0.0;
+        for (int k = kb; k < ke; ++k) s = s + lprod[k];
+        epilogue<OP>(r, s, x, b, y, omega, OP == OP_JACOBI ? ldiag[tid] : 0.0);
+    }
+}
+
+template <int OP>
+__global__ __launch_bounds__(kBlock) void k_rows_long(
+    const int* __restrict__ rows, const int* __restrict__ rowptr, const int* __restrict__ col,
+    const double* __restrict__ val, const double* __restrict__ x, const double* __restrict__ b,
+    double* __restrict__ y, double omega) {
+    __shared__ double lprod[kBlock];
+    __shared__ double ldiag;
+    const int tid = threadIdx.x;
+    const int r = rows[blockIdx.x];
+    const int z0 = rowptr[r], z1 = rowptr[r + 1];
+    double s = 0.0;
+    for (int base = z0; base < z1; base += kBlock) {
+        const int k = base + tid;
+        double p = 0.0;
+        if (k < z1) {
+            const int c = col[k];
+            const double v = val[k];
+            p = v * x[c];
+            if constexpr (OP == OP_JACOBI) {
+                if (c == r) ldiag = v;
+            }
+        }
+        lprod[tid] = p;
+        __syncthreads();
+        if (tid == 0) {
+            const int m = min(kBlock, z1 - base);
+            for (int j = 0; j < m; ++j) s = s + lprod[j];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) epilogue<OP>(r, s, x, b, y, omega, OP == OP_JACOBI ? ldiag : 0.0);
+}
+
+__global__ void k_jacobi_zero(int64_t n, const double* __restrict__ b,
+                              const double* __restrict__ diag, double omega,
+                              double* __restrict__ y) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const double u = b[i] - 0.0;
+        const double v = omega * u;
+        const double w = v / diag[i];
+        y[i] = 0.0 + w;
+    }
+}
+
+// x[row0 + i] for the caller's rows: s = sum_j ainv[j*n + (row0+i)] * b[j] (SPEC §S5, §S3).
+__global__ __launch_bounds__(kBlock) void k_dense_gemv(int64_t n_rows, int64_t n,
+                                                       int64_t row0,
+                                                       const double* __restrict__ ainv,
+                                                       const double* __restrict__ b,
+                                                       double* __restrict__ y) {
+    const int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    if (i >= n_rows) return;
+    const double* a = ainv + row0 + i;
+    double s = 0.0;
+    int64_t j = 0;
+    for (; j + 4 <= n; j += 4) {
+        const double p0 = a[(j + 0) * n] * b[j + 0];
+        const double p1 = a[(j + 1) * n] * b[j + 1];
+        const double p2 = a[(j + 2) * n] * b[j + 2];
+        const double p3 = a[(j + 3) * n] * b[j + 3];
+        s = s + p0;
+        s = s + p1;
+        s = s + p2;
+        s = s + p3;
+    }
+    for (; j < n; ++j) {
+        const double p = a[j * n] * b[j];
+        s = s + p;
+    }
+    y[i] = s;
+}
+
+__global__ void k_pack(int64_t n, const int* __restrict__ idx, const double* __restrict__ x,
+                       double* __restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = x[idx[i]];
+}
+
+__global__ void k_fill(int64_t n, double v, double* __restrict__ y) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = v;
+}
+
+__global__ void k_axpby(int64_t n, double a, const double* __restrict__ x, double bb,
+                        double* __restrict__ y) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const double u = a * x[i];
+        const double v = bb * y[i];
+        y[i] = u + v;
+    }
+}
+
+__device__ __forceinline__ double block_sum(double v, double* lds) {
+    // wave64 shuffle tree, then the 4 wave sums in fixed order
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) lds[w] = v;
+    __syncthreads();
+    double s = 0.0;
+    if (threadIdx.x == 0)
+        for (int k = 0; k < (int)(blockDim.x >> 6); ++k) s += lds[k];
+    return s;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dot_partial(int64_t n, const double* __restrict__ x,
+                                                        const double* __restrict__ y,
+                                                        double* __restrict__ partials) {
+    __shared__ double lds[kBlock / 64];
+    double v = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * kBlock)
+        v += x[i] * y[i];
+    const double s = block_sum(v, lds);
+    if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dot_final(int np, const double* __restrict__ partials,
+                                                      double* __restrict__ out) {
+    __shared__ double lds[kBlock / 64];
+    double v = 0.0;
+    for (int i = threadIdx.x; i < np; i += kBlock) v += partials[i];
+    const double s = block_sum(v, lds);
+    if (threadIdx.x == 0) *out = s;
+}
+
+inline int grid_for(int64_t n, int cap = 8192) {
+    int64_t g = (n + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    return (int)(g < cap ? g : cap);
+}
+
+template <int OP>
+void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
+                    double* y, double omega, hipStream_t s) {
+    if (ts.n_short > 0)
+        k_rows_tile<OP><<<ts.n_short, kBlock, 0, s>>>(ts.d_short, A.d_rowptr, A.d_col, A.d_val,
+                                                      x, b, y, omega);
+    if (ts.n_long > 0)
+        k_rows_long<OP><<<ts.n_long, kBlock, 0, s>>>(ts.d_long, A.d_rowptr, A.d_col, A.d_val, x,
+                                                     b, y, omega);
+}
+
+}  // namespace
+
+void launch_rows(const pamg_mat& A, const TileSet& ts, int op, const double* x, const double* b,
+                 const double* /*xold*/, double* y, double omega, hipStream_t s) {
+    switch (op) {
+        case OP_SPMV: launch_rows_op<OP_SPMV>(A, ts, x, b, y, omega, s); break;
+        case OP_RESID: launch_rows_op<OP_RESID>(A, ts, x, b, y, omega, s); break;
+        case OP_JACOBI: launch_rows_op<OP_JACOBI>(A, ts, x, b, y, omega, s); break;
+        default: launch_rows_op<OP_PROLONG>(A, ts, x, b, y, omega, s); break;
+    }
+}
+
+void launch_jacobi_zero(int64_t n, const double* b, const double* diag, double omega, double* y,
+                        hipStream_t s) {
+    if (n > 0) k_jacobi_zero<<<grid_for(n), kBlock, 0, s>>>(n, b, diag, omega, y);
+}
+
+void launch_dense_gemv(int64_t n_rows, int64_t n_cols, int64_t row0, const double* ainv_cm,
+                       const double* b, double* y, hipStream_t s) {
+    if (n_rows > 0)
+        k_dense_gemv<<<(int)((n_rows + kBlock - 1) / kBlock), kBlock, 0, s>>>(n_rows, n_cols,
+                                                                             row0, ainv_cm, b, y);
+}
+
+void launch_pack(int64_t n, const int* idx, const double* x, double* out, hipStream_t s) {
+    if (n > 0) k_pack<<<grid_for(n), kBlock, 0, s>>>(n, idx, x, out);
+}
+
+void launch_fill(int64_t n, double v, double* y, hipStream_t s) {
+    if (n > 0) k_fill<<<grid_for(n), kBlock, 0, s>>>(n, v, y);
+}
+
+void launch_axpby(int64_t n, double a, const double* x, double b, double* y, hipStream_t s) {
+    if (n > 0) k_axpby<<<grid_for(n), kBlock, 0, s>>>(n, a, x, b, y);
+}
+
+int dot_partials(int64_t n) { return grid_for(n, 1024); }
+
+void launch_dot(int64_t n, const double* x, const double* y, double* partials, int np,
+                double* out, hipStream_t s) {
+    k_dot_partial<<<np, kBlock, 0, s>>>(n, x, y, partials);
+    k_dot_final<<<1, kBlock, 0, s>>>(np, partials, out);
+}
+
+}  // namespace pamg

@@ -1,0 +1,94 @@
+// pamg_device.h — device-side objects of libpamg (context, plans, vectors, matrices,
+// hierarchy) and the kernel launchers of kernels.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "pamg_common.h"
+
+namespace pamg {
+
+// Row tiles of the LDS-staged CSR kernel (kernels.hip): each tile is a run of <= kTileRows
+// consecutive rows holding <= kTileNnz nonzeros; a row longer than kTileNnz is a tile of its
+// own in the "long" list.
+constexpr int kBlock = 256;
+constexpr int kTileRows = 256;
+constexpr int kTileNnz = 2048;
+
+enum RowOp : int {
+    OP_SPMV = 0,     // y = A x
+    OP_RESID = 1,    // y = b - A x
+    OP_JACOBI = 2,   // y = x + (omega (b - A x)) / a_ii
+    OP_PROLONG = 3,  // y = y + A x      (x += P e)
+};
+
+struct TileSet {
+    int2* d_short = nullptr;  // (row_begin, row_end)
+    int n_short = 0;
+    int* d_long = nullptr;  // single rows
+    int n_long = 0;
+};
+
+}  // namespace pamg
+
+struct pamg_ctx {
+    int device = 0;
+    hipStream_t s_comp = nullptr;  // compute stream
+    hipStream_t s_comm = nullptr;  // ghost exchange stream
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    ncclComm_t comm = nullptr;
+    int rank = 0, nranks = 1;
+    double* d_red = nullptr;  // reduction workspace (partials + result)
+    int red_cap = 0;
+    double* h_red = nullptr;  // pinned host scalar
+};
+
+struct pamg_plan {
+    pamg_ctx* ctx = nullptr;
+    int64_t n_own = 0, n_ghost = 0;
+    std::vector<int> nbr;
+    std::vector<int64_t> recv_off, send_off;  // n_nbr + 1
+    int* d_send_idx = nullptr;
+    double* d_sendbuf = nullptr;
+};
+
+struct pamg_vec {
+    pamg_ctx* ctx = nullptr;
+    int64_t n_own = 0, n_ghost = 0;
+    double* d = nullptr;  // n_own + n_ghost (+ padding)
+};
+
+struct pamg_mat {
+    pamg_ctx* ctx = nullptr;
+    int64_t nrows = 0, ncols = 0, nnz = 0;
+    int* d_rowptr = nullptr;
+    int* d_col = nullptr;
+    double* d_val = nullptr;
+    double* d_diag = nullptr;  // a_ii for square matrices (zero-guess Jacobi), else null
+    const pamg_plan* plan = nullptr;
+    pamg::TileSet interior;  // rows with own columns only (overlap with the exchange)
+    pamg::TileSet boundary;  // rows with >= 1 ghost column
+};
+
+namespace pamg {
+
+// kernels.hip launchers (all asynchronous on `s`).
+void launch_rows(const pamg_mat& A, const TileSet& ts, int op, const double* x, const double* b,
+                 const double* xold, double* y, double omega, hipStream_t s);
+void launch_jacobi_zero(int64_t n, const double* b, const double* diag, double omega, double* y,
+                        hipStream_t s);
+void launch_dense_gemv(int64_t n_rows, int64_t n_cols, int64_t row0, const double* ainv_cm,
+                       const double* b, double* y, hipStream_t s);
+void launch_pack(int64_t n, const int* idx, const double* x, double* out, hipStream_t s);
+void launch_fill(int64_t n, double v, double* y, hipStream_t s);
+void launch_axpby(int64_t n, double a, const double* x, double b, double* y, hipStream_t s);
+// Deterministic two-pass dot: writes the local sum to *out (device).
+void launch_dot(int64_t n, const double* x, const double* y, double* partials, int nparts,
+                double* out, hipStream_t s);
+int dot_partials(int64_t n);
+
+}  // namespace pamg

@@ -1,0 +1,887 @@
+// runtime.hip — C-ABI implementation of the device side of libpamg (include/pamg.h):
+// context and streams, RCCL communicator, exchange plans (PartitionedArrays' PRange ghost
+// layout), device vectors and matrices, mul!/residual/Jacobi with the ghost exchange
+// overlapped with the interior rows, and the V-cycle driver (SPEC.md §S6) replayed as a
+// captured hipGraph.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "pamg_device.h"
+
+using pamg::fail;
+
+std::string& pamg::last_error() {
+    static thread_local std::string msg;
+    return msg;
+}
+
+#define HIPC(expr)                                                                    \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            return fail(PAMG_E_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #expr,        \
+                        hipGetErrorString(e_));                                       \
+    } while (0)
+
+#define NCCLC(expr)                                                                   \
+    do {                                                                              \
+        ncclResult_t r_ = (expr);                                                     \
+        if (r_ != ncclSuccess)                                                        \
+            return fail(PAMG_E_RCCL, "%s:%d %s: %s", __FILE__, __LINE__, #expr,       \
+                        ncclGetErrorString(r_));                                      \
+    } while (0)
+
+#define CHECK(expr)                   \
+    do {                              \
+        int rc_ = (expr);             \
+        if (rc_ != PAMG_OK) return rc_; \
+    } while (0)
+
+namespace {
+
+constexpr int kVecPad = 8;  // trailing doubles so 16-byte vector loads never run off the end
+
+template <class T>
+int dalloc(T** p, int64_t n) {
+    *p = nullptr;
+    if (n <= 0) return PAMG_OK;
+    HIPC(hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (size_t)n));
+    return PAMG_OK;
+}
+
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+int set_device(const pamg_ctx* ctx) {
+    HIPC(hipSetDevice(ctx->device));
+    return PAMG_OK;
+}
+
+// Greedy tiling of the rows listed in `rows` (ascending) into runs of consecutive rows with
+// <= kTileRows rows and <= kTileNnz nonzeros; rows above the budget become "long" rows.
+int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
+                pamg::TileSet* ts) {
+    std::vector<int2> tiles;
+    std::vector<int> longr;
+    size_t i = 0;
+    while (i < rows.size()) {
+        const int r = rows[i];
+        const int64_t len = rp[r + 1] - rp[r];
+        if (len > pamg::kTileNnz) {
+            longr.push_back(r);
+            ++i;
+            continue;
+        }
+        int end = r + 1;
+        int64_t nz = len;
+        size_t j = i + 1;
+        while (j < rows.size() && rows[j] == end && end - r < pamg::kTileRows) {
+            const int64_t l2 = rp[end + 1] - rp[end];
+            if (l2 > pamg::kTileNnz || nz + l2 > pamg::kTileNnz) break;
+            nz += l2;
+            ++end;
+            ++j;
+        }
+        tiles.push_back(make_int2(r, end));
+        i = j;
+    }
+    ts->n_short = (int)tiles.size();
+    ts->n_long = (int)longr.size();
+    CHECK(dalloc(&ts->d_short, ts->n_short));
+    CHECK(dalloc(&ts->d_long, ts->n_long));
+    if (ts->n_short)
+        HIPC(hipMemcpy(ts->d_short, tiles.data(), sizeof(int2) * tiles.size(), hipMemcpyHostToDevice));
+    if (ts->n_long)
+        HIPC(hipMemcpy(ts->d_long, longr.data(), sizeof(int) * longr.size(), hipMemcpyHostToDevice));
+    return PAMG_OK;
+}
+
+void free_tiles(pamg::TileSet& ts) {
+    dfree(ts.d_short);
+    dfree(ts.d_long);
+    ts.n_short = ts.n_long = 0;
+}
+
+// Ghost exchange of plan on stream s: pack own values, grouped RCCL send/recv straight into
+// the ghost slots [n_own + recv_off[k], ...).
+int exchange_on(const pamg_plan* plan, double* x, hipStream_t s) {
+    pamg_ctx* ctx = plan->ctx;
+    const int nn = (int)plan->nbr.size();
+    if (nn == 0) return PAMG_OK;
+    if (!ctx->comm) return fail(PAMG_E_STATE, "exchange: plan has neighbours but no communicator");
+    pamg::launch_pack(plan->send_off[nn], plan->d_send_idx, x, plan->d_sendbuf, s);
+    NCCLC(ncclGroupStart());
+    for (int k = 0; k < nn; ++k) {
+        const size_t sc = (size_t)(plan->send_off[k + 1] - plan->send_off[k]);
+        const size_t rc = (size_t)(plan->recv_off[k + 1] - plan->recv_off[k]);
+        if (sc) NCCLC(ncclSend(plan->d_sendbuf + plan->send_off[k], sc, ncclDouble, plan->nbr[k], ctx->comm, s));
+        if (rc) NCCLC(ncclRecv(x + plan->n_own + plan->recv_off[k], rc, ncclDouble, plan->nbr[k], ctx->comm, s));
+    }
+    NCCLC(ncclGroupEnd());
+    return PAMG_OK;
+}
+
+// y = op(A, x[, b]) with x's ghosts exchanged first; interior rows overlap the exchange.
+int apply(pamg_ctx* ctx, const pamg_mat* A, int op, double* x, const double* b, double* y,
+          double omega) {
+    hipStream_t s = ctx->s_comp;
+    const bool comm = A->plan && !A->plan->nbr.empty();
+    if (comm) {
+        HIPC(hipEventRecord(ctx->ev_fork, s));
+        HIPC(hipStreamWaitEvent(ctx->s_comm, ctx->ev_fork, 0));
+        CHECK(exchange_on(A->plan, x, ctx->s_comm));
+        HIPC(hipEventRecord(ctx->ev_join, ctx->s_comm));
+    }
+    pamg::launch_rows(*A, A->interior, op, x, b, x, y, omega, s);
+    if (comm) HIPC(hipStreamWaitEvent(s, ctx->ev_join, 0));
+    pamg::launch_rows(*A, A->boundary, op, x, b, x, y, omega, s);
+    HIPC(hipGetLastError());
+    return PAMG_OK;
+}
+
+int reduce_scalar(pamg_ctx* ctx, int64_t n, const double* x, const double* y, double* out) {
+    hipStream_t s = ctx->s_comp;
+    const int np = pamg::dot_partials(n);
+    if (np + 1 > ctx->red_cap) return fail(PAMG_E_STATE, "reduction workspace too small");
+    double* res = ctx->d_red + ctx->red_cap - 1;
+    pamg::launch_dot(n, x, y, ctx->d_red, np, res, s);
+    if (ctx->comm && ctx->nranks > 1) NCCLC(ncclAllReduce(res, res, 1, ncclDouble, ncclSum, ctx->comm, s));
+    HIPC(hipMemcpyAsync(ctx->h_red, res, sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    *out = *ctx->h_red;
+    return PAMG_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ hierarchy type
+
+struct pamg_hier {
+    pamg_ctx* ctx = nullptr;
+    int L = 0;
+    std::vector<const pamg_mat*> A, P, R;
+    std::vector<double> omega;
+    // per-level work vectors (level 0: t, r only; x and b belong to the caller)
+    std::vector<double*> x, b, t, r;
+    std::vector<int64_t> nown;
+    // coarsest level
+    int64_t nc = 0;
+    double* d_ainv = nullptr;          // column-major nc x nc
+    std::vector<int64_t> coffs;        // nranks + 1
+    int64_t cmax = 0;                  // max rows per rank on the coarsest level
+    double* d_bgather = nullptr;       // nranks * cmax
+    double* d_bsend = nullptr;         // cmax
+    int* d_ccnt = nullptr;             // per-rank counts on device (gemv over ragged blocks)
+    // graph replay
+    bool use_graph = true;
+    hipGraphExec_t gexec = nullptr;
+    const double* g_x = nullptr;
+    const double* g_b = nullptr;
+    // profiling
+    bool prof = false;
+    std::vector<hipEvent_t> ev;
+    std::vector<std::pair<int, int>> ev_tag;  // (level, op) per event pair
+    std::vector<double> prof_ms;              // L * 6
+};
+
+namespace {
+
+int coarse_solve(pamg_hier* H, const double* bL, double* xL, hipStream_t s) {
+    pamg_ctx* ctx = H->ctx;
+    const int nr = (int)H->coffs.size() - 1;
+    const int me = ctx->rank;
+    const int64_t own0 = H->coffs[me], nown = H->coffs[me + 1] - own0;
+    if (nr == 1) {
+        pamg::launch_dense_gemv(nown, H->nc, 0, H->d_ainv, bL, xL, s);
+        return PAMG_OK;
+    }
+    // all-gather b_L in rank blocks of cmax, then the owned rows of Ainv * b_L
+    HIPC(hipMemcpyAsync(H->d_bsend, bL, sizeof(double) * nown, hipMemcpyDeviceToDevice, s));
+    NCCLC(ncclAllGather(H->d_bsend, H->d_bgather, (size_t)H->cmax, ncclDouble, ctx->comm, s));
+    // compact the gathered blocks into global order (ragged -> contiguous), in place safe:
+    // use d_bgather as source and d_bsend is too small, so copy rank blocks into xL-sized
+    // scratch: reuse the tail of d_bgather (allocated 2x)
+    double* dst = H->d_bgather + (size_t)nr * H->cmax;
+    for (int q = 0; q < nr; ++q) {
+        const int64_t c = H->coffs[q + 1] - H->coffs[q];
+        if (c)
+            HIPC(hipMemcpyAsync(dst + H->coffs[q], H->d_bgather + (size_t)q * H->cmax,
+                                sizeof(double) * c, hipMemcpyDeviceToDevice, s));
+    }
+    pamg::launch_dense_gemv(nown, H->nc, own0, H->d_ainv, dst, xL, s);
+    return PAMG_OK;
+}
+
+struct ProfScope {
+    pamg_hier* H;
+    int lev, op;
+    hipStream_t s;
+    ProfScope(pamg_hier* h, int l, int o, hipStream_t st) : H(h), lev(l), op(o), s(st) {
+        if (!H->prof) return;
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        (void)hipEventRecord(e, s);
+        H->ev.push_back(e);
+    }
+    ~ProfScope() {
+        if (!H->prof) return;
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        (void)hipEventRecord(e, s);
+        H->ev.push_back(e);
+        H->ev_tag.emplace_back(lev, op);
+    }
+};
+
+// One V-cycle (SPEC §S6), enqueued on the compute stream; result in x.
+int vcycle_enqueue(pamg_hier* H, double* x, const double* b) {
+    pamg_ctx* ctx = H->ctx;
+    hipStream_t s = ctx->s_comp;
+    const int L = H->L;
+    if (L == 1) {
+        ProfScope p(H, 0, 5, s);
+        return coarse_solve(H, b, x, s);
+    }
+    H->x[0] = x;
+    H->b[0] = const_cast<double*>(b);
+    for (int l = 0; l < L - 1; ++l) {
+        const pamg_mat* A = H->A[l];
+        if (l == 0) {
+            ProfScope p(H, l, 0, s);
+            CHECK(apply(ctx, A, pamg::OP_JACOBI, H->x[0], H->b[0], H->t[0], H->omega[0]));
+        } else {
+            ProfScope p(H, l, 0, s);
+            pamg::launch_jacobi_zero(H->nown[l], H->b[l], A->d_diag, H->omega[l], H->t[l], s);
+        }
+        {
+            ProfScope p(H, l, 1, s);
+            CHECK(apply(ctx, A, pamg::OP_RESID, H->t[l], H->b[l], H->r[l], 0.0));
+        }
+        {
+            ProfScope p(H, l, 2, s);
+            CHECK(apply(ctx, H->R[l], pamg::OP_SPMV, H->r[l], nullptr, H->b[l + 1], 0.0));
+        }
+    }
+    {
+        ProfScope p(H, L - 1, 5, s);
+        CHECK(coarse_solve(H, H->b[L - 1], H->x[L - 1], s));
+    }
+    for (int l = L - 2; l >= 0; --l) {
+        {
+            ProfScope p(H, l, 3, s);
+            CHECK(apply(ctx, H->P[l], pamg::OP_PROLONG, H->x[l + 1], nullptr, H->t[l], 0.0));
+        }
+        {
+            ProfScope p(H, l, 4, s);
+            CHECK(apply(ctx, H->A[l], pamg::OP_JACOBI, H->t[l], H->b[l], H->x[l], H->omega[l]));
+        }
+    }
+    HIPC(hipGetLastError());
+    return PAMG_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ C-ABI
+
+extern "C" {
+
+const char* pamg_version(void) { return "pamg 0.1 (gfx950)"; }
+const char* pamg_last_error(void) { return pamg::last_error().c_str(); }
+
+int pamg_ctx_create(int device, pamg_ctx** out) {
+    if (!out) return fail(PAMG_E_ARG, "ctx_create: out is NULL");
+    int ndev = 0;
+    HIPC(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(PAMG_E_ARG, "ctx_create: device %d of %d", device, ndev);
+    auto c = std::make_unique<pamg_ctx>();
+    c->device = device;
+    HIPC(hipSetDevice(device));
+    HIPC(hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking));
+    HIPC(hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking));
+    HIPC(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    HIPC(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    c->red_cap = 2048;
+    CHECK(dalloc(&c->d_red, c->red_cap));
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&c->h_red), sizeof(double)));
+    *out = c.release();
+    return PAMG_OK;
+}
+
+int pamg_ctx_destroy(pamg_ctx* ctx) {
+    if (!ctx) return PAMG_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->s_comp);
+    (void)hipStreamSynchronize(ctx->s_comm);
+    if (ctx->comm) ncclCommDestroy(ctx->comm);
+    dfree(ctx->d_red);
+    if (ctx->h_red) (void)hipHostFree(ctx->h_red);
+    (void)hipEventDestroy(ctx->ev_fork);
+    (void)hipEventDestroy(ctx->ev_join);
+    (void)hipStreamDestroy(ctx->s_comp);
+    (void)hipStreamDestroy(ctx->s_comm);
+    delete ctx;
+    return PAMG_OK;
+}
+
+int pamg_ctx_sync(pamg_ctx* ctx) {
+    if (!ctx) return fail(PAMG_E_ARG, "ctx_sync: NULL");
+    HIPC(hipStreamSynchronize(ctx->s_comm));
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_comm_unique_id(unsigned char id[128]) {
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    ncclUniqueId u;
+    NCCLC(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, 128);
+    return PAMG_OK;
+}
+
+int pamg_comm_init(pamg_ctx* ctx, int nranks, int rank, const unsigned char id[128]) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks)
+        return fail(PAMG_E_ARG, "comm_init: bad args");
+    CHECK(set_device(ctx));
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    NCCLC(ncclCommInitRank(&ctx->comm, nranks, u, rank));
+    ctx->rank = rank;
+    ctx->nranks = nranks;
+    return PAMG_OK;
+}
+
+int pamg_comm_rank(const pamg_ctx* ctx, int* rank, int* nranks) {
+    if (!ctx) return fail(PAMG_E_ARG, "comm_rank: NULL");
+    if (rank) *rank = ctx->rank;
+    if (nranks) *nranks = ctx->nranks;
+    return PAMG_OK;
+}
+
+int pamg_plan_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, int n_nbr,
+                     const int32_t* nbr_rank, const int64_t* recv_counts,
+                     const int64_t* send_counts, const int64_t* send_idx, pamg_plan** out) {
+    if (!ctx || !out || n_own < 0 || n_ghost < 0 || n_nbr < 0)
+        return fail(PAMG_E_ARG, "plan_create: bad args");
+    if (n_nbr > 0 && (!nbr_rank || !recv_counts || !send_counts))
+        return fail(PAMG_E_ARG, "plan_create: neighbour arrays missing");
+    if (n_own >= INT32_MAX || n_own + n_ghost >= INT32_MAX)
+        return fail(PAMG_E_OVERFLOW, "plan_create: sizes exceed int32");
+    CHECK(set_device(ctx));
+    auto p = std::make_unique<pamg_plan>();
+    p->ctx = ctx;
+    p->n_own = n_own;
+    p->n_ghost = n_ghost;
+    p->nbr.assign(nbr_rank, nbr_rank + n_nbr);
+    p->recv_off.assign(n_nbr + 1, 0);
+    p->send_off.assign(n_nbr + 1, 0);
+    for (int k = 0; k < n_nbr; ++k) {
+        if (nbr_rank[k] < 0 || nbr_rank[k] >= ctx->nranks || nbr_rank[k] == ctx->rank)
+            return fail(PAMG_E_ARG, "plan_create: bad neighbour rank %d", nbr_rank[k]);
+        p->recv_off[k + 1] = p->recv_off[k] + recv_counts[k];
+        p->send_off[k + 1] = p->send_off[k] + send_counts[k];
+    }
+    if (p->recv_off[n_nbr] != n_ghost)
+        return fail(PAMG_E_ARG, "plan_create: recv counts sum %lld != n_ghost %lld",
+                    (long long)p->recv_off[n_nbr], (long long)n_ghost);
+    const int64_t ns = p->send_off[n_nbr];
+    std::vector<int> idx(ns);
+    for (int64_t k = 0; k < ns; ++k) {
+        if (send_idx[k] < 0 || send_idx[k] >= n_own)
+            return fail(PAMG_E_ARG, "plan_create: send index %lld out of range", (long long)send_idx[k]);
+        idx[k] = (int)send_idx[k];
+    }
+    CHECK(dalloc(&p->d_send_idx, ns));
+    CHECK(dalloc(&p->d_sendbuf, ns));
+    if (ns) HIPC(hipMemcpy(p->d_send_idx, idx.data(), sizeof(int) * ns, hipMemcpyHostToDevice));
+    *out = p.release();
+    return PAMG_OK;
+}
+
+int pamg_plan_destroy(pamg_plan* p) {
+    if (!p) return PAMG_OK;
+    (void)hipSetDevice(p->ctx->device);
+    dfree(p->d_send_idx);
+    dfree(p->d_sendbuf);
+    delete p;
+    return PAMG_OK;
+}
+
+int pamg_vec_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, pamg_vec** out) {
+    if (!ctx || !out || n_own < 0 || n_ghost < 0) return fail(PAMG_E_ARG, "vec_create: bad args");
+    CHECK(set_device(ctx));
+    auto v = std::make_unique<pamg_vec>();
+    v->ctx = ctx;
+    v->n_own = n_own;
+    v->n_ghost = n_ghost;
+    CHECK(dalloc(&v->d, n_own + n_ghost + kVecPad));
+    HIPC(hipMemsetAsync(v->d, 0, sizeof(double) * (n_own + n_ghost + kVecPad), ctx->s_comp));
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    *out = v.release();
+    return PAMG_OK;
+}
+
+int pamg_vec_destroy(pamg_vec* v) {
+    if (!v) return PAMG_OK;
+    (void)hipSetDevice(v->ctx->device);
+    (void)hipStreamSynchronize(v->ctx->s_comp);
+    dfree(v->d);
+    delete v;
+    return PAMG_OK;
+}
+
+int pamg_vec_size(const pamg_vec* v, int64_t* n_own, int64_t* n_ghost) {
+    if (!v) return fail(PAMG_E_ARG, "vec_size: NULL");
+    if (n_own) *n_own = v->n_own;
+    if (n_ghost) *n_ghost = v->n_ghost;
+    return PAMG_OK;
+}
+
+int pamg_vec_upload(pamg_ctx* ctx, pamg_vec* v, const double* own) {
+    if (!ctx || !v || (!own && v->n_own)) return fail(PAMG_E_ARG, "vec_upload: bad args");
+    CHECK(set_device(ctx));
+    if (v->n_own) HIPC(hipMemcpyAsync(v->d, own, sizeof(double) * v->n_own, hipMemcpyHostToDevice, ctx->s_comp));
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_vec_download(pamg_ctx* ctx, const pamg_vec* v, double* own) {
+    if (!ctx || !v || (!own && v->n_own)) return fail(PAMG_E_ARG, "vec_download: bad args");
+    CHECK(set_device(ctx));
+    if (v->n_own) HIPC(hipMemcpyAsync(own, v->d, sizeof(double) * v->n_own, hipMemcpyDeviceToHost, ctx->s_comp));
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_vec_device_ptr(pamg_vec* v, double** dptr) {
+    if (!v || !dptr) return fail(PAMG_E_ARG, "vec_device_ptr: bad args");
+    *dptr = v->d;
+    return PAMG_OK;
+}
+
+int pamg_vec_fill(pamg_ctx* ctx, pamg_vec* v, double value) {
+    if (!ctx || !v) return fail(PAMG_E_ARG, "vec_fill: bad args");
+    CHECK(set_device(ctx));
+    pamg::launch_fill(v->n_own, value, v->d, ctx->s_comp);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_vec_copy(pamg_ctx* ctx, const pamg_vec* src, pamg_vec* dst) {
+    if (!ctx || !src || !dst || src->n_own != dst->n_own) return fail(PAMG_E_ARG, "vec_copy: shape mismatch");
+    CHECK(set_device(ctx));
+    if (src->n_own)
+        HIPC(hipMemcpyAsync(dst->d, src->d, sizeof(double) * src->n_own, hipMemcpyDeviceToDevice, ctx->s_comp));
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_vec_axpby(pamg_ctx* ctx, double a, const pamg_vec* x, double b, pamg_vec* y) {
+    if (!ctx || !x || !y || x->n_own != y->n_own) return fail(PAMG_E_ARG, "vec_axpby: shape mismatch");
+    CHECK(set_device(ctx));
+    pamg::launch_axpby(x->n_own, a, x->d, b, y->d, ctx->s_comp);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_vec_dot(pamg_ctx* ctx, const pamg_vec* x, const pamg_vec* y, double* out) {
+    if (!ctx || !x || !y || !out || x->n_own != y->n_own) return fail(PAMG_E_ARG, "vec_dot: shape mismatch");
+    CHECK(set_device(ctx));
+    return reduce_scalar(ctx, x->n_own, x->d, y->d, out);
+}
+
+int pamg_vec_nrm2(pamg_ctx* ctx, const pamg_vec* x, double* out) {
+    if (!ctx || !x || !out) return fail(PAMG_E_ARG, "vec_nrm2: bad args");
+    CHECK(set_device(ctx));
+    double s = 0.0;
+    CHECK(reduce_scalar(ctx, x->n_own, x->d, x->d, &s));
+    *out = std::sqrt(s);
+    return PAMG_OK;
+}
+
+int pamg_exchange(pamg_ctx* ctx, const pamg_plan* plan, pamg_vec* x) {
+    if (!ctx || !plan || !x) return fail(PAMG_E_ARG, "exchange: bad args");
+    if (x->n_own != plan->n_own || x->n_ghost < plan->n_ghost)
+        return fail(PAMG_E_ARG, "exchange: vector does not fit the plan");
+    CHECK(set_device(ctx));
+    CHECK(exchange_on(plan, x->d, ctx->s_comp));
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* rowptr,
+                    const void* col, int col_is_64, const double* val, int index_base,
+                    const pamg_plan* plan, pamg_mat** out) {
+    if (!ctx || !out || nrows < 0 || ncols < 0 || !rowptr || (index_base != 0 && index_base != 1))
+        return fail(PAMG_E_ARG, "mat_upload: bad args");
+    const int64_t nnz = rowptr[nrows] - index_base;
+    if (nnz < 0 || (nnz > 0 && (!col || !val))) return fail(PAMG_E_ARG, "mat_upload: bad arrays");
+    if (nnz >= INT32_MAX - 16 || nrows >= INT32_MAX || ncols >= INT32_MAX)
+        return fail(PAMG_E_OVERFLOW, "mat_upload: nnz/rows/cols exceed the int32 device layout");
+    const int64_t n_own_cols = plan ? plan->n_own : ncols;
+    if (plan && plan->n_own + plan->n_ghost != ncols)
+        return fail(PAMG_E_ARG, "mat_upload: ncols %lld != plan own+ghost %lld", (long long)ncols,
+                    (long long)(plan->n_own + plan->n_ghost));
+    CHECK(set_device(ctx));
+    std::vector<int64_t> rp(nrows + 1);
+    std::vector<int> ci(nnz + kVecPad, 0);
+    for (int64_t i = 0; i <= nrows; ++i) rp[i] = rowptr[i] - index_base;
+    for (int64_t i = 0; i < nrows; ++i)
+        if (rp[i + 1] < rp[i]) return fail(PAMG_E_ARG, "mat_upload: rowptr not monotone at %lld", (long long)i);
+    if (rp[0] != 0) return fail(PAMG_E_ARG, "mat_upload: rowptr[0] != index_base");
+    for (int64_t k = 0; k < nnz; ++k) {
+        const int64_t c = (col_is_64 ? static_cast<const int64_t*>(col)[k]
+                                     : (int64_t) static_cast<const int32_t*>(col)[k]) - index_base;
+        if (c < 0 || c >= ncols) return fail(PAMG_E_ARG, "mat_upload: column %lld out of range", (long long)c);
+        ci[k] = (int)c;
+    }
+    auto A = std::make_unique<pamg_mat>();
+    A->ctx = ctx;
+    A->nrows = nrows;
+    A->ncols = ncols;
+    A->nnz = nnz;
+    A->plan = plan;
+    // classify rows: interior (own columns only) or boundary (>= 1 ghost column)
+    std::vector<int> inner, bnd;
+    std::vector<double> diag(nrows, 0.0);
+    bool has_all_diag = (n_own_cols == nrows);
+    for (int64_t i = 0; i < nrows; ++i) {
+        bool g = false, d = false;
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+            g |= ci[k] >= n_own_cols;
+            if (ci[k] == i && n_own_cols == nrows) {
+                diag[i] = val[k];
+                d = true;
+            }
+        }
+        if (!d || diag[i] == 0.0) has_all_diag = false;
+        (g ? bnd : inner).push_back((int)i);
+    }
+    std::vector<int> rp32(nrows + 1);
+    for (int64_t i = 0; i <= nrows; ++i) rp32[i] = (int)rp[i];
+    CHECK(dalloc(&A->d_rowptr, nrows + 1));
+    CHECK(dalloc(&A->d_col, nnz + kVecPad));
+    CHECK(dalloc(&A->d_val, nnz + kVecPad));
+    HIPC(hipMemcpy(A->d_rowptr, rp32.data(), sizeof(int) * (nrows + 1), hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(A->d_col, ci.data(), sizeof(int) * (nnz + kVecPad), hipMemcpyHostToDevice));
+    HIPC(hipMemset(A->d_val, 0, sizeof(double) * (nnz + kVecPad)));
+    if (nnz) HIPC(hipMemcpy(A->d_val, val, sizeof(double) * nnz, hipMemcpyHostToDevice));
+    if (has_all_diag && nrows > 0) {
+        CHECK(dalloc(&A->d_diag, nrows));
+        HIPC(hipMemcpy(A->d_diag, diag.data(), sizeof(double) * nrows, hipMemcpyHostToDevice));
+    }
+    CHECK(build_tiles(rp, inner, &A->interior));
+    CHECK(build_tiles(rp, bnd, &A->boundary));
+    *out = A.release();
+    return PAMG_OK;
+}
+
+int pamg_mat_destroy(pamg_mat* A) {
+    if (!A) return PAMG_OK;
+    (void)hipSetDevice(A->ctx->device);
+    (void)hipStreamSynchronize(A->ctx->s_comp);
+    dfree(A->d_rowptr);
+    dfree(A->d_col);
+    dfree(A->d_val);
+    dfree(A->d_diag);
+    free_tiles(A->interior);
+    free_tiles(A->boundary);
+    delete A;
+    return PAMG_OK;
+}
+
+int pamg_mat_info(const pamg_mat* A, int64_t* nrows, int64_t* ncols, int64_t* nnz) {
+    if (!A) return fail(PAMG_E_ARG, "mat_info: NULL");
+    if (nrows) *nrows = A->nrows;
+    if (ncols) *ncols = A->ncols;
+    if (nnz) *nnz = A->nnz;
+    return PAMG_OK;
+}
+
+static int check_vec_for(const pamg_mat* A, const pamg_vec* x, const char* who) {
+    const int64_t need_ghost = A->plan ? A->plan->n_ghost : 0;
+    const int64_t own = A->plan ? A->plan->n_own : A->ncols;
+    if (x->n_own != own || x->n_ghost < need_ghost)
+        return fail(PAMG_E_ARG, "%s: input vector (%lld own, %lld ghost) does not fit the matrix columns (%lld own, %lld ghost)",
+                    who, (long long)x->n_own, (long long)x->n_ghost, (long long)own, (long long)need_ghost);
+    return PAMG_OK;
+}
+
+int pamg_spmv(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, pamg_vec* y) {
+    if (!ctx || !A || !x || !y) return fail(PAMG_E_ARG, "spmv: NULL");
+    CHECK(check_vec_for(A, x, "spmv"));
+    if (y->n_own != A->nrows) return fail(PAMG_E_ARG, "spmv: output size mismatch");
+    if (x == y) return fail(PAMG_E_ARG, "spmv: x and y must differ");
+    CHECK(set_device(ctx));
+    CHECK(apply(ctx, A, pamg::OP_SPMV, x->d, nullptr, y->d, 0.0));
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_residual(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec* b, pamg_vec* r,
+                  double* nrm2) {
+    if (!ctx || !A || !x || !b || !r) return fail(PAMG_E_ARG, "residual: NULL");
+    CHECK(check_vec_for(A, x, "residual"));
+    if (b->n_own != A->nrows || r->n_own != A->nrows || r == x)
+        return fail(PAMG_E_ARG, "residual: size mismatch or aliasing");
+    CHECK(set_device(ctx));
+    CHECK(apply(ctx, A, pamg::OP_RESID, x->d, b->d, r->d, 0.0));
+    if (nrm2) {
+        double s = 0.0;
+        CHECK(reduce_scalar(ctx, r->n_own, r->d, r->d, &s));
+        *nrm2 = std::sqrt(s);
+    }
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_jacobi(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec* b, pamg_vec* tmp,
+                double omega, int nsweeps) {
+    if (!ctx || !A || !x || !b || !tmp || nsweeps < 0) return fail(PAMG_E_ARG, "jacobi: bad args");
+    CHECK(check_vec_for(A, x, "jacobi"));
+    CHECK(check_vec_for(A, tmp, "jacobi"));
+    if (!A->d_diag) return fail(PAMG_E_SETUP, "jacobi: matrix is not square or lacks a nonzero diagonal");
+    if (b->n_own != A->nrows || tmp == x) return fail(PAMG_E_ARG, "jacobi: size mismatch or aliasing");
+    CHECK(set_device(ctx));
+    double* cur = x->d;
+    double* nxt = tmp->d;
+    for (int k = 0; k < nsweeps; ++k) {
+        CHECK(apply(ctx, A, pamg::OP_JACOBI, cur, b->d, nxt, omega));
+        std::swap(cur, nxt);
+    }
+    if (cur != x->d)
+        HIPC(hipMemcpyAsync(x->d, cur, sizeof(double) * x->n_own, hipMemcpyDeviceToDevice, ctx->s_comp));
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* const* P,
+                     pamg_mat* const* R, const double* omega, int64_t n_coarse,
+                     const double* ainv, const int64_t* coarse_offsets, pamg_hier** out) {
+    if (!ctx || !out || nlevels < 1 || !A || !omega || !ainv || n_coarse < 1)
+        return fail(PAMG_E_ARG, "hier_create: bad args");
+    if (nlevels > 1 && (!P || !R)) return fail(PAMG_E_ARG, "hier_create: P/R missing");
+    CHECK(set_device(ctx));
+    auto H = std::make_unique<pamg_hier>();
+    H->ctx = ctx;
+    H->L = nlevels;
+    H->use_graph = ctx->nranks == 1;
+    const int L = nlevels;
+    H->A.assign(A, A + L);
+    H->P.assign(L, nullptr);
+    H->R.assign(L, nullptr);
+    H->omega.assign(omega, omega + L);
+    H->x.assign(L, nullptr);
+    H->b.assign(L, nullptr);
+    H->t.assign(L, nullptr);
+    H->r.assign(L, nullptr);
+    H->nown.assign(L, 0);
+    for (int l = 0; l < L; ++l) {
+        if (!A[l]) return fail(PAMG_E_ARG, "hier_create: A[%d] is NULL", l);
+        H->nown[l] = A[l]->nrows;
+        if (l < L - 1) {
+            if (!P[l] || !R[l]) return fail(PAMG_E_ARG, "hier_create: P/R[%d] is NULL", l);
+            H->P[l] = P[l];
+            H->R[l] = R[l];
+            if (!A[l]->d_diag) return fail(PAMG_E_SETUP, "hier_create: A[%d] lacks a nonzero diagonal", l);
+            if (P[l]->nrows != A[l]->nrows || R[l]->nrows != A[l + 1]->nrows)
+                return fail(PAMG_E_ARG, "hier_create: level %d operator shapes inconsistent", l);
+        }
+    }
+    // ghost capacity of each level's vectors = max over the plans that read them
+    for (int l = 0; l < L; ++l) {
+        int64_t g = 0;
+        if (A[l]->plan) g = std::max(g, A[l]->plan->n_ghost);
+        if (l < L - 1 && R[l]->plan) g = std::max(g, R[l]->plan->n_ghost);
+        if (l > 0 && P[l - 1]->plan) g = std::max(g, P[l - 1]->plan->n_ghost);
+        const int64_t n = H->nown[l] + g + kVecPad;
+        if (l > 0) {
+            CHECK(dalloc(&H->x[l], n));
+            CHECK(dalloc(&H->b[l], n));
+            HIPC(hipMemset(H->x[l], 0, sizeof(double) * n));
+            HIPC(hipMemset(H->b[l], 0, sizeof(double) * n));
+        }
+        if (l < L - 1) {
+            CHECK(dalloc(&H->t[l], n));
+            CHECK(dalloc(&H->r[l], n));
+            HIPC(hipMemset(H->t[l], 0, sizeof(double) * n));
+            HIPC(hipMemset(H->r[l], 0, sizeof(double) * n));
+        }
+    }
+    // coarsest level
+    H->nc = n_coarse;
+    const int nr = ctx->nranks;
+    H->coffs.assign(nr + 1, 0);
+    if (coarse_offsets) {
+        for (int q = 0; q <= nr; ++q) H->coffs[q] = coarse_offsets[q];
+    } else {
+        if (nr != 1) return fail(PAMG_E_ARG, "hier_create: coarse_offsets required with %d ranks", nr);
+        H->coffs[1] = n_coarse;
+    }
+    if (H->coffs[nr] != n_coarse || H->coffs[ctx->rank + 1] - H->coffs[ctx->rank] != A[L - 1]->nrows)
+        return fail(PAMG_E_ARG, "hier_create: coarse offsets inconsistent with the coarsest matrix");
+    for (int q = 0; q < nr; ++q) H->cmax = std::max(H->cmax, H->coffs[q + 1] - H->coffs[q]);
+    CHECK(dalloc(&H->d_ainv, n_coarse * n_coarse));
+    HIPC(hipMemcpy(H->d_ainv, ainv, sizeof(double) * n_coarse * n_coarse, hipMemcpyHostToDevice));
+    if (nr > 1) {
+        CHECK(dalloc(&H->d_bgather, (int64_t)nr * H->cmax + n_coarse + kVecPad));
+        CHECK(dalloc(&H->d_bsend, H->cmax + kVecPad));
+        HIPC(hipMemset(H->d_bsend, 0, sizeof(double) * (H->cmax + kVecPad)));
+    }
+    H->prof_ms.assign((size_t)L * 6, 0.0);
+    *out = H.release();
+    return PAMG_OK;
+}
+
+static void drop_graph(pamg_hier* H) {
+    if (H->gexec) (void)hipGraphExecDestroy(H->gexec);
+    H->gexec = nullptr;
+    H->g_x = H->g_b = nullptr;
+}
+
+int pamg_hier_destroy(pamg_hier* H) {
+    if (!H) return PAMG_OK;
+    (void)hipSetDevice(H->ctx->device);
+    (void)hipStreamSynchronize(H->ctx->s_comp);
+    drop_graph(H);
+    for (int l = 0; l < H->L; ++l) {
+        if (l > 0) {
+            dfree(H->x[l]);
+            dfree(H->b[l]);
+        }
+        dfree(H->t[l]);
+        dfree(H->r[l]);
+    }
+    dfree(H->d_ainv);
+    dfree(H->d_bgather);
+    dfree(H->d_bsend);
+    for (auto e : H->ev) (void)hipEventDestroy(e);
+    delete H;
+    return PAMG_OK;
+}
+
+int pamg_hier_set_graph(pamg_hier* H, int enable) {
+    if (!H) return fail(PAMG_E_ARG, "hier_set_graph: NULL");
+    H->use_graph = enable != 0;
+    if (!H->use_graph) drop_graph(H);
+    return PAMG_OK;
+}
+
+int pamg_hier_profile(pamg_hier* H, int enable) {
+    if (!H) return fail(PAMG_E_ARG, "hier_profile: NULL");
+    H->prof = enable != 0;
+    return PAMG_OK;
+}
+
+int pamg_hier_profile_read(pamg_hier* H, double* out) {
+    if (!H || !out) return fail(PAMG_E_ARG, "hier_profile_read: bad args");
+    CHECK(set_device(H->ctx));
+    HIPC(hipStreamSynchronize(H->ctx->s_comp));
+    for (size_t k = 0; k < H->ev_tag.size(); ++k) {
+        float ms = 0.f;
+        HIPC(hipEventElapsedTime(&ms, H->ev[2 * k], H->ev[2 * k + 1]));
+        H->prof_ms[(size_t)H->ev_tag[k].first * 6 + H->ev_tag[k].second] += ms;
+    }
+    for (auto e : H->ev) (void)hipEventDestroy(e);
+    H->ev.clear();
+    H->ev_tag.clear();
+    std::copy(H->prof_ms.begin(), H->prof_ms.end(), out);
+    std::fill(H->prof_ms.begin(), H->prof_ms.end(), 0.0);
+    return PAMG_OK;
+}
+
+static int vcycle_common(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles) {
+    if (!ctx || !H || !x || !b || ncycles < 0 || H->ctx != ctx) return fail(PAMG_E_ARG, "vcycle: bad args");
+    const pamg_mat* A0 = H->A[0];
+    CHECK(check_vec_for(A0, x, "vcycle"));
+    if (b->n_own != A0->nrows) return fail(PAMG_E_ARG, "vcycle: b size mismatch");
+    CHECK(set_device(ctx));
+    if (H->use_graph && !H->prof) {
+        if (!H->gexec || H->g_x != x->d || H->g_b != b->d) {
+            drop_graph(H);
+            hipGraph_t g;
+            HIPC(hipStreamBeginCapture(ctx->s_comp, hipStreamCaptureModeThreadLocal));
+            int rc = vcycle_enqueue(H, x->d, b->d);
+            hipError_t e2 = hipStreamEndCapture(ctx->s_comp, &g);
+            if (rc != PAMG_OK) return rc;
+            if (e2 != hipSuccess) return fail(PAMG_E_HIP, "vcycle: capture failed: %s", hipGetErrorString(e2));
+            HIPC(hipGraphInstantiate(&H->gexec, g, nullptr, nullptr, 0));
+            (void)hipGraphDestroy(g);
+            H->g_x = x->d;
+            H->g_b = b->d;
+        }
+        for (int k = 0; k < ncycles; ++k) HIPC(hipGraphLaunch(H->gexec, ctx->s_comp));
+    } else {
+        for (int k = 0; k < ncycles; ++k) CHECK(vcycle_enqueue(H, x->d, b->d));
+    }
+    return PAMG_OK;
+}
+
+int pamg_vcycle_async(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles) {
+    return vcycle_common(ctx, H, x, b, ncycles);
+}
+
+int pamg_vcycle(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles,
+                double* res_hist) {
+    if (!res_hist) {
+        CHECK(vcycle_common(ctx, H, x, b, ncycles));
+        HIPC(hipStreamSynchronize(ctx->s_comp));
+        return PAMG_OK;
+    }
+    if (!H || H->L < 1 || (!H->t[0] && H->L > 1)) return fail(PAMG_E_ARG, "vcycle: bad hierarchy");
+    for (int k = 0; k < ncycles; ++k) {
+        CHECK(vcycle_common(ctx, H, x, b, 1));
+        // r = b - A x into the level-0 residual buffer (1-level hierarchies use a temporary)
+        double* r = H->L > 1 ? H->r[0] : nullptr;
+        double* tmp = nullptr;
+        if (!r) {
+            CHECK(dalloc(&tmp, H->nown[0] + kVecPad));
+            r = tmp;
+        }
+        int rc = apply(ctx, H->A[0], pamg::OP_RESID, x->d, b->d, r, 0.0);
+        double s = 0.0;
+        if (rc == PAMG_OK) rc = reduce_scalar(ctx, H->nown[0], r, r, &s);
+        dfree(tmp);
+        CHECK(rc);
+        res_hist[k] = std::sqrt(s);
+    }
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_bench_spmv(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, pamg_vec* y, int reps,
+                    double* avg_ms) {
+    if (!ctx || !A || !x || !y || reps < 1 || !avg_ms) return fail(PAMG_E_ARG, "bench_spmv: bad args");
+    CHECK(check_vec_for(A, x, "bench_spmv"));
+    CHECK(set_device(ctx));
+    hipEvent_t e0, e1;
+    HIPC(hipEventCreate(&e0));
+    HIPC(hipEventCreate(&e1));
+    hipStream_t s = ctx->s_comp;
+    pamg::launch_rows(*A, A->interior, pamg::OP_SPMV, x->d, nullptr, x->d, y->d, 0.0, s);
+    pamg::launch_rows(*A, A->boundary, pamg::OP_SPMV, x->d, nullptr, x->d, y->d, 0.0, s);
+    HIPC(hipEventRecord(e0, s));
+    for (int k = 0; k < reps; ++k) {
+        pamg::launch_rows(*A, A->interior, pamg::OP_SPMV, x->d, nullptr, x->d, y->d, 0.0, s);
+        pamg::launch_rows(*A, A->boundary, pamg::OP_SPMV, x->d, nullptr, x->d, y->d, 0.0, s);
+    }
+    HIPC(hipEventRecord(e1, s));
+    HIPC(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, e0, e1));
+    *avg_ms = ms / reps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return PAMG_OK;
+}
+
+}  // extern "C"
