@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""bench.py — V-cycle throughput of the MI355X AMG solve path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2] / metric line): 3D 7-point Poisson, 512^3 = 134,217,728
+fp64 unknowns, smoothed-aggregation hierarchy (SPEC.md §S4), V(1,1) weighted-Jacobi cycles
+(SPEC.md §S6). A "step" is one V-cycle over the whole (global) problem; with N GPUs the
+grid is row-partitioned into N slabs (strong scaling: total work fixed) and each V-cycle
+exchanges ghosts over RCCL.
+
+    python bench.py [--gpus N --steps K --warmup W]          # N=1
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line. Timed region: barrier + device sync, K V-cycles (hipGraph
+replay on one part), device sync + barrier; max over ranks. Inputs are resident in HBM.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "V-cycle iters/sec + fine-SpMV HBM GB/s, 3D Poisson 128M dofs at 1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md:36 (spec)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=512, help="grid points per side")
+    ap.add_argument("--kind", default="poisson3d", choices=["poisson2d", "poisson3d", "aniso3d"])
+    ap.add_argument("--max-coarse", type=int, default=1000)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-cycles", type=int, default=1)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    import torch.distributed as dist
+
+    import parallel_amg_amd as pa
+    from parallel_amg_amd import _lib
+    from parallel_amg_amd.partitioned import Context, PVector, mul
+    from parallel_amg_amd.solver import OPS, AMGSolver
+
+    _lib.lib()  # fail loudly if libpamg.so is missing
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        be = pa.DistributedBackend()
+    else:
+        be = pa.SequentialBackend(1)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+
+    t0 = time.time()
+    A, offs, xs = pa.generate_problem(be, args.kind, args.n)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=args.max_coarse), log=log)
+    t_setup = time.time() - t0
+    log(f"setup {t_setup:.1f}s, {H.nlevels} levels")
+
+    ctx = Context(local, be)
+    S = AMGSolver(ctx, H, part=rank, graph=not args.no_graph)
+    A0 = S.A[0]
+    xst = PVector(ctx, A0.n_own_cols, A0.n_ghost, xs[rank])
+    b = PVector(ctx, A0.nrows)
+    mul(b, A0, xst)
+    x = S.new_vector()
+    del xst
+    t_upload = time.time() - t0 - t_setup
+    log(f"upload {t_upload:.1f}s")
+
+    # ---- warmup + timed region -------------------------------------------------------
+    if args.warmup:
+        S.vcycle(x, b, args.warmup)
+    barrier()
+    ctx.sync()
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    S.vcycle_async(x, b, args.steps)
+    ctx.sync()
+    torch.cuda.synchronize()
+    barrier()
+    te = time.perf_counter()
+    dt = te - ts
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    vps = args.steps / dt
+
+    # ---- per-kernel timing (HIP events on the compute stream, eager) ------------------
+    kprof = max(3, min(args.steps, 10))
+    prof = S.profile(x, b, kprof) / kprof          # ms per V-cycle per (level, op)
+    obytes = S.op_bytes()                           # algorithmic bytes per (level, op)
+    post_ms = float(prof[0, 4]) if S.L > 1 else float(prof[0, 5])
+    post_bytes = float(obytes[0, 4]) if S.L > 1 else float(obytes[0, 5])
+    achieved = post_bytes / (post_ms * 1e-3) / 1e9
+    spmv_ms = ctypes_bench_spmv(ctx, A0, x, S)
+    spmv_bytes = S.rowsum_bytes(A0.nnz, A0.nrows, A0.n_own_cols + A0.n_ghost, 0)
+    spmv_gbps = spmv_bytes / (spmv_ms * 1e-3) / 1e9
+    hist = S.vcycle(x, b, 1, res_hist=True)
+
+    levels = [{"rows": int(H.levels[l][rank].A.nrows), "nnz": int(H.levels[l][rank].A.nnz),
+               "ms": {op: round(float(prof[l, k]), 4) for k, op in enumerate(OPS) if prof[l, k] > 0}}
+              for l in range(S.L)]
+    if rank == 0:
+        log(json.dumps({"levels": levels}))
+
+    # ---- CPU baseline: the oracle V-cycle on this same hierarchy (rank 0, N=1) --------
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        cpu = cpu_baseline(H, xs[0], args.cpu_cycles, log)
+
+    if rank == 0:
+        gl_rows = int(H.offsets(0)[-1])
+        out = {
+            "metric": METRIC,
+            "value": round(vps, 4),
+            "unit": "V-cycles/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SPEC.md §S2 grid operator, b = A x*, x0 = 0)",
+            "config": {
+                "workload": f"{args.kind} {args.n}^3 fp64, SA-AMG V(1,1) weighted-Jacobi, "
+                            f"{world} part(s)",
+                "n": gl_rows, "nnz_fine": int(sum(H.levels[0][p].A.nnz for p in H.levels[0])) if world == 1
+                else None, "levels": S.L, "max_coarse": args.max_coarse,
+                "parallelism": f"row-slab partition p{world} (RCCL ghost exchange)",
+                "graph": not args.no_graph,
+            },
+            "fine_spmv_GBps": round(spmv_gbps, 1),
+            "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
+            "roofline": {
+                "kernel": "k_rows_tile<OP_JACOBI> (level-0 post-smoothing)",
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                "bytes_per_launch": int(post_bytes), "ms_per_launch": round(post_ms, 4),
+            },
+            "cpu_baseline": cpu,
+            "setup_s": round(t_setup, 1),
+            "final_residual": float(hist[0]),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def ctypes_bench_spmv(ctx, A0, x, S, reps=20) -> float:
+    import ctypes as C
+
+    from parallel_amg_amd._lib import call
+    from parallel_amg_amd.partitioned import PVector
+    y = PVector(ctx, A0.nrows)
+    ms = C.c_double()
+    call("pamg_bench_spmv", ctx.handle, A0.handle, x.handle, y.handle, reps, C.byref(ms))
+    return ms.value
+
+
+def cpu_baseline(H, xstar, ncycles, log):
+    """Time the CPU oracle's V-cycle (oracle/pamg_oracle.c, OpenMP) on the same hierarchy."""
+    from oracle import oracle as O
+    lv = [H.levels[l][0] for l in range(H.nlevels)]
+    Ho = O.hierarchy_from_levels([p.A for p in lv], [p.P for p in lv[:-1]], [p.R for p in lv[:-1]],
+                                 [p.omega for p in lv], H.ainv)
+    A0 = lv[0].A
+    x = np.zeros(A0.nrows)
+    rhs = np.ascontiguousarray(xstar)  # any rhs: the cycle's work does not depend on values
+    t = time.perf_counter()
+    O.lib().orc_solve(Ho._h, x, rhs, ncycles, None)
+    dt = time.perf_counter() - t
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    log(f"cpu baseline: {ncycles} V-cycle(s) in {dt:.2f}s on {cores} threads")
+    return {"value": round(ncycles / dt, 5), "unit": "V-cycles/s", "cores": cores, "kind": "port",
+            "sample": f"{ncycles} full V-cycle(s) of the same {A0.nrows}-row hierarchy by the C "
+                      f"oracle (oracle/pamg_oracle.c, OpenMP, int64 indices); reference "
+                      f"(Julia/PartitionedArrays) not runnable: no code in /root/reference"}
+
+
+if __name__ == "__main__":
+    main()

@@ -57,6 +57,10 @@ def lib():
         L.orc_offs_get.argtypes = [vp, C.c_int, _i64p]
         L.orc_ainv_get.argtypes = [vp, _f64p]
         L.orc_solve.argtypes = [vp, _f64p, _f64p, C.c_int, vp]
+        L.orc_hier_new.restype = vp
+        L.orc_hier_new.argtypes = [C.c_int]
+        L.orc_hier_set.argtypes = [vp, C.c_int, C.c_int, i64, i64, vp, vp, vp, dbl]
+        L.orc_hier_set_ainv.argtypes = [vp, i64, _f64p]
         _lib = L
     return _lib
 
@@ -196,4 +200,22 @@ def setup(A: CSR, nparts: int = 1, theta: float = 0.02, max_levels: int = 20,
     H.ainv = np.empty(nL * nL)
     L.orc_ainv_get(h, H.ainv)
     H.ainv = H.ainv.reshape(nL, nL).T.copy()  # stored column-major -> row-major matrix
+    return H
+
+
+def hierarchy_from_levels(A, P, R, omega, ainv_colmajor) -> Hierarchy:
+    """Oracle hierarchy holding the given level operators (objects with rowptr (int64),
+    col (int32) and val arrays, e.g. the product's host CSR) — no setup is run. Used to time
+    the oracle V-cycle on the product's own hierarchy (bench cpu_baseline)."""
+    L = lib()
+    h = L.orc_hier_new(len(A))
+    H = Hierarchy(_h=h)
+    for l, M in enumerate(A):
+        for which, X in ((0, M), (1, P[l] if l < len(P) else None), (2, R[l] if l < len(R) else None)):
+            if X is None:
+                continue
+            col = np.ascontiguousarray(X.col, np.int32)
+            L.orc_hier_set(h, l, which, X.nrows, X.ncols, X.rowptr.ctypes.data, col.ctypes.data,
+                           X.val.ctypes.data, float(omega[l]) if which == 0 else 0.0)
+    L.orc_hier_set_ainv(h, int(round(len(ainv_colmajor) ** 0.5)), np.ascontiguousarray(ainv_colmajor))
     return H

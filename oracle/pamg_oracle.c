@@ -457,3 +457,36 @@ void orc_solve(const ohier* h, double* x, const double* b, int ncycles, double* 
     }
     free(r);
 }
+
+/* ------------------------------------------------------------------ external hierarchy */
+/* Build an oracle hierarchy from given level operators (int32 columns are widened), so the
+ * oracle V-cycle can be timed on the very hierarchy the product built (bench cpu_baseline)
+ * or checked against it. which: 0 = A, 1 = P, 2 = R. */
+ohier* orc_hier_new(int nlev) {
+    ohier* h = calloc(1, sizeof(ohier));
+    h->nlev = nlev > ORC_MAXL ? ORC_MAXL : nlev;
+    h->nparts = 1;
+    for (int l = 0; l < h->nlev; ++l) {
+        h->offs[l] = calloc(2, sizeof(i64));
+    }
+    return h;
+}
+
+void orc_hier_set(ohier* h, int l, int which, i64 nr, i64 nc, const i64* rp, const int32_t* col,
+                  const double* val, double omega) {
+    ocsr* a = which == 0 ? &h->A[l] : which == 1 ? &h->P[l] : &h->R[l];
+    a->nr = nr; a->nc = nc; a->nnz = rp[nr] - rp[0];
+    a->rp = malloc(sizeof(i64) * (nr + 1));
+    a->col = malloc(sizeof(i64) * (a->nnz + 1));
+    a->val = malloc(sizeof(double) * (a->nnz + 1));
+#pragma omp parallel for schedule(static)
+    for (i64 i = 0; i <= nr; ++i) a->rp[i] = rp[i] - rp[0];
+#pragma omp parallel for schedule(static)
+    for (i64 k = 0; k < a->nnz; ++k) { a->col[k] = col[k]; a->val[k] = val[k]; }
+    if (which == 0) { h->omega[l] = omega; h->offs[l][1] = nr; }
+}
+
+void orc_hier_set_ainv(ohier* h, i64 n, const double* ainv) {
+    h->ainv = malloc(sizeof(double) * (size_t)(n * n + 1));
+    memcpy(h->ainv, ainv, sizeof(double) * (size_t)(n * n));
+}

@@ -32,9 +32,13 @@ class HCSR:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h and _lib._lib is not None:
-            _lib._lib.pamg_hcsr_destroy(h)
-            self._h = None
+        lib = getattr(_lib, "_lib", None) if _lib is not None else None
+        if h and lib is not None:
+            try:
+                lib.pamg_hcsr_destroy(h)
+            except Exception:  # pragma: no cover - shutdown ordering
+                pass
+        self._h = None
 
     @classmethod
     def from_arrays(cls, rowptr, col, val, ncols) -> "HCSR":

@@ -1,0 +1,223 @@
+"""Device PartitionedArrays surface over libpamg (reference README.md:2).
+
+PartitionedArrays.jl names → this module:
+
+=========================================  ==========================================
+``PRange`` part (own + ghost ids)          ``HostPlan`` (hierarchy.py) → ``DevicePlan``
+``PVector``                                ``PVector`` (own values then ghost slots)
+``PSparseMatrix`` part                     ``PSparseMatrix`` (own rows, local columns)
+``mul!(y, A, x)``                          ``mul(y, A, x)``
+``consistent!(x) |> wait``                 ``consistent(x, plan)``
+``own_values(x)``                          ``x.own_values()``
+``dot(x, y)`` / ``norm(x)``                ``dot(x, y)`` / ``norm(x)``
+``axpy!`` / ``copy!`` / ``fill!``          ``axpby`` / ``copy`` / ``fill``
+=========================================  ==========================================
+
+One process drives one GPU and one part (the ``with_mpi`` shape); with more than one part
+the context owns an RCCL communicator and ``mul`` overlaps the RCCL ghost exchange with the
+interior rows. Everything here calls the C-ABI; there is no host fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as _L
+from ._lib import call, ptr
+from .hcsr import HCSR
+from .hierarchy import HostPlan
+
+
+def _release(obj, fn):
+    """Destroy a libpamg handle once (safe during interpreter shutdown)."""
+    h = getattr(obj, "_h", None)
+    lib = getattr(_L, "_lib", None) if _L is not None else None
+    if h and lib is not None:
+        try:
+            getattr(lib, fn)(h)
+        except Exception:  # pragma: no cover - shutdown ordering
+            pass
+    obj._h = None
+
+
+class Context:
+    """A GPU (``pamg_ctx``) plus, for multi-part runs, its RCCL communicator."""
+
+    def __init__(self, device: int = 0, backend=None):
+        h = C.c_void_p()
+        call("pamg_ctx_create", device, C.byref(h))
+        self._h = h
+        self.device = device
+        self.rank, self.nranks = 0, 1
+        if backend is not None and backend.nparts > 1:
+            if not backend.distributed:
+                raise ValueError("device runs need one part per process (DistributedBackend)")
+            self._init_comm(backend)
+
+    def _init_comm(self, backend):
+        import torch
+        uid = C.create_string_buffer(128)
+        if backend.rank == 0:
+            call("pamg_comm_unique_id", uid)
+        t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8).clone()
+        backend.dist.broadcast(t, src=0, group=backend.group)
+        raw = bytes(t.numpy().tobytes())
+        call("pamg_comm_init", self._h, backend.nparts, backend.rank, raw)
+        self.rank, self.nranks = backend.rank, backend.nparts
+
+    @property
+    def handle(self):
+        return self._h
+
+    def sync(self):
+        call("pamg_ctx_sync", self._h)
+
+    def close(self):
+        _release(self, "pamg_ctx_destroy")
+
+    def __del__(self):
+        self.close()
+
+
+class DevicePlan:
+    """Device exchange plan built from a ``HostPlan`` (``pamg_plan``)."""
+
+    def __init__(self, ctx: Context, plan: HostPlan):
+        self.ctx, self.host = ctx, plan
+        nb = np.asarray(plan.nbrs, np.int32)
+        rc = np.asarray(plan.recv_counts, np.int64)
+        sc = np.asarray(plan.send_counts, np.int64)
+        si = np.asarray(plan.send_idx if plan.send_idx is not None else [], np.int64)
+        h = C.c_void_p()
+        call("pamg_plan_create", ctx.handle, plan.n_own, plan.n_ghost, len(nb), ptr(nb), ptr(rc),
+             ptr(sc), ptr(si), C.byref(h))
+        self._h = h
+        self.n_own, self.n_ghost = plan.n_own, plan.n_ghost
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        _release(self, "pamg_plan_destroy")
+
+
+class PVector:
+    """Device vector of one part: ``n_own`` own values followed by ``n_ghost`` ghost slots."""
+
+    def __init__(self, ctx: Context, n_own: int, n_ghost: int = 0, values=None):
+        h = C.c_void_p()
+        call("pamg_vec_create", ctx.handle, n_own, n_ghost, C.byref(h))
+        self._h, self.ctx, self.n_own, self.n_ghost = h, ctx, n_own, n_ghost
+        if values is not None:
+            self.set(values)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set(self, own):
+        own = np.ascontiguousarray(own, np.float64)
+        if own.shape != (self.n_own,):
+            raise ValueError(f"expected {self.n_own} own values, got {own.shape}")
+        call("pamg_vec_upload", self.ctx.handle, self._h, ptr(own))
+
+    def own_values(self) -> np.ndarray:
+        out = np.empty(self.n_own, np.float64)
+        call("pamg_vec_download", self.ctx.handle, self._h, ptr(out))
+        return out
+
+    def device_ptr(self) -> int:
+        p = C.c_void_p()
+        call("pamg_vec_device_ptr", self._h, C.byref(p))
+        return p.value
+
+    def fill(self, v: float):
+        call("pamg_vec_fill", self.ctx.handle, self._h, float(v))
+
+    def __del__(self):
+        _release(self, "pamg_vec_destroy")
+
+
+class PSparseMatrix:
+    """Device CSR of one part: own rows, columns local to ``plan`` (own, then ghosts)."""
+
+    def __init__(self, ctx: Context, M: HCSR, plan: HostPlan | None = None,
+                 dplan: DevicePlan | None = None):
+        self.ctx = ctx
+        if plan is not None and dplan is None and plan.nbrs:
+            dplan = DevicePlan(ctx, plan)
+        self.plan = dplan
+        if plan is not None:
+            col = plan.localize(M.col) if (plan.n_ghost or plan.col0) else M.col
+            ncols = plan.n_own + plan.n_ghost
+        else:
+            col, ncols = M.col, M.ncols
+        col = np.ascontiguousarray(col, np.int32)
+        h = C.c_void_p()
+        call("pamg_mat_upload", ctx.handle, M.nrows, ncols, ptr(M.rowptr), ptr(col), 0,
+             ptr(M.val), 0, dplan.handle if dplan is not None else None, C.byref(h))
+        self._h = h
+        self.nrows, self.ncols, self.nnz = M.nrows, ncols, M.nnz
+        self.n_own_cols = plan.n_own if plan is not None else ncols
+        self.n_ghost = plan.n_ghost if plan is not None else 0
+
+    @property
+    def handle(self):
+        return self._h
+
+    def new_input_vector(self) -> PVector:
+        return PVector(self.ctx, self.n_own_cols, self.n_ghost)
+
+    def new_output_vector(self) -> PVector:
+        return PVector(self.ctx, self.nrows)
+
+    def __del__(self):
+        _release(self, "pamg_mat_destroy")
+
+
+def mul(y: PVector, A: PSparseMatrix, x: PVector) -> PVector:
+    """``mul!(y, A, x)``: ghost exchange of x (overlapped with interior rows), y = A x."""
+    call("pamg_spmv", A.ctx.handle, A.handle, x.handle, y.handle)
+    return y
+
+
+def residual(r: PVector, A: PSparseMatrix, x: PVector, b: PVector, with_norm=False):
+    nrm = C.c_double()
+    call("pamg_residual", A.ctx.handle, A.handle, x.handle, b.handle, r.handle,
+         C.byref(nrm) if with_norm else None)
+    return nrm.value if with_norm else r
+
+
+def jacobi(x: PVector, A: PSparseMatrix, b: PVector, tmp: PVector, omega: float, nsweeps: int = 1):
+    call("pamg_jacobi", A.ctx.handle, A.handle, x.handle, b.handle, tmp.handle, float(omega), nsweeps)
+    return x
+
+
+def consistent(x: PVector, plan: DevicePlan) -> PVector:
+    """``consistent!(x) |> wait``: owners' values into x's ghost slots."""
+    call("pamg_exchange", x.ctx.handle, plan.handle, x.handle)
+    return x
+
+
+def dot(x: PVector, y: PVector) -> float:
+    out = C.c_double()
+    call("pamg_vec_dot", x.ctx.handle, x.handle, y.handle, C.byref(out))
+    return out.value
+
+
+def norm(x: PVector) -> float:
+    out = C.c_double()
+    call("pamg_vec_nrm2", x.ctx.handle, x.handle, C.byref(out))
+    return out.value
+
+
+def axpby(a: float, x: PVector, b: float, y: PVector) -> PVector:
+    call("pamg_vec_axpby", x.ctx.handle, float(a), x.handle, float(b), y.handle)
+    return y
+
+
+def copy(dst: PVector, src: PVector) -> PVector:
+    call("pamg_vec_copy", src.ctx.handle, src.handle, dst.handle)
+    return dst

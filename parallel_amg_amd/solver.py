@@ -1,0 +1,108 @@
+"""Device AMG solver: uploads one part of a ``HostHierarchy`` and runs V-cycles (SPEC §S6).
+
+``AMGSolver`` is the preconditioner object an AMG-on-PartitionedArrays driver would pass
+around (``ldiv!``-style ``vcycle``); the cycle itself is one C-ABI call (``pamg_vcycle``),
+replayed as a hipGraph on one part.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import call, ptr
+from .hierarchy import HostHierarchy
+from .partitioned import Context, PSparseMatrix, PVector, _release
+
+OPS = ("jacobi_pre", "residual", "restrict", "prolong", "jacobi_post", "coarse")
+
+
+class AMGSolver:
+    def __init__(self, ctx: Context, H: HostHierarchy, part: int = 0, graph: bool | None = None):
+        self.ctx, self.part, self.L = ctx, part, H.nlevels
+        self.A, self.P, self.R, self.omega = [], [], [], []
+        for l in range(H.nlevels):
+            lp = H.levels[l][part]
+            self.A.append(PSparseMatrix(ctx, lp.A, lp.planA))
+            self.omega.append(lp.omega)
+            if l < H.nlevels - 1:
+                self.P.append(PSparseMatrix(ctx, lp.P, lp.planP))
+                self.R.append(PSparseMatrix(ctx, lp.R, lp.planR))
+        self.level_rows = [int(H.levels[l][part].A.nrows) for l in range(H.nlevels)]
+        self.n_coarse = H.n_coarse
+        L = self.L
+        arrA = (C.c_void_p * L)(*[a.handle for a in self.A])
+        arrP = (C.c_void_p * L)(*([p.handle for p in self.P] + [None]))
+        arrR = (C.c_void_p * L)(*([r.handle for r in self.R] + [None]))
+        om = np.asarray(self.omega, np.float64)
+        coffs = np.asarray(H.offsets(L - 1), np.int64) if H.nparts > 1 else None
+        self._ainv = np.ascontiguousarray(H.ainv, np.float64)
+        h = C.c_void_p()
+        call("pamg_hier_create", ctx.handle, L, arrA, arrP, arrR, ptr(om), H.n_coarse,
+             ptr(self._ainv), ptr(coffs) if coffs is not None else None, C.byref(h))
+        self._h = h
+        if graph is not None:
+            self.set_graph(graph)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_graph(self, enable: bool):
+        call("pamg_hier_set_graph", self._h, int(bool(enable)))
+
+    def new_vector(self) -> PVector:
+        """A level-0 vector with room for the fine-level ghosts."""
+        return self.A[0].new_input_vector()
+
+    def vcycle(self, x: PVector, b: PVector, ncycles: int = 1, res_hist: bool = False):
+        if res_hist:
+            hist = np.zeros(ncycles)
+            call("pamg_vcycle", self.ctx.handle, self._h, x.handle, b.handle, ncycles, ptr(hist))
+            return hist
+        call("pamg_vcycle", self.ctx.handle, self._h, x.handle, b.handle, ncycles, None)
+        return None
+
+    def vcycle_async(self, x: PVector, b: PVector, ncycles: int = 1):
+        call("pamg_vcycle_async", self.ctx.handle, self._h, x.handle, b.handle, ncycles)
+
+    def profile(self, x: PVector, b: PVector, ncycles: int) -> np.ndarray:
+        """Eager V-cycles with HIP events around every op; returns ms per (level, op) summed
+        over the cycles (shape L x 6, columns = OPS)."""
+        call("pamg_hier_profile", self._h, 1)
+        try:
+            call("pamg_vcycle_async", self.ctx.handle, self._h, x.handle, b.handle, ncycles)
+            out = np.zeros(self.L * 6)
+            call("pamg_hier_profile_read", self._h, ptr(out))
+        finally:
+            call("pamg_hier_profile", self._h, 0)
+        return out.reshape(self.L, 6)
+
+    # ---- algorithmic byte model (SURVEY.md §8d / BASELINE.md) --------------------------
+    @staticmethod
+    def rowsum_bytes(nnz: int, nrows: int, ncols_read: int, extra_vec_rw: int) -> int:
+        """12 B/nnz (fp64 value + int32 column) + 4 (n+1) row pointers + 8 B per x entry read
+        once + 8 B per output row + 8 B per extra own vector read or written."""
+        return 12 * nnz + 4 * (nrows + 1) + 8 * ncols_read + 8 * nrows + 8 * nrows * extra_vec_rw
+
+    def op_bytes(self) -> np.ndarray:
+        """Algorithmic bytes per (level, op) of one V-cycle on this part (L x 6)."""
+        out = np.zeros((self.L, 6))
+        for l in range(self.L):
+            n = self.level_rows[l]
+            if l == self.L - 1:
+                nc = self.n_coarse
+                out[l, 5] = 8 * nc * n + 8 * nc + 8 * n
+                continue
+            A, P, R = self.A[l], self.P[l], self.R[l]
+            ncx = A.n_own_cols + A.n_ghost
+            # jacobi: x (read once), b, x' ; zero-guess form on l >= 1 reads b, diag, writes x'
+            out[l, 0] = self.rowsum_bytes(A.nnz, n, ncx, 1) if l == 0 else 24 * n
+            out[l, 1] = self.rowsum_bytes(A.nnz, n, ncx, 1)
+            out[l, 2] = self.rowsum_bytes(R.nnz, R.nrows, R.n_own_cols + R.n_ghost, 0)
+            out[l, 3] = self.rowsum_bytes(P.nnz, n, P.n_own_cols + P.n_ghost, 1)
+            out[l, 4] = self.rowsum_bytes(A.nnz, n, ncx, 1)
+        return out
+
+    def __del__(self):
+        _release(self, "pamg_hier_destroy")

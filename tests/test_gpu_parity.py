@@ -1,0 +1,152 @@
+"""GPU parity: libpamg's HIP kernels (through the C-ABI) against the CPU oracle (SPEC.md).
+
+Bit-exact for every row-sum op and for whole V-cycles (SPEC §S3 fixes the summation order);
+norms/dots within 1e-12 relative (tree reductions)."""
+import numpy as np
+import pytest
+
+import parallel_amg_amd as pa
+from oracle import oracle as O
+from parallel_amg_amd._lib import PamgError
+from parallel_amg_amd.hcsr import HCSR
+from parallel_amg_amd.partitioned import PSparseMatrix, PVector, axpby, dot, jacobi, mul, norm, residual
+from parallel_amg_amd.solver import AMGSolver
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.asarray(a, np.float64).view(np.int64)
+
+
+def random_csr(rng, lengths, ncols, square=False):
+    rows, cols, vals = [0], [], []
+    for i, m in enumerate(lengths):
+        m = min(max(m, 1) if square else m, ncols)
+        c = rng.choice(ncols, size=m, replace=False)
+        if square and m > 0 and i not in c:
+            c[0] = i
+        c = np.sort(c)
+        v = rng.standard_normal(m)
+        if square and m > 0:
+            v[c == i] = 4.0 + abs(v[c == i]) + m
+        cols.append(c)
+        vals.append(v)
+        rows.append(rows[-1] + m)
+    rp = np.asarray(rows, np.int64)
+    col = np.concatenate(cols).astype(np.int64) if cols else np.zeros(0, np.int64)
+    val = np.concatenate(vals) if vals else np.zeros(0)
+    return O.CSR(rp, col, val, ncols)
+
+
+def upload(ctx, M: O.CSR):
+    h = HCSR.from_arrays(M.rowptr, M.col.astype(np.int32), M.val, M.ncols)
+    return PSparseMatrix(ctx, h), h
+
+
+LENGTHS = {
+    "stencil7": [7] * 3000,
+    "ragged": [0, 1, 7, 27, 73, 0, 500, 3, 2049, 64, 1, 0] * 40,
+    "long": [5000, 1, 2047, 2048, 2049, 0, 9000],
+    "one_row": [13],
+    "empty_rows": [0] * 100,
+}
+
+
+@pytest.mark.parametrize("case", list(LENGTHS))
+def test_spmv_residual_bit_exact(ctx, case):
+    rng = np.random.default_rng(11)
+    lengths = LENGTHS[case]
+    ncols = max(max(lengths) + 1, len(lengths) + 7)
+    M = random_csr(rng, lengths, ncols)
+    A, _h = upload(ctx, M)
+    xh = rng.standard_normal(ncols)
+    bh = rng.standard_normal(len(lengths))
+    x = PVector(ctx, ncols, 0, xh)
+    y = PVector(ctx, len(lengths))
+    mul(y, A, x)
+    assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
+    b = PVector(ctx, len(lengths), 0, bh)
+    r = PVector(ctx, len(lengths))
+    residual(r, A, x, b)
+    assert np.array_equal(bits(r.own_values()), bits(O.residual(M, xh, bh)))
+
+
+@pytest.mark.parametrize("case", ["stencil7", "ragged", "long", "one_row"])
+def test_jacobi_bit_exact(ctx, case):
+    rng = np.random.default_rng(5)
+    lengths = LENGTHS[case]
+    n = max(max(lengths) + 1, len(lengths))
+    lengths = lengths + [3] * (n - len(lengths))
+    M = random_csr(rng, lengths, n, square=True)
+    A, _h = upload(ctx, M)
+    xh, bh = rng.standard_normal(n), rng.standard_normal(n)
+    x, b, t = PVector(ctx, n, 0, xh), PVector(ctx, n, 0, bh), PVector(ctx, n)
+    jacobi(x, A, b, t, 0.7, 3)
+    ref = xh
+    for _ in range(3):
+        ref = O.jacobi(M, ref, bh, 0.7)
+    assert np.array_equal(bits(x.own_values()), bits(ref))
+
+
+def test_blas1(ctx):
+    rng = np.random.default_rng(3)
+    n = 100_003
+    xh, yh = rng.standard_normal(n), rng.standard_normal(n)
+    x, y = PVector(ctx, n, 0, xh), PVector(ctx, n, 0, yh)
+    assert dot(x, y) == pytest.approx(float(np.dot(xh, yh)), rel=1e-12)
+    assert norm(x) == pytest.approx(float(np.linalg.norm(xh)), rel=1e-12)
+    axpby(2.5, x, -0.5, y)
+    assert np.array_equal(bits(y.own_values()), bits(2.5 * xh + (-0.5) * yh))
+
+
+def test_shape_errors_raise(ctx):
+    M = O.generate("poisson2d", 8, 8, 1)
+    A, _h = upload(ctx, M)
+    x = PVector(ctx, 63)
+    y = PVector(ctx, 64)
+    with pytest.raises(PamgError):
+        mul(y, A, x)
+
+
+CONFIGS = [("poisson2d", 64, 300), ("poisson3d", 24, 100), ("aniso3d", 20, 300), ("poisson3d", 12, 1000)]
+
+
+@pytest.mark.parametrize("kind,n,max_coarse", CONFIGS)
+def test_vcycle_bit_exact(ctx, kind, n, max_coarse):
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, kind, n)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse))
+    S = AMGSolver(ctx, H)
+    xst = PVector(ctx, S.A[0].nrows, 0, xs[0])
+    b = PVector(ctx, S.A[0].nrows)
+    mul(b, S.A[0], xst)
+    Ao = O.generate(kind, *O.grid_shape(kind, n))
+    bo = O.spmv(Ao, O.xstar(Ao.nrows))
+    assert np.array_equal(bits(b.own_values()), bits(bo))
+    Ho = O.setup(Ao, max_coarse=max_coarse)
+    assert Ho.nlevels == H.nlevels
+    x = S.new_vector()
+    hist = S.vcycle(x, b, 6, res_hist=True)
+    xo, ho = Ho.solve(bo, 6, res_hist=True)
+    assert np.array_equal(bits(x.own_values()), bits(xo))
+    np.testing.assert_allclose(hist, ho, rtol=1e-12)
+    assert hist[-1] < hist[0]
+
+
+def test_graph_equals_eager(ctx):
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 20)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=100))
+    S = AMGSolver(ctx, H)
+    b = PVector(ctx, S.A[0].nrows)
+    mul(b, S.A[0], PVector(ctx, S.A[0].nrows, 0, xs[0]))
+    out = []
+    for g in (True, False):
+        S.set_graph(g)
+        x = S.new_vector()
+        S.vcycle(x, b, 5)
+        out.append(x.own_values())
+    assert np.array_equal(bits(out[0]), bits(out[1]))
+    prof = S.profile(S.new_vector(), b, 2)
+    assert prof.shape == (H.nlevels, 6) and prof[0, 4] > 0
