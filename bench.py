@@ -180,7 +180,8 @@ def ctypes_bench_spmv(ctx, A0, x, S, reps=20) -> float:
     from parallel_amg_amd.partitioned import PVector
     y = PVector(ctx, A0.nrows)
     ms = C.c_double()
-    call("pamg_bench_spmv", ctx.handle, A0.handle, x.handle, y.handle, reps, C.byref(ms))
+    call("pamg_bench_rowop", ctx.handle, A0.handle, 0, x.handle, None, y.handle, 0.0, reps,
+         C.byref(ms))
     return ms.value
 
 

@@ -122,10 +122,16 @@ int pamg_vcycle_async(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* 
 int pamg_hier_profile(pamg_hier* H, int enable);
 int pamg_hier_profile_read(pamg_hier* H, double* ms_per_level_op /* nlevels*6 */);
 
-/* Micro-benchmark hook: `reps` back-to-back y = A x launches (no exchange), returning the
- * average kernel time in ms measured with HIP events on the launch stream. */
-int pamg_bench_spmv(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, pamg_vec* y, int reps,
-                    double* avg_ms);
+/* Micro-benchmark hook: `reps` back-to-back launches of one row operation of A (op 0 SpMV,
+ * 1 residual, 2 Jacobi, 3 prolongate-add; no exchange), returning the average time per
+ * launch in ms measured with HIP events on the launch stream. */
+int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, const pamg_vec* b,
+                     pamg_vec* y, double omega, int reps, double* avg_ms);
+
+/* Tuning knobs applied to later pamg_mat_upload calls: "rows_kernel" (0 | 1),
+ * "tile_nnz" (1024 | 2048 | 4096), "tile_rows" (256 | 512), "xcd_remap" (0 | 1). */
+int pamg_set_option(const char* key, int64_t value);
+int pamg_get_option(const char* key, int64_t* value);
 
 /* ------------------------------------------------------------------ host setup (SPEC §S4) */
 /* Host CSR: int64 rowptr, int32 columns (global ids), fp64 values. */

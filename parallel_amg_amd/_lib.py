@@ -67,7 +67,9 @@ SIGNATURES = {
     "pamg_vcycle_async": [vp, vp, vp, vp, i32],
     "pamg_hier_profile": [vp, i32],
     "pamg_hier_profile_read": [vp, vp],
-    "pamg_bench_spmv": [vp, vp, vp, vp, i32, pdbl],
+    "pamg_bench_rowop": [vp, vp, i32, vp, vp, vp, dbl, i32, pdbl],
+    "pamg_set_option": [C.c_char_p, i64],
+    "pamg_get_option": [C.c_char_p, pi64],
     "pamg_hcsr_create": [i64, i64, i64, pvp],
     "pamg_hcsr_destroy": [vp],
     "pamg_hcsr_info": [vp, pi64, pi64, pi64],

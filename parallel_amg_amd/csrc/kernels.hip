@@ -38,9 +38,10 @@ __device__ __forceinline__ void epilogue(int r, double s, const double* __restri
     }
 }
 
+// Variant 0 (first version, kept for A/B): row pointers first, then the column stream.
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_rows_tile(
-    const int2* __restrict__ tiles, const int* __restrict__ rowptr, const int* __restrict__ col,
+    const int4* __restrict__ tiles, const int* __restrict__ rowptr, const int* __restrict__ col,
     const double* __restrict__ val, const double* __restrict__ x, const double* __restrict__ b,
     double* __restrict__ y, double omega) {
     __shared__ __attribute__((aligned(16))) double lprod[kTileNnz + 8];
@@ -48,7 +49,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile(
     __shared__ double ldiag[OP == OP_JACOBI ? kTileRows : 1];
 
     const int tid = threadIdx.x;
-    const int2 t = tiles[blockIdx.x];
+    const int4 t = tiles[blockIdx.x];
     const int r0 = t.x, nr = t.y - t.x;
     for (int i = tid; i <= nr; i += kBlock) lrp[i] = rowptr[r0 + i];
     __syncthreads();
@@ -82,6 +83,218 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile(
         double s = 0.0;
         for (int k = kb; k < ke; ++k) s = s + lprod[k];
         epilogue<OP>(r, s, x, b, y, omega, OP == OP_JACOBI ? ldiag[tid] : 0.0);
+    }
+}
+
+// Variant 1: the tile descriptor carries its nonzero range, so the column/value stream of
+// every lane (TNNZ / 1024 groups of 4 nonzeros: one int4 + two double2 loads each) is issued
+// at kernel entry together with the row-pointer slice; all x gathers of a lane are then
+// issued back to back (branch-free: invalid lanes gather x[0] and discard it) before the
+// products go to LDS. XCD=true maps contiguous tile chunks to each XCD (blocks b and b+8
+// share an XCD) so neighbouring tiles' x lines stay in one L2.
+template <int OP, int TNNZ, int TROWS, bool XCD>
+__global__ __launch_bounds__(kBlock) void k_rows_tile2(
+    const int4* __restrict__ tiles, int ntiles, const int* __restrict__ rowptr,
+    const int* __restrict__ col, const double* __restrict__ val, const double* __restrict__ x,
+    const double* __restrict__ b, double* __restrict__ y, double omega,
+    const double* __restrict__ diag) {
+    // diag != nullptr (Jacobi only): a_ii from the stored diagonal instead of the in-tile
+    // detection (same value, SPEC §S3; trades 8 B/row of reads for one barrier).
+    constexpr int G = TNNZ / (4 * kBlock);
+    static_assert(G >= 1 && TNNZ % (4 * kBlock) == 0, "tile budget must be a multiple of 1024");
+    __shared__ __attribute__((aligned(16))) double lprod[TNNZ + 8];
+    __shared__ int lrp[TROWS + 1];
+    __shared__ double ldiag[OP == OP_JACOBI ? TROWS : 1];
+
+    int bid = blockIdx.x;
+    if constexpr (XCD) {
+        const int per = (ntiles + 7) >> 3;
+        bid = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+        if (bid >= ntiles) return;
+    }
+    const int tid = threadIdx.x;
+    const int4 t = tiles[bid];
+    const int r0 = t.x, nr = t.y - t.x, z0 = t.z, z1 = t.w;
+    const int za = z0 & ~3;
+
+    int4 c4[G];
+    double2 va[G], vb[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const int g = za + 4 * (tid + j * kBlock);
+        const int gs = g < z1 ? g : za;  // clamp: never read past the (padded) arrays
+        c4[j] = *reinterpret_cast<const int4*>(col + gs);
+        va[j] = *reinterpret_cast<const double2*>(val + gs);
+        vb[j] = *reinterpret_cast<const double2*>(val + gs + 2);
+    }
+    for (int i = tid; i <= nr; i += kBlock) lrp[i] = rowptr[r0 + i];
+    if constexpr (OP == OP_JACOBI) {
+        if (!diag) __syncthreads();
+    }
+
+    double xv[G][4];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const int g = za + 4 * (tid + j * kBlock);
+        const int cc[4] = {c4[j].x, c4[j].y, c4[j].z, c4[j].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool ok = (g + e >= z0) & (g + e < z1);
+            xv[j][e] = x[ok ? cc[e] : 0];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const int g = za + 4 * (tid + j * kBlock);
+        const int cc[4] = {c4[j].x, c4[j].y, c4[j].z, c4[j].w};
+        const double vv[4] = {va[j].x, va[j].y, vb[j].x, vb[j].y};
+        double p[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int k = g + e;
+            const bool ok = (k >= z0) & (k < z1);
+            p[e] = ok ? vv[e] * xv[j][e] : 0.0;
+            if constexpr (OP == OP_JACOBI) {
+                const int rl = cc[e] - r0;
+                if (!diag && ok && rl >= 0 && rl < nr && k >= lrp[rl] && k < lrp[rl + 1])
+                    ldiag[rl] = vv[e];
+            }
+        }
+        *reinterpret_cast<double2*>(&lprod[g - za]) = make_double2(p[0], p[1]);
+        *reinterpret_cast<double2*>(&lprod[g - za + 2]) = make_double2(p[2], p[3]);
+    }
+    __syncthreads();
+    for (int rr = tid; rr < nr; rr += kBlock) {
+        const int kb = lrp[rr] - za, ke = lrp[rr + 1] - za;
+        double s = 0.0;
+        for (int k = kb; k < ke; ++k) s = s + lprod[k];
+        double d = 0.0;
+        if constexpr (OP == OP_JACOBI) d = diag ? diag[r0 + rr] : ldiag[rr];
+        epilogue<OP>(r0 + rr, s, x, b, y, omega, d);
+    }
+}
+
+// Variant 2: wave tiles (<= 64 rows, <= WNNZ nonzeros) walked by a persistent grid, each wave
+// keeping the NEXT tile's column/value stream in flight (registers) while it gathers, sums and
+// stores the current one. No workgroup barrier anywhere: every wave owns an LDS slice; the
+// tile descriptors come 64 at a time (one per lane) and are broadcast with readlane; the row
+// bounds live in the lanes of their rows (phase 2 is one lane per row, as in variant 1).
+template <int OP, int WNNZ>
+__global__ __launch_bounds__(kBlock) void k_rows_wave(
+    const int4* __restrict__ tiles, int ntiles, const int* __restrict__ rowptr,
+    const int* __restrict__ col, const double* __restrict__ val, const double* __restrict__ x,
+    const double* __restrict__ b, double* __restrict__ y, double omega,
+    const double* __restrict__ diag) {
+    constexpr int G = WNNZ / 256;
+    constexpr int W = kBlock / 64;
+    static_assert(G >= 1 && WNNZ % 256 == 0, "wave tile budget must be a multiple of 256");
+    __shared__ __attribute__((aligned(16))) double lprod_all[W][WNNZ + 8];
+    __shared__ double ldiag_all[OP == OP_JACOBI ? W : 1][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double* lprod = lprod_all[w];
+    double* ldiag = ldiag_all[OP == OP_JACOBI ? w : 0];
+    const int stride = gridDim.x * W;
+    const int t0 = blockIdx.x * W + w;
+    if (t0 >= ntiles) return;
+    const int nit = (ntiles - t0 + stride - 1) / stride;
+    const int4 z4 = make_int4(0, 0, 0, 0);
+
+    auto bcast = [](const int4& v, int l) {
+        return make_int4(__builtin_amdgcn_readlane(v.x, l), __builtin_amdgcn_readlane(v.y, l),
+                         __builtin_amdgcn_readlane(v.z, l), __builtin_amdgcn_readlane(v.w, l));
+    };
+    int4 db = z4, dnb = z4;
+    if (lane < nit) db = tiles[t0 + lane * stride];
+    if (64 + lane < nit) dnb = tiles[t0 + (64 + lane) * stride];
+
+    int4 c4[G];
+    double2 va[G], vb[G];
+    auto load = [&](const int4& d) {
+        const int za = d.z & ~3;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int g = za + 4 * (lane + 64 * j);
+            const int gs = g < d.w ? g : za;
+            c4[j] = *reinterpret_cast<const int4*>(col + gs);
+            va[j] = *reinterpret_cast<const double2*>(val + gs);
+            vb[j] = *reinterpret_cast<const double2*>(val + gs + 2);
+        }
+    };
+    int4 dcur = bcast(db, 0);
+    load(dcur);
+    for (int i = 0; i < nit; ++i) {
+        const int4 d = dcur;
+        int4 cc4[G];
+        double2 ca[G], cb[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            cc4[j] = c4[j];
+            ca[j] = va[j];
+            cb[j] = vb[j];
+        }
+        // prefetch: next tile's stream (and, every 64 tiles, the descriptor batch after next)
+        const int in = i + 1;
+        if (in < nit) {
+            if ((in & 63) == 0) {
+                db = dnb;
+                if (in + 64 + lane < nit) dnb = tiles[t0 + (in + 64 + lane) * stride];
+            }
+            dcur = bcast(db, in & 63);
+            load(dcur);
+        }
+        const int r0 = d.x, nr = d.y - d.x, z0 = d.z, z1 = d.w, za = z0 & ~3;
+        int rs = 0, re = 0;
+        if (lane < nr) {
+            rs = rowptr[r0 + lane];
+            re = rowptr[r0 + lane + 1];
+        }
+        double xv[G][4];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int g = za + 4 * (lane + 64 * j);
+            const int cc[4] = {cc4[j].x, cc4[j].y, cc4[j].z, cc4[j].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool ok = (g + e >= z0) & (g + e < z1);
+                xv[j][e] = x[ok ? cc[e] : 0];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int g = za + 4 * (lane + 64 * j);
+            const int cc[4] = {cc4[j].x, cc4[j].y, cc4[j].z, cc4[j].w};
+            const double vv[4] = {ca[j].x, ca[j].y, cb[j].x, cb[j].y};
+            double p[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = g + e;
+                const bool ok = (k >= z0) & (k < z1);
+                p[e] = ok ? vv[e] * xv[j][e] : 0.0;
+                if constexpr (OP == OP_JACOBI) {
+                    if (!diag) {
+                        const int rl = cc[e] - r0;
+                        const int rlc = (rl >= 0 && rl < nr) ? rl : 0;
+                        const int lo = __shfl(rs, rlc, 64), hi = __shfl(re, rlc, 64);
+                        if (ok && rl >= 0 && rl < nr && k >= lo && k < hi) ldiag[rl] = vv[e];
+                    }
+                }
+            }
+            *reinterpret_cast<double2*>(&lprod[g - za]) = make_double2(p[0], p[1]);
+            *reinterpret_cast<double2*>(&lprod[g - za + 2]) = make_double2(p[2], p[3]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < nr) {
+            double s = 0.0;
+            for (int k = rs - za; k < re - za; ++k) s = s + lprod[k];
+            double dd = 0.0;
+            if constexpr (OP == OP_JACOBI) dd = diag ? diag[r0 + lane] : ldiag[lane];
+            epilogue<OP>(r0 + lane, s, x, b, y, omega, dd);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -220,12 +433,59 @@ inline int grid_for(int64_t n, int cap = 8192) {
     return (int)(g < cap ? g : cap);
 }
 
+template <int OP, int TNNZ, int TROWS>
+void launch_tile2(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
+                  double* y, double omega, hipStream_t s) {
+    const double* dg = (OP == OP_JACOBI && A.jacobi_diag) ? A.d_diag : nullptr;
+    if (A.xcd_remap) {
+        const int grid = ((ts.n_short + 7) / 8) * 8;
+        k_rows_tile2<OP, TNNZ, TROWS, true><<<grid, kBlock, 0, s>>>(
+            ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg);
+    } else {
+        k_rows_tile2<OP, TNNZ, TROWS, false><<<ts.n_short, kBlock, 0, s>>>(
+            ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg);
+    }
+}
+
+template <int OP, int WNNZ>
+void launch_wave(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
+                 double* y, double omega, hipStream_t s) {
+    static int grid_cap = 0;  // resident blocks on the whole chip (persistent grid)
+    if (grid_cap == 0) {
+        int nb = 0, dev = 0, ncu = 256;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rows_wave<OP, WNNZ>, kBlock, 0);
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        grid_cap = (nb > 0 ? nb : 1) * ncu;
+    }
+    const int need = (ts.n_short + kBlock / 64 - 1) / (kBlock / 64);
+    const int grid = need < grid_cap ? need : grid_cap;
+    const double* dg = (OP == OP_JACOBI && A.jacobi_diag) ? A.d_diag : nullptr;
+    k_rows_wave<OP, WNNZ><<<grid, kBlock, 0, s>>>(ts.d_short, ts.n_short, A.d_rowptr, A.d_col,
+                                                  A.d_val, x, b, y, omega, dg);
+}
+
 template <int OP>
 void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
                     double* y, double omega, hipStream_t s) {
-    if (ts.n_short > 0)
-        k_rows_tile<OP><<<ts.n_short, kBlock, 0, s>>>(ts.d_short, A.d_rowptr, A.d_col, A.d_val,
-                                                      x, b, y, omega);
+    if (ts.n_short > 0) {
+        if (A.rows_kernel == 2) {
+            if (ts.tile_nnz == 256) launch_wave<OP, 256>(A, ts, x, b, y, omega, s);
+            else if (ts.tile_nnz == 1024) launch_wave<OP, 1024>(A, ts, x, b, y, omega, s);
+            else launch_wave<OP, 512>(A, ts, x, b, y, omega, s);
+        } else if (A.rows_kernel == 0 && ts.tile_nnz == kTileNnz && ts.tile_rows == kTileRows) {
+            k_rows_tile<OP><<<ts.n_short, kBlock, 0, s>>>(ts.d_short, A.d_rowptr, A.d_col,
+                                                          A.d_val, x, b, y, omega);
+        } else if (ts.tile_nnz == 1024) {
+            launch_tile2<OP, 1024, 256>(A, ts, x, b, y, omega, s);
+        } else if (ts.tile_nnz == 4096 && ts.tile_rows == 512) {
+            launch_tile2<OP, 4096, 512>(A, ts, x, b, y, omega, s);
+        } else if (ts.tile_nnz == 4096) {
+            launch_tile2<OP, 4096, 256>(A, ts, x, b, y, omega, s);
+        } else {
+            launch_tile2<OP, 2048, 256>(A, ts, x, b, y, omega, s);
+        }
+    }
     if (ts.n_long > 0)
         k_rows_long<OP><<<ts.n_long, kBlock, 0, s>>>(ts.d_long, A.d_rowptr, A.d_col, A.d_val, x,
                                                      b, y, omega);

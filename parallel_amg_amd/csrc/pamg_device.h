@@ -27,11 +27,24 @@ enum RowOp : int {
 };
 
 struct TileSet {
-    int2* d_short = nullptr;  // (row_begin, row_end)
+    int4* d_short = nullptr;  // (row_begin, row_end, nnz_begin, nnz_end)
     int n_short = 0;
     int* d_long = nullptr;  // single rows
     int n_long = 0;
+    int tile_nnz = kTileNnz, tile_rows = kTileRows;  // budget the tiles were cut with
 };
+
+// Tuning knobs (pamg_set_option): kernel variant and tile budget used by later uploads.
+struct Options {
+    // defaults = fastest measured on MI355X at 512^3 (profiles/r01_kbench_*.jsonl):
+    // variant 1 with 1024-nonzero / 256-row tiles
+    int rows_kernel = 1;       // 0: rowptr-first tile, 1: descriptor-driven tile, 2: wave tiles
+    int tile_nnz = 1024;       // 256 / 512 / 1024 / 2048 / 4096
+    int tile_rows = kTileRows; // 64 / 256 / 512
+    int xcd_remap = 0;         // 1: contiguous tile chunks per XCD
+    int jacobi_diag = 0;       // 1: Jacobi reads the stored diagonal (no in-tile detection)
+};
+Options& options();
 
 }  // namespace pamg
 
@@ -72,6 +85,9 @@ struct pamg_mat {
     const pamg_plan* plan = nullptr;
     pamg::TileSet interior;  // rows with own columns only (overlap with the exchange)
     pamg::TileSet boundary;  // rows with >= 1 ghost column
+    int rows_kernel = 1;     // variant fixed at upload (pamg::Options)
+    int xcd_remap = 0;
+    int jacobi_diag = 0;
 };
 
 namespace pamg {

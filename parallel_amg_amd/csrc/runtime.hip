@@ -19,6 +19,11 @@ std::string& pamg::last_error() {
     return msg;
 }
 
+pamg::Options& pamg::options() {
+    static Options o;
+    return o;
+}
+
 #define HIPC(expr)                                                                    \
     do {                                                                              \
         hipError_t e_ = (expr);                                                       \
@@ -68,28 +73,34 @@ int set_device(const pamg_ctx* ctx) {
 // <= kTileRows rows and <= kTileNnz nonzeros; rows above the budget become "long" rows.
 int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
                 pamg::TileSet* ts) {
-    std::vector<int2> tiles;
+    const auto& opt = pamg::options();
+    const int tnnz = opt.tile_nnz, trows = opt.tile_rows;
+    ts->tile_nnz = tnnz;
+    ts->tile_rows = trows;
+    std::vector<int4> tiles;
     std::vector<int> longr;
     size_t i = 0;
     while (i < rows.size()) {
         const int r = rows[i];
         const int64_t len = rp[r + 1] - rp[r];
-        if (len > pamg::kTileNnz) {
+        // the kernel streams [rp[r] & ~3, end): the alignment head counts against the budget
+        const int64_t head = rp[r] & 3;
+        if (head + len > tnnz) {
             longr.push_back(r);
             ++i;
             continue;
         }
         int end = r + 1;
-        int64_t nz = len;
+        int64_t nz = head + len;
         size_t j = i + 1;
-        while (j < rows.size() && rows[j] == end && end - r < pamg::kTileRows) {
+        while (j < rows.size() && rows[j] == end && end - r < trows) {
             const int64_t l2 = rp[end + 1] - rp[end];
-            if (l2 > pamg::kTileNnz || nz + l2 > pamg::kTileNnz) break;
+            if (nz + l2 > tnnz) break;
             nz += l2;
             ++end;
             ++j;
         }
-        tiles.push_back(make_int2(r, end));
+        tiles.push_back(make_int4(r, end, (int)rp[r], (int)rp[end]));
         i = j;
     }
     ts->n_short = (int)tiles.size();
@@ -97,7 +108,7 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
     CHECK(dalloc(&ts->d_short, ts->n_short));
     CHECK(dalloc(&ts->d_long, ts->n_long));
     if (ts->n_short)
-        HIPC(hipMemcpy(ts->d_short, tiles.data(), sizeof(int2) * tiles.size(), hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(ts->d_short, tiles.data(), sizeof(int4) * tiles.size(), hipMemcpyHostToDevice));
     if (ts->n_long)
         HIPC(hipMemcpy(ts->d_long, longr.data(), sizeof(int) * longr.size(), hipMemcpyHostToDevice));
     return PAMG_OK;
@@ -290,6 +301,8 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b) {
 }  // namespace
 
 // ------------------------------------------------------------------ C-ABI
+
+static int check_tile_options(const pamg::Options& o);
 
 extern "C" {
 
@@ -531,6 +544,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     if (plan && plan->n_own + plan->n_ghost != ncols)
         return fail(PAMG_E_ARG, "mat_upload: ncols %lld != plan own+ghost %lld", (long long)ncols,
                     (long long)(plan->n_own + plan->n_ghost));
+    CHECK(check_tile_options(pamg::options()));
     CHECK(set_device(ctx));
     std::vector<int64_t> rp(nrows + 1);
     std::vector<int> ci(nnz + kVecPad, 0);
@@ -546,6 +560,9 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     }
     auto A = std::make_unique<pamg_mat>();
     A->ctx = ctx;
+    A->rows_kernel = pamg::options().rows_kernel;
+    A->xcd_remap = pamg::options().xcd_remap;
+    A->jacobi_diag = pamg::options().jacobi_diag;
     A->nrows = nrows;
     A->ncols = ncols;
     A->nnz = nnz;
@@ -858,21 +875,66 @@ int pamg_vcycle(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int
     return PAMG_OK;
 }
 
-int pamg_bench_spmv(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, pamg_vec* y, int reps,
-                    double* avg_ms) {
-    if (!ctx || !A || !x || !y || reps < 1 || !avg_ms) return fail(PAMG_E_ARG, "bench_spmv: bad args");
-    CHECK(check_vec_for(A, x, "bench_spmv"));
+int pamg_set_option(const char* key, int64_t value) {
+    if (!key) return fail(PAMG_E_ARG, "set_option: NULL key");
+    auto& o = pamg::options();
+    const std::string k(key);
+    if (k == "rows_kernel" && value >= 0 && value <= 2) o.rows_kernel = (int)value;
+    else if (k == "tile_nnz" && (value == 256 || value == 512 || value == 1024 || value == 2048 || value == 4096))
+        o.tile_nnz = (int)value;
+    else if (k == "tile_rows" && (value == 64 || value == 256 || value == 512)) o.tile_rows = (int)value;
+    else if (k == "xcd_remap" && (value == 0 || value == 1)) o.xcd_remap = (int)value;
+    else if (k == "jacobi_diag" && (value == 0 || value == 1)) o.jacobi_diag = (int)value;
+    else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
+    return PAMG_OK;
+}
+
+// Kernel variants and the tile shapes they are instantiated for (kernels.hip dispatch).
+static int check_tile_options(const pamg::Options& o) {
+    const int k = o.rows_kernel, n = o.tile_nnz, r = o.tile_rows;
+    bool ok = false;
+    if (k == 0) ok = (n == 2048 && r == 256);
+    if (k == 1) ok = (r == 256 && (n == 1024 || n == 2048 || n == 4096)) || (r == 512 && n == 4096);
+    if (k == 2) ok = (r == 64 && (n == 256 || n == 512 || n == 1024));
+    if (!ok)
+        return fail(PAMG_E_ARG, "options: rows_kernel %d has no instance for tile_nnz %d / tile_rows %d",
+                    k, n, r);
+    return PAMG_OK;
+}
+
+int pamg_get_option(const char* key, int64_t* value) {
+    if (!key || !value) return fail(PAMG_E_ARG, "get_option: bad args");
+    const auto& o = pamg::options();
+    const std::string k(key);
+    if (k == "rows_kernel") *value = o.rows_kernel;
+    else if (k == "tile_nnz") *value = o.tile_nnz;
+    else if (k == "tile_rows") *value = o.tile_rows;
+    else if (k == "xcd_remap") *value = o.xcd_remap;
+    else if (k == "jacobi_diag") *value = o.jacobi_diag;
+    else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
+    return PAMG_OK;
+}
+
+int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, const pamg_vec* b,
+                     pamg_vec* y, double omega, int reps, double* avg_ms) {
+    if (!ctx || !A || !x || !y || reps < 1 || !avg_ms || op < 0 || op > 3)
+        return fail(PAMG_E_ARG, "bench_rowop: bad args");
+    if ((op == pamg::OP_RESID || op == pamg::OP_JACOBI) && !b) return fail(PAMG_E_ARG, "bench_rowop: b needed");
+    if (op == pamg::OP_JACOBI && !A->d_diag) return fail(PAMG_E_SETUP, "bench_rowop: jacobi needs a square matrix");
+    if (x == y) return fail(PAMG_E_ARG, "bench_rowop: x and y must differ");
+    CHECK(check_vec_for(A, x, "bench_rowop"));
     CHECK(set_device(ctx));
     hipEvent_t e0, e1;
     HIPC(hipEventCreate(&e0));
     HIPC(hipEventCreate(&e1));
     hipStream_t s = ctx->s_comp;
-    pamg::launch_rows(*A, A->interior, pamg::OP_SPMV, x->d, nullptr, x->d, y->d, 0.0, s);
-    pamg::launch_rows(*A, A->boundary, pamg::OP_SPMV, x->d, nullptr, x->d, y->d, 0.0, s);
+    const double* bd = b ? b->d : nullptr;
+    pamg::launch_rows(*A, A->interior, op, x->d, bd, x->d, y->d, omega, s);
+    pamg::launch_rows(*A, A->boundary, op, x->d, bd, x->d, y->d, omega, s);
     HIPC(hipEventRecord(e0, s));
     for (int k = 0; k < reps; ++k) {
-        pamg::launch_rows(*A, A->interior, pamg::OP_SPMV, x->d, nullptr, x->d, y->d, 0.0, s);
-        pamg::launch_rows(*A, A->boundary, pamg::OP_SPMV, x->d, nullptr, x->d, y->d, 0.0, s);
+        pamg::launch_rows(*A, A->interior, op, x->d, bd, x->d, y->d, omega, s);
+        pamg::launch_rows(*A, A->boundary, op, x->d, bd, x->d, y->d, omega, s);
     }
     HIPC(hipEventRecord(e1, s));
     HIPC(hipEventSynchronize(e1));

@@ -48,13 +48,36 @@ LENGTHS = {
     "stencil7": [7] * 3000,
     "ragged": [0, 1, 7, 27, 73, 0, 500, 3, 2049, 64, 1, 0] * 40,
     "long": [5000, 1, 2047, 2048, 2049, 0, 9000],
+    "budget_edge": [1021, 1022, 1023, 1024, 1, 2045, 2046, 2047, 2048, 3, 4093, 4094, 4095, 4096, 2, 511] * 3,
     "one_row": [13],
     "empty_rows": [0] * 100,
 }
 
+# (rows_kernel, tile_nnz, tile_rows, xcd_remap) — every tuning configuration must be bit-exact
+TILE_CONFIGS = [(0, 2048, 256, 0, 0), (1, 2048, 256, 0, 0), (1, 2048, 256, 1, 1), (1, 1024, 256, 0, 0),
+                (1, 4096, 256, 0, 0), (1, 4096, 512, 1, 0), (2, 256, 64, 0, 0), (2, 512, 64, 0, 0),
+                (2, 512, 64, 0, 1), (2, 1024, 64, 0, 0)]
+OPT_KEYS = ("rows_kernel", "tile_nnz", "tile_rows", "xcd_remap", "jacobi_diag")
+
+
+@pytest.fixture(params=TILE_CONFIGS, ids=lambda c: "k{}_{}x{}_xcd{}_dg{}".format(*c))
+def tile_cfg(request, built):
+    import ctypes
+    from parallel_amg_amd._lib import call
+    old = []
+    for k in OPT_KEYS:
+        v = ctypes.c_int64()
+        call("pamg_get_option", k.encode(), ctypes.byref(v))
+        old.append(v.value)
+    for k, v in zip(OPT_KEYS, request.param):
+        call("pamg_set_option", k.encode(), v)
+    yield request.param
+    for k, v in zip(OPT_KEYS, old):
+        call("pamg_set_option", k.encode(), v)
+
 
 @pytest.mark.parametrize("case", list(LENGTHS))
-def test_spmv_residual_bit_exact(ctx, case):
+def test_spmv_residual_bit_exact(ctx, case, tile_cfg):
     rng = np.random.default_rng(11)
     lengths = LENGTHS[case]
     ncols = max(max(lengths) + 1, len(lengths) + 7)
@@ -65,15 +88,24 @@ def test_spmv_residual_bit_exact(ctx, case):
     x = PVector(ctx, ncols, 0, xh)
     y = PVector(ctx, len(lengths))
     mul(y, A, x)
-    assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
+    ref = O.spmv(M, xh)
+    assert np.array_equal(bits(y.own_values()), bits(ref))
     b = PVector(ctx, len(lengths), 0, bh)
     r = PVector(ctx, len(lengths))
     residual(r, A, x, b)
     assert np.array_equal(bits(r.own_values()), bits(O.residual(M, xh, bh)))
+    # prolongate-add: y <- y + A x (the op the V-cycle applies with P)
+    import ctypes
+    from parallel_amg_amd._lib import call
+    ms = ctypes.c_double()
+    yy = PVector(ctx, len(lengths), 0, bh)
+    call("pamg_bench_rowop", ctx.handle, A.handle, 3, x.handle, None, yy.handle, 0.0, 1, ctypes.byref(ms))
+    # two launches (warm-up + 1 timed): bh + s + s, in that order
+    assert np.array_equal(bits(yy.own_values()), bits((bh + ref) + ref))
 
 
-@pytest.mark.parametrize("case", ["stencil7", "ragged", "long", "one_row"])
-def test_jacobi_bit_exact(ctx, case):
+@pytest.mark.parametrize("case", ["stencil7", "ragged", "long", "budget_edge", "one_row"])
+def test_jacobi_bit_exact(ctx, case, tile_cfg):
     rng = np.random.default_rng(5)
     lengths = LENGTHS[case]
     n = max(max(lengths) + 1, len(lengths))
@@ -113,7 +145,7 @@ CONFIGS = [("poisson2d", 64, 300), ("poisson3d", 24, 100), ("aniso3d", 20, 300),
 
 
 @pytest.mark.parametrize("kind,n,max_coarse", CONFIGS)
-def test_vcycle_bit_exact(ctx, kind, n, max_coarse):
+def test_vcycle_bit_exact(ctx, kind, n, max_coarse, tile_cfg):
     be = pa.SequentialBackend(1)
     A, offs, xs = pa.generate_problem(be, kind, n)
     H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse))

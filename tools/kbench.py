@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmark: row-operation kernels of libpamg on the hierarchy matrices.
+
+For each tuning configuration (pamg_set_option) the level operators are re-uploaded and every
+row op is timed with HIP events (pamg_bench_rowop); prints one JSON line per measurement with
+the algorithmic bytes and the achieved GB/s. Dev tool, not part of the ABI.
+
+    python tools/kbench.py --n 512 --levels 1      # fine matrix only (no setup)
+    python tools/kbench.py --n 256 --levels 3      # hierarchy levels 0..2 (A, R, P)
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import itertools
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import parallel_amg_amd as pa  # noqa: E402
+from parallel_amg_amd._lib import call  # noqa: E402
+from parallel_amg_amd.partitioned import Context, PSparseMatrix, PVector  # noqa: E402
+from parallel_amg_amd.solver import AMGSolver  # noqa: E402
+
+OPNAME = {0: "spmv", 1: "residual", 2: "jacobi", 3: "prolong"}
+
+
+def set_opts(**kw):
+    for k, v in kw.items():
+        call("pamg_set_option", k.encode(), int(v))
+
+
+def bench(ctx, M, op, reps):
+    x = PVector(ctx, M.n_own_cols, M.n_ghost, np.random.default_rng(1).standard_normal(M.n_own_cols))
+    b = PVector(ctx, M.nrows, 0, np.ones(M.nrows))
+    y = PVector(ctx, M.nrows)
+    ms = C.c_double()
+    call("pamg_bench_rowop", ctx.handle, M.handle, op, x.handle, b.handle, y.handle, 0.6, reps,
+         C.byref(ms))
+    extra = {0: 0, 1: 1, 2: 1, 3: 1}[op]
+    byt = AMGSolver.rowsum_bytes(M.nnz, M.nrows, M.n_own_cols + M.n_ghost, extra)
+    return ms.value, byt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--levels", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--configs", default="0:2048:256:0,1:2048:256:0,1:2048:256:1,1:4096:256:0,1:4096:512:0,1:1024:256:0")
+    ap.add_argument("--ops", default="0,2")
+    args = ap.parse_args()
+    ctx = Context(0)
+    be = pa.SequentialBackend(1)
+    t = time.time()
+    A, offs, xs = pa.generate_problem(be, "poisson3d", args.n)
+    mats = {"A0": (A[0], None)}
+    if args.levels > 1:
+        H = pa.build_hierarchy(be, A, offs)
+        for l in range(min(args.levels, H.nlevels - 1)):
+            lp = H.levels[l][0]
+            mats[f"A{l}"] = (lp.A, lp.planA)
+            mats[f"R{l}"] = (lp.R, lp.planR)
+            mats[f"P{l}"] = (lp.P, lp.planP)
+    print(f"# setup {time.time() - t:.1f}s", file=sys.stderr, flush=True)
+    ops = [int(o) for o in args.ops.split(",")]
+    for cfg in args.configs.split(","):
+        vals = [int(v) for v in cfg.split(":")] + [0]
+        kern, tnnz, trows, xcd, jd = vals[:5]
+        set_opts(tile_rows=256)
+        set_opts(rows_kernel=kern, tile_nnz=tnnz, tile_rows=trows, xcd_remap=xcd, jacobi_diag=jd)
+        for name, (M, plan) in mats.items():
+            D = PSparseMatrix(ctx, M, plan)
+            for op in ops:
+                if op == 2 and not name.startswith("A"):
+                    continue
+                if op == 3 and not name.startswith("P"):
+                    continue
+                ms, byt = bench(ctx, D, op, args.reps)
+                print(json.dumps({"cfg": cfg, "mat": name, "op": OPNAME[op], "rows": D.nrows, "nnz": D.nnz,
+                                  "ms": round(ms, 4), "GBps": round(byt / ms / 1e6, 1)}), flush=True)
+            del D
+
+
+if __name__ == "__main__":
+    main()
