@@ -40,12 +40,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=512, help="grid points per side")
+    ap.add_argument("--grid", type=int, default=512, help="grid points per side")
     ap.add_argument("--kind", default="poisson3d", choices=["poisson2d", "poisson3d", "aniso3d"])
     ap.add_argument("--max-coarse", type=int, default=1000)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-cycles", type=int, default=1)
+    ap.add_argument("--transport", choices=["rccl", "host"], default="rccl",
+                    help="host = debug transport (ranks may share one GPU; not a perf mode)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -63,25 +65,34 @@ def main():
     from parallel_amg_amd.solver import OPS, AMGSolver
 
     _lib.lib()  # fail loudly if libpamg.so is missing
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    dev = local % max(ndev, 1)
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.transport == "rccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
         be = pa.DistributedBackend()
     else:
         be = pa.SequentialBackend(1)
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            if args.transport == "rccl":
+                dist.barrier(device_ids=[dev])
+            else:
+                dist.barrier()
 
     t0 = time.time()
-    A, offs, xs = pa.generate_problem(be, args.kind, args.n)
+    A, offs, xs = pa.generate_problem(be, args.kind, args.grid)
     H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=args.max_coarse), log=log)
     t_setup = time.time() - t0
     log(f"setup {t_setup:.1f}s, {H.nlevels} levels")
 
-    ctx = Context(local, be)
-    S = AMGSolver(ctx, H, part=rank, graph=not args.no_graph)
+    ctx = Context(dev, be, transport=args.transport)
+    # hipGraph replay on one part; multi-part cycles run eagerly (RCCL + host-side exchange)
+    S = AMGSolver(ctx, H, part=rank, graph=(not args.no_graph) and world == 1)
     A0 = S.A[0]
     xst = PVector(ctx, A0.n_own_cols, A0.n_ghost, xs[rank])
     b = PVector(ctx, A0.nrows)
@@ -105,7 +116,8 @@ def main():
     te = time.perf_counter()
     dt = te - ts
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64,
+                         device="cuda" if args.transport == "rccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     vps = args.steps / dt
@@ -133,6 +145,15 @@ def main():
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         cpu = cpu_baseline(H, xs[0], args.cpu_cycles, log)
 
+    # HBM traffic of the dominant kernel from the committed rocprofv3 PMC passes of this exact
+    # workload (tools/pmc_traffic.py; counters cannot be read from inside the process)
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, "profiles", "r01_pmc", "traffic_jacobi_512.json")
+    if args.kind == "poisson3d" and args.grid == 512 and world == 1 and os.path.exists(pmc):
+        rec = json.load(open(pmc))
+        if rec:
+            traffic, traffic_src = float(rec[0]["traffic_bytes"]), os.path.relpath(pmc, ROOT)
+
     if rank == 0:
         gl_rows = int(H.offsets(0)[-1])
         out = {
@@ -149,19 +170,21 @@ def main():
             "dtype": "f64",
             "data": "synthetic (SPEC.md §S2 grid operator, b = A x*, x0 = 0)",
             "config": {
-                "workload": f"{args.kind} {args.n}^3 fp64, SA-AMG V(1,1) weighted-Jacobi, "
+                "workload": f"{args.kind} {args.grid}^3 fp64, SA-AMG V(1,1) weighted-Jacobi, "
                             f"{world} part(s)",
                 "n": gl_rows, "nnz_fine": int(sum(H.levels[0][p].A.nnz for p in H.levels[0])) if world == 1
                 else None, "levels": S.L, "max_coarse": args.max_coarse,
                 "parallelism": f"row-slab partition p{world} (RCCL ghost exchange)",
-                "graph": not args.no_graph,
+                "graph": (not args.no_graph) and world == 1,
+                "transport": args.transport if world > 1 else None,
             },
             "fine_spmv_GBps": round(spmv_gbps, 1),
             "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
             "roofline": {
                 "kernel": "k_rows_tile<OP_JACOBI> (level-0 post-smoothing)",
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic, "traffic_source": traffic_src,
                 "bytes_per_launch": int(post_bytes), "ms_per_launch": round(post_ms, 4),
             },
             "cpu_baseline": cpu,

@@ -57,6 +57,17 @@ int pamg_ctx_sync(pamg_ctx* ctx);
 int pamg_comm_unique_id(unsigned char id[128]);
 int pamg_comm_init(pamg_ctx* ctx, int nranks, int rank, const unsigned char id[128]);
 int pamg_comm_rank(const pamg_ctx* ctx, int* rank, int* nranks);
+/* Debug transport (PartitionedArrays' debug-backend role): instead of RCCL, every exchange is
+ * staged through host buffers and handed to `fn` (synchronously, no overlap). Lets several
+ * ranks share ONE GPU (RCCL refuses that) so the multi-part data path can be tested on a
+ * one-GPU machine. op 0: neighbour exchange — for k < n, send send_counts[k] doubles to
+ * peer[k] and receive recv_counts[k] doubles from it (buffers concatenated in k order);
+ * op 1: all-gather of send_counts[0] doubles per rank into recvbuf (rank order);
+ * op 2: all-reduce (sum) of send_counts[0] doubles into recvbuf. Return 0 on success. */
+typedef int (*pamg_host_comm_fn)(void* user, int op, int n, const int32_t* peer,
+                                 const int64_t* send_counts, const double* sendbuf,
+                                 const int64_t* recv_counts, double* recvbuf);
+int pamg_comm_init_host(pamg_ctx* ctx, int nranks, int rank, pamg_host_comm_fn fn, void* user);
 
 /* ------------------------------------------------------------------ exchange plan */
 /* Replaces PRange / ExchangeGraph: ghosts [n_own, n_own+n_ghost) grouped by neighbour in

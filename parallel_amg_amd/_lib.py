@@ -40,6 +40,7 @@ SIGNATURES = {
     "pamg_comm_unique_id": [C.c_char_p],
     "pamg_comm_init": [vp, i32, i32, C.c_char_p],
     "pamg_comm_rank": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
+    "pamg_comm_init_host": [vp, i32, i32, vp, vp],
     "pamg_plan_create": [vp, i64, i64, i32, vp, vp, vp, vp, pvp],
     "pamg_plan_destroy": [vp],
     "pamg_vec_create": [vp, i64, i64, pvp],

@@ -55,6 +55,9 @@ struct pamg_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
+    pamg_host_comm_fn host_fn = nullptr;  // debug transport (pamg_comm_init_host)
+    void* host_user = nullptr;
+    std::vector<double> h_send, h_recv;   // staging for the debug transport
     double* d_red = nullptr;  // reduction workspace (partials + result)
     int red_cap = 0;
     double* h_red = nullptr;  // pinned host scalar

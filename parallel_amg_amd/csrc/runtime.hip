@@ -126,8 +126,27 @@ int exchange_on(const pamg_plan* plan, double* x, hipStream_t s) {
     pamg_ctx* ctx = plan->ctx;
     const int nn = (int)plan->nbr.size();
     if (nn == 0) return PAMG_OK;
-    if (!ctx->comm) return fail(PAMG_E_STATE, "exchange: plan has neighbours but no communicator");
+    if (!ctx->comm && !ctx->host_fn)
+        return fail(PAMG_E_STATE, "exchange: plan has neighbours but no communicator");
     pamg::launch_pack(plan->send_off[nn], plan->d_send_idx, x, plan->d_sendbuf, s);
+    if (ctx->host_fn) {  // debug transport: synchronous host staging
+        const int64_t ns = plan->send_off[nn], nr = plan->recv_off[nn];
+        ctx->h_send.resize(ns + 1);
+        ctx->h_recv.resize(nr + 1);
+        std::vector<int64_t> sc(nn), rc(nn);
+        for (int k = 0; k < nn; ++k) {
+            sc[k] = plan->send_off[k + 1] - plan->send_off[k];
+            rc[k] = plan->recv_off[k + 1] - plan->recv_off[k];
+        }
+        if (ns) HIPC(hipMemcpyAsync(ctx->h_send.data(), plan->d_sendbuf, sizeof(double) * ns, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        if (ctx->host_fn(ctx->host_user, 0, nn, plan->nbr.data(), sc.data(), ctx->h_send.data(), rc.data(),
+                         ctx->h_recv.data()) != 0)
+            return fail(PAMG_E_RCCL, "exchange: host transport failed");
+        if (nr) HIPC(hipMemcpyAsync(x + plan->n_own, ctx->h_recv.data(), sizeof(double) * nr, hipMemcpyHostToDevice, s));
+        HIPC(hipStreamSynchronize(s));
+        return PAMG_OK;
+    }
     NCCLC(ncclGroupStart());
     for (int k = 0; k < nn; ++k) {
         const size_t sc = (size_t)(plan->send_off[k + 1] - plan->send_off[k]);
@@ -143,7 +162,11 @@ int exchange_on(const pamg_plan* plan, double* x, hipStream_t s) {
 int apply(pamg_ctx* ctx, const pamg_mat* A, int op, double* x, const double* b, double* y,
           double omega) {
     hipStream_t s = ctx->s_comp;
-    const bool comm = A->plan && !A->plan->nbr.empty();
+    bool comm = A->plan && !A->plan->nbr.empty();
+    if (comm && ctx->host_fn) {  // debug transport: exchange first, no overlap
+        CHECK(exchange_on(A->plan, x, s));
+        comm = false;
+    }
     if (comm) {
         HIPC(hipEventRecord(ctx->ev_fork, s));
         HIPC(hipStreamWaitEvent(ctx->s_comm, ctx->ev_fork, 0));
@@ -167,6 +190,13 @@ int reduce_scalar(pamg_ctx* ctx, int64_t n, const double* x, const double* y, do
     HIPC(hipMemcpyAsync(ctx->h_red, res, sizeof(double), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     *out = *ctx->h_red;
+    if (ctx->host_fn && ctx->nranks > 1) {
+        const int64_t one = 1;
+        double sum = 0.0;
+        if (ctx->host_fn(ctx->host_user, 2, 1, nullptr, &one, out, &one, &sum) != 0)
+            return fail(PAMG_E_RCCL, "allreduce: host transport failed");
+        *out = sum;
+    }
     return PAMG_OK;
 }
 
@@ -215,7 +245,18 @@ int coarse_solve(pamg_hier* H, const double* bL, double* xL, hipStream_t s) {
     }
     // all-gather b_L in rank blocks of cmax, then the owned rows of Ainv * b_L
     HIPC(hipMemcpyAsync(H->d_bsend, bL, sizeof(double) * nown, hipMemcpyDeviceToDevice, s));
-    NCCLC(ncclAllGather(H->d_bsend, H->d_bgather, (size_t)H->cmax, ncclDouble, ctx->comm, s));
+    if (ctx->host_fn) {
+        ctx->h_send.resize(H->cmax + 1);
+        ctx->h_recv.resize((size_t)nr * H->cmax + 1);
+        HIPC(hipMemcpyAsync(ctx->h_send.data(), H->d_bsend, sizeof(double) * H->cmax, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        const int64_t cnt = H->cmax, tot = (int64_t)nr * H->cmax;
+        if (ctx->host_fn(ctx->host_user, 1, nr, nullptr, &cnt, ctx->h_send.data(), &tot, ctx->h_recv.data()) != 0)
+            return fail(PAMG_E_RCCL, "allgather: host transport failed");
+        HIPC(hipMemcpyAsync(H->d_bgather, ctx->h_recv.data(), sizeof(double) * tot, hipMemcpyHostToDevice, s));
+    } else {
+        NCCLC(ncclAllGather(H->d_bsend, H->d_bgather, (size_t)H->cmax, ncclDouble, ctx->comm, s));
+    }
     // compact the gathered blocks into global order (ragged -> contiguous), in place safe:
     // use d_bgather as source and d_bsend is too small, so copy rank blocks into xL-sized
     // scratch: reuse the tail of d_bgather (allocated 2x)
@@ -366,6 +407,17 @@ int pamg_comm_init(pamg_ctx* ctx, int nranks, int rank, const unsigned char id[1
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
     NCCLC(ncclCommInitRank(&ctx->comm, nranks, u, rank));
+    ctx->rank = rank;
+    ctx->nranks = nranks;
+    return PAMG_OK;
+}
+
+int pamg_comm_init_host(pamg_ctx* ctx, int nranks, int rank, pamg_host_comm_fn fn, void* user) {
+    if (!ctx || !fn || nranks < 1 || rank < 0 || rank >= nranks)
+        return fail(PAMG_E_ARG, "comm_init_host: bad args");
+    if (ctx->comm) return fail(PAMG_E_STATE, "comm_init_host: context already has an RCCL communicator");
+    ctx->host_fn = fn;
+    ctx->host_user = user;
     ctx->rank = rank;
     ctx->nranks = nranks;
     return PAMG_OK;
@@ -788,6 +840,8 @@ int pamg_hier_destroy(pamg_hier* H) {
 
 int pamg_hier_set_graph(pamg_hier* H, int enable) {
     if (!H) return fail(PAMG_E_ARG, "hier_set_graph: NULL");
+    if (enable && H->ctx->host_fn)
+        return fail(PAMG_E_STATE, "hier_set_graph: the host debug transport cannot be graph-captured");
     H->use_graph = enable != 0;
     if (!H->use_graph) drop_graph(H);
     return PAMG_OK;

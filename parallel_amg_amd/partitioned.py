@@ -41,19 +41,95 @@ def _release(obj, fn):
     obj._h = None
 
 
-class Context:
-    """A GPU (``pamg_ctx``) plus, for multi-part runs, its RCCL communicator."""
+HOST_COMM_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int32),
+                           C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                           C.POINTER(C.c_double))
 
-    def __init__(self, device: int = 0, backend=None):
+
+def _host_comm_callback(backend):
+    """pamg_host_comm_fn over torch.distributed (gloo): op 0 neighbour exchange, 1 all-gather,
+    2 all-reduce (see include/pamg.h)."""
+    import torch
+    dist, group = backend.dist, backend.group
+
+    def view(p, n):
+        return np.ctypeslib.as_array(p, (n,)) if n else np.zeros(0)
+
+    def fn(_user, op, n, peer, sc, sbuf, rc, rbuf):
+        try:
+            if op == 0:
+                ns = sum(sc[k] for k in range(n))
+                nr = sum(rc[k] for k in range(n))
+                s_all, r_all = view(sbuf, ns), view(rbuf, nr)
+                reqs, so, ro = [], 0, 0
+                recvs = []
+                for k in range(n):
+                    q = int(peer[k])
+                    if sc[k]:
+                        t = torch.from_numpy(s_all[so:so + sc[k]].copy())
+                        reqs.append(dist.isend(t, dst=q, group=group))
+                    if rc[k]:
+                        t = torch.empty(rc[k], dtype=torch.float64)
+                        reqs.append(dist.irecv(t, src=q, group=group))
+                        recvs.append((ro, t))
+                    so += sc[k]
+                    ro += rc[k]
+                for r in reqs:
+                    r.wait()
+                for o, t in recvs:
+                    r_all[o:o + len(t)] = t.numpy()
+            elif op == 1:
+                cnt = sc[0]
+                t = torch.from_numpy(view(sbuf, cnt).copy())
+                outs = [torch.empty(cnt, dtype=torch.float64) for _ in range(backend.nparts)]
+                dist.all_gather(outs, t, group=group)
+                r_all = view(rbuf, cnt * backend.nparts)
+                for q, o in enumerate(outs):
+                    r_all[q * cnt:(q + 1) * cnt] = o.numpy()
+            elif op == 2:
+                cnt = sc[0]
+                t = torch.from_numpy(view(sbuf, cnt).copy())
+                dist.all_reduce(t, group=group)
+                view(rbuf, cnt)[:] = t.numpy()
+            else:
+                return -1
+            return 0
+        except Exception:  # pragma: no cover - reported as PAMG_E_RCCL by the library
+            import traceback
+            traceback.print_exc()
+            return -1
+
+    return HOST_COMM_FN(fn)
+
+
+class Context:
+    """A GPU (``pamg_ctx``) plus, for multi-part runs, its RCCL communicator (or the host
+    debug transport)."""
+
+    def __init__(self, device: int = 0, backend=None, transport: str = "rccl"):
         h = C.c_void_p()
         call("pamg_ctx_create", device, C.byref(h))
         self._h = h
         self.device = device
         self.rank, self.nranks = 0, 1
+        self._hostfn = None
         if backend is not None and backend.nparts > 1:
             if not backend.distributed:
                 raise ValueError("device runs need one part per process (DistributedBackend)")
-            self._init_comm(backend)
+            if transport == "rccl":
+                self._init_comm(backend)
+            elif transport == "host":
+                self._init_host_comm(backend)
+            else:
+                raise ValueError(f"unknown transport {transport!r}")
+
+    def _init_host_comm(self, backend):
+        """Debug transport: ghost exchanges staged through host memory over the backend's gloo
+        group (several ranks may then share one GPU; RCCL refuses that)."""
+        self._hostfn = _host_comm_callback(backend)
+        call("pamg_comm_init_host", self._h, backend.nparts, backend.rank,
+             C.cast(self._hostfn, C.c_void_p), None)
+        self.rank, self.nranks = backend.rank, backend.nparts
 
     def _init_comm(self, backend):
         import torch

@@ -1,0 +1,91 @@
+"""Multi-part device path: N processes (one part each, RCCL ghost exchange inside libpamg,
+gloo for the host setup) must reproduce the global-view oracle's multi-part V-cycle bit for
+bit (SPEC §S7: the operators are the global ones, only their storage is partitioned).
+
+On a one-GPU box all ranks share device 0 (RCCL permitting); the driver's 8-GPU node runs
+the same code one rank per device."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, kind, n, max_coarse, ncycles, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), OMP_NUM_THREADS="2")
+    import torch
+    import torch.distributed as dist
+
+    import parallel_amg_amd as pa
+    from parallel_amg_amd.partitioned import Context, PVector, mul
+    from parallel_amg_amd.solver import AMGSolver
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        be = pa.DistributedBackend()
+        A, offs, xs = pa.generate_problem(be, kind, n)
+        H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse))
+        ndev = max(1, torch.cuda.device_count())
+        # RCCL needs one device per rank; with fewer GPUs than ranks use the host transport
+        ctx = Context(rank % ndev, be, transport="rccl" if ndev >= world else "host")
+        S = AMGSolver(ctx, H, part=rank)
+        A0 = S.A[0]
+        xst = PVector(ctx, A0.n_own_cols, A0.n_ghost, xs[rank])
+        b = PVector(ctx, A0.nrows)
+        mul(b, A0, xst)
+        x = S.new_vector()
+        hist = S.vcycle(x, b, ncycles, res_hist=True)
+        out = (rank, "ok", b.own_values(), x.own_values(), hist)
+        q.put(out)
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None, None))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,kind,n,max_coarse", [(2, "poisson3d", 20, 100), (3, "poisson2d", 60, 200)])
+def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, built):
+    from oracle import oracle as O
+    ncycles = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, n, max_coarse, ncycles, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r = q.get(timeout=300)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert res[r][1] == "ok", res[r][1]
+    Ao = O.generate(kind, *O.grid_shape(kind, n))
+    bo = O.spmv(Ao, O.xstar(Ao.nrows))
+    Ho = O.setup(Ao, nparts=world, max_coarse=max_coarse)
+    xo, ho = Ho.solve(bo, ncycles, res_hist=True)
+    b = np.concatenate([res[r][2] for r in range(world)])
+    x = np.concatenate([res[r][3] for r in range(world)])
+    bits = lambda a: np.asarray(a, np.float64).view(np.int64)
+    assert np.array_equal(bits(b), bits(bo))
+    assert np.array_equal(bits(x), bits(xo))
+    for r in range(world):
+        np.testing.assert_allclose(res[r][4], ho, rtol=1e-12)
