@@ -1,0 +1,89 @@
+"""C-ABI boundary (include/pamg.h) on CPU: libpamg.so loads, exports every declared entry point,
+the ctypes table binds all of them, and the host-side error convention holds (status codes +
+pamg_last_error). No device compute here (no GPU in the CPU suite)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pamg.h")
+
+
+def declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(pamg_\w+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_the_boundary():
+    names = declared()
+    for must in ("pamg_ctx_create", "pamg_mat_upload", "pamg_spmv", "pamg_residual", "pamg_jacobi",
+                 "pamg_exchange", "pamg_hier_create", "pamg_vcycle", "pamg_comm_init",
+                 "pamg_setup_spgemm", "pamg_setup_aggregate"):
+        assert must in names
+    assert len(names) >= 50
+
+
+def test_library_exports_every_declared_symbol(built):
+    from parallel_amg_amd import _lib
+    lib_path = _lib.LIB_PATH
+    out = subprocess.run(["nm", "-D", "--defined-only", lib_path], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (pamg_\w+)", out))
+    missing = [n for n in declared() if n not in exported]
+    assert not missing, missing
+    # the ctypes binding covers the whole boundary (and nothing that is not declared)
+    assert sorted(_lib.SIGNATURES) == declared()
+    L = _lib.lib()
+    for n in declared():
+        assert getattr(L, n) is not None
+
+
+def test_error_convention(built):
+    from parallel_amg_amd import _lib
+    from parallel_amg_amd._lib import PamgError, call
+    L = _lib.lib()
+    assert L.pamg_version().startswith(b"pamg")
+    rc = L.pamg_hcsr_info(None, None, None, None)
+    assert rc == -1 and b"invalid handle" in L.pamg_last_error()
+    with pytest.raises(PamgError) as e:
+        call("pamg_gen_grid", 7, 4, 4, 4, 0.0, 0, 64, C.byref(C.c_void_p()))
+    assert e.value.code == -1
+    with pytest.raises(PamgError):
+        call("pamg_set_option", b"no_such_key", 1)
+    v = C.c_int64()
+    call("pamg_set_option", b"tile_nnz", 2048)
+    call("pamg_get_option", b"tile_nnz", C.byref(v))
+    assert v.value == 2048
+    call("pamg_set_option", b"tile_nnz", 1024)
+
+
+def test_setup_errors_are_reported(built):
+    from parallel_amg_amd import hcsr as HC
+    from parallel_amg_amd._lib import PamgError
+    import numpy as np
+    # a row without a diagonal -> PAMG_E_SETUP from the Gershgorin bound (SPEC §S3 needs a_ii)
+    M = HC.HCSR.from_arrays(np.array([0, 1, 2]), np.array([1, 1], np.int32), np.array([1.0, 2.0]), 2)
+    with pytest.raises(PamgError) as e:
+        HC.gershgorin(M, 0)
+    assert e.value.code == -5
+    # non-SPD coarse matrix -> PAMG_E_SETUP from the Cholesky inverse (SPEC §S5)
+    M = HC.HCSR.from_arrays(np.array([0, 2, 4]), np.array([0, 1, 0, 1], np.int32), np.array([1.0, 2.0, 2.0, 1.0]), 2)
+    with pytest.raises(PamgError) as e:
+        HC.cholinv(M)
+    assert e.value.code == -5
+
+
+def test_product_never_imports_the_oracle():
+    """The product package must not touch oracle/ (the checker) — grep its sources."""
+    pkg = os.path.join(ROOT, "parallel_amg_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                txt = open(os.path.join(dirpath, f)).read()
+                assert "import oracle" not in txt and "from oracle" not in txt, f
+                assert "libpamg_oracle" not in txt and not re.search(r"#include\s*[<\"].*oracle", txt), f
+                assert not re.search(r"\borc_\w+\(", txt), f
