@@ -181,7 +181,7 @@ def main():
             "fine_spmv_GBps": round(spmv_gbps, 1),
             "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
             "roofline": {
-                "kernel": "k_rows_tile<OP_JACOBI> (level-0 post-smoothing)",
+                "kernel": "k_rows_tile2<OP_JACOBI,1024,256> (level-0 post-smoothing Jacobi)",
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic, "traffic_source": traffic_src,

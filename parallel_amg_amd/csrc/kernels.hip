@@ -15,6 +15,8 @@
 //   phase 2  one lane per row adds its products from LDS in storage order and applies the
 //            epilogue (SpMV / residual / Jacobi / prolongate-add), coalesced stores.
 // Rows longer than the tile budget go to k_rows_long (one workgroup per row, chunked).
+#include <type_traits>
+
 #include "pamg_device.h"
 
 namespace pamg {
@@ -92,7 +94,23 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile(
 // issued back to back (branch-free: invalid lanes gather x[0] and discard it) before the
 // products go to LDS. XCD=true maps contiguous tile chunks to each XCD (blocks b and b+8
 // share an XCD) so neighbouring tiles' x lines stay in one L2.
-template <int OP, int TNNZ, int TROWS, bool XCD>
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int4 stream_load(const int4* p, std::true_type /*nt*/) {
+    const i32x4 v = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(p));
+    return make_int4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ double2 stream_load(const double2* p, std::true_type /*nt*/) {
+    const f64x2 v = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(p));
+    return make_double2(v.x, v.y);
+}
+template <class T>
+__device__ __forceinline__ T stream_load(const T* p, std::false_type) {
+    return *p;
+}
+
+template <int OP, int TNNZ, int TROWS, bool XCD, bool NT = false>
 __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     const int4* __restrict__ tiles, int ntiles, const int* __restrict__ rowptr,
     const int* __restrict__ col, const double* __restrict__ val, const double* __restrict__ x,
@@ -123,11 +141,29 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     for (int j = 0; j < G; ++j) {
         const int g = za + 4 * (tid + j * kBlock);
         const int gs = g < z1 ? g : za;  // clamp: never read past the (padded) arrays
-        c4[j] = *reinterpret_cast<const int4*>(col + gs);
-        va[j] = *reinterpret_cast<const double2*>(val + gs);
-        vb[j] = *reinterpret_cast<const double2*>(val + gs + 2);
+        // NT: the once-read matrix stream goes non-temporal so the x lines (reused by the
+        // z+-1 / y+-1 neighbour rows) keep their place in the XCD's L2
+        using nt = std::integral_constant<bool, NT>;
+        c4[j] = stream_load(reinterpret_cast<const int4*>(col + gs), nt{});
+        va[j] = stream_load(reinterpret_cast<const double2*>(val + gs), nt{});
+        vb[j] = stream_load(reinterpret_cast<const double2*>(val + gs + 2), nt{});
     }
     for (int i = tid; i <= nr; i += kBlock) lrp[i] = rowptr[r0 + i];
+    // one row per lane: fetch the epilogue's own-row operands (b, old x, y, a_ii) now, so
+    // their latency hides under the column stream instead of trailing the LDS phase
+    constexpr bool ONE_ROW = TROWS <= kBlock;
+    double pb = 0.0, px = 0.0, py = 0.0, pd = 0.0;
+    if constexpr (ONE_ROW) {
+        if (tid < nr) {
+            const int r = r0 + tid;
+            if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[r];
+            if constexpr (OP == OP_JACOBI) {
+                px = x[r];
+                if (diag) pd = diag[r];
+            }
+            if constexpr (OP == OP_PROLONG) py = y[r];
+        }
+    }
     if constexpr (OP == OP_JACOBI) {
         if (!diag) __syncthreads();
     }
@@ -164,13 +200,35 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
         *reinterpret_cast<double2*>(&lprod[g - za + 2]) = make_double2(p[2], p[3]);
     }
     __syncthreads();
-    for (int rr = tid; rr < nr; rr += kBlock) {
-        const int kb = lrp[rr] - za, ke = lrp[rr + 1] - za;
-        double s = 0.0;
-        for (int k = kb; k < ke; ++k) s = s + lprod[k];
-        double d = 0.0;
-        if constexpr (OP == OP_JACOBI) d = diag ? diag[r0 + rr] : ldiag[rr];
-        epilogue<OP>(r0 + rr, s, x, b, y, omega, d);
+    if constexpr (ONE_ROW) {
+        if (tid < nr) {
+            const int kb = lrp[tid] - za, ke = lrp[tid + 1] - za;
+            double s = 0.0;
+            for (int k = kb; k < ke; ++k) s = s + lprod[k];
+            const int r = r0 + tid;
+            if constexpr (OP == OP_SPMV) {
+                y[r] = s;
+            } else if constexpr (OP == OP_RESID) {
+                y[r] = pb - s;
+            } else if constexpr (OP == OP_JACOBI) {
+                const double d = diag ? pd : ldiag[tid];
+                const double u = pb - s;
+                const double v = omega * u;
+                const double w = v / d;
+                y[r] = px + w;
+            } else {
+                y[r] = py + s;
+            }
+        }
+    } else {
+        for (int rr = tid; rr < nr; rr += kBlock) {
+            const int kb = lrp[rr] - za, ke = lrp[rr + 1] - za;
+            double s = 0.0;
+            for (int k = kb; k < ke; ++k) s = s + lprod[k];
+            double d = 0.0;
+            if constexpr (OP == OP_JACOBI) d = diag ? diag[r0 + rr] : ldiag[rr];
+            epilogue<OP>(r0 + rr, s, x, b, y, omega, d);
+        }
     }
 }
 
@@ -440,6 +498,9 @@ void launch_tile2(const pamg_mat& A, const TileSet& ts, const double* x, const d
     if (A.xcd_remap) {
         const int grid = ((ts.n_short + 7) / 8) * 8;
         k_rows_tile2<OP, TNNZ, TROWS, true><<<grid, kBlock, 0, s>>>(
+            ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg);
+    } else if (A.stream_nt) {
+        k_rows_tile2<OP, TNNZ, TROWS, false, true><<<ts.n_short, kBlock, 0, s>>>(
             ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg);
     } else {
         k_rows_tile2<OP, TNNZ, TROWS, false><<<ts.n_short, kBlock, 0, s>>>(

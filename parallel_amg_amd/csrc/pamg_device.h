@@ -43,6 +43,8 @@ struct Options {
     int tile_rows = kTileRows; // 64 / 256 / 512
     int xcd_remap = 0;         // 1: contiguous tile chunks per XCD
     int jacobi_diag = 0;       // 1: Jacobi reads the stored diagonal (no in-tile detection)
+    int stream_nt = 0;         // 1: non-temporal loads for the matrix stream (variant 1)
+    int tile_order = 1;        // 1: banded XCD-blocked tile order (see build_tiles)
 };
 Options& options();
 
@@ -91,6 +93,7 @@ struct pamg_mat {
     int rows_kernel = 1;     // variant fixed at upload (pamg::Options)
     int xcd_remap = 0;
     int jacobi_diag = 0;
+    int stream_nt = 0;
 };
 
 namespace pamg {

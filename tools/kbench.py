@@ -71,10 +71,10 @@ def main():
     print(f"# setup {time.time() - t:.1f}s", file=sys.stderr, flush=True)
     ops = [int(o) for o in args.ops.split(",")]
     for cfg in args.configs.split(","):
-        vals = [int(v) for v in cfg.split(":")] + [0]
-        kern, tnnz, trows, xcd, jd = vals[:5]
-        set_opts(tile_rows=256)
-        set_opts(rows_kernel=kern, tile_nnz=tnnz, tile_rows=trows, xcd_remap=xcd, jacobi_diag=jd)
+        vals = [int(v) for v in cfg.split(":")] + [0, 0, 0]
+        kern, tnnz, trows, xcd, jd, nt, order = vals[:7]
+        set_opts(rows_kernel=kern, tile_nnz=tnnz, tile_rows=trows, xcd_remap=xcd, jacobi_diag=jd,
+                 stream_nt=nt, tile_order=order)
         for name, (M, plan) in mats.items():
             D = PSparseMatrix(ctx, M, plan)
             for op in ops:
