@@ -128,6 +128,12 @@ int pamg_hier_set_graph(pamg_hier* H, int enable);
 int pamg_vcycle(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles,
                 double* res_hist);
 int pamg_vcycle_async(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles);
+/* Preconditioned CG on level 0 with one V-cycle (zero initial guess) as the preconditioner
+ * (SPEC §S8; the Krylov caller of the path, e.g. IterativeSolvers.cg!(x, A, b; Pl = amg)).
+ * Stops when ||r_k|| <= rtol ||r_0|| or after maxit iterations; *iters = iterations done;
+ * res_hist (maxit + 1 entries, may be NULL) gets ||r_0||, ||r_1||, ... */
+int pamg_pcg(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, double rtol,
+             int maxit, int* iters, double* res_hist);
 /* Kernel timing of the last pamg_vcycle/_async (events on the compute stream): per level,
  * milliseconds spent in [jacobi_pre, residual, restrict, prolong, jacobi_post, coarse]. */
 int pamg_hier_profile(pamg_hier* H, int enable);

@@ -61,6 +61,8 @@ def lib():
         L.orc_hier_new.argtypes = [C.c_int]
         L.orc_hier_set.argtypes = [vp, C.c_int, C.c_int, i64, i64, vp, vp, vp, dbl]
         L.orc_hier_set_ainv.argtypes = [vp, i64, _f64p]
+        L.orc_pcg.restype = C.c_int
+        L.orc_pcg.argtypes = [vp, _f64p, _f64p, dbl, C.c_int, vp]
         _lib = L
     return _lib
 
@@ -157,6 +159,13 @@ class Hierarchy:
         lib().orc_solve(self._h, x, np.ascontiguousarray(b, np.float64), ncycles,
                         hist.ctypes.data if res_hist else None)
         return (x, hist) if res_hist else x
+
+    def pcg(self, b, rtol=1e-8, maxit=100, x0=None):
+        """SPEC §S8 PCG with one V-cycle as preconditioner: (x, iterations, history)."""
+        x = np.zeros(len(b)) if x0 is None else np.array(x0, np.float64, copy=True)
+        hist = np.zeros(maxit + 1)
+        k = lib().orc_pcg(self._h, x, np.ascontiguousarray(b, np.float64), rtol, maxit, hist.ctypes.data)
+        return x, k, hist[:k + 1]
 
     def __del__(self):
         if self._h and _lib is not None:

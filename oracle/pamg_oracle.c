@@ -490,3 +490,51 @@ void orc_hier_set_ainv(ohier* h, i64 n, const double* ainv) {
     h->ainv = malloc(sizeof(double) * (size_t)(n * n + 1));
     memcpy(h->ainv, ainv, sizeof(double) * (size_t)(n * n));
 }
+
+/* ------------------------------------------------------------------ PCG §S8 */
+
+static double dot_seq(i64 n, const double* x, const double* y) {
+    double s = 0.0;
+    for (i64 i = 0; i < n; ++i) { double p = x[i] * y[i]; s = s + p; }
+    return s;
+}
+
+static void axpby(i64 n, double a, const double* x, double b, double* y) {
+    for (i64 i = 0; i < n; ++i) { double u = a * x[i], v = b * y[i]; y[i] = u + v; }
+}
+
+/* Returns the iteration count; hist (maxit+1, may be NULL) gets ||r_k||. */
+int orc_pcg(const ohier* h, double* x, const double* b, double rtol, int maxit, double* hist) {
+    const ocsr* A = &h->A[0];
+    const i64 n = A->nr;
+    double* r = malloc(sizeof(double) * (n + 1));
+    double* z = malloc(sizeof(double) * (n + 1));
+    double* p = malloc(sizeof(double) * (n + 1));
+    double* q = malloc(sizeof(double) * (n + 1));
+    orc_residual(n, A->rp, A->col, A->val, x, b, r);
+    const double nr0 = sqrt(dot_seq(n, r, r));
+    if (hist) hist[0] = nr0;
+    int k = 0;
+    if (nr0 > 0.0 && maxit > 0) {
+        vcycle(h, 0, z, r, 1);
+        memcpy(p, z, sizeof(double) * n);
+        double rz = dot_seq(n, r, z);
+        while (k < maxit) {
+            ++k;
+            orc_spmv(n, A->rp, A->col, A->val, p, q);
+            const double alpha = rz / dot_seq(n, p, q);
+            axpby(n, alpha, p, 1.0, x);
+            axpby(n, -alpha, q, 1.0, r);
+            const double nr = sqrt(dot_seq(n, r, r));
+            if (hist) hist[k] = nr;
+            if (nr <= rtol * nr0) break;
+            vcycle(h, 0, z, r, 1);
+            const double rz_new = dot_seq(n, r, z);
+            const double beta = rz_new / rz;
+            rz = rz_new;
+            axpby(n, 1.0, z, beta, p);
+        }
+    }
+    free(r); free(z); free(p); free(q);
+    return k;
+}

@@ -66,6 +66,7 @@ SIGNATURES = {
     "pamg_hier_set_graph": [vp, i32],
     "pamg_vcycle": [vp, vp, vp, vp, i32, vp],
     "pamg_vcycle_async": [vp, vp, vp, vp, i32],
+    "pamg_pcg": [vp, vp, vp, vp, dbl, i32, C.POINTER(C.c_int), vp],
     "pamg_hier_profile": [vp, i32],
     "pamg_hier_profile_read": [vp, vp],
     "pamg_bench_rowop": [vp, vp, i32, vp, vp, vp, dbl, i32, pdbl],

@@ -246,6 +246,9 @@ struct pamg_hier {
     hipGraphExec_t gexec = nullptr;
     const double* g_x = nullptr;
     const double* g_b = nullptr;
+    bool g_zero0 = false;
+    // PCG workspace (level-0 layout, allocated on first use)
+    double *pcg_r = nullptr, *pcg_z = nullptr, *pcg_p = nullptr, *pcg_q = nullptr;
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev;
@@ -313,8 +316,10 @@ struct ProfScope {
     }
 };
 
-// One V-cycle (SPEC §S6), enqueued on the compute stream; result in x.
-int vcycle_enqueue(pamg_hier* H, double* x, const double* b) {
+// One V-cycle (SPEC §S6), enqueued on the compute stream; result in x. zero0: the level-0
+// initial guess is zero (preconditioner use), so the level-0 pre-smoothing takes the
+// zero-guess form too (bit-identical to the full sweep from x = 0, SPEC §S3).
+int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false) {
     pamg_ctx* ctx = H->ctx;
     hipStream_t s = ctx->s_comp;
     const int L = H->L;
@@ -326,7 +331,7 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b) {
     H->b[0] = const_cast<double*>(b);
     for (int l = 0; l < L - 1; ++l) {
         const pamg_mat* A = H->A[l];
-        if (l == 0) {
+        if (l == 0 && !zero0) {
             ProfScope p(H, l, 0, s);
             CHECK(apply(ctx, A, pamg::OP_JACOBI, H->x[0], H->b[0], H->t[0], H->omega[0]));
         } else {
@@ -861,6 +866,10 @@ int pamg_hier_destroy(pamg_hier* H) {
     dfree(H->d_ainv);
     dfree(H->d_bgather);
     dfree(H->d_bsend);
+    dfree(H->pcg_r);
+    dfree(H->pcg_z);
+    dfree(H->pcg_p);
+    dfree(H->pcg_q);
     for (auto e : H->ev) (void)hipEventDestroy(e);
     delete H;
     return PAMG_OK;
@@ -898,31 +907,40 @@ int pamg_hier_profile_read(pamg_hier* H, double* out) {
     return PAMG_OK;
 }
 
+// ncycles V-cycles on raw device vectors (graph replay when enabled; the captured graph is
+// keyed on the vector addresses and the zero-guess flag).
+static int vcycle_raw(pamg_hier* H, double* x, const double* b, int ncycles, bool zero0) {
+    pamg_ctx* ctx = H->ctx;
+    if (zero0 && ncycles != 1) return fail(PAMG_E_ARG, "vcycle: zero initial guess applies to one cycle");
+    if (H->use_graph && !H->prof) {
+        if (!H->gexec || H->g_x != x || H->g_b != b || H->g_zero0 != zero0) {
+            drop_graph(H);
+            hipGraph_t g;
+            HIPC(hipStreamBeginCapture(ctx->s_comp, hipStreamCaptureModeThreadLocal));
+            int rc = vcycle_enqueue(H, x, b, zero0);
+            hipError_t e2 = hipStreamEndCapture(ctx->s_comp, &g);
+            if (rc != PAMG_OK) return rc;
+            if (e2 != hipSuccess) return fail(PAMG_E_HIP, "vcycle: capture failed: %s", hipGetErrorString(e2));
+            HIPC(hipGraphInstantiate(&H->gexec, g, nullptr, nullptr, 0));
+            (void)hipGraphDestroy(g);
+            H->g_x = x;
+            H->g_b = b;
+            H->g_zero0 = zero0;
+        }
+        for (int k = 0; k < ncycles; ++k) HIPC(hipGraphLaunch(H->gexec, ctx->s_comp));
+    } else {
+        for (int k = 0; k < ncycles; ++k) CHECK(vcycle_enqueue(H, x, b, zero0 && k == 0));
+    }
+    return PAMG_OK;
+}
+
 static int vcycle_common(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles) {
     if (!ctx || !H || !x || !b || ncycles < 0 || H->ctx != ctx) return fail(PAMG_E_ARG, "vcycle: bad args");
     const pamg_mat* A0 = H->A[0];
     CHECK(check_vec_for(A0, x, "vcycle"));
     if (b->n_own != A0->nrows) return fail(PAMG_E_ARG, "vcycle: b size mismatch");
     CHECK(set_device(ctx));
-    if (H->use_graph && !H->prof) {
-        if (!H->gexec || H->g_x != x->d || H->g_b != b->d) {
-            drop_graph(H);
-            hipGraph_t g;
-            HIPC(hipStreamBeginCapture(ctx->s_comp, hipStreamCaptureModeThreadLocal));
-            int rc = vcycle_enqueue(H, x->d, b->d);
-            hipError_t e2 = hipStreamEndCapture(ctx->s_comp, &g);
-            if (rc != PAMG_OK) return rc;
-            if (e2 != hipSuccess) return fail(PAMG_E_HIP, "vcycle: capture failed: %s", hipGetErrorString(e2));
-            HIPC(hipGraphInstantiate(&H->gexec, g, nullptr, nullptr, 0));
-            (void)hipGraphDestroy(g);
-            H->g_x = x->d;
-            H->g_b = b->d;
-        }
-        for (int k = 0; k < ncycles; ++k) HIPC(hipGraphLaunch(H->gexec, ctx->s_comp));
-    } else {
-        for (int k = 0; k < ncycles; ++k) CHECK(vcycle_enqueue(H, x->d, b->d));
-    }
-    return PAMG_OK;
+    return vcycle_raw(H, x->d, b->d, ncycles, false);
 }
 
 int pamg_vcycle_async(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles) {
@@ -954,6 +972,67 @@ int pamg_vcycle(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int
         res_hist[k] = std::sqrt(s);
     }
     HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+// Preconditioned CG with one V-cycle from a zero guess as M^-1 (SPEC §S8). The V(1,1) cycle
+// with R = P^T and the same weighted Jacobi before and after is symmetric, so CG applies.
+int pamg_pcg(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, double rtol,
+             int maxit, int* iters, double* res_hist) {
+    if (!ctx || !H || !x || !b || maxit < 0 || !(rtol >= 0.0) || H->ctx != ctx)
+        return fail(PAMG_E_ARG, "pcg: bad args");
+    const pamg_mat* A = H->A[0];
+    CHECK(check_vec_for(A, x, "pcg"));
+    if (b->n_own != A->nrows) return fail(PAMG_E_ARG, "pcg: b size mismatch");
+    CHECK(set_device(ctx));
+    const int64_t n = A->nrows;
+    int64_t g = A->plan ? A->plan->n_ghost : 0;
+    if (H->L > 1 && H->R[0]->plan) g = std::max(g, H->R[0]->plan->n_ghost);
+    const int64_t cap = n + g + kVecPad;
+    if (!H->pcg_r) {
+        CHECK(dalloc(&H->pcg_r, cap));
+        CHECK(dalloc(&H->pcg_z, cap));
+        CHECK(dalloc(&H->pcg_p, cap));
+        CHECK(dalloc(&H->pcg_q, cap));
+        for (double* p : {H->pcg_r, H->pcg_z, H->pcg_p, H->pcg_q})
+            HIPC(hipMemset(p, 0, sizeof(double) * cap));
+    }
+    hipStream_t s = ctx->s_comp;
+    double *r = H->pcg_r, *z = H->pcg_z, *p = H->pcg_p, *q = H->pcg_q;
+    CHECK(apply(ctx, A, pamg::OP_RESID, x->d, b->d, r, 0.0));
+    double rr = 0.0;
+    CHECK(reduce_scalar(ctx, n, r, r, &rr));
+    const double nr0 = std::sqrt(rr);
+    if (res_hist) res_hist[0] = nr0;
+    int k = 0;
+    if (nr0 > 0.0 && maxit > 0) {
+        CHECK(vcycle_raw(H, z, r, 1, true));
+        HIPC(hipMemcpyAsync(p, z, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+        double rz = 0.0;
+        CHECK(reduce_scalar(ctx, n, r, z, &rz));
+        while (k < maxit) {
+            ++k;
+            CHECK(apply(ctx, A, pamg::OP_SPMV, p, nullptr, q, 0.0));
+            double pq = 0.0;
+            CHECK(reduce_scalar(ctx, n, p, q, &pq));
+            const double alpha = rz / pq;
+            pamg::launch_axpby(n, alpha, p, 1.0, x->d, s);
+            pamg::launch_axpby(n, -alpha, q, 1.0, r, s);
+            CHECK(reduce_scalar(ctx, n, r, r, &rr));
+            const double nr = std::sqrt(rr);
+            if (res_hist) res_hist[k] = nr;
+            if (nr <= rtol * nr0) break;
+            CHECK(vcycle_raw(H, z, r, 1, true));
+            double rz_new = 0.0;
+            CHECK(reduce_scalar(ctx, n, r, z, &rz_new));
+            const double beta = rz_new / rz;
+            rz = rz_new;
+            pamg::launch_axpby(n, 1.0, z, beta, p, s);
+        }
+    }
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(s));
+    if (iters) *iters = k;
     return PAMG_OK;
 }
 

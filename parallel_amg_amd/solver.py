@@ -63,6 +63,14 @@ class AMGSolver:
         call("pamg_vcycle", self.ctx.handle, self._h, x.handle, b.handle, ncycles, None)
         return None
 
+    def pcg(self, x: PVector, b: PVector, rtol: float = 1e-8, maxit: int = 100):
+        """CG preconditioned by one V-cycle (SPEC §S8); returns (iterations, ||r_k|| history)."""
+        hist = np.zeros(maxit + 1)
+        it = C.c_int()
+        call("pamg_pcg", self.ctx.handle, self._h, x.handle, b.handle, float(rtol), int(maxit),
+             C.byref(it), ptr(hist))
+        return it.value, hist[: it.value + 1]
+
     def vcycle_async(self, x: PVector, b: PVector, ncycles: int = 1):
         call("pamg_vcycle_async", self.ctx.handle, self._h, x.handle, b.handle, ncycles)
 

@@ -167,6 +167,28 @@ def test_vcycle_bit_exact(ctx, kind, n, max_coarse, tile_cfg):
     assert hist[-1] < hist[0]
 
 
+@pytest.mark.parametrize("kind,n,max_coarse", [("poisson3d", 24, 100), ("aniso3d", 20, 300), ("poisson2d", 96, 200)])
+def test_pcg_matches_oracle(ctx, kind, n, max_coarse):
+    """SPEC §S8: same iteration count, iterates within 1e-8 (dots are reductions)."""
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, kind, n)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse))
+    S = AMGSolver(ctx, H)
+    b = PVector(ctx, S.A[0].nrows)
+    mul(b, S.A[0], PVector(ctx, S.A[0].nrows, 0, xs[0]))
+    Ao = O.generate(kind, *O.grid_shape(kind, n))
+    bo = O.spmv(Ao, O.xstar(Ao.nrows))
+    Ho = O.setup(Ao, max_coarse=max_coarse)
+    xo, ko, ho = Ho.pcg(bo, 1e-10, 60)
+    x = S.new_vector()
+    k, h = S.pcg(x, b, 1e-10, 60)
+    assert k == ko and k < 30
+    np.testing.assert_allclose(h, ho, rtol=1e-6)
+    xg = x.own_values()
+    assert np.linalg.norm(xg - xo) <= 1e-8 * np.linalg.norm(xo)
+    assert np.linalg.norm(xg - xs[0]) <= 1e-8 * np.linalg.norm(xs[0])
+
+
 def test_graph_equals_eager(ctx):
     be = pa.SequentialBackend(1)
     A, offs, xs = pa.generate_problem(be, "poisson3d", 20)
