@@ -133,21 +133,52 @@ int pamg_gen_grid(int kind, int64_t nx, int64_t ny, int64_t nz, double eps, int6
     double d = 4.0, vxy = -1.0, vz = -1.0;
     if (kind == 1) d = 6.0;
     if (kind == 2) { d = 4.0 + 2.0 * eps; vz = -eps; }
-    const int64_t pxy = nx * ny;
+    const int64_t pxy = nx * ny, m = r1 - r0;
     try {
-        return build_rows(r1 - r0, n, out, [&]() {
-            return [&](int64_t i, std::vector<int32_t>& C, std::vector<double>& V) {
-                const int64_t r = r0 + i, x = r % nx, y = (r / nx) % ny, z = r / pxy;
-                if (z > 0) { C.push_back((int32_t)(r - pxy)); V.push_back(vz); }
-                if (y > 0) { C.push_back((int32_t)(r - nx)); V.push_back(vxy); }
-                if (x > 0) { C.push_back((int32_t)(r - 1)); V.push_back(vxy); }
-                C.push_back((int32_t)r); V.push_back(d);
-                if (x < nx - 1) { C.push_back((int32_t)(r + 1)); V.push_back(vxy); }
-                if (y < ny - 1) { C.push_back((int32_t)(r + nx)); V.push_back(vxy); }
-                if (z < nz - 1) { C.push_back((int32_t)(r + pxy)); V.push_back(vz); }
-                return true;
-            };
-        });
+        // two passes straight into the final arrays: closed-form row lengths, then fill
+        auto M = std::make_unique<pamg_hcsr>();
+        M->nr = m;
+        M->nc = n;
+        M->rp.assign(m + 1, 0);
+        auto row_len = [&](int64_t r) {
+            const int64_t x = r % nx, y = (r / nx) % ny, z = r / pxy;
+            return (int64_t)1 + (z > 0) + (y > 0) + (x > 0) + (x < nx - 1) + (y < ny - 1) + (z < nz - 1);
+        };
+        const int nt = std::max(1, omp_get_max_threads());
+        std::vector<int64_t> part(nt + 1, 0);
+#pragma omp parallel num_threads(nt)
+        {
+            const int t = omp_get_thread_num();
+            const int64_t lo = m * t / nt, hi = m * (t + 1) / nt;
+            int64_t s = 0;
+            for (int64_t i = lo; i < hi; ++i) {
+                s += row_len(r0 + i);
+                M->rp[i + 1] = s;
+            }
+            part[t + 1] = s;
+#pragma omp barrier
+#pragma omp single
+            for (int u = 0; u < nt; ++u) part[u + 1] += part[u];
+            for (int64_t i = lo; i < hi; ++i) M->rp[i + 1] += part[t];
+        }
+        M->col.resize(M->rp[m]);
+        M->val.resize(M->rp[m]);
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < m; ++i) {
+            const int64_t r = r0 + i, x = r % nx, y = (r / nx) % ny, z = r / pxy;
+            int64_t k = M->rp[i];
+            int32_t* C = M->col.data();
+            double* V = M->val.data();
+            if (z > 0) { C[k] = (int32_t)(r - pxy); V[k++] = vz; }
+            if (y > 0) { C[k] = (int32_t)(r - nx); V[k++] = vxy; }
+            if (x > 0) { C[k] = (int32_t)(r - 1); V[k++] = vxy; }
+            C[k] = (int32_t)r; V[k++] = d;
+            if (x < nx - 1) { C[k] = (int32_t)(r + 1); V[k++] = vxy; }
+            if (y < ny - 1) { C[k] = (int32_t)(r + nx); V[k++] = vxy; }
+            if (z < nz - 1) { C[k] = (int32_t)(r + pxy); V[k++] = vz; }
+        }
+        *out = M.release();
+        return PAMG_OK;
     } catch (...) {
         return fail(PAMG_E_NOMEM, "gen_grid: out of host memory");
     }
@@ -327,14 +358,23 @@ int pamg_setup_spgemm(const pamg_hcsr* X, int64_t y0, const pamg_hcsr* Yown,
                         }
                     }
                 }
-                std::vector<int32_t> order(L.size());
-                for (size_t t = 0; t < L.size(); ++t) order[t] = (int32_t)t;
-                std::sort(order.begin(), order.end(), [&](int32_t u, int32_t v) { return L[u] < L[v]; });
-                for (int32_t t : order) {
-                    C.push_back(L[t]);
-                    V.push_back(S[t]);
+                // output in column order; P[j] still indexes column j's accumulator
+                const size_t m = L.size();
+                if (m <= 32) {
+                    for (size_t u = 1; u < m; ++u) {
+                        const int32_t v = L[u];
+                        size_t w = u;
+                        for (; w > 0 && L[w - 1] > v; --w) L[w] = L[w - 1];
+                        L[w] = v;
+                    }
+                } else {
+                    std::sort(L.begin(), L.end());
                 }
-                for (int32_t j : L) P[j] = -1;
+                for (int32_t j : L) {
+                    C.push_back(j);
+                    V.push_back(S[P[j]]);
+                    P[j] = -1;
+                }
                 return true;
             };
         });
