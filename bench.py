@@ -41,7 +41,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--grid", type=int, default=512, help="grid points per side")
-    ap.add_argument("--kind", default="poisson3d", choices=["poisson2d", "poisson3d", "aniso3d"])
+    ap.add_argument("--kind", default="poisson3d",
+                    choices=["poisson2d", "poisson3d", "aniso3d", "elastic3d"])
+    ap.add_argument("--matrix", default=None,
+                    help="Matrix Market file (e.g. SuiteSparse Flan_1565.mtx) instead of --kind")
     ap.add_argument("--max-coarse", type=int, default=1000)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
@@ -85,7 +88,12 @@ def main():
                 dist.barrier()
 
     t0 = time.time()
-    A, offs, xs = pa.generate_problem(be, args.kind, args.grid)
+    if args.matrix:
+        A, offs, xs = pa.load_problem(be, args.matrix)
+        workload = f"{os.path.basename(args.matrix)} ({int(offs[-1])} rows) fp64"
+    else:
+        A, offs, xs = pa.generate_problem(be, args.kind, args.grid)
+        workload = f"{args.kind} {args.grid}^{2 if args.kind == 'poisson2d' else 3} fp64"
     H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=args.max_coarse), log=log)
     t_setup = time.time() - t0
     log(f"setup {t_setup:.1f}s, {H.nlevels} levels")
@@ -149,7 +157,8 @@ def main():
     # workload (tools/pmc_traffic.py; counters cannot be read from inside the process)
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "r01_pmc", "traffic_jacobi_512.json")
-    if args.kind == "poisson3d" and args.grid == 512 and world == 1 and os.path.exists(pmc):
+    if (not args.matrix and args.kind == "poisson3d" and args.grid == 512 and world == 1
+            and os.path.exists(pmc)):
         rec = json.load(open(pmc))
         if rec:
             traffic, traffic_src = float(rec[0]["traffic_bytes"]), os.path.relpath(pmc, ROOT)
@@ -170,7 +179,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (SPEC.md §S2 grid operator, b = A x*, x0 = 0)",
             "config": {
-                "workload": f"{args.kind} {args.grid}^3 fp64, SA-AMG V(1,1) weighted-Jacobi, "
+                "workload": f"{workload}, SA-AMG V(1,1) weighted-Jacobi, "
                             f"{world} part(s)",
                 "n": gl_rows, "nnz_fine": int(sum(H.levels[0][p].A.nnz for p in H.levels[0])) if world == 1
                 else None, "levels": S.L, "max_coarse": args.max_coarse,

@@ -160,6 +160,10 @@ int pamg_hcsr_data(pamg_hcsr* M, int64_t** rowptr, int32_t** col, double** val);
 int pamg_gen_grid(int kind, int64_t nx, int64_t ny, int64_t nz, double eps, int64_t r0,
                   int64_t r1, pamg_hcsr** out);
 int pamg_gen_xstar(int64_t i0, int64_t n, uint64_t seed, double* out);
+/* Rows [r0, r1) (r1 < 0: all) of a square Matrix Market coordinate file (real / integer /
+ * pattern, general / symmetric), 1-based on disk, returned 0-based with ascending columns;
+ * duplicates are summed in file order (BASELINE.json configs[4], SuiteSparse Flan_1565). */
+int pamg_read_mtx(const char* path, int64_t r0, int64_t r1, int64_t* n_global, pamg_hcsr** out);
 /* Gershgorin bound over own rows; A's rows are global rows row0.. (diagonal at col row0+i). */
 int pamg_setup_gershgorin(const pamg_hcsr* A, int64_t row0, double* rho);
 /* Decoupled standard aggregation (SPEC §S4.2-3): agg[i] local aggregate id or -1. */

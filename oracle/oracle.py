@@ -17,7 +17,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "libpamg_oracle.so")
 SEED = 20240807
-KINDS = {"poisson2d": 0, "poisson3d": 1, "aniso3d": 2}
+KINDS = {"poisson2d": 0, "poisson3d": 1, "aniso3d": 2, "elastic3d": 3}
 
 _i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
 _f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
@@ -95,7 +95,7 @@ def grid_shape(kind: str, n: int):
 def generate(kind: str, nx: int, ny: int, nz: int, eps: float = 1e-3, r0: int = 0, r1=None) -> CSR:
     """Rows [r0, r1) of the SPEC §S2 grid operator (global column ids)."""
     L = lib()
-    n = nx * ny * nz
+    n = nx * ny * nz * (3 if kind == "elastic3d" else 1)
     r1 = n if r1 is None else r1
     k = KINDS[kind]
     nnz = L.orc_gen_rows(k, nx, ny, nz, eps, r0, r1, None, None, None)

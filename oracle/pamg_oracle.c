@@ -50,8 +50,34 @@ static void stencil_vals(int kind, double eps, double* diag, double* vxy, double
 
 /* Rows [r0, r1) of the grid operator; rowptr relative (rowptr[0] = 0), global col ids.
  * Returns nnz written. Pass col == NULL to count only. */
+/* kind 3 = elastic3d (SPEC §S2): 3 unknowns per node of an nx*ny*nz grid, row 3*node+d,
+ * A = L27 (x) B with L27 the 27-point Dirichlet Laplacian (26 / -1) and B = 4I - J (3x3). */
+static i64 gen_elastic(i64 nx, i64 ny, i64 nz, i64 r0, i64 r1, i64* rowptr, i64* col, double* val) {
+    i64 k = 0;
+    if (rowptr) rowptr[0] = 0;
+    for (i64 r = r0; r < r1; ++r) {
+        const i64 node = r / 3, d = r % 3;
+        const i64 x = node % nx, y = (node / nx) % ny, z = node / (nx * ny);
+        for (int dz = -1; dz <= 1; ++dz)
+            for (int dy = -1; dy <= 1; ++dy)
+                for (int dx = -1; dx <= 1; ++dx) {
+                    const i64 X = x + dx, Y = y + dy, Z = z + dz;
+                    if (X < 0 || Y < 0 || Z < 0 || X >= nx || Y >= ny || Z >= nz) continue;
+                    const i64 m = X + nx * (Y + ny * Z);
+                    const double l = (m == node) ? 26.0 : -1.0;
+                    for (int e = 0; e < 3; ++e) {
+                        if (col) { col[k] = 3 * m + e; val[k] = l * ((e == d) ? 3.0 : -1.0); }
+                        ++k;
+                    }
+                }
+        if (rowptr) rowptr[r - r0 + 1] = k;
+    }
+    return k;
+}
+
 i64 orc_gen_rows(int kind, i64 nx, i64 ny, i64 nz, double eps, i64 r0, i64 r1,
                  i64* rowptr, i64* col, double* val) {
+    if (kind == 3) return gen_elastic(nx, ny, nz, r0, r1, rowptr, col, val);
     double d, vxy, vz;
     stencil_vals(kind, eps, &d, &vxy, &vz);
     const i64 pxy = nx * ny;

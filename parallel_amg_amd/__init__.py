@@ -6,7 +6,7 @@ kernels for SpMV / residual / weighted Jacobi / restriction / prolongation, RCCL
 exchange, and a host smoothed-aggregation setup.
 """
 from .backend import DistributedBackend, SequentialBackend  # noqa: F401
-from .hierarchy import SAParams, build_hierarchy, generate_problem  # noqa: F401
+from .hierarchy import SAParams, build_hierarchy, generate_problem, load_problem  # noqa: F401
 
 __all__ = ["SequentialBackend", "DistributedBackend", "SAParams", "build_hierarchy",
-           "generate_problem"]
+           "generate_problem", "load_problem"]

@@ -1,0 +1,124 @@
+// mtx.cpp — Matrix Market reader for the "SuiteSparse Flan_1565" configuration
+// (BASELINE.json configs[4]) and any other SPD matrix handed to the solver as a file.
+//
+// Reads `%%MatrixMarket matrix coordinate {real|integer|pattern} {general|symmetric}` and
+// returns the rows [r0, r1) as host CSR (SPEC §S1: 0-based, columns ascending; duplicate
+// (i, j) entries are summed in file order; symmetric files are expanded, the mirrored entry
+// of (i, j, v) being (j, i, v)). Each rank of a partitioned run reads only its own rows'
+// entries. The file is memory-mapped and parsed without locale-dependent stdio.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "pamg_common.h"
+
+using pamg::fail;
+
+namespace {
+
+struct Mapped {
+    const char* p = nullptr;
+    size_t n = 0;
+    int fd = -1;
+    ~Mapped() {
+        if (p) munmap(const_cast<char*>(p), n);
+        if (fd >= 0) close(fd);
+    }
+};
+
+inline const char* skip_ws(const char* s, const char* e) {
+    while (s < e && (*s == ' ' || *s == '\t' || *s == '\r')) ++s;
+    return s;
+}
+
+inline const char* next_line(const char* s, const char* e) {
+    while (s < e && *s != '\n') ++s;
+    return s < e ? s + 1 : e;
+}
+
+struct Entry {
+    int64_t r, c;
+    double v;
+    int64_t seq;  // file order (for duplicate summation)
+};
+
+}  // namespace
+
+extern "C" int pamg_read_mtx(const char* path, int64_t r0, int64_t r1, int64_t* n_global,
+                             pamg_hcsr** out) {
+    if (!path || !out) return fail(PAMG_E_ARG, "read_mtx: bad args");
+    Mapped m;
+    m.fd = open(path, O_RDONLY);
+    if (m.fd < 0) return fail(PAMG_E_ARG, "read_mtx: cannot open %s", path);
+    struct stat st;
+    if (fstat(m.fd, &st) != 0 || st.st_size == 0) return fail(PAMG_E_ARG, "read_mtx: empty file %s", path);
+    m.n = (size_t)st.st_size;
+    void* mp = mmap(nullptr, m.n, PROT_READ, MAP_PRIVATE, m.fd, 0);
+    if (mp == MAP_FAILED) return fail(PAMG_E_NOMEM, "read_mtx: mmap failed");
+    m.p = static_cast<const char*>(mp);
+    const char *s = m.p, *e = m.p + m.n;
+
+    // banner
+    std::string banner(s, next_line(s, e) - s);
+    for (auto& ch : banner) ch = (char)std::tolower((unsigned char)ch);
+    if (banner.rfind("%%matrixmarket", 0) != 0 || banner.find("coordinate") == std::string::npos)
+        return fail(PAMG_E_ARG, "read_mtx: only '%%%%MatrixMarket matrix coordinate' files are supported");
+    const bool pattern = banner.find("pattern") != std::string::npos;
+    const bool symmetric = banner.find("symmetric") != std::string::npos;
+    if (banner.find("complex") != std::string::npos || banner.find("hermitian") != std::string::npos ||
+        banner.find("skew") != std::string::npos)
+        return fail(PAMG_E_ARG, "read_mtx: complex / hermitian / skew-symmetric files are not supported");
+    s = next_line(s, e);
+    while (s < e && (*s == '%' || *s == '\n')) s = next_line(s, e);
+    char* q = nullptr;
+    const long long nr = std::strtoll(s, &q, 10);
+    const long long nc = std::strtoll(q, &q, 10);
+    const long long nz = std::strtoll(q, &q, 10);
+    if (nr <= 0 || nc != nr || nz < 0) return fail(PAMG_E_ARG, "read_mtx: need a square matrix (got %lld x %lld)", nr, nc);
+    if (nr >= INT32_MAX) return fail(PAMG_E_OVERFLOW, "read_mtx: n >= 2^31");
+    if (r1 < 0) r1 = nr;
+    if (r0 < 0 || r1 > nr || r0 > r1) return fail(PAMG_E_ARG, "read_mtx: bad row range");
+    s = next_line(q, e);
+
+    std::vector<Entry> ent;
+    int64_t seq = 0;
+    for (long long k = 0; k < nz; ++k) {
+        s = skip_ws(s, e);
+        if (s >= e) return fail(PAMG_E_ARG, "read_mtx: file ends after %lld of %lld entries", k, nz);
+        const long long i = std::strtoll(s, &q, 10) - 1;
+        const long long j = std::strtoll(q, &q, 10) - 1;
+        const double v = pattern ? 1.0 : std::strtod(q, &q);
+        if (i < 0 || i >= nr || j < 0 || j >= nc) return fail(PAMG_E_ARG, "read_mtx: entry %lld out of range", k + 1);
+        if (i >= r0 && i < r1) ent.push_back({i, j, v, seq++});
+        if (symmetric && i != j && j >= r0 && j < r1) ent.push_back({j, i, v, seq++});
+        s = next_line(q, e);
+    }
+    std::sort(ent.begin(), ent.end(), [](const Entry& a, const Entry& b) {
+        return a.r != b.r ? a.r < b.r : (a.c != b.c ? a.c < b.c : a.seq < b.seq);
+    });
+    auto M = std::make_unique<pamg_hcsr>();
+    M->nr = r1 - r0;
+    M->nc = nr;
+    M->rp.assign(M->nr + 1, 0);
+    for (size_t t = 0; t < ent.size(); ++t) {
+        if (t > 0 && ent[t].r == ent[t - 1].r && ent[t].c == ent[t - 1].c) {
+            M->val.back() = M->val.back() + ent[t].v;  // duplicates: summed in file order
+            continue;
+        }
+        M->col.push_back((int32_t)ent[t].c);
+        M->val.push_back(ent[t].v);
+        M->rp[ent[t].r - r0 + 1]++;
+    }
+    for (int64_t i = 0; i < M->nr; ++i) M->rp[i + 1] += M->rp[i];
+    if (n_global) *n_global = nr;
+    *out = M.release();
+    return PAMG_OK;
+}

@@ -81,6 +81,37 @@ int build_rows(int64_t nr, int64_t nc, pamg_hcsr** out, RowFn&& fill_factory) {
     return PAMG_OK;
 }
 
+// SPEC §S2 elastic3d: 3 unknowns per node (row 3*node + d), A = L27 (x) (4I - J); the
+// Flan_1565 stand-in (BASELINE.json configs[4]: ~73-81 nonzeros per row, SPD).
+int gen_elastic(int64_t nx, int64_t ny, int64_t nz, int64_t r0, int64_t r1, pamg_hcsr** out) {
+    const int64_t n = 3 * nx * ny * nz;
+    if (r0 < 0 || r1 > n || r0 > r1) return fail(PAMG_E_ARG, "gen_grid: bad row range");
+    if (n >= (int64_t)INT32_MAX) return fail(PAMG_E_OVERFLOW, "gen_grid: n >= 2^31");
+    try {
+        return build_rows(r1 - r0, n, out, [&]() {
+            return [&](int64_t i, std::vector<int32_t>& C, std::vector<double>& V) {
+                const int64_t r = r0 + i, node = r / 3, d = r % 3;
+                const int64_t x = node % nx, y = (node / nx) % ny, z = node / (nx * ny);
+                for (int dz = -1; dz <= 1; ++dz)
+                    for (int dy = -1; dy <= 1; ++dy)
+                        for (int dx = -1; dx <= 1; ++dx) {
+                            const int64_t X = x + dx, Y = y + dy, Z = z + dz;
+                            if (X < 0 || Y < 0 || Z < 0 || X >= nx || Y >= ny || Z >= nz) continue;
+                            const int64_t m = X + nx * (Y + ny * Z);
+                            const double l = (m == node) ? 26.0 : -1.0;
+                            for (int e = 0; e < 3; ++e) {
+                                C.push_back((int32_t)(3 * m + e));
+                                V.push_back(l * ((e == d) ? 3.0 : -1.0));
+                            }
+                        }
+                return true;
+            };
+        });
+    } catch (...) {
+        return fail(PAMG_E_NOMEM, "gen_grid: out of host memory");
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -125,8 +156,9 @@ int pamg_hcsr_data(pamg_hcsr* M, int64_t** rowptr, int32_t** col, double** val) 
 // SPEC §S2. Row entries in ascending column order: z-, y-, x-, diag, x+, y+, z+.
 int pamg_gen_grid(int kind, int64_t nx, int64_t ny, int64_t nz, double eps, int64_t r0,
                   int64_t r1, pamg_hcsr** out) {
-    if (!out || nx < 1 || ny < 1 || nz < 1 || kind < 0 || kind > 2)
+    if (!out || nx < 1 || ny < 1 || nz < 1 || kind < 0 || kind > 3)
         return fail(PAMG_E_ARG, "gen_grid: bad args");
+    if (kind == 3) return gen_elastic(nx, ny, nz, r0, r1, out);
     const int64_t n = nx * ny * nz;
     if (r0 < 0 || r1 > n || r0 > r1) return fail(PAMG_E_ARG, "gen_grid: bad row range");
     if (n >= (int64_t)INT32_MAX) return fail(PAMG_E_OVERFLOW, "gen_grid: n >= 2^31");

@@ -81,6 +81,14 @@ def gen_grid(kind: int, nx: int, ny: int, nz: int, eps: float, r0: int, r1: int)
     return HCSR(h)
 
 
+def read_mtx(path: str, r0: int = 0, r1: int = -1):
+    """Rows [r0, r1) of a Matrix Market file -> (HCSR, n_global)."""
+    h = C.c_void_p()
+    n = C.c_int64()
+    call("pamg_read_mtx", str(path).encode(), r0, r1, C.byref(n), C.byref(h))
+    return HCSR(h), n.value
+
+
 def gen_xstar(i0: int, n: int, seed: int) -> np.ndarray:
     out = np.empty(n, np.float64)
     call("pamg_gen_xstar", i0, n, seed, ptr(out))

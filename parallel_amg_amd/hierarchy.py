@@ -15,7 +15,7 @@ import numpy as np
 from . import hcsr as H
 from .hcsr import HCSR
 
-KIND = {"poisson2d": 0, "poisson3d": 1, "aniso3d": 2}
+KIND = {"poisson2d": 0, "poisson3d": 1, "aniso3d": 2, "elastic3d": 3}
 SEED = 20240807
 
 
@@ -155,9 +155,21 @@ def generate_problem(backend, kind: str, n: int, eps: float = 1e-3):
     Returns (A_parts, offsets, xstar_parts). b is formed by the caller's SpMV (device, §S3),
     or with ``spmv_host`` for CPU use."""
     nx, ny, nz = (n, n, 1) if kind == "poisson2d" else (n, n, n)
-    N = nx * ny * nz
+    N = nx * ny * nz * (3 if kind == "elastic3d" else 1)
     offs = np.array([(p * N) // backend.nparts for p in range(backend.nparts + 1)], np.int64)
     A = {p: H.gen_grid(KIND[kind], nx, ny, nz, eps, int(offs[p]), int(offs[p + 1])) for p in backend.parts}
+    xs = {p: H.gen_xstar(int(offs[p]), int(offs[p + 1] - offs[p]), SEED) for p in backend.parts}
+    return A, offs, xs
+
+
+def load_problem(backend, path: str):
+    """Partitioned rows of a Matrix Market matrix (pamg_read_mtx; BASELINE.json configs[4],
+    SuiteSparse Flan_1565) and the SPEC §S2 synthetic solution x* for b = A x*. Each part reads
+    only its own rows; the partition is the uniform row partition of SPEC §S7."""
+    head = H.read_mtx(path, 0, 0)
+    N = head[1]
+    offs = np.array([(p * N) // backend.nparts for p in range(backend.nparts + 1)], np.int64)
+    A = {p: H.read_mtx(path, int(offs[p]), int(offs[p + 1]))[0] for p in backend.parts}
     xs = {p: H.gen_xstar(int(offs[p]), int(offs[p + 1] - offs[p]), SEED) for p in backend.parts}
     return A, offs, xs
 

@@ -142,7 +142,8 @@ def test_shape_errors_raise(ctx):
         mul(y, A, x)
 
 
-CONFIGS = [("poisson2d", 64, 300), ("poisson3d", 24, 100), ("aniso3d", 20, 300), ("poisson3d", 12, 1000)]
+CONFIGS = [("poisson2d", 64, 300), ("poisson3d", 24, 100), ("aniso3d", 20, 300), ("poisson3d", 12, 1000),
+           ("elastic3d", 10, 200)]
 
 
 @pytest.mark.parametrize("kind,n,max_coarse", CONFIGS)
