@@ -1,0 +1,86 @@
+"""Full-size checks (BASELINE.json sizes) through properties that need no oracle run:
+
+* 512^3 fine matrix (the metric's workload): A*1 on the GPU equals the exact integer row sums
+  6 - (#neighbours) for all 134M rows; A*x* matches the host's SPEC §S3 row sums on sampled rows.
+* 256^3 hierarchy: a V-cycle is linear and scaling by 2 is exact in binary floating point, so
+  V(2x, 2b) must equal 2 V(x, b) bit for bit; two runs are bit-identical (determinism); the
+  residual falls every cycle; graph replay equals eager launches.
+"""
+import numpy as np
+import pytest
+
+import parallel_amg_amd as pa
+from parallel_amg_amd.partitioned import PSparseMatrix, PVector, axpby, mul
+from parallel_amg_amd.solver import AMGSolver
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.asarray(a, np.float64).view(np.int64)
+
+
+def test_fine_512_rowsums(ctx):
+    n = 512
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", n)
+    A0 = A[0]
+    assert A0.nnz == 937_951_232
+    D = PSparseMatrix(ctx, A0)
+    N = A0.nrows
+    ones = PVector(ctx, N, 0, np.ones(N))
+    y = PVector(ctx, N)
+    mul(y, D, ones)
+    got = y.own_values()
+    cnt = np.diff(A0.rowptr)                 # 1 + #neighbours
+    assert np.array_equal(got, 6.0 - (cnt - 1).astype(np.float64))
+    # A x* on sampled rows against the SPEC row sum computed on the host
+    x = PVector(ctx, N, 0, xs[0])
+    mul(y, D, x)
+    got = y.own_values()
+    rng = np.random.default_rng(1)
+    for i in rng.integers(0, N, 2000):
+        s = 0.0
+        for k in range(A0.rowptr[i], A0.rowptr[i + 1]):
+            s = s + A0.val[k] * xs[0][A0.col[k]]
+        assert got[i] == s
+
+
+@pytest.fixture(scope="module")
+def h256(ctx):
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 256)
+    H = pa.build_hierarchy(be, A, offs)
+    S = AMGSolver(ctx, H)
+    b = PVector(ctx, S.A[0].nrows)
+    mul(b, S.A[0], PVector(ctx, S.A[0].nrows, 0, xs[0]))
+    return S, b
+
+
+def test_vcycle_scaling_by_two_is_exact(ctx, h256):
+    S, b = h256
+    n = S.A[0].nrows
+    rng = np.random.default_rng(7)
+    x0 = rng.standard_normal(n)
+    x1 = PVector(ctx, n, 0, x0)
+    S.vcycle(x1, b, 2)
+    b2 = PVector(ctx, n)
+    axpby(2.0, b, 0.0, b2)                   # exact: 2*b + 0*b2
+    x2 = PVector(ctx, n, 0, 2.0 * x0)
+    S.vcycle(x2, b2, 2)
+    assert np.array_equal(bits(x2.own_values()), bits(2.0 * x1.own_values()))
+
+
+def test_vcycle_deterministic_and_converging(ctx, h256):
+    S, b = h256
+    out = []
+    for graph in (True, False, True):
+        S.set_graph(graph)
+        x = S.new_vector()
+        hist = S.vcycle(x, b, 4, res_hist=True)
+        out.append((x.own_values(), hist))
+        assert np.all(np.diff(hist) < 0)
+    S.set_graph(True)
+    assert np.array_equal(bits(out[0][0]), bits(out[1][0]))
+    assert np.array_equal(bits(out[0][0]), bits(out[2][0]))
+    np.testing.assert_array_equal(out[0][1], out[2][1])
