@@ -100,7 +100,8 @@ def main():
 
     ctx = Context(dev, be, transport=args.transport)
     # hipGraph replay on one part; multi-part cycles run eagerly (RCCL + host-side exchange)
-    S = AMGSolver(ctx, H, part=rank, graph=(not args.no_graph) and world == 1)
+    use_graph = (not args.no_graph) and (world == 1 or args.transport == "rccl")
+    S = AMGSolver(ctx, H, part=rank, graph=use_graph)
     A0 = S.A[0]
     xst = PVector(ctx, A0.n_own_cols, A0.n_ghost, xs[rank])
     b = PVector(ctx, A0.nrows)
@@ -109,6 +110,19 @@ def main():
     del xst
     t_upload = time.time() - t0 - t_setup
     log(f"upload {t_upload:.1f}s")
+
+    # ---- multi-part graph self-check: graph replay (RCCL captured) and eager launches must
+    # give the same bits on every rank, else the timed run uses eager launches
+    if use_graph and world > 1:
+        xa, xb = S.new_vector(), S.new_vector()
+        S.vcycle(xa, b, 2)
+        S.set_graph(False)
+        S.vcycle(xb, b, 2)
+        same = bool(np.array_equal(xa.own_values().view(np.int64), xb.own_values().view(np.int64)))
+        ok = be.allreduce_max({rank: 0.0 if same else 1.0}) == 0.0
+        S.set_graph(ok)
+        del xa, xb
+        log(f"multi-part graph self-check: {'ok' if ok else 'MISMATCH -> eager'}")
 
     # ---- warmup + timed region -------------------------------------------------------
     if args.warmup:
@@ -184,7 +198,7 @@ def main():
                 "n": gl_rows, "nnz_fine": int(sum(H.levels[0][p].A.nnz for p in H.levels[0])) if world == 1
                 else None, "levels": S.L, "max_coarse": args.max_coarse,
                 "parallelism": f"row-slab partition p{world} (RCCL ghost exchange)",
-                "graph": (not args.no_graph) and world == 1,
+                "graph": S.graph_state(),
                 "transport": args.transport if world > 1 else None,
             },
             "fine_spmv_GBps": round(spmv_gbps, 1),

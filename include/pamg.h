@@ -122,8 +122,12 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
                      const double* ainv_colmajor, const int64_t* coarse_offsets,
                      pamg_hier** out);
 int pamg_hier_destroy(pamg_hier* H);
-/* 1 = replay the V-cycle as a captured hipGraph (default 1 on one part), 0 = eager launches. */
+/* 1 = replay the V-cycle as a captured hipGraph (default 1 on one part and with RCCL; the
+ * host debug transport cannot be captured), 0 = eager launches. A failed capture falls back
+ * to eager launches (same RCCL sequence) and is reported on stderr. */
 int pamg_hier_set_graph(pamg_hier* H, int enable);
+/* enabled: graph replay currently on; captured: a graph exists; failed: a capture failed. */
+int pamg_hier_graph_state(const pamg_hier* H, int* enabled, int* captured, int* failed);
 /* x <- V(x) ncycles times (SPEC §S6); res_hist (ncycles, may be NULL) gets ||b - A x||. */
 int pamg_vcycle(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles,
                 double* res_hist);

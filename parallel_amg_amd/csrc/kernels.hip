@@ -110,16 +110,16 @@ __device__ __forceinline__ T stream_load(const T* p, std::false_type) {
     return *p;
 }
 
-template <int OP, int TNNZ, int TROWS, bool XCD, bool NT = false>
-__global__ __launch_bounds__(kBlock) void k_rows_tile2(
+template <int OP, int TNNZ, int TROWS, bool XCD, bool NT = false, int BS = kBlock>
+__global__ __launch_bounds__(BS) void k_rows_tile2(
     const int4* __restrict__ tiles, int ntiles, const int* __restrict__ rowptr,
     const int* __restrict__ col, const double* __restrict__ val, const double* __restrict__ x,
     const double* __restrict__ b, double* __restrict__ y, double omega,
     const double* __restrict__ diag) {
     // diag != nullptr (Jacobi only): a_ii from the stored diagonal instead of the in-tile
     // detection (same value, SPEC §S3; trades 8 B/row of reads for one barrier).
-    constexpr int G = TNNZ / (4 * kBlock);
-    static_assert(G >= 1 && TNNZ % (4 * kBlock) == 0, "tile budget must be a multiple of 1024");
+    constexpr int G = TNNZ / (4 * BS);
+    static_assert(G >= 1 && TNNZ % (4 * BS) == 0, "tile budget must be a multiple of 4 x block");
     __shared__ __attribute__((aligned(16))) double lprod[TNNZ + 8];
     __shared__ int lrp[TROWS + 1];
     __shared__ double ldiag[OP == OP_JACOBI ? TROWS : 1];
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     double2 va[G], vb[G];
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-        const int g = za + 4 * (tid + j * kBlock);
+        const int g = za + 4 * (tid + j * BS);
         const int gs = g < z1 ? g : za;  // clamp: never read past the (padded) arrays
         // NT: the once-read matrix stream goes non-temporal so the x lines (reused by the
         // z+-1 / y+-1 neighbour rows) keep their place in the XCD's L2
@@ -148,10 +148,10 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
         va[j] = stream_load(reinterpret_cast<const double2*>(val + gs), nt{});
         vb[j] = stream_load(reinterpret_cast<const double2*>(val + gs + 2), nt{});
     }
-    for (int i = tid; i <= nr; i += kBlock) lrp[i] = rowptr[r0 + i];
+    for (int i = tid; i <= nr; i += BS) lrp[i] = rowptr[r0 + i];
     // one row per lane: fetch the epilogue's own-row operands (b, old x, y, a_ii) now, so
     // their latency hides under the column stream instead of trailing the LDS phase
-    constexpr bool ONE_ROW = TROWS <= kBlock;
+    constexpr bool ONE_ROW = TROWS <= BS;
     double pb = 0.0, px = 0.0, py = 0.0, pd = 0.0;
     if constexpr (ONE_ROW) {
         if (tid < nr) {
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     double xv[G][4];
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-        const int g = za + 4 * (tid + j * kBlock);
+        const int g = za + 4 * (tid + j * BS);
         const int cc[4] = {c4[j].x, c4[j].y, c4[j].z, c4[j].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     }
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-        const int g = za + 4 * (tid + j * kBlock);
+        const int g = za + 4 * (tid + j * BS);
         const int cc[4] = {c4[j].x, c4[j].y, c4[j].z, c4[j].w};
         const double vv[4] = {va[j].x, va[j].y, vb[j].x, vb[j].y};
         double p[4];
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
             }
         }
     } else {
-        for (int rr = tid; rr < nr; rr += kBlock) {
+        for (int rr = tid; rr < nr; rr += BS) {
             const int kb = lrp[rr] - za, ke = lrp[rr + 1] - za;
             double s = 0.0;
             for (int k = kb; k < ke; ++k) s = s + lprod[k];
@@ -537,6 +537,14 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
         } else if (A.rows_kernel == 0 && ts.tile_nnz == kTileNnz && ts.tile_rows == kTileRows) {
             k_rows_tile<OP><<<ts.n_short, kBlock, 0, s>>>(ts.d_short, A.d_rowptr, A.d_col,
                                                           A.d_val, x, b, y, omega);
+        } else if (ts.tile_nnz == 512 && ts.tile_rows == 128) {
+            const double* dg = (OP == OP_JACOBI && A.jacobi_diag) ? A.d_diag : nullptr;
+            k_rows_tile2<OP, 512, 128, false, false, 128><<<ts.n_short, 128, 0, s>>>(
+                ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg);
+        } else if (ts.tile_nnz == 2048 && ts.tile_rows == 512) {
+            const double* dg = (OP == OP_JACOBI && A.jacobi_diag) ? A.d_diag : nullptr;
+            k_rows_tile2<OP, 2048, 512, false, false, 512><<<ts.n_short, 512, 0, s>>>(
+                ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg);
         } else if (ts.tile_nnz == 1024) {
             launch_tile2<OP, 1024, 256>(A, ts, x, b, y, omega, s);
         } else if (ts.tile_nnz == 4096 && ts.tile_rows == 512) {

@@ -247,6 +247,7 @@ struct pamg_hier {
     const double* g_x = nullptr;
     const double* g_b = nullptr;
     bool g_zero0 = false;
+    bool graph_failed = false;
     // PCG workspace (level-0 layout, allocated on first use)
     double *pcg_r = nullptr, *pcg_z = nullptr, *pcg_p = nullptr, *pcg_q = nullptr;
     // profiling
@@ -776,7 +777,9 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
     auto H = std::make_unique<pamg_hier>();
     H->ctx = ctx;
     H->L = nlevels;
-    H->use_graph = ctx->nranks == 1;
+    // graph replay on one part and on RCCL multi-part runs (RCCL captures its p2p and
+    // collectives); never with the host debug transport (host callbacks)
+    H->use_graph = ctx->nranks == 1 || (ctx->comm != nullptr && !ctx->host_fn);
     const int L = nlevels;
     H->A.assign(A, A + L);
     H->P.assign(L, nullptr);
@@ -884,6 +887,14 @@ int pamg_hier_set_graph(pamg_hier* H, int enable) {
     return PAMG_OK;
 }
 
+int pamg_hier_graph_state(const pamg_hier* H, int* enabled, int* captured, int* failed) {
+    if (!H) return fail(PAMG_E_ARG, "hier_graph_state: NULL");
+    if (enabled) *enabled = H->use_graph ? 1 : 0;
+    if (captured) *captured = H->gexec ? 1 : 0;
+    if (failed) *failed = H->graph_failed ? 1 : 0;
+    return PAMG_OK;
+}
+
 int pamg_hier_profile(pamg_hier* H, int enable) {
     if (!H) return fail(PAMG_E_ARG, "hier_profile: NULL");
     H->prof = enable != 0;
@@ -912,21 +923,37 @@ int pamg_hier_profile_read(pamg_hier* H, double* out) {
 static int vcycle_raw(pamg_hier* H, double* x, const double* b, int ncycles, bool zero0) {
     pamg_ctx* ctx = H->ctx;
     if (zero0 && ncycles != 1) return fail(PAMG_E_ARG, "vcycle: zero initial guess applies to one cycle");
-    if (H->use_graph && !H->prof) {
-        if (!H->gexec || H->g_x != x || H->g_b != b || H->g_zero0 != zero0) {
-            drop_graph(H);
-            hipGraph_t g;
-            HIPC(hipStreamBeginCapture(ctx->s_comp, hipStreamCaptureModeThreadLocal));
-            int rc = vcycle_enqueue(H, x, b, zero0);
+    if (H->use_graph && !H->prof && (!H->gexec || H->g_x != x || H->g_b != b || H->g_zero0 != zero0)) {
+        // Capture one cycle (RCCL exchanges included on several parts: RCCL records its
+        // send/recv/all-gather as graph nodes). If capture fails, fall back to eager launches
+        // for this hierarchy: both paths issue the same RCCL sequence, so ranks that did
+        // capture and ranks that did not still match.
+        drop_graph(H);
+        hipGraph_t g = nullptr;
+        int rc = PAMG_OK;
+        hipError_t e1 = hipStreamBeginCapture(ctx->s_comp, hipStreamCaptureModeThreadLocal);
+        if (e1 == hipSuccess) {
+            rc = vcycle_enqueue(H, x, b, zero0);
             hipError_t e2 = hipStreamEndCapture(ctx->s_comp, &g);
-            if (rc != PAMG_OK) return rc;
-            if (e2 != hipSuccess) return fail(PAMG_E_HIP, "vcycle: capture failed: %s", hipGetErrorString(e2));
-            HIPC(hipGraphInstantiate(&H->gexec, g, nullptr, nullptr, 0));
-            (void)hipGraphDestroy(g);
-            H->g_x = x;
-            H->g_b = b;
-            H->g_zero0 = zero0;
+            if (rc == PAMG_OK && e2 == hipSuccess && g &&
+                hipGraphInstantiate(&H->gexec, g, nullptr, nullptr, 0) == hipSuccess) {
+                H->g_x = x;
+                H->g_b = b;
+                H->g_zero0 = zero0;
+            } else {
+                H->gexec = nullptr;
+            }
+            if (g) (void)hipGraphDestroy(g);
         }
+        if (!H->gexec) {
+            (void)hipGetLastError();
+            H->use_graph = false;
+            H->graph_failed = true;
+            fprintf(stderr, "[pamg] V-cycle graph capture failed (%s); using eager launches\n",
+                    pamg::last_error().c_str());
+        }
+    }
+    if (H->use_graph && !H->prof && H->gexec) {
         for (int k = 0; k < ncycles; ++k) HIPC(hipGraphLaunch(H->gexec, ctx->s_comp));
     } else {
         for (int k = 0; k < ncycles; ++k) CHECK(vcycle_enqueue(H, x, b, zero0 && k == 0));
@@ -1043,7 +1070,7 @@ int pamg_set_option(const char* key, int64_t value) {
     if (k == "rows_kernel" && value >= 0 && value <= 2) o.rows_kernel = (int)value;
     else if (k == "tile_nnz" && (value == 256 || value == 512 || value == 1024 || value == 2048 || value == 4096))
         o.tile_nnz = (int)value;
-    else if (k == "tile_rows" && (value == 64 || value == 256 || value == 512)) o.tile_rows = (int)value;
+    else if (k == "tile_rows" && (value == 64 || value == 128 || value == 256 || value == 512)) o.tile_rows = (int)value;
     else if (k == "xcd_remap" && (value == 0 || value == 1)) o.xcd_remap = (int)value;
     else if (k == "jacobi_diag" && (value == 0 || value == 1)) o.jacobi_diag = (int)value;
     else if (k == "stream_nt" && (value == 0 || value == 1)) o.stream_nt = (int)value;
@@ -1057,7 +1084,9 @@ static int check_tile_options(const pamg::Options& o) {
     const int k = o.rows_kernel, n = o.tile_nnz, r = o.tile_rows;
     bool ok = false;
     if (k == 0) ok = (n == 2048 && r == 256);
-    if (k == 1) ok = (r == 256 && (n == 1024 || n == 2048 || n == 4096)) || (r == 512 && n == 4096);
+    if (k == 1)
+        ok = (r == 256 && (n == 1024 || n == 2048 || n == 4096)) || (r == 512 && (n == 2048 || n == 4096)) ||
+             (r == 128 && n == 512);
     if (k == 2) ok = (r == 64 && (n == 256 || n == 512 || n == 1024));
     if (!ok)
         return fail(PAMG_E_ARG, "options: rows_kernel %d has no instance for tile_nnz %d / tile_rows %d",

@@ -51,6 +51,11 @@ class AMGSolver:
     def set_graph(self, enable: bool):
         call("pamg_hier_set_graph", self._h, int(bool(enable)))
 
+    def graph_state(self) -> dict:
+        e, c, f = C.c_int(), C.c_int(), C.c_int()
+        call("pamg_hier_graph_state", self._h, C.byref(e), C.byref(c), C.byref(f))
+        return {"enabled": bool(e.value), "captured": bool(c.value), "failed": bool(f.value)}
+
     def new_vector(self) -> PVector:
         """A level-0 vector with room for the fine-level ghosts."""
         return self.A[0].new_input_vector()
