@@ -45,6 +45,8 @@ def main():
                     choices=["poisson2d", "poisson3d", "aniso3d", "elastic3d"])
     ap.add_argument("--matrix", default=None,
                     help="Matrix Market file (e.g. SuiteSparse Flan_1565.mtx) instead of --kind")
+    ap.add_argument("--partition", choices=["uniform", "nnz"], default="uniform",
+                    help="row partition of a --matrix over N GPUs (SPEC §S7)")
     ap.add_argument("--max-coarse", type=int, default=1000)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
@@ -89,7 +91,7 @@ def main():
 
     t0 = time.time()
     if args.matrix:
-        A, offs, xs = pa.load_problem(be, args.matrix)
+        A, offs, xs = pa.load_problem(be, args.matrix, partition=args.partition)
         workload = f"{os.path.basename(args.matrix)} ({int(offs[-1])} rows) fp64"
     else:
         A, offs, xs = pa.generate_problem(be, args.kind, args.grid)

@@ -168,6 +168,9 @@ int pamg_gen_xstar(int64_t i0, int64_t n, uint64_t seed, double* out);
  * pattern, general / symmetric), 1-based on disk, returned 0-based with ascending columns;
  * duplicates are summed in file order (BASELINE.json configs[4], SuiteSparse Flan_1565). */
 int pamg_read_mtx(const char* path, int64_t r0, int64_t r1, int64_t* n_global, pamg_hcsr** out);
+/* Entries per row of a Matrix Market file (symmetric mirrored): weights for the nnz-balanced
+ * row partition (SPEC §S7). counts may be NULL to query *n_global only. */
+int pamg_mtx_row_counts(const char* path, int64_t* n_global, int64_t* counts);
 /* Gershgorin bound over own rows; A's rows are global rows row0.. (diagonal at col row0+i). */
 int pamg_setup_gershgorin(const pamg_hcsr* A, int64_t row0, double* rho);
 /* Decoupled standard aggregation (SPEC §S4.2-3): agg[i] local aggregate id or -1. */

@@ -174,10 +174,12 @@ class Hierarchy:
 
 
 def setup(A: CSR, nparts: int = 1, theta: float = 0.02, max_levels: int = 20,
-          max_coarse: int = 1000) -> Hierarchy:
-    """SPEC §S4-§S5 smoothed-aggregation setup (global view, decoupled by parts)."""
+          max_coarse: int = 1000, offsets=None) -> Hierarchy:
+    """SPEC §S4-§S5 smoothed-aggregation setup (global view, decoupled by parts; `offsets`
+    overrides the uniform partition of SPEC §S7)."""
     L = lib()
-    offs = uniform_offsets(A.nrows, nparts)
+    offs = uniform_offsets(A.nrows, nparts) if offsets is None else np.asarray(offsets, np.int64)
+    nparts = len(offs) - 1
     h = L.orc_setup(A.nrows, A.rowptr, A.col, A.val, nparts, offs, theta, max_levels, max_coarse)
     H = Hierarchy(_h=h)
     if L.orc_status(h) != 0:

@@ -52,6 +52,48 @@ struct Entry {
 
 }  // namespace
 
+// Entries per row after symmetric expansion (duplicates counted separately): the weights of
+// the nnz-balanced partition (SPEC §S7). counts == NULL: only *n_global is returned.
+extern "C" int pamg_mtx_row_counts(const char* path, int64_t* n_global, int64_t* counts) {
+    if (!path || !n_global) return fail(PAMG_E_ARG, "mtx_row_counts: bad args");
+    Mapped m;
+    m.fd = open(path, O_RDONLY);
+    if (m.fd < 0) return fail(PAMG_E_ARG, "mtx_row_counts: cannot open %s", path);
+    struct stat st;
+    if (fstat(m.fd, &st) != 0 || st.st_size == 0) return fail(PAMG_E_ARG, "mtx_row_counts: empty file");
+    m.n = (size_t)st.st_size;
+    void* mp = mmap(nullptr, m.n, PROT_READ, MAP_PRIVATE, m.fd, 0);
+    if (mp == MAP_FAILED) return fail(PAMG_E_NOMEM, "mtx_row_counts: mmap failed");
+    m.p = static_cast<const char*>(mp);
+    const char *s = m.p, *e = m.p + m.n;
+    std::string banner(s, next_line(s, e) - s);
+    for (auto& ch : banner) ch = (char)std::tolower((unsigned char)ch);
+    if (banner.rfind("%%matrixmarket", 0) != 0 || banner.find("coordinate") == std::string::npos)
+        return fail(PAMG_E_ARG, "mtx_row_counts: not a coordinate Matrix Market file");
+    const bool symmetric = banner.find("symmetric") != std::string::npos;
+    s = next_line(s, e);
+    while (s < e && (*s == '%' || *s == '\n')) s = next_line(s, e);
+    char* q = nullptr;
+    const long long nr = std::strtoll(s, &q, 10);
+    (void)std::strtoll(q, &q, 10);
+    const long long nz = std::strtoll(q, &q, 10);
+    if (nr <= 0) return fail(PAMG_E_ARG, "mtx_row_counts: bad size line");
+    *n_global = nr;
+    if (!counts) return PAMG_OK;
+    std::fill(counts, counts + nr, 0);
+    s = next_line(q, e);
+    for (long long k = 0; k < nz && s < e; ++k) {
+        s = skip_ws(s, e);
+        const long long i = std::strtoll(s, &q, 10) - 1;
+        const long long j = std::strtoll(q, &q, 10) - 1;
+        if (i < 0 || i >= nr || j < 0 || j >= nr) return fail(PAMG_E_ARG, "mtx_row_counts: entry out of range");
+        counts[i]++;
+        if (symmetric && i != j) counts[j]++;
+        s = next_line(q, e);
+    }
+    return PAMG_OK;
+}
+
 extern "C" int pamg_read_mtx(const char* path, int64_t r0, int64_t r1, int64_t* n_global,
                              pamg_hcsr** out) {
     if (!path || !out) return fail(PAMG_E_ARG, "read_mtx: bad args");

@@ -89,6 +89,14 @@ def read_mtx(path: str, r0: int = 0, r1: int = -1):
     return HCSR(h), n.value
 
 
+def mtx_row_counts(path: str) -> np.ndarray:
+    n = C.c_int64()
+    call("pamg_mtx_row_counts", str(path).encode(), C.byref(n), None)
+    out = np.zeros(n.value, np.int64)
+    call("pamg_mtx_row_counts", str(path).encode(), C.byref(n), ptr(out))
+    return out
+
+
 def gen_xstar(i0: int, n: int, seed: int) -> np.ndarray:
     out = np.empty(n, np.float64)
     call("pamg_gen_xstar", i0, n, seed, ptr(out))

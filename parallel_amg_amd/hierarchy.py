@@ -162,13 +162,28 @@ def generate_problem(backend, kind: str, n: int, eps: float = 1e-3):
     return A, offs, xs
 
 
-def load_problem(backend, path: str):
+def balanced_offsets(row_counts: np.ndarray, nparts: int) -> np.ndarray:
+    """SPEC §S7 nnz-balanced partition: o_p = first row r with sum_{i<r} len_i >= floor(p*nnz/P)."""
+    pre = np.zeros(len(row_counts) + 1, np.int64)
+    np.cumsum(row_counts, out=pre[1:])
+    tot = int(pre[-1])
+    targets = np.array([(p * tot) // nparts for p in range(nparts + 1)], np.int64)
+    offs = np.searchsorted(pre, targets, side="left").astype(np.int64)
+    offs[0], offs[-1] = 0, len(row_counts)
+    return offs
+
+
+def load_problem(backend, path: str, partition: str = "uniform"):
     """Partitioned rows of a Matrix Market matrix (pamg_read_mtx; BASELINE.json configs[4],
     SuiteSparse Flan_1565) and the SPEC §S2 synthetic solution x* for b = A x*. Each part reads
-    only its own rows; the partition is the uniform row partition of SPEC §S7."""
+    only its own rows; the partition is SPEC §S7's uniform one, or nnz-balanced
+    (``partition="nnz"``: equal nonzeros per part, for matrices with irregular rows)."""
     head = H.read_mtx(path, 0, 0)
     N = head[1]
-    offs = np.array([(p * N) // backend.nparts for p in range(backend.nparts + 1)], np.int64)
+    if partition == "nnz" and backend.nparts > 1:
+        offs = balanced_offsets(H.mtx_row_counts(path), backend.nparts)
+    else:
+        offs = np.array([(p * N) // backend.nparts for p in range(backend.nparts + 1)], np.int64)
     A = {p: H.read_mtx(path, int(offs[p]), int(offs[p + 1]))[0] for p in backend.parts}
     xs = {p: H.gen_xstar(int(offs[p]), int(offs[p + 1] - offs[p]), SEED) for p in backend.parts}
     return A, offs, xs

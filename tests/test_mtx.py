@@ -73,6 +73,39 @@ def test_elastic_generator_and_setup_bit_exact(built):
         assert np.array_equal(bits(full), bits(Ho.A[l].val))
 
 
+def _irregular_spd(seed=0):
+    rng = np.random.default_rng(seed)
+    A = O.generate("poisson2d", 40, 40, 1).to_scipy().tolil()
+    for i in range(200):  # a dense-ish corner: rows 0..199 get ~40 extra couplings
+        for j in rng.choice(200, 40, replace=False):
+            if j != i:
+                A[i, j] = A[j, i] = -0.01
+    A = A.tocsr()
+    A.setdiag(A.diagonal() + abs(A).sum(axis=1).A1)   # strictly diagonally dominant -> SPD
+    A.sort_indices()
+    return A
+
+
+def test_nnz_balanced_partition(tmp_path, built):
+    A = _irregular_spd()
+    path = _write(tmp_path, A.tocoo(), "irr.mtx", "symmetric")
+    counts = HC.mtx_row_counts(path)
+    assert np.array_equal(counts, np.diff(A.indptr))
+    be = pa.SequentialBackend(3)
+    Ap, offs, xs = pa.load_problem(be, path, partition="nnz")
+    per = [Ap[p].nnz for p in range(3)]
+    assert max(per) - min(per) <= max(np.diff(A.indptr)) + 2      # balanced to one row
+    assert offs[1] < A.shape[0] // 3                              # the dense corner is split off
+    H = pa.build_hierarchy(be, Ap, offs, pa.SAParams(max_coarse=50))
+    Ao = O.CSR(A.indptr.astype(np.int64), A.indices.astype(np.int64), A.data.copy(), A.shape[1])
+    Ho = O.setup(Ao, offsets=offs, max_coarse=50)
+    assert H.nlevels == Ho.nlevels
+    for l in range(H.nlevels):
+        full = np.concatenate([H.levels[l][p].A.val for p in range(3)])
+        assert np.array_equal(bits(full), bits(Ho.A[l].val))
+        assert np.array_equal(H.offsets(l), Ho.offsets[l])
+
+
 def test_load_problem_partitions_like_the_generator(tmp_path, built):
     Ao = O.generate("poisson3d", 6, 6, 6)
     path = _write(tmp_path, Ao.to_scipy().tocoo(), "p.mtx", "symmetric")
