@@ -232,6 +232,123 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
     }
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops (lgkmcnt), NOT for
+// its outstanding global loads (no vmcnt), so a prefetch issued before it stays in flight.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Variant 3: variant 1's tile body in a persistent grid. Block b walks tiles b, b+G, b+2G, ...
+// (G = grid, a multiple of 8, so a block stays on one XCD's slice of the banded tile order)
+// and issues the NEXT tile's descriptor-driven column/value stream right after the current
+// tile's x gathers, so the HBM stream of tile t+1 overlaps the LDS sum / epilogue of tile t.
+// Barriers are LDS-only (lds_barrier) so the prefetch is never drained by a __syncthreads().
+template <int OP, int TNNZ, int TROWS>
+__global__ __launch_bounds__(kBlock) void k_rows_pers(
+    const int4* __restrict__ tiles, int ntiles, const int* __restrict__ rowptr,
+    const int* __restrict__ col, const double* __restrict__ val, const double* __restrict__ x,
+    const double* __restrict__ b, double* __restrict__ y, double omega) {
+    constexpr int G = TNNZ / (4 * kBlock);
+    static_assert(G >= 1 && TROWS <= kBlock, "one row per lane");
+    __shared__ __attribute__((aligned(16))) double lprod[TNNZ + 8];
+    __shared__ int lrp[TROWS + 1];
+    __shared__ double ldiag[OP == OP_JACOBI ? TROWS : 1];
+    const int tid = threadIdx.x;
+    int t = blockIdx.x;
+    if (t >= ntiles) return;
+    int4 d = tiles[t];
+    int4 c4[G];
+    double2 va[G], vb[G];
+    auto load = [&](const int4& dd) {
+        const int za = dd.z & ~3;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int g = za + 4 * (tid + j * kBlock);
+            const int gs = g < dd.w ? g : za;
+            c4[j] = *reinterpret_cast<const int4*>(col + gs);
+            va[j] = *reinterpret_cast<const double2*>(val + gs);
+            vb[j] = *reinterpret_cast<const double2*>(val + gs + 2);
+        }
+    };
+    load(d);
+    for (; t < ntiles; t += gridDim.x) {
+        const int r0 = d.x, nr = d.y - d.x, z0 = d.z, z1 = d.w, za = z0 & ~3;
+        int4 cc4[G];
+        double2 ca[G], cb[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            cc4[j] = c4[j];
+            ca[j] = va[j];
+            cb[j] = vb[j];
+        }
+        for (int i = tid; i <= nr; i += kBlock) lrp[i] = rowptr[r0 + i];
+        double pb = 0.0, px = 0.0, py = 0.0;
+        if (tid < nr) {
+            const int r = r0 + tid;
+            if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[r];
+            if constexpr (OP == OP_JACOBI) px = x[r];
+            if constexpr (OP == OP_PROLONG) py = y[r];
+        }
+        double xv[G][4];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int g = za + 4 * (tid + j * kBlock);
+            const int cc[4] = {cc4[j].x, cc4[j].y, cc4[j].z, cc4[j].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool ok = (g + e >= z0) & (g + e < z1);
+                xv[j][e] = x[ok ? cc[e] : 0];
+            }
+        }
+        // prefetch the next tile's stream behind the gathers (counted vmcnt keeps it in flight)
+        const int tn = t + gridDim.x;
+        if (tn < ntiles) {
+            d = tiles[tn];
+            load(d);
+        }
+        lds_barrier();  // lrp visible (and the previous tile's phase 2 is done with lprod)
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int g = za + 4 * (tid + j * kBlock);
+            const int cc[4] = {cc4[j].x, cc4[j].y, cc4[j].z, cc4[j].w};
+            const double vv[4] = {ca[j].x, ca[j].y, cb[j].x, cb[j].y};
+            double p[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = g + e;
+                const bool ok = (k >= z0) & (k < z1);
+                p[e] = ok ? vv[e] * xv[j][e] : 0.0;
+                if constexpr (OP == OP_JACOBI) {
+                    const int rl = cc[e] - r0;
+                    if (ok && rl >= 0 && rl < nr && k >= lrp[rl] && k < lrp[rl + 1]) ldiag[rl] = vv[e];
+                }
+            }
+            *reinterpret_cast<double2*>(&lprod[g - za]) = make_double2(p[0], p[1]);
+            *reinterpret_cast<double2*>(&lprod[g - za + 2]) = make_double2(p[2], p[3]);
+        }
+        lds_barrier();
+        if (tid < nr) {
+            const int kb = lrp[tid] - za, ke = lrp[tid + 1] - za;
+            double s = 0.0;
+            for (int k = kb; k < ke; ++k) s = s + lprod[k];
+            const int r = r0 + tid;
+            if constexpr (OP == OP_SPMV) {
+                y[r] = s;
+            } else if constexpr (OP == OP_RESID) {
+                y[r] = pb - s;
+            } else if constexpr (OP == OP_JACOBI) {
+                const double u = pb - s;
+                const double v = omega * u;
+                const double w = v / ldiag[tid];
+                y[r] = px + w;
+            } else {
+                y[r] = py + s;
+            }
+        }
+        lds_barrier();  // phase 2 done before the next tile rewrites lrp / lprod / ldiag
+    }
+}
+
 // Variant 2: wave tiles (<= 64 rows, <= WNNZ nonzeros) walked by a persistent grid, each wave
 // keeping the NEXT tile's column/value stream in flight (registers) while it gathers, sums and
 // stores the current one. No workgroup barrier anywhere: every wave owns an LDS slice; the
@@ -526,11 +643,31 @@ void launch_wave(const pamg_mat& A, const TileSet& ts, const double* x, const do
                                                   A.d_val, x, b, y, omega, dg);
 }
 
+template <int OP, int TNNZ, int TROWS>
+void launch_pers(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
+                 double* y, double omega, hipStream_t s) {
+    static int grid_cap = 0;  // resident blocks on the chip, a multiple of 8 (XCDs)
+    if (grid_cap == 0) {
+        int nb = 0, dev = 0, ncu = 256;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rows_pers<OP, TNNZ, TROWS>, kBlock, 0);
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        grid_cap = ((nb > 0 ? nb : 1) * ncu) & ~7;
+        if (grid_cap < 8) grid_cap = 8;
+    }
+    const int grid = ts.n_short < grid_cap ? ts.n_short : grid_cap;
+    k_rows_pers<OP, TNNZ, TROWS><<<grid, kBlock, 0, s>>>(ts.d_short, ts.n_short, A.d_rowptr,
+                                                        A.d_col, A.d_val, x, b, y, omega);
+}
+
 template <int OP>
 void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
                     double* y, double omega, hipStream_t s) {
     if (ts.n_short > 0) {
-        if (A.rows_kernel == 2) {
+        if (A.rows_kernel == 3) {
+            if (ts.tile_nnz == 2048) launch_pers<OP, 2048, 256>(A, ts, x, b, y, omega, s);
+            else launch_pers<OP, 1024, 256>(A, ts, x, b, y, omega, s);
+        } else if (A.rows_kernel == 2) {
             if (ts.tile_nnz == 256) launch_wave<OP, 256>(A, ts, x, b, y, omega, s);
             else if (ts.tile_nnz == 1024) launch_wave<OP, 1024>(A, ts, x, b, y, omega, s);
             else launch_wave<OP, 512>(A, ts, x, b, y, omega, s);

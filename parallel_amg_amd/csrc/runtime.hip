@@ -1067,7 +1067,7 @@ int pamg_set_option(const char* key, int64_t value) {
     if (!key) return fail(PAMG_E_ARG, "set_option: NULL key");
     auto& o = pamg::options();
     const std::string k(key);
-    if (k == "rows_kernel" && value >= 0 && value <= 2) o.rows_kernel = (int)value;
+    if (k == "rows_kernel" && value >= 0 && value <= 3) o.rows_kernel = (int)value;
     else if (k == "tile_nnz" && (value == 256 || value == 512 || value == 1024 || value == 2048 || value == 4096))
         o.tile_nnz = (int)value;
     else if (k == "tile_rows" && (value == 64 || value == 128 || value == 256 || value == 512)) o.tile_rows = (int)value;
@@ -1088,6 +1088,7 @@ static int check_tile_options(const pamg::Options& o) {
         ok = (r == 256 && (n == 1024 || n == 2048 || n == 4096)) || (r == 512 && (n == 2048 || n == 4096)) ||
              (r == 128 && n == 512);
     if (k == 2) ok = (r == 64 && (n == 256 || n == 512 || n == 1024));
+    if (k == 3) ok = (r == 256 && (n == 1024 || n == 2048));
     if (!ok)
         return fail(PAMG_E_ARG, "options: rows_kernel %d has no instance for tile_nnz %d / tile_rows %d",
                     k, n, r);

@@ -57,7 +57,8 @@ LENGTHS = {
 TILE_CONFIGS = [(0, 2048, 256, 0, 0, 0, 0), (1, 2048, 256, 0, 0, 0, 0), (1, 2048, 256, 1, 1, 0, 0),
                 (1, 1024, 256, 0, 0, 0, 0), (1, 1024, 256, 0, 0, 1, 1), (1, 4096, 256, 0, 0, 1, 0),
                 (1, 4096, 512, 1, 0, 0, 0), (2, 256, 64, 0, 0, 0, 0), (2, 512, 64, 0, 0, 0, 1),
-                (2, 512, 64, 0, 1, 0, 0), (2, 1024, 64, 0, 0, 0, 0)]
+                (2, 512, 64, 0, 1, 0, 0), (2, 1024, 64, 0, 0, 0, 0), (3, 1024, 256, 0, 0, 0, 1),
+                (3, 2048, 256, 0, 0, 0, 0), (1, 512, 128, 0, 0, 0, 1), (1, 2048, 512, 0, 0, 0, 1)]
 OPT_KEYS = ("rows_kernel", "tile_nnz", "tile_rows", "xcd_remap", "jacobi_diag", "stream_nt", "tile_order")
 
 
