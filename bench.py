@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--cpu-cycles", type=int, default=1)
     ap.add_argument("--transport", choices=["rccl", "host"], default="rccl",
                     help="host = debug transport (ranks may share one GPU; not a perf mode)")
+    ap.add_argument("--setup", choices=["gpu", "host"], default="gpu",
+                    help="where the Galerkin products of the setup run (same bits either way)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -89,6 +91,7 @@ def main():
             else:
                 dist.barrier()
 
+    ctx = Context(dev, be, transport=args.transport)
     t0 = time.time()
     if args.matrix:
         A, offs, xs = pa.load_problem(be, args.matrix, partition=args.partition)
@@ -96,11 +99,11 @@ def main():
     else:
         A, offs, xs = pa.generate_problem(be, args.kind, args.grid)
         workload = f"{args.kind} {args.grid}^{2 if args.kind == 'poisson2d' else 3} fp64"
-    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=args.max_coarse), log=log)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=args.max_coarse), log=log,
+                           device=ctx if args.setup == "gpu" else None)
     t_setup = time.time() - t0
-    log(f"setup {t_setup:.1f}s, {H.nlevels} levels")
+    log(f"setup {t_setup:.1f}s ({args.setup} products), {H.nlevels} levels")
 
-    ctx = Context(dev, be, transport=args.transport)
     # hipGraph replay on one part; multi-part cycles run eagerly (RCCL + host-side exchange)
     use_graph = (not args.no_graph) and (world == 1 or args.transport == "rccl")
     S = AMGSolver(ctx, H, part=rank, graph=use_graph)
@@ -214,6 +217,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "setup_s": round(t_setup, 1),
+            "setup_products": args.setup,
             "final_residual": float(hist[0]),
         }
         print(json.dumps(out), flush=True)

@@ -191,6 +191,14 @@ int pamg_setup_smooth(const pamg_hcsr* A, int64_t row0, const pamg_hcsr* T, pamg
  * rows = coarse ids c0..c1-1, columns = global fine ids, ascending (SPEC §S4.7). */
 int pamg_setup_transpose(const pamg_hcsr* P, int64_t row0, int64_t c0, int64_t c1,
                          pamg_hcsr** out);
+/* GPU-side setup products: the contracts of pamg_setup_spgemm and
+ * pamg_setup_transpose above, bit-identical results, computed on ctx's GPU (host CSR in and
+ * out; device memory is released before returning). */
+int pamg_dev_spgemm(pamg_ctx* ctx, const pamg_hcsr* X, int64_t y0, const pamg_hcsr* Yown,
+                    const int64_t* ghost_ids, int64_t n_ghost, const pamg_hcsr* Yghost,
+                    pamg_hcsr** out);
+int pamg_dev_transpose(pamg_ctx* ctx, const pamg_hcsr* P, int64_t row0, int64_t c0, int64_t c1,
+                       pamg_hcsr** out);
 /* Row-wise concatenation of k CSR pieces with equal row counts (part order = column order). */
 int pamg_setup_hstack_rows(int k, const pamg_hcsr* const* pieces, pamg_hcsr** out);
 /* Dense Cholesky inverse of a full (single-piece) matrix, column-major out (SPEC §S5). */

@@ -87,6 +87,8 @@ SIGNATURES = {
     "pamg_setup_spgemm": [vp, i64, vp, vp, i64, vp, pvp],
     "pamg_setup_smooth": [vp, i64, vp, vp, dbl],
     "pamg_setup_transpose": [vp, i64, i64, i64, pvp],
+    "pamg_dev_spgemm": [vp, vp, i64, vp, vp, i64, vp, pvp],
+    "pamg_dev_transpose": [vp, vp, i64, i64, i64, pvp],
     "pamg_setup_hstack_rows": [i32, vp, pvp],
     "pamg_setup_cholinv": [vp, vp],
 }

@@ -123,13 +123,17 @@ def tentative(agg: np.ndarray, n_agg: int, coarse0: int, ncols_global: int) -> H
     return HCSR(h)
 
 
-def spgemm(X: HCSR, y0: int, Yown: HCSR, ghost_ids=None, Yghost: HCSR | None = None) -> HCSR:
+def spgemm(X: HCSR, y0: int, Yown: HCSR, ghost_ids=None, Yghost: HCSR | None = None,
+           device=None) -> HCSR:
+    """C = X * Y (SPEC §S4.5). ``device``: a partitioned.Context -> the GPU routine
+    (pamg_dev_spgemm, same result bit for bit), else the host one."""
     h = C.c_void_p()
+    fn, pre = ("pamg_dev_spgemm", (device.handle,)) if device is not None else ("pamg_setup_spgemm", ())
     if ghost_ids is None or len(ghost_ids) == 0:
-        call("pamg_setup_spgemm", X.handle, y0, Yown.handle, None, 0, None, C.byref(h))
+        call(fn, *pre, X.handle, y0, Yown.handle, None, 0, None, C.byref(h))
     else:
         g = np.ascontiguousarray(ghost_ids, np.int64)
-        call("pamg_setup_spgemm", X.handle, y0, Yown.handle, ptr(g), len(g), Yghost.handle, C.byref(h))
+        call(fn, *pre, X.handle, y0, Yown.handle, ptr(g), len(g), Yghost.handle, C.byref(h))
     return HCSR(h)
 
 
@@ -138,9 +142,12 @@ def smooth(A: HCSR, row0: int, T: HCSR, AT: HCSR, omega: float) -> HCSR:
     return AT
 
 
-def transpose(P: HCSR, row0: int, c0: int, c1: int) -> HCSR:
+def transpose(P: HCSR, row0: int, c0: int, c1: int, device=None) -> HCSR:
     h = C.c_void_p()
-    call("pamg_setup_transpose", P.handle, row0, c0, c1, C.byref(h))
+    if device is not None:
+        call("pamg_dev_transpose", device.handle, P.handle, row0, c0, c1, C.byref(h))
+    else:
+        call("pamg_setup_transpose", P.handle, row0, c0, c1, C.byref(h))
     return HCSR(h)
 
 

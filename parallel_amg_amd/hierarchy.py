@@ -190,8 +190,13 @@ def load_problem(backend, path: str, partition: str = "uniform"):
 
 
 def build_hierarchy(backend, A: dict, offsets: np.ndarray, params: SAParams = SAParams(),
-                    log=None) -> HostHierarchy:
-    """SPEC §S4: levels until n <= max_coarse / max_levels / stalled coarsening."""
+                    log=None, device=None) -> HostHierarchy:
+    """SPEC §S4: levels until n <= max_coarse / max_levels / stalled coarsening.
+
+    ``device`` (a partitioned.Context): the Galerkin products (A T, A P, R (A P)) and the
+    transposes run on that GPU (spgemm.hip, SURVEY §8f-4) — bit-identical to the host routines;
+    strength, aggregation and the coarsest inverse stay on the host (§8f-4)."""
+    dv = device
     parts = backend.parts
     offs = np.asarray(offsets, np.int64)
     levels = []
@@ -217,11 +222,11 @@ def build_hierarchy(backend, A: dict, offsets: np.ndarray, params: SAParams = SA
         Tg = fetch_rows(backend, planA, T)
         P = {}
         for p in parts:
-            AT = H.spgemm(A[p], int(offs[p]), T[p], planA[p].ghost_ids, Tg[p])
+            AT = H.spgemm(A[p], int(offs[p]), T[p], planA[p].ghost_ids, Tg[p], device=dv)
             P[p] = H.smooth(A[p], int(offs[p]), T[p], AT, omega)
         del T, Tg
         Pg = fetch_rows(backend, planA, P)
-        AP = {p: H.spgemm(A[p], int(offs[p]), P[p], planA[p].ghost_ids, Pg[p]) for p in parts}
+        AP = {p: H.spgemm(A[p], int(offs[p]), P[p], planA[p].ghost_ids, Pg[p], device=dv) for p in parts}
         del Pg
         # R = P^T: each part transposes its rows per coarse owner and ships the pieces
         pieces_local, sends = {}, {}
@@ -230,7 +235,7 @@ def build_hierarchy(backend, A: dict, offsets: np.ndarray, params: SAParams = SA
                   if backend.nparts > 1 else [p])
             sends[p] = {}
             for q in qs:
-                piece = H.transpose(P[p], int(offs[p]), int(coffs[q]), int(coffs[q + 1]))
+                piece = H.transpose(P[p], int(offs[p]), int(coffs[q]), int(coffs[q + 1]), device=dv)
                 if q == p:
                     pieces_local[p] = piece
                 else:
@@ -253,7 +258,7 @@ def build_hierarchy(backend, A: dict, offsets: np.ndarray, params: SAParams = SA
                    else np.zeros(0, np.int64)) for q in parts}
         planR = build_plans(backend, ghR, offs)
         APg = fetch_rows(backend, planR, AP)
-        Ac = {q: H.spgemm(R[q], int(offs[q]), AP[q], planR[q].ghost_ids, APg[q]) for q in parts}
+        Ac = {q: H.spgemm(R[q], int(offs[q]), AP[q], planR[q].ghost_ids, APg[q], device=dv) for q in parts}
         del AP, APg
         ghP = {p: (ghost_ids(P[p], int(coffs[p]), int(coffs[p + 1])) if backend.nparts > 1
                    else np.zeros(0, np.int64)) for p in parts}

@@ -1,0 +1,113 @@
+"""GPU-side setup (csrc/spgemm.hip): pamg_dev_spgemm / pamg_dev_transpose against
+the host routines of the same contract (setup.cpp, themselves pinned to the oracle by
+test_setup_cpu.py), bit for bit, and whole hierarchies built with the products on the GPU
+against the oracle's."""
+import numpy as np
+import pytest
+
+import parallel_amg_amd as pa
+from oracle import oracle as O
+from parallel_amg_amd import hcsr as HC
+from parallel_amg_amd._lib import PamgError
+from parallel_amg_amd.hcsr import HCSR
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.asarray(a, np.float64).view(np.int64)
+
+
+def rand_csr(rng, lengths, ncols, col0=0):
+    rp, cols, vals = [0], [], []
+    for m in lengths:
+        m = min(m, ncols)
+        c = np.sort(rng.choice(ncols, size=m, replace=False)) + col0
+        cols.append(c)
+        v = rng.standard_normal(m)
+        v[rng.random(m) < 0.05] = 0.0   # explicit zeros and -0.0 products too
+        vals.append(v)
+        rp.append(rp[-1] + m)
+    col = np.concatenate(cols).astype(np.int32) if cols else np.zeros(0, np.int32)
+    val = np.concatenate(vals) if vals else np.zeros(0)
+    return HCSR.from_arrays(np.asarray(rp, np.int64), col, val, ncols + col0)
+
+
+def same(A: HCSR, B: HCSR):
+    assert A.nrows == B.nrows
+    assert np.array_equal(A.rowptr, B.rowptr)
+    assert np.array_equal(A.col, B.col)
+    assert np.array_equal(bits(A.val), bits(B.val))
+
+
+CASES = {
+    # (X row lengths, Y row lengths, Y columns): small / LDS bins / capped bin / global overflow
+    "stencil": ([7] * 2000, [4] * 2500, 900),
+    "ragged": ([0, 1, 3, 30, 0, 120, 2, 600] * 40, [0, 2, 9, 1, 40, 5] * 60, 5000),
+    "wide_few_cols": ([900] * 20, [60] * 1000, 300),
+    "overflow": ([300] * 6 + [2] * 50, [50] * 400, 100_000),
+    "empty": ([], [3] * 10, 20),
+    "zero_nnz": ([0] * 30, [0] * 30, 10),
+}
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_dev_spgemm_bit_exact(ctx, case):
+    rng = np.random.default_rng(7)
+    xl, yl, ncy = CASES[case]
+    Y = rand_csr(rng, yl, ncy)
+    X = rand_csr(rng, xl, len(yl))
+    same(HC.spgemm(X, 0, Y, device=ctx), HC.spgemm(X, 0, Y))
+
+
+def test_dev_spgemm_ghost_rows(ctx):
+    """Y = own rows [y0, y0+n) plus ghost rows (the partitioned products of §S7)."""
+    rng = np.random.default_rng(8)
+    y0, n_own, ng_total = 500, 300, 1000
+    Yown = rand_csr(rng, rng.integers(0, 12, n_own), 4000)
+    gids = np.sort(rng.choice(np.r_[0:y0, y0 + n_own:ng_total + n_own], 200, replace=False)).astype(np.int64)
+    Yg = rand_csr(rng, rng.integers(0, 12, len(gids)), 4000)
+    cols = np.r_[np.arange(y0, y0 + n_own), gids]
+    rp, cc, vv = [0], [], []
+    for _ in range(400):
+        c = np.sort(rng.choice(cols, rng.integers(0, 25), replace=False))
+        cc.append(c)
+        vv.append(rng.standard_normal(len(c)))
+        rp.append(rp[-1] + len(c))
+    X = HCSR.from_arrays(np.asarray(rp, np.int64), np.concatenate(cc).astype(np.int32),
+                         np.concatenate(vv), ng_total + n_own)
+    same(HC.spgemm(X, y0, Yown, gids, Yg, device=ctx), HC.spgemm(X, y0, Yown, gids, Yg))
+    with pytest.raises(PamgError):   # a column that is neither own nor ghost
+        HC.spgemm(X, y0, Yown, gids[:10], HC.HCSR.from_arrays(Yg.rowptr[:11], Yg.col[:Yg.rowptr[10]],
+                                                               Yg.val[:Yg.rowptr[10]], 4000), device=ctx)
+
+
+@pytest.mark.parametrize("rng_cols", [(0, 700), (100, 350), (0, 0), (650, 700)])
+def test_dev_transpose_bit_exact(ctx, rng_cols):
+    rng = np.random.default_rng(9)
+    P = rand_csr(rng, rng.integers(0, 9, 3000), 700)
+    c0, c1 = rng_cols
+    same(HC.transpose(P, 1234, c0, c1, device=ctx), HC.transpose(P, 1234, c0, c1))
+
+
+@pytest.mark.parametrize("kind,n,nparts,max_coarse", [("poisson3d", 24, 1, 100), ("aniso3d", 20, 1, 300),
+                                                      ("elastic3d", 9, 1, 100), ("poisson3d", 16, 3, 60),
+                                                      ("poisson2d", 64, 2, 100)])
+def test_device_setup_matches_oracle(ctx, kind, n, nparts, max_coarse):
+    be = pa.SequentialBackend(nparts)
+    A, offs, _ = pa.generate_problem(be, kind, n)
+    params = pa.SAParams(max_coarse=max_coarse)
+    Hd = pa.build_hierarchy(be, A, offs, params, device=ctx)
+    Hh = pa.build_hierarchy(be, A, offs, params)
+    Ho = O.setup(O.generate(kind, *O.grid_shape(kind, n)), nparts=nparts, max_coarse=max_coarse)
+    assert Hd.nlevels == Hh.nlevels == Ho.nlevels
+    for l in range(Hd.nlevels):
+        for p in range(nparts):
+            d, h = Hd.levels[l][p], Hh.levels[l][p]
+            same(d.A, h.A)
+            if d.P is not None:
+                same(d.P, h.P)
+                same(d.R, h.R)
+        full = np.concatenate([Hd.levels[l][p].A.val for p in range(nparts)])
+        assert np.array_equal(bits(full), bits(Ho.A[l].val))
+    assert np.array_equal(bits(Hd.ainv), bits(Hh.ainv))
