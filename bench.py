@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--partition", choices=["uniform", "nnz"], default="uniform",
                     help="row partition of a --matrix over N GPUs (SPEC §S7)")
     ap.add_argument("--max-coarse", type=int, default=1000)
+    ap.add_argument("--agglomerate", type=int, default=32768,
+                    help="levels >= 1 with <= this many rows are one part, replicated (0: off)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-cycles", type=int, default=1)
@@ -99,7 +101,7 @@ def main():
     else:
         A, offs, xs = pa.generate_problem(be, args.kind, args.grid)
         workload = f"{args.kind} {args.grid}^{2 if args.kind == 'poisson2d' else 3} fp64"
-    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=args.max_coarse), log=log,
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=args.max_coarse, agglomerate=args.agglomerate), log=log,
                            device=ctx if args.setup == "gpu" else None)
     t_setup = time.time() - t0
     log(f"setup {t_setup:.1f}s ({args.setup} products), {H.nlevels} levels")
@@ -205,6 +207,8 @@ def main():
                 "parallelism": f"row-slab partition p{world} (RCCL ghost exchange)",
                 "graph": S.graph_state(),
                 "transport": args.transport if world > 1 else None,
+                # levels >= this one are held whole on every rank (SPEC §S7 agglomeration)
+                "replicated_from_level": int(S.rep_level) if world > 1 else None,
             },
             "fine_spmv_GBps": round(spmv_gbps, 1),
             "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),

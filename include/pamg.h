@@ -114,12 +114,17 @@ int pamg_jacobi(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec* b
 
 /* ------------------------------------------------------------------ hierarchy / V-cycle */
 /* Levels 0..nlevels-1; P[l], R[l] for l < nlevels-1 (NULL entries otherwise). The coarsest
- * level is solved with Ainv (column-major, n_coarse x n_coarse, SPEC §S5); coarse_offsets
- * (nranks+1 entries, NULL for one part) gives each rank's rows of the coarsest level.
+ * level is solved with Ainv (column-major, n_coarse x n_coarse, SPEC §S5).
+ * Several ranks: levels >= rep_level (1 <= rep_level <= nlevels-1) are held whole on every
+ * rank — the agglomerated tail of SPEC §S7, or just the coarsest level (rep_level =
+ * nlevels-1). R[rep_level-1] yields this rank's rows [rep_offsets[rank], rep_offsets[rank+1])
+ * of level rep_level, which are all-gathered; P[rep_level-1] and the tail's matrices read
+ * whole vectors (no plan). A[rep_level] is whole unless rep_level = nlevels-1. One rank:
+ * rep_level and rep_offsets are ignored (NULL allowed).
  * The hierarchy references (does not own) the matrices: keep them alive. */
 int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* const* P,
                      pamg_mat* const* R, const double* omega, int64_t n_coarse,
-                     const double* ainv_colmajor, const int64_t* coarse_offsets,
+                     const double* ainv_colmajor, int rep_level, const int64_t* rep_offsets,
                      pamg_hier** out);
 int pamg_hier_destroy(pamg_hier* H);
 /* 1 = replay the V-cycle as a captured hipGraph (default 1 on one part and with RCCL; the

@@ -43,7 +43,7 @@ def lib():
         L.orc_residual.argtypes = [i64, _i64p, _i64p, _f64p, _f64p, _f64p, _f64p]
         L.orc_jacobi.argtypes = [i64, _i64p, _i64p, _f64p, _f64p, _f64p, dbl, _f64p]
         L.orc_setup.restype = vp
-        L.orc_setup.argtypes = [i64, _i64p, _i64p, _f64p, C.c_int, _i64p, dbl, C.c_int, i64]
+        L.orc_setup.argtypes = [i64, _i64p, _i64p, _f64p, C.c_int, _i64p, dbl, C.c_int, i64, i64]
         L.orc_free.argtypes = [vp]
         L.orc_status.argtypes = [vp]
         L.orc_nlev.argtypes = [vp]
@@ -174,13 +174,15 @@ class Hierarchy:
 
 
 def setup(A: CSR, nparts: int = 1, theta: float = 0.02, max_levels: int = 20,
-          max_coarse: int = 1000, offsets=None) -> Hierarchy:
+          max_coarse: int = 1000, offsets=None, agglomerate: int = 32768) -> Hierarchy:
     """SPEC §S4-§S5 smoothed-aggregation setup (global view, decoupled by parts; `offsets`
-    overrides the uniform partition of SPEC §S7)."""
+    overrides the uniform partition of SPEC §S7; levels >= 1 with <= `agglomerate` rows are
+    one part, SPEC §S7 agglomeration — 0 disables it)."""
     L = lib()
     offs = uniform_offsets(A.nrows, nparts) if offsets is None else np.asarray(offsets, np.int64)
     nparts = len(offs) - 1
-    h = L.orc_setup(A.nrows, A.rowptr, A.col, A.val, nparts, offs, theta, max_levels, max_coarse)
+    h = L.orc_setup(A.nrows, A.rowptr, A.col, A.val, nparts, offs, theta, max_levels, max_coarse,
+                    agglomerate)
     H = Hierarchy(_h=h)
     if L.orc_status(h) != 0:
         raise RuntimeError("oracle setup: coarse Cholesky failed")

@@ -375,7 +375,8 @@ void orc_free(ohier* h) {
 
 /* Setup (§S4). offs: nparts+1 fine row offsets. */
 ohier* orc_setup(i64 n, const i64* rp, const i64* col, const double* val, int nparts,
-                 const i64* offs, double theta, int max_levels, i64 max_coarse) {
+                 const i64* offs, double theta, int max_levels, i64 max_coarse,
+                 i64 agglomerate) {
     ohier* h = calloc(1, sizeof(ohier));
     h->nparts = nparts;
     h->A[0] = csr_copy(n, n, rp, col, val);
@@ -387,6 +388,12 @@ ohier* orc_setup(i64 n, const i64* rp, const i64* col, const double* val, int np
         ocsr* A = &h->A[l];
         h->rho[l] = gershgorin(A);
         h->omega[l] = 4.0 / (3.0 * h->rho[l]);
+        /* SPEC §S7 agglomeration: from the first level l >= 1 with <= agglomerate rows on,
+         * the whole level is one part (part 0 owns every row; the others are empty) */
+        if (l >= 1 && agglomerate > 0 && A->nr <= agglomerate) {
+            h->offs[l][0] = 0;
+            for (int q = 1; q <= nparts; ++q) h->offs[l][q] = A->nr;
+        }
         if (A->nr <= max_coarse || l + 1 >= max_levels) break;
         h->agg[l] = malloc(sizeof(i64) * (A->nr + 1));
         i64* coffs = malloc(sizeof(i64) * (nparts + 1));

@@ -61,7 +61,7 @@ SIGNATURES = {
     "pamg_spmv": [vp, vp, vp, vp],
     "pamg_residual": [vp, vp, vp, vp, vp, pdbl],
     "pamg_jacobi": [vp, vp, vp, vp, vp, dbl, i32],
-    "pamg_hier_create": [vp, i32, vp, vp, vp, vp, i64, vp, vp, pvp],
+    "pamg_hier_create": [vp, i32, vp, vp, vp, vp, i64, vp, i32, vp, pvp],
     "pamg_hier_destroy": [vp],
     "pamg_hier_set_graph": [vp, i32],
     "pamg_hier_graph_state": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)],

@@ -236,11 +236,14 @@ struct pamg_hier {
     // coarsest level
     int64_t nc = 0;
     double* d_ainv = nullptr;          // column-major nc x nc
+    // replicated tail (SPEC §S7 agglomeration): levels >= rep are held whole on every rank;
+    // the restriction into level rep yields this rank's rows [coffs[me], coffs[me+1]), which
+    // are all-gathered (in blocks of cmax) into the whole vector
+    int rep = 0;
     std::vector<int64_t> coffs;        // nranks + 1
-    int64_t cmax = 0;                  // max rows per rank on the coarsest level
-    double* d_bgather = nullptr;       // nranks * cmax
+    int64_t cmax = 0;                  // max rows per rank of level rep
+    double* d_bgather = nullptr;       // nranks * cmax (+ nc scratch for the one-level case)
     double* d_bsend = nullptr;         // cmax
-    int* d_ccnt = nullptr;             // per-rank counts on device (gemv over ragged blocks)
     // graph replay
     bool use_graph = true;
     hipGraphExec_t gexec = nullptr;
@@ -259,17 +262,11 @@ struct pamg_hier {
 
 namespace {
 
-int coarse_solve(pamg_hier* H, const double* bL, double* xL, hipStream_t s) {
+// All-gather this rank's block of level H->rep (in d_bsend) into the rank blocks of
+// d_bgather, then compact them into global order at dst.
+int gather_rep(pamg_hier* H, double* dst, hipStream_t s) {
     pamg_ctx* ctx = H->ctx;
     const int nr = (int)H->coffs.size() - 1;
-    const int me = ctx->rank;
-    const int64_t own0 = H->coffs[me], nown = H->coffs[me + 1] - own0;
-    if (nr == 1) {
-        pamg::launch_dense_gemv(nown, H->nc, 0, H->d_ainv, bL, xL, s);
-        return PAMG_OK;
-    }
-    // all-gather b_L in rank blocks of cmax, then the owned rows of Ainv * b_L
-    HIPC(hipMemcpyAsync(H->d_bsend, bL, sizeof(double) * nown, hipMemcpyDeviceToDevice, s));
     if (ctx->host_fn) {
         ctx->h_send.resize(H->cmax + 1);
         ctx->h_recv.resize((size_t)nr * H->cmax + 1);
@@ -282,17 +279,30 @@ int coarse_solve(pamg_hier* H, const double* bL, double* xL, hipStream_t s) {
     } else {
         NCCLC(ncclAllGather(H->d_bsend, H->d_bgather, (size_t)H->cmax, ncclDouble, ctx->comm, s));
     }
-    // compact the gathered blocks into global order (ragged -> contiguous), in place safe:
-    // use d_bgather as source and d_bsend is too small, so copy rank blocks into xL-sized
-    // scratch: reuse the tail of d_bgather (allocated 2x)
-    double* dst = H->d_bgather + (size_t)nr * H->cmax;
     for (int q = 0; q < nr; ++q) {
         const int64_t c = H->coffs[q + 1] - H->coffs[q];
         if (c)
             HIPC(hipMemcpyAsync(dst + H->coffs[q], H->d_bgather + (size_t)q * H->cmax,
                                 sizeof(double) * c, hipMemcpyDeviceToDevice, s));
     }
-    pamg::launch_dense_gemv(nown, H->nc, own0, H->d_ainv, dst, xL, s);
+    return PAMG_OK;
+}
+
+// x_L = Ainv b_L. b_L is whole on every rank, except for a one-level hierarchy on several
+// ranks (level 0 is the caller's distributed vector): gather it, solve the own rows.
+int coarse_solve(pamg_hier* H, const double* bL, double* xL, hipStream_t s) {
+    pamg_ctx* ctx = H->ctx;
+    const int nr = (int)H->coffs.size() - 1;
+    if (H->L > 1 || nr == 1) {
+        pamg::launch_dense_gemv(H->nc, H->nc, 0, H->d_ainv, bL, xL, s);
+        return PAMG_OK;
+    }
+    const int me = ctx->rank;
+    const int64_t own0 = H->coffs[me], nown = H->coffs[me + 1] - own0;
+    HIPC(hipMemcpyAsync(H->d_bsend, bL, sizeof(double) * nown, hipMemcpyDeviceToDevice, s));
+    double* full = H->d_bgather + (size_t)nr * H->cmax;
+    CHECK(gather_rep(H, full, s));
+    pamg::launch_dense_gemv(nown, H->nc, own0, H->d_ainv, full, xL, s);
     return PAMG_OK;
 }
 
@@ -345,7 +355,12 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false)
         }
         {
             ProfScope p(H, l, 2, s);
-            CHECK(apply(ctx, H->R[l], pamg::OP_SPMV, H->r[l], nullptr, H->b[l + 1], 0.0));
+            if (l + 1 == H->rep && ctx->nranks > 1) {  // into the replicated tail
+                CHECK(apply(ctx, H->R[l], pamg::OP_SPMV, H->r[l], nullptr, H->d_bsend, 0.0));
+                CHECK(gather_rep(H, H->b[l + 1], s));
+            } else {
+                CHECK(apply(ctx, H->R[l], pamg::OP_SPMV, H->r[l], nullptr, H->b[l + 1], 0.0));
+            }
         }
     }
     {
@@ -769,18 +784,36 @@ int pamg_jacobi(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec* b
 
 int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* const* P,
                      pamg_mat* const* R, const double* omega, int64_t n_coarse,
-                     const double* ainv, const int64_t* coarse_offsets, pamg_hier** out) {
+                     const double* ainv, int rep_level, const int64_t* rep_offsets,
+                     pamg_hier** out) {
     if (!ctx || !out || nlevels < 1 || !A || !omega || !ainv || n_coarse < 1)
         return fail(PAMG_E_ARG, "hier_create: bad args");
     if (nlevels > 1 && (!P || !R)) return fail(PAMG_E_ARG, "hier_create: P/R missing");
+    const int L = nlevels, nr = ctx->nranks, me = ctx->rank;
+    if (nr == 1 || L == 1) rep_level = L - 1;
+    if (rep_level < (L > 1 ? 1 : 0) || rep_level > L - 1)
+        return fail(PAMG_E_ARG, "hier_create: rep_level %d outside [1, %d]", rep_level, L - 1);
+    if (nr > 1 && !rep_offsets)
+        return fail(PAMG_E_ARG, "hier_create: rep_offsets required with %d ranks", nr);
     CHECK(set_device(ctx));
     auto H = std::make_unique<pamg_hier>();
     H->ctx = ctx;
     H->L = nlevels;
+    H->rep = rep_level;
     // graph replay on one part and on RCCL multi-part runs (RCCL captures its p2p and
     // collectives); never with the host debug transport (host callbacks)
-    H->use_graph = ctx->nranks == 1 || (ctx->comm != nullptr && !ctx->host_fn);
-    const int L = nlevels;
+    H->use_graph = nr == 1 || (ctx->comm != nullptr && !ctx->host_fn);
+    H->coffs.assign(nr + 1, 0);
+    if (rep_offsets) {
+        for (int q = 0; q <= nr; ++q) H->coffs[q] = rep_offsets[q];
+    } else {
+        H->coffs[1] = A[rep_level]->nrows;
+    }
+    for (int q = 0; q < nr; ++q) {
+        if (H->coffs[q + 1] < H->coffs[q]) return fail(PAMG_E_ARG, "hier_create: rep_offsets not monotone");
+        H->cmax = std::max(H->cmax, H->coffs[q + 1] - H->coffs[q]);
+    }
+    const int64_t n_rep = H->coffs[nr], rep_own = H->coffs[me + 1] - H->coffs[me];
     H->A.assign(A, A + L);
     H->P.assign(L, nullptr);
     H->R.assign(L, nullptr);
@@ -792,15 +825,24 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
     H->nown.assign(L, 0);
     for (int l = 0; l < L; ++l) {
         if (!A[l]) return fail(PAMG_E_ARG, "hier_create: A[%d] is NULL", l);
-        H->nown[l] = A[l]->nrows;
-        if (l < L - 1) {
-            if (!P[l] || !R[l]) return fail(PAMG_E_ARG, "hier_create: P/R[%d] is NULL", l);
-            H->P[l] = P[l];
-            H->R[l] = R[l];
-            if (!A[l]->d_diag) return fail(PAMG_E_SETUP, "hier_create: A[%d] lacks a nonzero diagonal", l);
-            if (P[l]->nrows != A[l]->nrows || R[l]->nrows != A[l + 1]->nrows)
-                return fail(PAMG_E_ARG, "hier_create: level %d operator shapes inconsistent", l);
-        }
+        // levels >= rep are whole on every rank (the coarsest may be passed distributed: only
+        // its inverse is used)
+        H->nown[l] = (l == rep_level && L > 1) ? n_rep : A[l]->nrows;
+    }
+    if (L > 1 && nr > 1 && rep_level < L - 1 && A[rep_level]->nrows != n_rep)
+        return fail(PAMG_E_ARG, "hier_create: A[%d] must be whole (%lld rows) on every rank",
+                    rep_level, (long long)n_rep);
+    for (int l = 0; l < L - 1; ++l) {
+        if (!P[l] || !R[l]) return fail(PAMG_E_ARG, "hier_create: P/R[%d] is NULL", l);
+        H->P[l] = P[l];
+        H->R[l] = R[l];
+        if (!A[l]->d_diag) return fail(PAMG_E_SETUP, "hier_create: A[%d] lacks a nonzero diagonal", l);
+        const int64_t r_rows = (l + 1 == rep_level) ? rep_own : H->nown[l + 1];
+        if (P[l]->nrows != A[l]->nrows || R[l]->nrows != r_rows)
+            return fail(PAMG_E_ARG, "hier_create: level %d operator shapes inconsistent", l);
+        if (l + 1 >= rep_level && (P[l]->plan || P[l]->ncols != H->nown[l + 1]))
+            return fail(PAMG_E_ARG, "hier_create: P[%d] must read the whole level-%d vector (no plan, %lld columns)",
+                        l, l + 1, (long long)H->nown[l + 1]);
     }
     // ghost capacity of each level's vectors = max over the plans that read them
     for (int l = 0; l < L; ++l) {
@@ -824,21 +866,15 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
     }
     // coarsest level
     H->nc = n_coarse;
-    const int nr = ctx->nranks;
-    H->coffs.assign(nr + 1, 0);
-    if (coarse_offsets) {
-        for (int q = 0; q <= nr; ++q) H->coffs[q] = coarse_offsets[q];
-    } else {
-        if (nr != 1) return fail(PAMG_E_ARG, "hier_create: coarse_offsets required with %d ranks", nr);
-        H->coffs[1] = n_coarse;
-    }
-    if (H->coffs[nr] != n_coarse || H->coffs[ctx->rank + 1] - H->coffs[ctx->rank] != A[L - 1]->nrows)
-        return fail(PAMG_E_ARG, "hier_create: coarse offsets inconsistent with the coarsest matrix");
-    for (int q = 0; q < nr; ++q) H->cmax = std::max(H->cmax, H->coffs[q + 1] - H->coffs[q]);
+    if (H->nown[L - 1] != n_coarse && !(L == 1 && nr > 1))
+        return fail(PAMG_E_ARG, "hier_create: coarsest level has %lld rows, n_coarse = %lld",
+                    (long long)H->nown[L - 1], (long long)n_coarse);
+    if (L == 1 && (n_rep != n_coarse || rep_own != A[0]->nrows))
+        return fail(PAMG_E_ARG, "hier_create: rep_offsets inconsistent with the one-level hierarchy");
     CHECK(dalloc(&H->d_ainv, n_coarse * n_coarse));
     HIPC(hipMemcpy(H->d_ainv, ainv, sizeof(double) * n_coarse * n_coarse, hipMemcpyHostToDevice));
     if (nr > 1) {
-        CHECK(dalloc(&H->d_bgather, (int64_t)nr * H->cmax + n_coarse + kVecPad));
+        CHECK(dalloc(&H->d_bgather, (int64_t)nr * H->cmax + n_rep + kVecPad));
         CHECK(dalloc(&H->d_bsend, H->cmax + kVecPad));
         HIPC(hipMemset(H->d_bsend, 0, sizeof(double) * (H->cmax + kVecPad)));
     }

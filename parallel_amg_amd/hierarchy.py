@@ -24,6 +24,9 @@ class SAParams:
     theta: float = 0.02
     max_levels: int = 20
     max_coarse: int = 1000
+    # SPEC §S7 agglomeration: levels >= 1 with <= this many global rows are built as one part
+    # and replicated on every part; 0 = decoupled on every level
+    agglomerate: int = 32768
 
 
 @dataclass
@@ -128,6 +131,7 @@ class LevelPart:
     R: HCSR = None                  # own coarse rows (next level) x global fine cols
     planP: HostPlan = None          # column space: next level
     planR: HostPlan = None          # column space: this level
+    whole: bool = False             # agglomerated level: every part holds all rows (§S7)
 
 
 @dataclass
@@ -137,6 +141,10 @@ class HostHierarchy:
     levels: list            # list of dict part -> LevelPart
     ainv: np.ndarray        # column-major n_c x n_c (SPEC §S5)
     n_coarse: int
+    # first level held whole on every part (agglomerated tail; the coarsest level otherwise)
+    # and how the restriction into it distributes its rows over the parts
+    rep_level: int = 0
+    rep_offsets: np.ndarray = None
 
     @property
     def nlevels(self):
@@ -146,7 +154,16 @@ class HostHierarchy:
         return next(iter(self.levels[l].values())).offsets
 
     def nnz(self, l, which="A"):
-        return sum(getattr(lp, which).nnz for lp in self.levels[l].values() if getattr(lp, which) is not None)
+        lps = list(self.levels[l].values())
+        if lps[0].whole:
+            lps = lps[:1]
+        return sum(getattr(lp, which).nnz for lp in lps if getattr(lp, which) is not None)
+
+    def part_rows(self, l, which="A"):
+        """The level's matrix as the list of distinct row blocks in part order (one block for a
+        whole, agglomerated level)."""
+        lps = [self.levels[l][p] for p in sorted(self.levels[l])]
+        return [getattr(lps[0], which)] if lps[0].whole else [getattr(lp, which) for lp in lps]
 
 
 def generate_problem(backend, kind: str, n: int, eps: float = 1e-3):
@@ -190,7 +207,7 @@ def load_problem(backend, path: str, partition: str = "uniform"):
 
 
 def build_hierarchy(backend, A: dict, offsets: np.ndarray, params: SAParams = SAParams(),
-                    log=None, device=None) -> HostHierarchy:
+                    log=None, device=None, _level0: int = 0) -> HostHierarchy:
     """SPEC §S4: levels until n <= max_coarse / max_levels / stalled coarsening.
 
     ``device`` (a partitioned.Context): the Galerkin products (A T, A P, R (A P)) and the
@@ -201,9 +218,11 @@ def build_hierarchy(backend, A: dict, offsets: np.ndarray, params: SAParams = SA
     offs = np.asarray(offsets, np.int64)
     levels = []
     while True:
+        n = int(offs[-1])
+        if backend.nparts > 1 and levels and 0 < params.agglomerate and n <= params.agglomerate:
+            return _replicated_tail(backend, A, offs, levels, params, log, device)
         rho = backend.allreduce_max({p: H.gershgorin(A[p], int(offs[p])) for p in parts})
         omega = 4.0 / (3.0 * rho)
-        n = int(offs[-1])
         ghosts = {p: (ghost_ids(A[p], int(offs[p]), int(offs[p + 1])) if backend.nparts > 1
                       else np.zeros(0, np.int64)) for p in parts}
         planA = build_plans(backend, ghosts, offs)
@@ -267,7 +286,7 @@ def build_hierarchy(backend, A: dict, offsets: np.ndarray, params: SAParams = SA
             lp = lev[p]
             lp.agg, lp.P, lp.R, lp.planP, lp.planR = aggs[p][0], P[p], R[p], planP[p], planR[p]
         if log:
-            log(f"level {len(levels) - 1}: n={n} nnz={sum(A[p].nnz for p in parts)} -> n_c={nc}")
+            log(f"level {_level0 + len(levels) - 1}: n={n} nnz={sum(A[p].nnz for p in parts)} -> n_c={nc}")
         A, offs = Ac, coffs
     # coarsest level: every part assembles the full matrix and the same Cholesky inverse
     last = levels[-1]
@@ -276,7 +295,30 @@ def build_hierarchy(backend, A: dict, offsets: np.ndarray, params: SAParams = SA
     else:
         full = _gather_full(backend, {p: last[p].A for p in parts}, offs)
     ainv = H.cholinv(full)
-    return HostHierarchy(backend.nparts, parts, levels, ainv, int(offs[-1]))
+    return HostHierarchy(backend.nparts, parts, levels, ainv, int(offs[-1]),
+                         rep_level=len(levels) - 1, rep_offsets=offs)
+
+
+def _replicated_tail(backend, A: dict, offs, levels: list, params: SAParams, log, device):
+    """SPEC §S7 agglomeration: gather the level on every part and set up the rest of the
+    hierarchy as one part (the same work on every part, so the replicas are identical)."""
+    from dataclasses import replace
+    from .backend import SequentialBackend
+    n = int(offs[-1])
+    full = _gather_full(backend, A, offs)
+    sub = build_hierarchy(SequentialBackend(1), {0: full}, np.array([0, n], np.int64),
+                          replace(params, agglomerate=0, max_levels=params.max_levels - len(levels)),
+                          (lambda m: log(m + " (whole on every part)")) if log else None, device,
+                          _level0=len(levels))
+    for p in backend.parts:  # the prolongation into the tail reads the whole vector
+        levels[-1][p].planP = None
+    for l in range(sub.nlevels):
+        lp = sub.levels[l][0]
+        lp.offsets = np.array([0] + [lp.A.nrows] * backend.nparts, np.int64)
+        lp.whole = True
+        levels.append({p: lp for p in backend.parts})
+    return HostHierarchy(backend.nparts, backend.parts, levels, sub.ainv, sub.n_coarse,
+                         rep_level=len(levels) - sub.nlevels, rep_offsets=np.asarray(offs, np.int64))
 
 
 def _gather_full(backend, A: dict, offs) -> HCSR:

@@ -21,12 +21,15 @@ class AMGSolver:
     def __init__(self, ctx: Context, H: HostHierarchy, part: int = 0, graph: bool | None = None):
         self.ctx, self.part, self.L = ctx, part, H.nlevels
         self.A, self.P, self.R, self.omega = [], [], [], []
+        # levels >= rep are whole on every part (agglomerated tail / coarsest level): the
+        # prolongation into rep - 1 reads that whole vector, so its columns stay global
+        rep = H.rep_level if H.nparts > 1 else H.nlevels - 1
         for l in range(H.nlevels):
             lp = H.levels[l][part]
             self.A.append(PSparseMatrix(ctx, lp.A, lp.planA))
             self.omega.append(lp.omega)
             if l < H.nlevels - 1:
-                self.P.append(PSparseMatrix(ctx, lp.P, lp.planP))
+                self.P.append(PSparseMatrix(ctx, lp.P, None if l + 1 >= rep else lp.planP))
                 self.R.append(PSparseMatrix(ctx, lp.R, lp.planR))
         self.level_rows = [int(H.levels[l][part].A.nrows) for l in range(H.nlevels)]
         self.n_coarse = H.n_coarse
@@ -35,11 +38,12 @@ class AMGSolver:
         arrP = (C.c_void_p * L)(*([p.handle for p in self.P] + [None]))
         arrR = (C.c_void_p * L)(*([r.handle for r in self.R] + [None]))
         om = np.asarray(self.omega, np.float64)
-        coffs = np.asarray(H.offsets(L - 1), np.int64) if H.nparts > 1 else None
+        roffs = np.asarray(H.rep_offsets, np.int64) if H.nparts > 1 else None
+        self.rep_level = rep
         self._ainv = np.ascontiguousarray(H.ainv, np.float64)
         h = C.c_void_p()
         call("pamg_hier_create", ctx.handle, L, arrA, arrP, arrR, ptr(om), H.n_coarse,
-             ptr(self._ainv), ptr(coffs) if coffs is not None else None, C.byref(h))
+             ptr(self._ainv), int(rep), ptr(roffs) if roffs is not None else None, C.byref(h))
         self._h = h
         if graph is not None:
             self.set_graph(graph)

@@ -37,7 +37,7 @@ def sha(a):
 def make(name, kind, n, nparts, max_coarse, ncycles, full):
     A = O.generate(kind, *O.grid_shape(kind, n))
     b = O.spmv(A, O.xstar(A.nrows))
-    H = O.setup(A, nparts=nparts, max_coarse=max_coarse)
+    H = O.setup(A, nparts=nparts, max_coarse=max_coarse, agglomerate=0)  # decoupled on every level
     x, hist = H.solve(b, ncycles, res_hist=True)
     out = {"kind": kind, "n": n, "nparts": nparts, "max_coarse": max_coarse, "ncycles": ncycles,
            "nlevels": H.nlevels, "b_sha": sha(b), "x_sha": sha(x), "x": x if full else x[:64],

@@ -20,7 +20,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, kind, n, max_coarse, q):
+def _worker(rank, world, port, kind, n, max_coarse, agglomerate, q):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), OMP_NUM_THREADS="1")
@@ -32,18 +32,20 @@ def _worker(rank, world, port, kind, n, max_coarse, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         be = pa.DistributedBackend()
         A, offs, xs = pa.generate_problem(be, kind, n)
-        H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse))
+        prm = pa.SAParams(max_coarse=max_coarse, agglomerate=agglomerate)
+        H = pa.build_hierarchy(be, A, offs, prm)
         Ao = O.generate(kind, *O.grid_shape(kind, n))
-        Ho = O.setup(Ao, nparts=world, max_coarse=max_coarse)
+        Ho = O.setup(Ao, nparts=world, max_coarse=max_coarse, agglomerate=agglomerate)
         bits = lambda a: np.asarray(a, np.float64).view(np.int64)
         assert H.nlevels == Ho.nlevels, (H.nlevels, Ho.nlevels)
         # same plans as the in-process (debug) backend
         Hs = pa.build_hierarchy(pa.SequentialBackend(world), *pa.generate_problem(pa.SequentialBackend(world), kind, n)[:2],
-                                pa.SAParams(max_coarse=max_coarse))
+                                prm)
         for l in range(H.nlevels):
             lp = H.levels[l][rank]
             o = Ho.offsets[l]
-            a, b = int(o[rank]), int(o[rank + 1])
+            # agglomerated (whole) levels: every rank holds all rows
+            a, b = (0, int(o[-1])) if lp.whole else (int(o[rank]), int(o[rank + 1]))
             assert np.array_equal(lp.offsets, o)
             Ar = Ho.A[l]
             sl = slice(Ar.rowptr[a], Ar.rowptr[b])
@@ -60,12 +62,12 @@ def _worker(rank, world, port, kind, n, max_coarse, q):
                 Pr = Ho.P[l]
                 sl = slice(Pr.rowptr[a], Pr.rowptr[b])
                 assert np.array_equal(lp.P.col, Pr.col[sl]) and np.array_equal(bits(lp.P.val), bits(Pr.val[sl]))
-                co = Ho.offsets[l + 1]
-                ca, cb = int(co[rank]), int(co[rank + 1])
+                co = H.rep_offsets if l + 1 == H.rep_level else Ho.offsets[l + 1]
+                ca, cb = (0, int(co[-1])) if lp.whole else (int(co[rank]), int(co[rank + 1]))
                 Rr = Ho.R[l]
                 sl = slice(Rr.rowptr[ca], Rr.rowptr[cb])
                 assert np.array_equal(lp.R.col, Rr.col[sl]) and np.array_equal(bits(lp.R.val), bits(Rr.val[sl]))
-                assert np.array_equal(np.where(lp.agg >= 0, lp.agg + co[rank], -1), Ho.agg[l][a:b])
+                assert np.array_equal(np.where(lp.agg >= 0, lp.agg + ca, -1), Ho.agg[l][a:b])
         assert np.array_equal(bits(H.ainv), bits(Ho.ainv.T.reshape(-1)))
         q.put((rank, "ok"))
     except Exception as e:  # report to the parent
@@ -76,16 +78,18 @@ def _worker(rank, world, port, kind, n, max_coarse, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kind,n,max_coarse", [
-    (2, "poisson2d", 48, 100),        # BASELINE.json configs[0] shape (2 parts on CPU), reduced
-    (2, "poisson3d", 14, 60),
-    (3, "aniso3d", 12, 80),
+@pytest.mark.parametrize("world,kind,n,max_coarse,agglomerate", [
+    (2, "poisson2d", 48, 100, 0),     # BASELINE.json configs[0] shape (2 parts on CPU), reduced
+    (2, "poisson2d", 48, 100, 32768),
+    (2, "poisson3d", 14, 60, 0),
+    (3, "aniso3d", 12, 80, 0),
+    (3, "aniso3d", 12, 80, 200),      # agglomerated from level 2 on
 ])
-def test_distributed_setup_matches_oracle(world, kind, n, max_coarse, built):
+def test_distributed_setup_matches_oracle(world, kind, n, max_coarse, agglomerate, built):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, n, max_coarse, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, n, max_coarse, agglomerate, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in procs)

@@ -24,7 +24,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, kind, n, max_coarse, ncycles, q):
+def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, q):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), OMP_NUM_THREADS="2")
@@ -38,7 +38,7 @@ def _worker(rank, world, port, kind, n, max_coarse, ncycles, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         be = pa.DistributedBackend()
         A, offs, xs = pa.generate_problem(be, kind, n)
-        H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse))
+        H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse, agglomerate=agglomerate))
         ndev = max(1, torch.cuda.device_count())
         # RCCL needs one device per rank; with fewer GPUs than ranks use the host transport
         ctx = Context(rank % ndev, be, transport="rccl" if ndev >= world else "host")
@@ -59,14 +59,20 @@ def _worker(rank, world, port, kind, n, max_coarse, ncycles, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kind,n,max_coarse", [(2, "poisson3d", 20, 100), (3, "poisson2d", 60, 200)])
-def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, built):
+@pytest.mark.parametrize("world,kind,n,max_coarse,agglomerate", [
+    (2, "poisson3d", 20, 100, 0),       # decoupled on every level, coarsest gathered
+    (2, "poisson3d", 20, 100, 32768),   # agglomerated from level 1 on (SPEC §S7)
+    (3, "poisson2d", 60, 200, 0),
+    (3, "aniso3d", 16, 30, 600),        # agglomerated from level 2 on
+    (2, "poisson2d", 20, 1000, 0),      # one level: the distributed coarsest solve
+])
+def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, agglomerate, built):
     from oracle import oracle as O
     ncycles = 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, n, max_coarse, ncycles, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, n, max_coarse, agglomerate, ncycles, q))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -80,7 +86,7 @@ def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, built):
         assert res[r][1] == "ok", res[r][1]
     Ao = O.generate(kind, *O.grid_shape(kind, n))
     bo = O.spmv(Ao, O.xstar(Ao.nrows))
-    Ho = O.setup(Ao, nparts=world, max_coarse=max_coarse)
+    Ho = O.setup(Ao, nparts=world, max_coarse=max_coarse, agglomerate=agglomerate)
     xo, ho = Ho.solve(bo, ncycles, res_hist=True)
     b = np.concatenate([res[r][2] for r in range(world)])
     x = np.concatenate([res[r][3] for r in range(world)])

@@ -108,6 +108,6 @@ def test_device_setup_matches_oracle(ctx, kind, n, nparts, max_coarse):
             if d.P is not None:
                 same(d.P, h.P)
                 same(d.R, h.R)
-        full = np.concatenate([Hd.levels[l][p].A.val for p in range(nparts)])
+        full = np.concatenate([M.val for M in Hd.part_rows(l)])
         assert np.array_equal(bits(full), bits(Ho.A[l].val))
     assert np.array_equal(bits(Hd.ainv), bits(Hh.ainv))

@@ -69,7 +69,7 @@ def test_elastic_generator_and_setup_bit_exact(built):
     Ho = O.setup(Ao, nparts=2, max_coarse=60)
     assert H.nlevels == Ho.nlevels
     for l in range(H.nlevels):
-        full = np.concatenate([H.levels[l][p].A.val for p in range(2)])
+        full = np.concatenate([M.val for M in H.part_rows(l)])
         assert np.array_equal(bits(full), bits(Ho.A[l].val))
 
 
@@ -101,7 +101,7 @@ def test_nnz_balanced_partition(tmp_path, built):
     Ho = O.setup(Ao, offsets=offs, max_coarse=50)
     assert H.nlevels == Ho.nlevels
     for l in range(H.nlevels):
-        full = np.concatenate([H.levels[l][p].A.val for p in range(3)])
+        full = np.concatenate([M.val for M in H.part_rows(l)])
         assert np.array_equal(bits(full), bits(Ho.A[l].val))
         assert np.array_equal(H.offsets(l), Ho.offsets[l])
 

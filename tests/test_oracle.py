@@ -106,7 +106,7 @@ def test_aggregation_semicoarsening_aniso():
 @pytest.mark.parametrize("kind,n,nparts", [("poisson2d", 48, 1), ("poisson3d", 12, 2), ("aniso3d", 10, 3)])
 def test_galerkin_and_prolongator_against_scipy(kind, n, nparts):
     A = O.generate(kind, *O.grid_shape(kind, n))
-    H = O.setup(A, nparts=nparts, max_coarse=20)
+    H = O.setup(A, nparts=nparts, max_coarse=20, agglomerate=0)
     for l in range(H.nlevels - 1):
         Al, P, R = H.A[l].to_scipy(), H.P[l].to_scipy(), H.R[l].to_scipy()
         assert (R - P.T).nnz == 0 and np.array_equal((R - P.T).toarray(), np.zeros(R.shape))
@@ -171,7 +171,7 @@ def test_golden_fixtures(path):
     b = O.spmv(A, O.xstar(A.nrows))
     sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
     assert sha(b) == str(g["b_sha"])
-    H = O.setup(A, nparts=nparts, max_coarse=int(g["max_coarse"]))
+    H = O.setup(A, nparts=nparts, max_coarse=int(g["max_coarse"]), agglomerate=0)
     assert H.nlevels == int(g["nlevels"])
     assert np.array_equal(bits(H.omega), bits(g["omega"]))
     for l in range(H.nlevels):

@@ -29,18 +29,20 @@ def _rows(M, a, b):
     return M.rowptr[a:b + 1] - M.rowptr[a], M.col[sl], M.val[sl]
 
 
-def check_against_oracle(kind, n, nparts, max_coarse):
+def check_against_oracle(kind, n, nparts, max_coarse, agglomerate=32768):
     be = pa.SequentialBackend(nparts)
     A, offs, xs = pa.generate_problem(be, kind, n)
-    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse))
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse, agglomerate=agglomerate))
     Ao = O.generate(kind, *O.grid_shape(kind, n))
-    Ho = O.setup(Ao, nparts=nparts, max_coarse=max_coarse)
+    Ho = O.setup(Ao, nparts=nparts, max_coarse=max_coarse, agglomerate=agglomerate)
     assert H.nlevels == Ho.nlevels
     assert np.array_equal(np.concatenate([xs[p] for p in range(nparts)]), O.xstar(Ao.nrows))
     for l in range(H.nlevels):
+        assert np.array_equal(H.offsets(l), Ho.offsets[l])
         for p in range(nparts):
             lp, o = H.levels[l][p], Ho.offsets[l]
-            a, b = int(o[p]), int(o[p + 1])
+            # an agglomerated (whole) level: every part holds all rows
+            a, b = (0, int(o[-1])) if lp.whole else (int(o[p]), int(o[p + 1]))
             rp, c, v = _rows(Ho.A[l], a, b)
             assert np.array_equal(lp.A.rowptr, rp) and np.array_equal(lp.A.col, c)
             assert np.array_equal(bits(lp.A.val), bits(v))
@@ -49,11 +51,13 @@ def check_against_oracle(kind, n, nparts, max_coarse):
                 rp, c, v = _rows(Ho.P[l], a, b)
                 assert np.array_equal(lp.P.rowptr, rp) and np.array_equal(lp.P.col, c)
                 assert np.array_equal(bits(lp.P.val), bits(v))
-                co = Ho.offsets[l + 1]
-                rp, c, v = _rows(Ho.R[l], int(co[p]), int(co[p + 1]))
+                # rows of R = the next level's rows as this level's aggregation numbered them
+                co = H.rep_offsets if l + 1 == H.rep_level else Ho.offsets[l + 1]
+                ca, cb = (0, int(co[-1])) if lp.whole else (int(co[p]), int(co[p + 1]))
+                rp, c, v = _rows(Ho.R[l], ca, cb)
                 assert np.array_equal(lp.R.rowptr, rp) and np.array_equal(lp.R.col, c)
                 assert np.array_equal(bits(lp.R.val), bits(v))
-                assert np.array_equal(np.where(lp.agg >= 0, lp.agg + co[p], -1), Ho.agg[l][a:b])
+                assert np.array_equal(np.where(lp.agg >= 0, lp.agg + ca, -1), Ho.agg[l][a:b])
     assert np.array_equal(bits(H.ainv), bits(Ho.ainv.T.reshape(-1)))
     return H
 
@@ -62,8 +66,17 @@ def check_against_oracle(kind, n, nparts, max_coarse):
     ("poisson2d", 50, 1, 100), ("poisson3d", 18, 1, 60), ("aniso3d", 14, 1, 100),
     ("poisson3d", 18, 2, 60), ("poisson2d", 41, 3, 80), ("aniso3d", 13, 4, 120),
 ])
-def test_host_setup_bit_exact(kind, n, nparts, max_coarse, built):
-    check_against_oracle(kind, n, nparts, max_coarse)
+@pytest.mark.parametrize("agglomerate", [0, 32768, 400])
+def test_host_setup_bit_exact(kind, n, nparts, max_coarse, agglomerate, built):
+    H = check_against_oracle(kind, n, nparts, max_coarse, agglomerate)
+    if nparts > 1:
+        whole = [H.levels[l][0].whole for l in range(H.nlevels)]
+        first = whole.index(True) if any(whole) else H.nlevels
+        assert not any(whole[:first]) and all(whole[first:])
+        if agglomerate == 0:
+            assert first == H.nlevels and H.rep_level == H.nlevels - 1
+        else:
+            assert H.rep_level == first or (first == H.nlevels and H.rep_level == H.nlevels - 1)
 
 
 def test_exchange_plans_are_consistent(built):
@@ -77,7 +90,7 @@ def test_exchange_plans_are_consistent(built):
                 P = getattr(H.levels[l][p], attr)
                 if P is None:
                     continue
-                o = H.offsets(l + 1 if nxt else l)
+                o = (H.rep_offsets if nxt and l + 1 == H.rep_level else H.offsets(l + 1 if nxt else l))
                 for k, q in enumerate(P.nbrs):
                     Q = getattr(H.levels[l][q], attr)
                     mine = P.ghost_ids[(P.ghost_ids >= o[q]) & (P.ghost_ids < o[q + 1])]
@@ -91,7 +104,7 @@ def test_host_setup_golden(path, built):
     nparts = int(g["nparts"])
     be = pa.SequentialBackend(nparts)
     A, offs, _ = pa.generate_problem(be, str(g["kind"]), int(g["n"]))
-    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=int(g["max_coarse"])))
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=int(g["max_coarse"]), agglomerate=0))
     assert H.nlevels == int(g["nlevels"])
     for l in range(H.nlevels):
         tags = ["A"] + (["P", "R"] if l < H.nlevels - 1 else [])
