@@ -662,27 +662,41 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     A->ncols = ncols;
     A->nnz = nnz;
     A->plan = plan;
-    // classify rows: interior (own columns only) or boundary (>= 1 ghost column)
+    // classify rows: interior (own columns only) or boundary (>= 1 ghost column). Also the
+    // row distance at which rows share x entries, for the banded tile order: per own column
+    // the largest gap between consecutive rows that read it (one grid plane for a stencil,
+    // one aggregate layer for a restriction); band = its 90th percentile over the columns.
     std::vector<int> inner, bnd;
     std::vector<double> diag(nrows, 0.0);
     bool has_all_diag = (n_own_cols == nrows);
-    int64_t band = 0;  // half-bandwidth over own columns (square matrices only)
+    std::vector<int> last_row(n_own_cols, -1), max_gap(n_own_cols, 0);
     for (int64_t i = 0; i < nrows; ++i) {
         bool g = false, d = false;
         for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-            g |= ci[k] >= n_own_cols;
-            if (ci[k] < n_own_cols && n_own_cols > 0) {
-                // half-bandwidth in row units (rectangular R/P: columns scaled to rows)
-                const int64_t cr = (int64_t)((double)ci[k] * (double)nrows / (double)n_own_cols);
-                band = std::max(band, std::abs(cr - i));
+            const int c = ci[k];
+            g |= c >= n_own_cols;
+            if (c < n_own_cols) {
+                if (last_row[c] >= 0) max_gap[c] = std::max(max_gap[c], (int)i - last_row[c]);
+                last_row[c] = (int)i;
             }
-            if (ci[k] == i && n_own_cols == nrows) {
+            if (c == i && n_own_cols == nrows) {
                 diag[i] = val[k];
                 d = true;
             }
         }
         if (!d || diag[i] == 0.0) has_all_diag = false;
         (g ? bnd : inner).push_back((int)i);
+    }
+    int64_t band = 0;
+    {
+        std::vector<int>().swap(last_row);
+        auto end = std::remove(max_gap.begin(), max_gap.end(), 0);
+        const size_t m = (size_t)(end - max_gap.begin());
+        if (m > 0) {
+            auto q = max_gap.begin() + (ptrdiff_t)((m * 9) / 10);
+            std::nth_element(max_gap.begin(), q, end);
+            band = *q;
+        }
     }
     std::vector<int> rp32(nrows + 1);
     for (int64_t i = 0; i <= nrows; ++i) rp32[i] = (int)rp[i];

@@ -62,7 +62,7 @@ def main():
     A, offs, xs = pa.generate_problem(be, "poisson3d", args.n)
     mats = {"A0": (A[0], None)}
     if args.levels > 1:
-        H = pa.build_hierarchy(be, A, offs)
+        H = pa.build_hierarchy(be, A, offs, device=ctx)
         for l in range(min(args.levels, H.nlevels - 1)):
             lp = H.levels[l][0]
             mats[f"A{l}"] = (lp.A, lp.planA)
