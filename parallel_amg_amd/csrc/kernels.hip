@@ -40,6 +40,23 @@ __device__ __forceinline__ void epilogue(int r, double s, const double* __restri
     }
 }
 
+// Sum of lp[kb..ke) left to right from +0.0 (SPEC §S3). The LDS loads go out 8 at a time
+// ahead of the dependent adds (one LDS latency per 8 products instead of per product — what
+// bounds the long rows of the coarse operators); slots past the row end contribute +0.0, which
+// leaves the sum's bits unchanged: a sum started at +0.0 is never -0.0, and s + (+0.0) == s
+// for every other s.
+__device__ __forceinline__ double row_sum_lds(const double* __restrict__ lp, int kb, int ke,
+                                              double s = 0.0) {
+    for (int k = kb; k < ke; k += 8) {
+        double p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] = (k + j < ke) ? lp[k + j] : 0.0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s = s + p[j];
+    }
+    return s;
+}
+
 // Variant 0 (first version, kept for A/B): row pointers first, then the column stream.
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_rows_tile(
@@ -82,8 +99,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile(
     if (tid < nr) {
         const int r = r0 + tid;
         const int kb = lrp[tid] - za, ke = lrp[tid + 1] - za;
-        double s = 0.0;
-        for (int k = kb; k < ke; ++k) s = s + lprod[k];
+        const double s = row_sum_lds(lprod, kb, ke);
         epilogue<OP>(r, s, x, b, y, omega, OP == OP_JACOBI ? ldiag[tid] : 0.0);
     }
 }
@@ -203,8 +219,7 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
     if constexpr (ONE_ROW) {
         if (tid < nr) {
             const int kb = lrp[tid] - za, ke = lrp[tid + 1] - za;
-            double s = 0.0;
-            for (int k = kb; k < ke; ++k) s = s + lprod[k];
+            const double s = row_sum_lds(lprod, kb, ke);
             const int r = r0 + tid;
             if constexpr (OP == OP_SPMV) {
                 y[r] = s;
@@ -223,8 +238,7 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
     } else {
         for (int rr = tid; rr < nr; rr += BS) {
             const int kb = lrp[rr] - za, ke = lrp[rr + 1] - za;
-            double s = 0.0;
-            for (int k = kb; k < ke; ++k) s = s + lprod[k];
+            const double s = row_sum_lds(lprod, kb, ke);
             double d = 0.0;
             if constexpr (OP == OP_JACOBI) d = diag ? diag[r0 + rr] : ldiag[rr];
             epilogue<OP>(r0 + rr, s, x, b, y, omega, d);
@@ -329,8 +343,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_pers(
         lds_barrier();
         if (tid < nr) {
             const int kb = lrp[tid] - za, ke = lrp[tid + 1] - za;
-            double s = 0.0;
-            for (int k = kb; k < ke; ++k) s = s + lprod[k];
+            const double s = row_sum_lds(lprod, kb, ke);
             const int r = r0 + tid;
             if constexpr (OP == OP_SPMV) {
                 y[r] = s;
@@ -478,7 +491,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_long(
     const int* __restrict__ rows, const int* __restrict__ rowptr, const int* __restrict__ col,
     const double* __restrict__ val, const double* __restrict__ x, const double* __restrict__ b,
     double* __restrict__ y, double omega) {
-    __shared__ double lprod[kBlock];
+    __shared__ double lprod[kBlock + 8];  // + 8: row_sum_lds reads (and discards) up to 7 past the end
     __shared__ double ldiag;
     const int tid = threadIdx.x;
     const int r = rows[blockIdx.x];
@@ -497,10 +510,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_long(
         }
         lprod[tid] = p;
         __syncthreads();
-        if (tid == 0) {
-            const int m = min(kBlock, z1 - base);
-            for (int j = 0; j < m; ++j) s = s + lprod[j];
-        }
+        if (tid == 0) s = row_sum_lds(lprod, 0, min(kBlock, z1 - base), s);
         __syncthreads();
     }
     if (tid == 0) epilogue<OP>(r, s, x, b, y, omega, OP == OP_JACOBI ? ldiag : 0.0);
