@@ -72,6 +72,10 @@ struct pamg_plan {
     std::vector<int64_t> recv_off, send_off;  // n_nbr + 1
     int* d_send_idx = nullptr;
     double* d_sendbuf = nullptr;
+    // per neighbour: first own index if its send list is one contiguous run (the boundary
+    // planes of a slab partition), else -1; all_contig: no pack kernel is needed at all
+    std::vector<int64_t> send_run;
+    bool all_contig = false;
 };
 
 struct pamg_vec {

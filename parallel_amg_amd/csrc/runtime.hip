@@ -149,7 +149,12 @@ int exchange_on(const pamg_plan* plan, double* x, hipStream_t s) {
     if (nn == 0) return PAMG_OK;
     if (!ctx->comm && !ctx->host_fn)
         return fail(PAMG_E_STATE, "exchange: plan has neighbours but no communicator");
-    pamg::launch_pack(plan->send_off[nn], plan->d_send_idx, x, plan->d_sendbuf, s);
+    // contiguous send lists go straight from x; the others are packed first
+    if (!plan->all_contig)
+        pamg::launch_pack(plan->send_off[nn], plan->d_send_idx, x, plan->d_sendbuf, s);
+    auto send_ptr = [&](int k) -> const double* {
+        return plan->send_run[k] >= 0 ? x + plan->send_run[k] : plan->d_sendbuf + plan->send_off[k];
+    };
     if (ctx->host_fn) {  // debug transport: synchronous host staging
         const int64_t ns = plan->send_off[nn], nr = plan->recv_off[nn];
         ctx->h_send.resize(ns + 1);
@@ -158,8 +163,10 @@ int exchange_on(const pamg_plan* plan, double* x, hipStream_t s) {
         for (int k = 0; k < nn; ++k) {
             sc[k] = plan->send_off[k + 1] - plan->send_off[k];
             rc[k] = plan->recv_off[k + 1] - plan->recv_off[k];
+            if (sc[k])
+                HIPC(hipMemcpyAsync(ctx->h_send.data() + plan->send_off[k], send_ptr(k),
+                                    sizeof(double) * sc[k], hipMemcpyDeviceToHost, s));
         }
-        if (ns) HIPC(hipMemcpyAsync(ctx->h_send.data(), plan->d_sendbuf, sizeof(double) * ns, hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
         if (ctx->host_fn(ctx->host_user, 0, nn, plan->nbr.data(), sc.data(), ctx->h_send.data(), rc.data(),
                          ctx->h_recv.data()) != 0)
@@ -172,7 +179,7 @@ int exchange_on(const pamg_plan* plan, double* x, hipStream_t s) {
     for (int k = 0; k < nn; ++k) {
         const size_t sc = (size_t)(plan->send_off[k + 1] - plan->send_off[k]);
         const size_t rc = (size_t)(plan->recv_off[k + 1] - plan->recv_off[k]);
-        if (sc) NCCLC(ncclSend(plan->d_sendbuf + plan->send_off[k], sc, ncclDouble, plan->nbr[k], ctx->comm, s));
+        if (sc) NCCLC(ncclSend(send_ptr(k), sc, ncclDouble, plan->nbr[k], ctx->comm, s));
         if (rc) NCCLC(ncclRecv(x + plan->n_own + plan->recv_off[k], rc, ncclDouble, plan->nbr[k], ctx->comm, s));
     }
     NCCLC(ncclGroupEnd());
@@ -504,6 +511,15 @@ int pamg_plan_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, int n_nbr,
         if (send_idx[k] < 0 || send_idx[k] >= n_own)
             return fail(PAMG_E_ARG, "plan_create: send index %lld out of range", (long long)send_idx[k]);
         idx[k] = (int)send_idx[k];
+    }
+    p->send_run.assign(n_nbr, -1);
+    p->all_contig = true;
+    for (int k = 0; k < n_nbr; ++k) {
+        const int64_t a = p->send_off[k], e = p->send_off[k + 1];
+        bool run = e > a;
+        for (int64_t j = a + 1; run && j < e; ++j) run = idx[j] == idx[j - 1] + 1;
+        if (run) p->send_run[k] = idx[a];
+        else if (e > a) p->all_contig = false;
     }
     CHECK(dalloc(&p->d_send_idx, ns));
     CHECK(dalloc(&p->d_sendbuf, ns));
