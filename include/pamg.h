@@ -154,8 +154,10 @@ int pamg_hier_profile_read(pamg_hier* H, double* ms_per_level_op /* nlevels*6 */
 int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, const pamg_vec* b,
                      pamg_vec* y, double omega, int reps, double* avg_ms);
 
-/* Tuning knobs applied to later pamg_mat_upload calls: "rows_kernel" (0 | 1),
- * "tile_nnz" (1024 | 2048 | 4096), "tile_rows" (256 | 512), "xcd_remap" (0 | 1). */
+/* Process-wide knobs. Applied to later pamg_mat_upload calls: "rows_kernel" (0..3, kernel
+ * variant), "tile_nnz" / "tile_rows" (tile budget; the valid pairs per variant are checked),
+ * "xcd_remap", "jacobi_diag", "stream_nt", "tile_order" (0 | 1). Applied at every exchange:
+ * "poison_ghosts" (0 | 1, debug: NaN-fill the ghost slots before each exchange). */
 int pamg_set_option(const char* key, int64_t value);
 int pamg_get_option(const char* key, int64_t* value);
 

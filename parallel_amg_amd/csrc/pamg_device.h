@@ -45,6 +45,7 @@ struct Options {
     int jacobi_diag = 0;       // 1: Jacobi reads the stored diagonal (no in-tile detection)
     int stream_nt = 0;         // 1: non-temporal loads for the matrix stream (variant 1)
     int tile_order = 1;        // 1: banded XCD-blocked tile order (see build_tiles)
+    int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };
 Options& options();
 

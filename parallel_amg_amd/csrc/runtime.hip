@@ -14,11 +14,6 @@
 
 using pamg::fail;
 
-std::string& pamg::last_error() {
-    static thread_local std::string msg;
-    return msg;
-}
-
 pamg::Options& pamg::options() {
     static Options o;
     return o;
@@ -149,6 +144,10 @@ int exchange_on(const pamg_plan* plan, double* x, hipStream_t s) {
     if (nn == 0) return PAMG_OK;
     if (!ctx->comm && !ctx->host_fn)
         return fail(PAMG_E_STATE, "exchange: plan has neighbours but no communicator");
+    // debug (SURVEY §5 race detection): NaN in the ghost slots before every exchange, so a
+    // row that reads a ghost before the exchange has landed shows up as NaN
+    if (pamg::options().poison_ghosts)
+        pamg::launch_fill(plan->recv_off[nn], __builtin_nan(""), x + plan->n_own, s);
     // contiguous send lists go straight from x; the others are packed first
     if (!plan->all_contig)
         pamg::launch_pack(plan->send_off[nn], plan->d_send_idx, x, plan->d_sendbuf, s);
@@ -396,8 +395,6 @@ static int check_tile_options(const pamg::Options& o);
 
 extern "C" {
 
-const char* pamg_version(void) { return "pamg 0.1 (gfx950)"; }
-const char* pamg_last_error(void) { return pamg::last_error().c_str(); }
 
 int pamg_ctx_create(int device, pamg_ctx** out) {
     if (!out) return fail(PAMG_E_ARG, "ctx_create: out is NULL");
@@ -1141,6 +1138,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "jacobi_diag" && (value == 0 || value == 1)) o.jacobi_diag = (int)value;
     else if (k == "stream_nt" && (value == 0 || value == 1)) o.stream_nt = (int)value;
     else if (k == "tile_order" && (value == 0 || value == 1)) o.tile_order = (int)value;
+    else if (k == "poison_ghosts" && (value == 0 || value == 1)) o.poison_ghosts = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -1172,6 +1170,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "jacobi_diag") *value = o.jacobi_diag;
     else if (k == "stream_nt") *value = o.stream_nt;
     else if (k == "tile_order") *value = o.tile_order;
+    else if (k == "poison_ghosts") *value = o.poison_ghosts;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

@@ -24,7 +24,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, q):
+def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, poison, q):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), OMP_NUM_THREADS="2")
@@ -33,8 +33,11 @@ def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, q):
 
     import parallel_amg_amd as pa
     from parallel_amg_amd.partitioned import Context, PVector, mul
+    from parallel_amg_amd._lib import call
     from parallel_amg_amd.solver import AMGSolver
     try:
+        # SURVEY §5 race check: ghosts are NaN until their exchange lands
+        call("pamg_set_option", b"poison_ghosts", int(poison))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         be = pa.DistributedBackend()
         A, offs, xs = pa.generate_problem(be, kind, n)
@@ -59,20 +62,21 @@ def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kind,n,max_coarse,agglomerate", [
-    (2, "poisson3d", 20, 100, 0),       # decoupled on every level, coarsest gathered
-    (2, "poisson3d", 20, 100, 32768),   # agglomerated from level 1 on (SPEC §S7)
-    (3, "poisson2d", 60, 200, 0),
-    (3, "aniso3d", 16, 30, 600),        # agglomerated from level 2 on
-    (2, "poisson2d", 20, 1000, 0),      # one level: the distributed coarsest solve
+@pytest.mark.parametrize("world,kind,n,max_coarse,agglomerate,poison", [
+    (2, "poisson3d", 20, 100, 0, 1),       # decoupled on every level, coarsest gathered
+    (2, "poisson3d", 20, 100, 32768, 0),   # agglomerated from level 1 on (SPEC §S7)
+    (3, "poisson2d", 60, 200, 0, 1),
+    (3, "aniso3d", 16, 30, 600, 1),        # agglomerated from level 2 on
+    (2, "poisson2d", 20, 1000, 0, 0),      # one level: the distributed coarsest solve
+    (4, "poisson3d", 24, 60, 0, 1),        # four parts, interior parts with two neighbours
 ])
-def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, agglomerate, built):
+def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, agglomerate, poison, built):
     from oracle import oracle as O
     ncycles = 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, n, max_coarse, agglomerate, ncycles, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, n, max_coarse, agglomerate, ncycles, poison, q))
              for r in range(world)]
     for p in procs:
         p.start()
