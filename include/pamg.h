@@ -131,6 +131,9 @@ int pamg_hier_destroy(pamg_hier* H);
  * host debug transport cannot be captured), 0 = eager launches. A failed capture falls back
  * to eager launches (same RCCL sequence) and is reported on stderr. */
 int pamg_hier_set_graph(pamg_hier* H, int enable);
+/* V(nu1, nu2): Jacobi sweeps before / after the coarse correction (SPEC §S6; default 1, 1;
+ * 1..64). The first pre-sweep on levels >= 1 is the zero-guess form. */
+int pamg_hier_set_sweeps(pamg_hier* H, int nu1, int nu2);
 /* enabled: graph replay currently on; captured: a graph exists; failed: a capture failed. */
 int pamg_hier_graph_state(const pamg_hier* H, int* enabled, int* captured, int* failed);
 /* x <- V(x) ncycles times (SPEC §S6); res_hist (ncycles, may be NULL) gets ||b - A x||. */

@@ -45,6 +45,7 @@ def lib():
         L.orc_setup.restype = vp
         L.orc_setup.argtypes = [i64, _i64p, _i64p, _f64p, C.c_int, _i64p, dbl, C.c_int, i64, i64]
         L.orc_free.argtypes = [vp]
+        L.orc_set_sweeps.argtypes = [vp, C.c_int, C.c_int]
         L.orc_status.argtypes = [vp]
         L.orc_nlev.argtypes = [vp]
         L.orc_omega.restype = dbl
@@ -152,6 +153,10 @@ class Hierarchy:
     @property
     def nlevels(self):
         return len(self.A)
+
+    def set_sweeps(self, nu1: int, nu2: int):
+        """SPEC §S6 V(nu1, nu2) (default V(1, 1))."""
+        lib().orc_set_sweeps(self._h, int(nu1), int(nu2))
 
     def solve(self, b, ncycles, x0=None, res_hist=False):
         x = np.zeros(len(b)) if x0 is None else np.array(x0, np.float64, copy=True)

@@ -362,7 +362,11 @@ typedef struct {
     double omega[ORC_MAXL], rho[ORC_MAXL];
     double* ainv;
     int status;
+    int nu1, nu2;  /* Jacobi sweeps before / after the coarse correction (SPEC §S6); 0 = 1 */
 } ohier;
+
+/* SPEC §S6 V(nu1, nu2): sweep counts of the pre- and post-smoothing (default 1, 1). */
+void orc_set_sweeps(ohier* h, int nu1, int nu2) { h->nu1 = nu1; h->nu2 = nu2; }
 
 void orc_free(ohier* h) {
     if (!h) return;
@@ -452,15 +456,18 @@ static void vcycle(const ohier* h, int l, double* x, const double* b, int zero_g
     }
     double* t = malloc(sizeof(double) * (n + 1));
     double* r = malloc(sizeof(double) * (n + 1));
-    if (zero_guess) {
-        for (i64 i = 0; i < n; ++i) {
-            double d = diag_of(A->rp, A->col, A->val, i, i);
-            double u = b[i] - 0.0, v = h->omega[l] * u, w = v / d;
-            x[i] = 0.0 + w;
+    const int nu1 = h->nu1 > 0 ? h->nu1 : 1, nu2 = h->nu2 > 0 ? h->nu2 : 1;
+    for (int sweep = 0; sweep < nu1; ++sweep) {
+        if (zero_guess && sweep == 0) {
+            for (i64 i = 0; i < n; ++i) {
+                double d = diag_of(A->rp, A->col, A->val, i, i);
+                double u = b[i] - 0.0, v = h->omega[l] * u, w = v / d;
+                x[i] = 0.0 + w;
+            }
+        } else {
+            orc_jacobi(n, A->rp, A->col, A->val, x, b, h->omega[l], t);
+            memcpy(x, t, sizeof(double) * n);
         }
-    } else {
-        orc_jacobi(n, A->rp, A->col, A->val, x, b, h->omega[l], t);
-        memcpy(x, t, sizeof(double) * n);
     }
     orc_residual(n, A->rp, A->col, A->val, x, b, r);
     const i64 nc = h->A[l + 1].nr;
@@ -470,8 +477,10 @@ static void vcycle(const ohier* h, int l, double* x, const double* b, int zero_g
     vcycle(h, l + 1, xc, bc, 1);
     orc_spmv(n, h->P[l].rp, h->P[l].col, h->P[l].val, xc, t);
     for (i64 i = 0; i < n; ++i) x[i] = x[i] + t[i];
-    orc_jacobi(n, A->rp, A->col, A->val, x, b, h->omega[l], t);
-    memcpy(x, t, sizeof(double) * n);
+    for (int sweep = 0; sweep < nu2; ++sweep) {
+        orc_jacobi(n, A->rp, A->col, A->val, x, b, h->omega[l], t);
+        memcpy(x, t, sizeof(double) * n);
+    }
     free(t); free(r); free(bc); free(xc);
 }
 

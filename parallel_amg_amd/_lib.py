@@ -64,6 +64,7 @@ SIGNATURES = {
     "pamg_hier_create": [vp, i32, vp, vp, vp, vp, i64, vp, i32, vp, pvp],
     "pamg_hier_destroy": [vp],
     "pamg_hier_set_graph": [vp, i32],
+    "pamg_hier_set_sweeps": [vp, i32, i32],
     "pamg_hier_graph_state": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "pamg_vcycle": [vp, vp, vp, vp, i32, vp],
     "pamg_vcycle_async": [vp, vp, vp, vp, i32],

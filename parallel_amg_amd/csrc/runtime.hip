@@ -260,6 +260,7 @@ struct pamg_hier {
     // PCG workspace (level-0 layout, allocated on first use)
     double *pcg_r = nullptr, *pcg_z = nullptr, *pcg_p = nullptr, *pcg_q = nullptr;
     // profiling
+    int nu1 = 1, nu2 = 1;  // V(nu1, nu2) Jacobi sweeps (SPEC §S6)
     bool prof = false;
     std::vector<hipEvent_t> ev;
     std::vector<std::pair<int, int>> ev_tag;  // (level, op) per event pair
@@ -346,26 +347,37 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false)
     }
     H->x[0] = x;
     H->b[0] = const_cast<double*>(b);
+    // V(nu1, nu2): the pre-smoothed iterate of level l ends in t[l] or r[l] (sweeps
+    // ping-pong between them); the residual goes to the other one; the post-smoothing
+    // sweeps ping-pong between x[l] and the spare so that the last one writes x[l]
+    std::vector<double*> cur(L, nullptr), spare(L, nullptr);
     for (int l = 0; l < L - 1; ++l) {
         const pamg_mat* A = H->A[l];
-        if (l == 0 && !zero0) {
+        double *c = H->t[l], *o = H->r[l];
+        {
             ProfScope p(H, l, 0, s);
-            CHECK(apply(ctx, A, pamg::OP_JACOBI, H->x[0], H->b[0], H->t[0], H->omega[0]));
-        } else {
-            ProfScope p(H, l, 0, s);
-            pamg::launch_jacobi_zero(H->nown[l], H->b[l], A->d_diag, H->omega[l], H->t[l], s);
+            if (l == 0 && !zero0)
+                CHECK(apply(ctx, A, pamg::OP_JACOBI, H->x[0], H->b[0], c, H->omega[0]));
+            else
+                pamg::launch_jacobi_zero(H->nown[l], H->b[l], A->d_diag, H->omega[l], c, s);
+            for (int k = 1; k < H->nu1; ++k) {
+                CHECK(apply(ctx, A, pamg::OP_JACOBI, c, H->b[l], o, H->omega[l]));
+                std::swap(c, o);
+            }
         }
+        cur[l] = c;
+        spare[l] = o;
         {
             ProfScope p(H, l, 1, s);
-            CHECK(apply(ctx, A, pamg::OP_RESID, H->t[l], H->b[l], H->r[l], 0.0));
+            CHECK(apply(ctx, A, pamg::OP_RESID, c, H->b[l], o, 0.0));
         }
         {
             ProfScope p(H, l, 2, s);
             if (l + 1 == H->rep && ctx->nranks > 1) {  // into the replicated tail
-                CHECK(apply(ctx, H->R[l], pamg::OP_SPMV, H->r[l], nullptr, H->d_bsend, 0.0));
+                CHECK(apply(ctx, H->R[l], pamg::OP_SPMV, o, nullptr, H->d_bsend, 0.0));
                 CHECK(gather_rep(H, H->b[l + 1], s));
             } else {
-                CHECK(apply(ctx, H->R[l], pamg::OP_SPMV, H->r[l], nullptr, H->b[l + 1], 0.0));
+                CHECK(apply(ctx, H->R[l], pamg::OP_SPMV, o, nullptr, H->b[l + 1], 0.0));
             }
         }
     }
@@ -376,11 +388,17 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false)
     for (int l = L - 2; l >= 0; --l) {
         {
             ProfScope p(H, l, 3, s);
-            CHECK(apply(ctx, H->P[l], pamg::OP_PROLONG, H->x[l + 1], nullptr, H->t[l], 0.0));
+            CHECK(apply(ctx, H->P[l], pamg::OP_PROLONG, H->x[l + 1], nullptr, cur[l], 0.0));
         }
         {
             ProfScope p(H, l, 4, s);
-            CHECK(apply(ctx, H->A[l], pamg::OP_JACOBI, H->t[l], H->b[l], H->x[l], H->omega[l]));
+            double* in = cur[l];
+            for (int k = 0; k < H->nu2; ++k) {
+                double* out = ((H->nu2 - k) % 2 == 1) ? H->x[l] : spare[l];
+                CHECK(apply(ctx, H->A[l], pamg::OP_JACOBI, in, H->b[l], out, H->omega[l]));
+                if (out == spare[l]) spare[l] = in;
+                in = out;
+            }
         }
     }
     HIPC(hipGetLastError());
@@ -947,6 +965,19 @@ int pamg_hier_set_graph(pamg_hier* H, int enable) {
         return fail(PAMG_E_STATE, "hier_set_graph: the host debug transport cannot be graph-captured");
     H->use_graph = enable != 0;
     if (!H->use_graph) drop_graph(H);
+    return PAMG_OK;
+}
+
+int pamg_hier_set_sweeps(pamg_hier* H, int nu1, int nu2) {
+    if (!H || nu1 < 1 || nu2 < 1 || nu1 > 64 || nu2 > 64)
+        return fail(PAMG_E_ARG, "hier_set_sweeps: need 1 <= nu1, nu2 <= 64");
+    if (H->nu1 != nu1 || H->nu2 != nu2) {
+        (void)hipSetDevice(H->ctx->device);
+        (void)hipStreamSynchronize(H->ctx->s_comp);
+        drop_graph(H);  // the captured cycle has the old sweep counts
+    }
+    H->nu1 = nu1;
+    H->nu2 = nu2;
     return PAMG_OK;
 }
 

@@ -55,6 +55,10 @@ class AMGSolver:
     def set_graph(self, enable: bool):
         call("pamg_hier_set_graph", self._h, int(bool(enable)))
 
+    def set_sweeps(self, nu1: int, nu2: int):
+        """V(nu1, nu2) weighted-Jacobi sweeps (SPEC §S6; default V(1, 1))."""
+        call("pamg_hier_set_sweeps", self._h, int(nu1), int(nu2))
+
     def graph_state(self) -> dict:
         e, c, f = C.c_int(), C.c_int(), C.c_int()
         call("pamg_hier_graph_state", self._h, C.byref(e), C.byref(c), C.byref(f))

@@ -207,3 +207,33 @@ def test_graph_equals_eager(ctx):
     assert np.array_equal(bits(out[0]), bits(out[1]))
     prof = S.profile(S.new_vector(), b, 2)
     assert prof.shape == (H.nlevels, 6) and prof[0, 4] > 0
+
+
+@pytest.mark.parametrize("nu1,nu2", [(2, 1), (1, 2), (2, 2), (3, 1), (3, 4)])
+def test_vcycle_sweeps_bit_exact(ctx, nu1, nu2):
+    """SPEC §S6 V(nu1, nu2): pre/post sweep ping-pong on the device vs the oracle's loops."""
+    kind, n, mc = "poisson3d", 16, 100
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, kind, n)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=mc))
+    S = AMGSolver(ctx, H)
+    S.set_sweeps(nu1, nu2)
+    b = PVector(ctx, S.A[0].nrows)
+    mul(b, S.A[0], PVector(ctx, S.A[0].nrows, 0, xs[0]))
+    Ao = O.generate(kind, n, n, n)
+    bo = O.spmv(Ao, O.xstar(Ao.nrows))
+    Ho = O.setup(Ao, max_coarse=mc)
+    Ho.set_sweeps(nu1, nu2)
+    xo, ho = Ho.solve(bo, 4, res_hist=True)
+    for graph in (True, False):
+        S.set_graph(graph)
+        x = S.new_vector()
+        hist = S.vcycle(x, b, 4, res_hist=True)
+        assert np.array_equal(bits(x.own_values()), bits(xo))
+        np.testing.assert_allclose(hist, ho, rtol=1e-12)
+    # more smoothing per cycle converges faster per cycle than V(1,1)
+    Ho.set_sweeps(1, 1)
+    _, h11 = Ho.solve(bo, 4, res_hist=True)
+    assert ho[-1] < h11[-1]
+    with pytest.raises(PamgError):
+        S.set_sweeps(0, 1)
