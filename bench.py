@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--cpu-cycles", type=int, default=1)
     ap.add_argument("--transport", choices=["rccl", "host"], default="rccl",
                     help="host = debug transport (ranks may share one GPU; not a perf mode)")
+    ap.add_argument("--sweeps", default="1,1", help="nu1,nu2 of the V(nu1,nu2) cycle (SPEC S6)")
     ap.add_argument("--setup", choices=["gpu", "host"], default="gpu",
                     help="where the Galerkin products of the setup run (same bits either way)")
     args = ap.parse_args()
@@ -109,6 +110,8 @@ def main():
     # hipGraph replay on one part; multi-part cycles run eagerly (RCCL + host-side exchange)
     use_graph = (not args.no_graph) and (world == 1 or args.transport == "rccl")
     S = AMGSolver(ctx, H, part=rank, graph=use_graph)
+    nu1, nu2 = (int(v) for v in args.sweeps.split(","))
+    S.set_sweeps(nu1, nu2)
     A0 = S.A[0]
     xst = PVector(ctx, A0.n_own_cols, A0.n_ghost, xs[rank])
     b = PVector(ctx, A0.nrows)
@@ -155,7 +158,7 @@ def main():
     kprof = max(3, min(args.steps, 10))
     prof = S.profile(x, b, kprof) / kprof          # ms per V-cycle per (level, op)
     obytes = S.op_bytes()                           # algorithmic bytes per (level, op)
-    post_ms = float(prof[0, 4]) if S.L > 1 else float(prof[0, 5])
+    post_ms = float(prof[0, 4]) / nu2 if S.L > 1 else float(prof[0, 5])  # one sweep
     post_bytes = float(obytes[0, 4]) if S.L > 1 else float(obytes[0, 5])
     achieved = post_bytes / (post_ms * 1e-3) / 1e9
     spmv_ms = ctypes_bench_spmv(ctx, A0, x, S)
@@ -172,7 +175,7 @@ def main():
     # ---- CPU baseline: the oracle V-cycle on this same hierarchy (rank 0, N=1) --------
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
-        cpu = cpu_baseline(H, xs[0], args.cpu_cycles, log)
+        cpu = cpu_baseline(H, xs[0], args.cpu_cycles, log, (nu1, nu2))
 
     # HBM traffic of the dominant kernel from the committed rocprofv3 PMC passes of this exact
     # workload (tools/pmc_traffic.py; counters cannot be read from inside the process)
@@ -200,7 +203,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (SPEC.md §S2 grid operator, b = A x*, x0 = 0)",
             "config": {
-                "workload": f"{workload}, SA-AMG V(1,1) weighted-Jacobi, "
+                "workload": f"{workload}, SA-AMG V({nu1},{nu2}) weighted-Jacobi, "
                             f"{world} part(s)",
                 "n": gl_rows, "nnz_fine": int(sum(H.levels[0][p].A.nnz for p in H.levels[0])) if world == 1
                 else None, "levels": S.L, "max_coarse": args.max_coarse,
@@ -241,12 +244,13 @@ def ctypes_bench_spmv(ctx, A0, x, S, reps=20) -> float:
     return ms.value
 
 
-def cpu_baseline(H, xstar, ncycles, log):
+def cpu_baseline(H, xstar, ncycles, log, sweeps=(1, 1)):
     """Time the CPU oracle's V-cycle (oracle/pamg_oracle.c, OpenMP) on the same hierarchy."""
     from oracle import oracle as O
     lv = [H.levels[l][0] for l in range(H.nlevels)]
     Ho = O.hierarchy_from_levels([p.A for p in lv], [p.P for p in lv[:-1]], [p.R for p in lv[:-1]],
                                  [p.omega for p in lv], H.ainv)
+    Ho.set_sweeps(*sweeps)
     A0 = lv[0].A
     x = np.zeros(A0.nrows)
     rhs = np.ascontiguousarray(xstar)  # any rhs: the cycle's work does not depend on values
