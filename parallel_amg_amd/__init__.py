@@ -6,7 +6,8 @@ kernels for SpMV / residual / weighted Jacobi / restriction / prolongation, RCCL
 exchange, and a host smoothed-aggregation setup.
 """
 from .backend import DistributedBackend, SequentialBackend  # noqa: F401
+from .checkpoint import load_hierarchy, save_hierarchy  # noqa: F401
 from .hierarchy import SAParams, build_hierarchy, generate_problem, load_problem  # noqa: F401
 
 __all__ = ["SequentialBackend", "DistributedBackend", "SAParams", "build_hierarchy",
-           "generate_problem", "load_problem"]
+           "generate_problem", "load_problem", "save_hierarchy", "load_hierarchy"]
