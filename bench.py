@@ -162,7 +162,7 @@ def main():
     post_bytes = float(obytes[0, 4]) if S.L > 1 else float(obytes[0, 5])
     achieved = post_bytes / (post_ms * 1e-3) / 1e9
     spmv_ms = ctypes_bench_spmv(ctx, A0, x, S)
-    spmv_bytes = S.rowsum_bytes(A0.nnz, A0.nrows, A0.n_own_cols + A0.n_ghost, 0)
+    spmv_bytes = S.rowsum_bytes(A0, 0)
     spmv_gbps = spmv_bytes / (spmv_ms * 1e-3) / 1e9
     hist = S.vcycle(x, b, 1, res_hist=True)
 

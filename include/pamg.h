@@ -102,6 +102,10 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols_local, const int
                     const pamg_plan* col_plan, pamg_mat** out);
 int pamg_mat_destroy(pamg_mat* A);
 int pamg_mat_info(const pamg_mat* A, int64_t* nrows, int64_t* ncols_local, int64_t* nnz);
+/* Bytes of matrix data one row operation streams in the layout chosen at upload: 8 B values +
+ * 4 B (or 3 B in 24-bit column tiles) columns per nonzero, 4 B row pointers, tile descriptors
+ * (+ 4-B column bases). The algorithmic byte model of the roofline adds the vectors. */
+int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
 int pamg_spmv(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, pamg_vec* y);

@@ -58,6 +58,7 @@ SIGNATURES = {
     "pamg_mat_upload": [vp, i64, i64, vp, vp, i32, vp, i32, vp, pvp],
     "pamg_mat_destroy": [vp],
     "pamg_mat_info": [vp, pi64, pi64, pi64],
+    "pamg_mat_stream_bytes": [vp, pi64],
     "pamg_spmv": [vp, vp, vp, vp],
     "pamg_residual": [vp, vp, vp, vp, vp, pdbl],
     "pamg_jacobi": [vp, vp, vp, vp, vp, dbl, i32],

@@ -126,12 +126,15 @@ __device__ __forceinline__ T stream_load(const T* p, std::false_type) {
     return *p;
 }
 
-template <int OP, int TNNZ, int TROWS, bool XCD, bool NT = false, int BS = kBlock>
+template <int OP, int TNNZ, int TROWS, bool XCD, bool NT = false, int BS = kBlock, bool C24 = false>
 __global__ __launch_bounds__(BS) void k_rows_tile2(
     const int4* __restrict__ tiles, int ntiles, const int* __restrict__ rowptr,
     const int* __restrict__ col, const double* __restrict__ val, const double* __restrict__ x,
     const double* __restrict__ b, double* __restrict__ y, double omega,
-    const double* __restrict__ diag) {
+    const double* __restrict__ diag, const uint16_t* __restrict__ clo = nullptr,
+    const uint8_t* __restrict__ chi = nullptr, const int* __restrict__ tbase = nullptr) {
+    // C24: the column stream is 3 B/nonzero — per-tile base + 16-bit low part (8 B per lane)
+    // + 8-bit high part (4 B per lane) instead of the 16-B int4 of 32-bit ids
     // diag != nullptr (Jacobi only): a_ii from the stored diagonal instead of the in-tile
     // detection (same value, SPEC §S3; trades 8 B/row of reads for one barrier).
     constexpr int G = TNNZ / (4 * BS);
@@ -160,7 +163,17 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
         // NT: the once-read matrix stream goes non-temporal so the x lines (reused by the
         // z+-1 / y+-1 neighbour rows) keep their place in the XCD's L2
         using nt = std::integral_constant<bool, NT>;
-        c4[j] = stream_load(reinterpret_cast<const int4*>(col + gs), nt{});
+        if constexpr (C24) {
+            const ushort4 lo = *reinterpret_cast<const ushort4*>(clo + gs);
+            const uchar4 hi = *reinterpret_cast<const uchar4*>(chi + gs);
+            const int cb = tbase[bid];
+            c4[j] = make_int4(cb + (int)((uint32_t)lo.x | ((uint32_t)hi.x << 16)),
+                              cb + (int)((uint32_t)lo.y | ((uint32_t)hi.y << 16)),
+                              cb + (int)((uint32_t)lo.z | ((uint32_t)hi.z << 16)),
+                              cb + (int)((uint32_t)lo.w | ((uint32_t)hi.w << 16)));
+        } else {
+            c4[j] = stream_load(reinterpret_cast<const int4*>(col + gs), nt{});
+        }
         va[j] = stream_load(reinterpret_cast<const double2*>(val + gs), nt{});
         vb[j] = stream_load(reinterpret_cast<const double2*>(val + gs + 2), nt{});
     }
@@ -629,6 +642,10 @@ void launch_tile2(const pamg_mat& A, const TileSet& ts, const double* x, const d
     } else if (A.stream_nt) {
         k_rows_tile2<OP, TNNZ, TROWS, false, true><<<ts.n_short, kBlock, 0, s>>>(
             ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg);
+    } else if (ts.c24 && A.d_clo) {
+        k_rows_tile2<OP, TNNZ, TROWS, false, false, kBlock, true><<<ts.n_short, kBlock, 0, s>>>(
+            ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg, A.d_clo,
+            A.d_chi, ts.d_base);
     } else {
         k_rows_tile2<OP, TNNZ, TROWS, false><<<ts.n_short, kBlock, 0, s>>>(
             ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg);

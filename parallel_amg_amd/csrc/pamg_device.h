@@ -32,6 +32,11 @@ struct TileSet {
     int* d_long = nullptr;  // single rows
     int n_long = 0;
     int tile_nnz = kTileNnz, tile_rows = kTileRows;  // budget the tiles were cut with
+    // 24-bit column stream: every tile's columns lie in [base, base + 2^24), so a column is
+    // stored as base (per tile) + 16-bit low part (pamg_mat::d_clo) + 8-bit high part (d_chi)
+    int* d_base = nullptr;  // per short tile (same order as d_short), when c24
+    bool c24 = false;
+    int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
 };
 
 // Tuning knobs (pamg_set_option): kernel variant and tile budget used by later uploads.
@@ -45,6 +50,7 @@ struct Options {
     int jacobi_diag = 0;       // 1: Jacobi reads the stored diagonal (no in-tile detection)
     int stream_nt = 0;         // 1: non-temporal loads for the matrix stream (variant 1)
     int tile_order = 1;        // 1: banded XCD-blocked tile order (see build_tiles)
+    int col24 = 1;             // 1: 3-byte column stream where every tile's span fits 2^24
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };
 Options& options();
@@ -90,11 +96,14 @@ struct pamg_mat {
     int64_t nrows = 0, ncols = 0, nnz = 0;
     int* d_rowptr = nullptr;
     int* d_col = nullptr;
+    uint16_t* d_clo = nullptr;  // 24-bit column stream (TileSet::c24): low 16 bits
+    uint8_t* d_chi = nullptr;   //   and high 8 bits of (column - tile base)
     double* d_val = nullptr;
     double* d_diag = nullptr;  // a_ii for square matrices (zero-guess Jacobi), else null
     const pamg_plan* plan = nullptr;
     pamg::TileSet interior;  // rows with own columns only (overlap with the exchange)
     pamg::TileSet boundary;  // rows with >= 1 ghost column
+    int64_t stream_bytes = 0;  // matrix bytes one apply reads (values, columns, row pointers, tiles)
     int rows_kernel = 1;     // variant fixed at upload (pamg::Options)
     int xcd_remap = 0;
     int jacobi_diag = 0;

@@ -87,7 +87,8 @@ static std::vector<int4> xcd_band_order(const std::vector<int4>& tiles, int64_t 
 }
 
 int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
-                pamg::TileSet* ts, int64_t band = 0) {
+                pamg::TileSet* ts, int64_t band, const std::vector<int>& ci,
+                std::vector<uint16_t>* lo, std::vector<uint8_t>* hi) {
     const auto& opt = pamg::options();
     const int tnnz = opt.tile_nnz, trows = opt.tile_rows;
     ts->tile_nnz = tnnz;
@@ -116,13 +117,48 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
             ++j;
         }
         tiles.push_back(make_int4(r, end, (int)rp[r], (int)rp[end]));
+        ts->nnz_short += rp[end] - rp[r];
         i = j;
     }
+    for (int r : longr) ts->nnz_long += rp[r + 1] - rp[r];
     if (opt.tile_order == 1 && band >= 64 && tiles.size() >= 64) tiles = xcd_band_order(tiles, band);
     ts->n_short = (int)tiles.size();
     ts->n_long = (int)longr.size();
     CHECK(dalloc(&ts->d_short, ts->n_short));
     CHECK(dalloc(&ts->d_long, ts->n_long));
+    // 24-bit column stream: usable when every tile's columns span < 2^24 (banded matrices;
+    // not for tiles that reach the ghost columns of a large part)
+    ts->c24 = false;
+    if (opt.col24 && !tiles.empty()) {
+        std::vector<int> base(tiles.size(), 0);
+        bool fits = true;
+        for (size_t t = 0; t < tiles.size() && fits; ++t) {
+            const int4 d = tiles[t];
+            int mn = INT32_MAX, mx = 0;
+            for (int k = d.z; k < d.w; ++k) {
+                mn = std::min(mn, ci[k]);
+                mx = std::max(mx, ci[k]);
+            }
+            if (d.w == d.z) mn = mx = 0;
+            base[t] = mn;
+            fits = (int64_t)mx - mn < (int64_t(1) << 24);
+        }
+        if (fits) {
+            if (lo->empty()) {
+                lo->assign(ci.size(), 0);
+                hi->assign(ci.size(), 0);
+            }
+            for (size_t t = 0; t < tiles.size(); ++t)
+                for (int k = tiles[t].z; k < tiles[t].w; ++k) {
+                    const uint32_t dlt = (uint32_t)(ci[k] - base[t]);
+                    (*lo)[k] = (uint16_t)(dlt & 0xffffu);
+                    (*hi)[k] = (uint8_t)(dlt >> 16);
+                }
+            CHECK(dalloc(&ts->d_base, (int64_t)tiles.size()));
+            HIPC(hipMemcpy(ts->d_base, base.data(), sizeof(int) * base.size(), hipMemcpyHostToDevice));
+            ts->c24 = true;
+        }
+    }
     if (ts->n_short)
         HIPC(hipMemcpy(ts->d_short, tiles.data(), sizeof(int4) * tiles.size(), hipMemcpyHostToDevice));
     if (ts->n_long)
@@ -133,6 +169,8 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
 void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_short);
     dfree(ts.d_long);
+    dfree(ts.d_base);
+    ts.c24 = false;
     ts.n_short = ts.n_long = 0;
 }
 
@@ -742,8 +780,24 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         CHECK(dalloc(&A->d_diag, nrows));
         HIPC(hipMemcpy(A->d_diag, diag.data(), sizeof(double) * nrows, hipMemcpyHostToDevice));
     }
-    CHECK(build_tiles(rp, inner, &A->interior, band));
-    CHECK(build_tiles(rp, bnd, &A->boundary, band));
+    std::vector<uint16_t> lo;
+    std::vector<uint8_t> hi;
+    CHECK(build_tiles(rp, inner, &A->interior, band, ci, &lo, &hi));
+    CHECK(build_tiles(rp, bnd, &A->boundary, band, ci, &lo, &hi));
+    // the bytes one apply streams: values, columns (3 B in 24-bit tile sets), row pointers,
+    // tile descriptors (+ bases)
+    A->stream_bytes = 8 * nnz + 4 * (nrows + 1);
+    for (const pamg::TileSet* t : {&A->interior, &A->boundary})
+        A->stream_bytes += (t->c24 ? 3 : 4) * t->nnz_short + 4 * t->nnz_long +
+                           (16 + (t->c24 ? 4 : 0)) * (int64_t)t->n_short + 4 * (int64_t)t->n_long;
+    if (!lo.empty()) {  // padded like d_col
+        lo.resize(nnz + kVecPad, 0);
+        hi.resize(nnz + kVecPad, 0);
+        CHECK(dalloc(&A->d_clo, nnz + kVecPad));
+        CHECK(dalloc(&A->d_chi, nnz + kVecPad));
+        HIPC(hipMemcpy(A->d_clo, lo.data(), sizeof(uint16_t) * lo.size(), hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(A->d_chi, hi.data(), sizeof(uint8_t) * hi.size(), hipMemcpyHostToDevice));
+    }
     *out = A.release();
     return PAMG_OK;
 }
@@ -754,6 +808,8 @@ int pamg_mat_destroy(pamg_mat* A) {
     (void)hipStreamSynchronize(A->ctx->s_comp);
     dfree(A->d_rowptr);
     dfree(A->d_col);
+    dfree(A->d_clo);
+    dfree(A->d_chi);
     dfree(A->d_val);
     dfree(A->d_diag);
     free_tiles(A->interior);
@@ -767,6 +823,12 @@ int pamg_mat_info(const pamg_mat* A, int64_t* nrows, int64_t* ncols, int64_t* nn
     if (nrows) *nrows = A->nrows;
     if (ncols) *ncols = A->ncols;
     if (nnz) *nnz = A->nnz;
+    return PAMG_OK;
+}
+
+int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes) {
+    if (!A || !bytes) return fail(PAMG_E_ARG, "mat_stream_bytes: bad args");
+    *bytes = A->stream_bytes;
     return PAMG_OK;
 }
 
@@ -1170,6 +1232,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "stream_nt" && (value == 0 || value == 1)) o.stream_nt = (int)value;
     else if (k == "tile_order" && (value == 0 || value == 1)) o.tile_order = (int)value;
     else if (k == "poison_ghosts" && (value == 0 || value == 1)) o.poison_ghosts = (int)value;
+    else if (k == "col24" && (value == 0 || value == 1)) o.col24 = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -1202,6 +1265,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "stream_nt") *value = o.stream_nt;
     else if (k == "tile_order") *value = o.tile_order;
     else if (k == "poison_ghosts") *value = o.poison_ghosts;
+    else if (k == "col24") *value = o.col24;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

@@ -238,6 +238,9 @@ class PSparseMatrix:
         self.nrows, self.ncols, self.nnz = M.nrows, ncols, M.nnz
         self.n_own_cols = plan.n_own if plan is not None else ncols
         self.n_ghost = plan.n_ghost if plan is not None else 0
+        sb = C.c_int64()
+        call("pamg_mat_stream_bytes", h, C.byref(sb))
+        self.stream_bytes = sb.value  # matrix bytes one row operation reads (uploaded layout)
 
     @property
     def handle(self):

@@ -101,10 +101,12 @@ class AMGSolver:
 
     # ---- algorithmic byte model (SURVEY.md §8d / BASELINE.md) --------------------------
     @staticmethod
-    def rowsum_bytes(nnz: int, nrows: int, ncols_read: int, extra_vec_rw: int) -> int:
-        """12 B/nnz (fp64 value + int32 column) + 4 (n+1) row pointers + 8 B per x entry read
-        once + 8 B per output row + 8 B per extra own vector read or written."""
-        return 12 * nnz + 4 * (nrows + 1) + 8 * ncols_read + 8 * nrows + 8 * nrows * extra_vec_rw
+    def rowsum_bytes(M, extra_vec_rw: int) -> int:
+        """Algorithmic bytes of one row operation of the device matrix M: the
+        matrix stream in its uploaded layout (pamg_mat_stream_bytes: 8 B values + 4 B, or 3 B
+        in 24-bit column tiles, columns per nonzero + row pointers + tile descriptors) + 8 B per
+        x entry read once + 8 B per output row + 8 B per extra own vector read or written."""
+        return M.stream_bytes + 8 * (M.n_own_cols + M.n_ghost) + 8 * M.nrows + 8 * M.nrows * extra_vec_rw
 
     def op_bytes(self) -> np.ndarray:
         """Algorithmic bytes per (level, op) of one V-cycle on this part (L x 6)."""
@@ -116,13 +118,12 @@ class AMGSolver:
                 out[l, 5] = 8 * nc * n + 8 * nc + 8 * n
                 continue
             A, P, R = self.A[l], self.P[l], self.R[l]
-            ncx = A.n_own_cols + A.n_ghost
             # jacobi: x (read once), b, x' ; zero-guess form on l >= 1 reads b, diag, writes x'
-            out[l, 0] = self.rowsum_bytes(A.nnz, n, ncx, 1) if l == 0 else 24 * n
-            out[l, 1] = self.rowsum_bytes(A.nnz, n, ncx, 1)
-            out[l, 2] = self.rowsum_bytes(R.nnz, R.nrows, R.n_own_cols + R.n_ghost, 0)
-            out[l, 3] = self.rowsum_bytes(P.nnz, n, P.n_own_cols + P.n_ghost, 1)
-            out[l, 4] = self.rowsum_bytes(A.nnz, n, ncx, 1)
+            out[l, 0] = self.rowsum_bytes(A, 1) if l == 0 else 24 * n
+            out[l, 1] = self.rowsum_bytes(A, 1)
+            out[l, 2] = self.rowsum_bytes(R, 0)
+            out[l, 3] = self.rowsum_bytes(P, 1)
+            out[l, 4] = self.rowsum_bytes(A, 1)
         return out
 
     def __del__(self):

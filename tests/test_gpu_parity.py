@@ -53,16 +53,19 @@ LENGTHS = {
     "empty_rows": [0] * 100,
 }
 
-# (rows_kernel, tile_nnz, tile_rows, xcd_remap) — every tuning configuration must be bit-exact
-TILE_CONFIGS = [(0, 2048, 256, 0, 0, 0, 0), (1, 2048, 256, 0, 0, 0, 0), (1, 2048, 256, 1, 1, 0, 0),
-                (1, 1024, 256, 0, 0, 0, 0), (1, 1024, 256, 0, 0, 1, 1), (1, 4096, 256, 0, 0, 1, 0),
-                (1, 4096, 512, 1, 0, 0, 0), (2, 256, 64, 0, 0, 0, 0), (2, 512, 64, 0, 0, 0, 1),
-                (2, 512, 64, 0, 1, 0, 0), (2, 1024, 64, 0, 0, 0, 0), (3, 1024, 256, 0, 0, 0, 1),
-                (3, 2048, 256, 0, 0, 0, 0), (1, 512, 128, 0, 0, 0, 1), (1, 2048, 512, 0, 0, 0, 1)]
-OPT_KEYS = ("rows_kernel", "tile_nnz", "tile_rows", "xcd_remap", "jacobi_diag", "stream_nt", "tile_order")
+# (rows_kernel, tile_nnz, tile_rows, xcd_remap, jacobi_diag, stream_nt, tile_order, col24):
+# every tuning configuration must be bit-exact
+TILE_CONFIGS = [(0, 2048, 256, 0, 0, 0, 0, 1), (1, 2048, 256, 0, 0, 0, 0, 1), (1, 2048, 256, 1, 1, 0, 0, 1),
+                (1, 1024, 256, 0, 0, 0, 0, 1), (1, 1024, 256, 0, 0, 1, 1, 1), (1, 4096, 256, 0, 0, 1, 0, 1),
+                (1, 4096, 512, 1, 0, 0, 0, 1), (2, 256, 64, 0, 0, 0, 0, 1), (2, 512, 64, 0, 0, 0, 1, 1),
+                (2, 512, 64, 0, 1, 0, 0, 1), (2, 1024, 64, 0, 0, 0, 0, 1), (3, 1024, 256, 0, 0, 0, 1, 1),
+                (3, 2048, 256, 0, 0, 0, 0, 1), (1, 512, 128, 0, 0, 0, 1, 1), (1, 2048, 512, 0, 0, 0, 1, 1),
+                (1, 1024, 256, 0, 0, 0, 1, 0), (1, 1024, 256, 0, 1, 0, 1, 1)]
+OPT_KEYS = ("rows_kernel", "tile_nnz", "tile_rows", "xcd_remap", "jacobi_diag", "stream_nt", "tile_order",
+            "col24")
 
 
-@pytest.fixture(params=TILE_CONFIGS, ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}".format(*c))
+@pytest.fixture(params=TILE_CONFIGS, ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}".format(*c))
 def tile_cfg(request, built):
     import ctypes
     from parallel_amg_amd._lib import call
@@ -237,3 +240,23 @@ def test_vcycle_sweeps_bit_exact(ctx, nu1, nu2):
     assert ho[-1] < h11[-1]
     with pytest.raises(PamgError):
         S.set_sweeps(0, 1)
+
+
+def test_stream_bytes_layout(ctx):
+    """pamg_mat_stream_bytes: 12 B/nnz + row pointers + 16-B tile descriptors in the 32-bit
+    layout; 3-B columns (+ a 4-B base per tile) in the 24-bit one (roofline byte model)."""
+    import ctypes
+    from parallel_amg_amd._lib import call
+    M = O.generate("poisson3d", 16, 16, 16)
+    n, nnz = M.nrows, len(M.col)
+    got = {}
+    for c24 in (0, 1):
+        call("pamg_set_option", b"col24", c24)
+        try:
+            A, _h = upload(ctx, M)
+        finally:
+            call("pamg_set_option", b"col24", 1)
+        got[c24] = A.stream_bytes
+    nt, rem = divmod(got[0] - 12 * nnz - 4 * (n + 1), 16)
+    assert rem == 0 and nt > 0
+    assert got[1] == 11 * nnz + 4 * (n + 1) + 20 * nt

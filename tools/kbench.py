@@ -44,7 +44,7 @@ def bench(ctx, M, op, reps):
     call("pamg_bench_rowop", ctx.handle, M.handle, op, x.handle, b.handle, y.handle, 0.6, reps,
          C.byref(ms))
     extra = {0: 0, 1: 1, 2: 1, 3: 1}[op]
-    byt = AMGSolver.rowsum_bytes(M.nnz, M.nrows, M.n_own_cols + M.n_ghost, extra)
+    byt = AMGSolver.rowsum_bytes(M, extra)
     return ms.value, byt
 
 
@@ -53,7 +53,8 @@ def main():
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--levels", type=int, default=1)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--configs", default="0:2048:256:0,1:2048:256:0,1:2048:256:1,1:4096:256:0,1:4096:512:0,1:1024:256:0")
+    ap.add_argument("--configs", default="1:1024:256:0:0:0:1:1,1:1024:256:0:0:0:1:0",
+                    help="kern:tile_nnz:tile_rows:xcd:jacobi_diag:stream_nt:tile_order:col24,...")
     ap.add_argument("--ops", default="0,2")
     args = ap.parse_args()
     ctx = Context(0)
@@ -71,10 +72,11 @@ def main():
     print(f"# setup {time.time() - t:.1f}s", file=sys.stderr, flush=True)
     ops = [int(o) for o in args.ops.split(",")]
     for cfg in args.configs.split(","):
-        vals = [int(v) for v in cfg.split(":")] + [0, 0, 0]
-        kern, tnnz, trows, xcd, jd, nt, order = vals[:7]
+        given = [int(v) for v in cfg.split(":")]
+        vals = given + [1, 1024, 256, 0, 0, 0, 0, 1][len(given):]  # defaults for missing fields
+        kern, tnnz, trows, xcd, jd, nt, order, c24 = vals[:8]
         set_opts(rows_kernel=kern, tile_nnz=tnnz, tile_rows=trows, xcd_remap=xcd, jacobi_diag=jd,
-                 stream_nt=nt, tile_order=order)
+                 stream_nt=nt, tile_order=order, col24=c24)
         for name, (M, plan) in mats.items():
             D = PSparseMatrix(ctx, M, plan)
             for op in ops:
