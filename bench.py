@@ -179,11 +179,15 @@ def main():
 
     # HBM traffic of the dominant kernel from the committed rocprofv3 PMC passes of this exact
     # workload (tools/pmc_traffic.py; counters cannot be read from inside the process)
+    # (only when the record was measured on the same column layout as this run)
+    c24 = A0.stream_bytes < 12 * A0.nnz
+    kname = ("k_rows_tile2<2, 1024, 256, false, false, 256, true>" if c24
+             else "k_rows_tile2<2, 1024, 256, false, false>")
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "r01_pmc", "traffic_jacobi_512.json")
     if (not args.matrix and args.kind == "poisson3d" and args.grid == 512 and world == 1
             and os.path.exists(pmc)):
-        rec = json.load(open(pmc))
+        rec = [r for r in json.load(open(pmc)) if r["kernel"] == kname]
         if rec:
             traffic, traffic_src = float(rec[0]["traffic_bytes"]), os.path.relpath(pmc, ROOT)
 
@@ -216,7 +220,8 @@ def main():
             "fine_spmv_GBps": round(spmv_gbps, 1),
             "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
             "roofline": {
-                "kernel": "k_rows_tile2<OP_JACOBI,1024,256> (level-0 post-smoothing Jacobi)",
+                "kernel": kname + " (level-0 post-smoothing Jacobi"
+                          + (", 24-bit column stream)" if c24 else ")"),
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic, "traffic_source": traffic_src,

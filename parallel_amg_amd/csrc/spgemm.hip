@@ -251,9 +251,15 @@ __device__ inline int bin_of(int64_t m, int64_t nc) {
     return b;
 }
 
-// product count m_i, bin (kBins = empty row) and bin population
-__global__ void k_row_products(const int64_t* xrp, const int32_t* xr, const int64_t* yrp,
-                               int64_t n, int64_t nc, int64_t* m, uint8_t* bin, int* bincnt) {
+// product count m_i, bin (kBins = empty row) and bin population. The bin counters are hit by
+// every row, so each block histograms its rows in LDS and adds once per bin (a global atomic
+// per row serialised on a handful of addresses: 0.24 s at 134M rows).
+__global__ __launch_bounds__(256) void k_row_products(const int64_t* xrp, const int32_t* xr,
+                                                      const int64_t* yrp, int64_t n, int64_t nc,
+                                                      int64_t* m, uint8_t* bin, int* bincnt) {
+    __shared__ int hist[kBins + 1];
+    if (threadIdx.x <= kBins) hist[threadIdx.x] = 0;
+    __syncthreads();
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         int64_t s = 0;
@@ -261,17 +267,33 @@ __global__ void k_row_products(const int64_t* xrp, const int32_t* xr, const int6
         m[i] = s;
         const int b = s == 0 ? kBins : bin_of(s, nc);
         bin[i] = (uint8_t)b;
-        atomicAdd(&bincnt[b], 1);
+        atomicAdd(&hist[b], 1);
     }
+    __syncthreads();
+    if (threadIdx.x <= kBins && hist[threadIdx.x]) atomicAdd(&bincnt[threadIdx.x], hist[threadIdx.x]);
 }
 
-__global__ void k_scatter_bins(const uint8_t* bin, int64_t n, const int64_t* binoff, int* cursor,
-                               int32_t* lists) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
+// rows -> per-bin lists: each block reserves one range per bin, then places its rows in it
+// (order inside a bin is irrelevant: every row's output position comes from the row pointers)
+__global__ __launch_bounds__(256) void k_scatter_bins(const uint8_t* bin, int64_t n,
+                                                      const int64_t* binoff, int* cursor,
+                                                      int32_t* lists) {
+    __shared__ int cnt[kBins + 1], base[kBins + 1];
+    if (threadIdx.x <= kBins) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = i0; i < n; i += step) atomicAdd(&cnt[bin[i]], 1);
+    __syncthreads();
+    if (threadIdx.x < kBins) {
+        base[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]) : 0;
+        cnt[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    for (int64_t i = i0; i < n; i += step) {
         const int b = bin[i];
         if (b >= kBins) continue;
-        lists[binoff[b] + atomicAdd(&cursor[b], 1)] = (int32_t)i;
+        lists[binoff[b] + base[b] + atomicAdd(&cnt[b], 1)] = (int32_t)i;
     }
 }
 

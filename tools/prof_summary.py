@@ -20,7 +20,8 @@ def main():
     a = ap.parse_args()
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(a.trace)):
-        name = r["Kernel_Name"].replace("pamg::(anonymous namespace)::", "").replace("void ", "")
+        name = (r["Kernel_Name"].replace("pamg::(anonymous namespace)::", "")
+                .replace("(anonymous namespace)::", "").replace("void ", ""))
         name = re.sub(r"\(.*", "", name)
         key = (name, int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"])))
         agg[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
