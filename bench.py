@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--transport", choices=["rccl", "host"], default="rccl",
                     help="host = debug transport (ranks may share one GPU; not a perf mode)")
     ap.add_argument("--sweeps", default="1,1", help="nu1,nu2 of the V(nu1,nu2) cycle (SPEC S6)")
+    ap.add_argument("--value-dict", action="store_true",
+                    help="opt-in per-tile 4-bit value dictionaries where a tile has <= 16 distinct "
+                         "values (exact; not the default layout)")
     ap.add_argument("--setup", choices=["gpu", "host"], default="gpu",
                     help="where the Galerkin products of the setup run (same bits either way)")
     args = ap.parse_args()
@@ -75,6 +78,7 @@ def main():
     from parallel_amg_amd.solver import OPS, AMGSolver
 
     _lib.lib()  # fail loudly if libpamg.so is missing
+    _lib.call("pamg_set_option", b"value_dict", int(args.value_dict))
     ndev = torch.cuda.device_count()
     dev = local % max(ndev, 1)
     torch.cuda.set_device(dev)
@@ -181,7 +185,9 @@ def main():
     # workload (tools/pmc_traffic.py; counters cannot be read from inside the process)
     # (only when the record was measured on the same column layout as this run)
     c24 = A0.stream_bytes < 12 * A0.nnz
-    kname = ("k_rows_tile2<2, 1024, 256, false, false, 256, true>" if c24
+    vd = A0.stream_bytes < 10 * A0.nnz
+    kname = ("k_rows_tile2<2, 1024, 256, false, false, 256, true, true>" if vd
+             else "k_rows_tile2<2, 1024, 256, false, false, 256, true>" if c24
              else "k_rows_tile2<2, 1024, 256, false, false>")
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "r01_pmc", "traffic_jacobi_512.json")
@@ -216,11 +222,13 @@ def main():
                 "transport": args.transport if world > 1 else None,
                 # levels >= this one are held whole on every rank (SPEC §S7 agglomeration)
                 "replicated_from_level": int(S.rep_level) if world > 1 else None,
+                "value_dict": bool(args.value_dict),
             },
             "fine_spmv_GBps": round(spmv_gbps, 1),
             "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
             "roofline": {
                 "kernel": kname + " (level-0 post-smoothing Jacobi"
+                          + (", value dictionaries" if vd else "")
                           + (", 24-bit column stream)" if c24 else ")"),
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),

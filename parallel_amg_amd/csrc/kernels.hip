@@ -126,15 +126,19 @@ __device__ __forceinline__ T stream_load(const T* p, std::false_type) {
     return *p;
 }
 
-template <int OP, int TNNZ, int TROWS, bool XCD, bool NT = false, int BS = kBlock, bool C24 = false>
+template <int OP, int TNNZ, int TROWS, bool XCD, bool NT = false, int BS = kBlock, bool C24 = false,
+          bool VD = false>
 __global__ __launch_bounds__(BS) void k_rows_tile2(
     const int4* __restrict__ tiles, int ntiles, const int* __restrict__ rowptr,
     const int* __restrict__ col, const double* __restrict__ val, const double* __restrict__ x,
     const double* __restrict__ b, double* __restrict__ y, double omega,
     const double* __restrict__ diag, const uint16_t* __restrict__ clo = nullptr,
-    const uint8_t* __restrict__ chi = nullptr, const int* __restrict__ tbase = nullptr) {
+    const uint8_t* __restrict__ chi = nullptr, const int* __restrict__ tbase = nullptr,
+    const uint8_t* __restrict__ vidx = nullptr, const double* __restrict__ vtab = nullptr) {
     // C24: the column stream is 3 B/nonzero — per-tile base + 16-bit low part (8 B per lane)
-    // + 8-bit high part (4 B per lane) instead of the 16-B int4 of 32-bit ids
+    // + 8-bit high part (4 B per lane) instead of the 16-B int4 of 32-bit ids.
+    // VD (opt-in): values are 4-bit indices (2 B per lane) into the tile's 16-value table,
+    // read through L1 (the same 128 B for every lane of the tile) — exact fp64 values.
     // diag != nullptr (Jacobi only): a_ii from the stored diagonal instead of the in-tile
     // detection (same value, SPEC §S3; trades 8 B/row of reads for one barrier).
     constexpr int G = TNNZ / (4 * BS);
@@ -156,6 +160,7 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
 
     int4 c4[G];
     double2 va[G], vb[G];
+    uint16_t vn[G];  // VD: four 4-bit value indices per lane group
 #pragma unroll
     for (int j = 0; j < G; ++j) {
         const int g = za + 4 * (tid + j * BS);
@@ -174,8 +179,12 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
         } else {
             c4[j] = stream_load(reinterpret_cast<const int4*>(col + gs), nt{});
         }
-        va[j] = stream_load(reinterpret_cast<const double2*>(val + gs), nt{});
-        vb[j] = stream_load(reinterpret_cast<const double2*>(val + gs + 2), nt{});
+        if constexpr (VD) {
+            vn[j] = *reinterpret_cast<const uint16_t*>(vidx + (gs >> 1));
+        } else {
+            va[j] = stream_load(reinterpret_cast<const double2*>(val + gs), nt{});
+            vb[j] = stream_load(reinterpret_cast<const double2*>(val + gs + 2), nt{});
+        }
     }
     for (int i = tid; i <= nr; i += BS) lrp[i] = rowptr[r0 + i];
     // one row per lane: fetch the epilogue's own-row operands (b, old x, y, a_ii) now, so
@@ -212,7 +221,17 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
     for (int j = 0; j < G; ++j) {
         const int g = za + 4 * (tid + j * BS);
         const int cc[4] = {c4[j].x, c4[j].y, c4[j].z, c4[j].w};
-        const double vv[4] = {va[j].x, va[j].y, vb[j].x, vb[j].y};
+        double vv[4];
+        if constexpr (VD) {
+            const double* tt = vtab + 16 * (size_t)bid;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) vv[e] = tt[(vn[j] >> (4 * e)) & 15];
+        } else {
+            vv[0] = va[j].x;
+            vv[1] = va[j].y;
+            vv[2] = vb[j].x;
+            vv[3] = vb[j].y;
+        }
         double p[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -642,6 +661,10 @@ void launch_tile2(const pamg_mat& A, const TileSet& ts, const double* x, const d
     } else if (A.stream_nt) {
         k_rows_tile2<OP, TNNZ, TROWS, false, true><<<ts.n_short, kBlock, 0, s>>>(
             ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg);
+    } else if (ts.c24 && A.d_clo && ts.vd && A.d_vidx) {
+        k_rows_tile2<OP, TNNZ, TROWS, false, false, kBlock, true, true><<<ts.n_short, kBlock, 0, s>>>(
+            ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg, A.d_clo,
+            A.d_chi, ts.d_base, A.d_vidx, ts.d_vtab);
     } else if (ts.c24 && A.d_clo) {
         k_rows_tile2<OP, TNNZ, TROWS, false, false, kBlock, true><<<ts.n_short, kBlock, 0, s>>>(
             ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg, A.d_clo,

@@ -36,6 +36,10 @@ struct TileSet {
     // stored as base (per tile) + 16-bit low part (pamg_mat::d_clo) + 8-bit high part (d_chi)
     int* d_base = nullptr;  // per short tile (same order as d_short), when c24
     bool c24 = false;
+    // value dictionary (opt-in, Options::value_dict): every tile has <= 16 distinct values;
+    // a value is a 4-bit index (pamg_mat::d_vidx) into the tile's 16-entry table
+    double* d_vtab = nullptr;  // 16 per short tile
+    bool vd = false;
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
 };
 
@@ -51,6 +55,7 @@ struct Options {
     int stream_nt = 0;         // 1: non-temporal loads for the matrix stream (variant 1)
     int tile_order = 1;        // 1: banded XCD-blocked tile order (see build_tiles)
     int col24 = 1;             // 1: 3-byte column stream where every tile's span fits 2^24
+    int value_dict = 0;        // 1 (opt-in): 4-bit per-tile value dictionaries where they fit
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };
 Options& options();
@@ -98,6 +103,7 @@ struct pamg_mat {
     int* d_col = nullptr;
     uint16_t* d_clo = nullptr;  // 24-bit column stream (TileSet::c24): low 16 bits
     uint8_t* d_chi = nullptr;   //   and high 8 bits of (column - tile base)
+    uint8_t* d_vidx = nullptr;  // value dictionary indices, two per byte (TileSet::vd)
     double* d_val = nullptr;
     double* d_diag = nullptr;  // a_ii for square matrices (zero-guess Jacobi), else null
     const pamg_plan* plan = nullptr;

@@ -86,9 +86,46 @@ static std::vector<int4> xcd_band_order(const std::vector<int4>& tiles, int64_t 
     return out;
 }
 
+// Opt-in value dictionaries of a 24-bit tile set: every tile holds <= 16 distinct values
+// (bit patterns, so -0.0 / NaN payloads survive); indices go to vidx (4 bits per entry).
+int build_value_dict(const std::vector<int4>& tiles, const double* val, pamg::TileSet* ts,
+                     std::vector<uint8_t>* vidx, size_t nslots) {
+    std::vector<double> tab(tiles.size() * 16, 0.0);
+    std::vector<uint8_t> slot;
+    for (size_t t = 0; t < tiles.size(); ++t) {
+        uint64_t key[16];
+        int nk = 0;
+        for (int k = tiles[t].z; k < tiles[t].w; ++k) {
+            uint64_t b;
+            std::memcpy(&b, &val[k], 8);
+            int j = 0;
+            while (j < nk && key[j] != b) ++j;
+            if (j == nk) {
+                if (nk == 16) return PAMG_OK;  // does not fit: plain values for this set
+                key[nk++] = b;
+                tab[t * 16 + j] = val[k];
+            }
+        }
+    }
+    if (vidx->empty()) vidx->assign(nslots, 0);
+    for (size_t t = 0; t < tiles.size(); ++t) {
+        const double* tt = &tab[t * 16];
+        for (int k = tiles[t].z; k < tiles[t].w; ++k) {
+            int j = 0;
+            while (std::memcmp(&tt[j], &val[k], 8) != 0) ++j;
+            (*vidx)[k >> 1] |= (uint8_t)(j << (4 * (k & 1)));
+        }
+    }
+    CHECK(dalloc(&ts->d_vtab, (int64_t)tab.size()));
+    HIPC(hipMemcpy(ts->d_vtab, tab.data(), sizeof(double) * tab.size(), hipMemcpyHostToDevice));
+    ts->vd = true;
+    return PAMG_OK;
+}
+
 int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
                 pamg::TileSet* ts, int64_t band, const std::vector<int>& ci,
-                std::vector<uint16_t>* lo, std::vector<uint8_t>* hi) {
+                std::vector<uint16_t>* lo, std::vector<uint8_t>* hi, const double* val,
+                std::vector<uint8_t>* vidx) {
     const auto& opt = pamg::options();
     const int tnnz = opt.tile_nnz, trows = opt.tile_rows;
     ts->tile_nnz = tnnz;
@@ -159,6 +196,9 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
             ts->c24 = true;
         }
     }
+    ts->vd = false;
+    if (opt.value_dict && ts->c24 && val)
+        CHECK(build_value_dict(tiles, val, ts, vidx, (ci.size() + 1) / 2 + 8));
     if (ts->n_short)
         HIPC(hipMemcpy(ts->d_short, tiles.data(), sizeof(int4) * tiles.size(), hipMemcpyHostToDevice));
     if (ts->n_long)
@@ -170,7 +210,8 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_short);
     dfree(ts.d_long);
     dfree(ts.d_base);
-    ts.c24 = false;
+    dfree(ts.d_vtab);
+    ts.c24 = ts.vd = false;
     ts.n_short = ts.n_long = 0;
 }
 
@@ -721,7 +762,8 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         if (c < 0 || c >= ncols) return fail(PAMG_E_ARG, "mat_upload: column %lld out of range", (long long)c);
         ci[k] = (int)c;
     }
-    auto A = std::make_unique<pamg_mat>();
+    // released through pamg_mat_destroy on every error path (no device memory leaks)
+    std::unique_ptr<pamg_mat, int (*)(pamg_mat*)> A(new pamg_mat, pamg_mat_destroy);
     A->ctx = ctx;
     A->rows_kernel = pamg::options().rows_kernel;
     A->xcd_remap = pamg::options().xcd_remap;
@@ -781,14 +823,19 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         HIPC(hipMemcpy(A->d_diag, diag.data(), sizeof(double) * nrows, hipMemcpyHostToDevice));
     }
     std::vector<uint16_t> lo;
-    std::vector<uint8_t> hi;
-    CHECK(build_tiles(rp, inner, &A->interior, band, ci, &lo, &hi));
-    CHECK(build_tiles(rp, bnd, &A->boundary, band, ci, &lo, &hi));
-    // the bytes one apply streams: values, columns (3 B in 24-bit tile sets), row pointers,
-    // tile descriptors (+ bases)
-    A->stream_bytes = 8 * nnz + 4 * (nrows + 1);
+    std::vector<uint8_t> hi, vidx;
+    CHECK(build_tiles(rp, inner, &A->interior, band, ci, &lo, &hi, val, &vidx));
+    CHECK(build_tiles(rp, bnd, &A->boundary, band, ci, &lo, &hi, val, &vidx));
+    if (!vidx.empty()) {
+        CHECK(dalloc(&A->d_vidx, (int64_t)vidx.size()));
+        HIPC(hipMemcpy(A->d_vidx, vidx.data(), vidx.size(), hipMemcpyHostToDevice));
+    }
+    // the bytes one apply streams: values (8 B, or a 4-bit index + the tile's 128-B table),
+    // columns (3 B in 24-bit tile sets), row pointers, tile descriptors (+ bases)
+    A->stream_bytes = 4 * (nrows + 1);
     for (const pamg::TileSet* t : {&A->interior, &A->boundary})
-        A->stream_bytes += (t->c24 ? 3 : 4) * t->nnz_short + 4 * t->nnz_long +
+        A->stream_bytes += (t->c24 ? 3 : 4) * t->nnz_short + 12 * t->nnz_long +
+                           (t->vd ? t->nnz_short / 2 + 128 * (int64_t)t->n_short : 8 * t->nnz_short) +
                            (16 + (t->c24 ? 4 : 0)) * (int64_t)t->n_short + 4 * (int64_t)t->n_long;
     if (!lo.empty()) {  // padded like d_col
         lo.resize(nnz + kVecPad, 0);
@@ -810,6 +857,7 @@ int pamg_mat_destroy(pamg_mat* A) {
     dfree(A->d_col);
     dfree(A->d_clo);
     dfree(A->d_chi);
+    dfree(A->d_vidx);
     dfree(A->d_val);
     dfree(A->d_diag);
     free_tiles(A->interior);
@@ -903,7 +951,7 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
     if (nr > 1 && !rep_offsets)
         return fail(PAMG_E_ARG, "hier_create: rep_offsets required with %d ranks", nr);
     CHECK(set_device(ctx));
-    auto H = std::make_unique<pamg_hier>();
+    std::unique_ptr<pamg_hier, int (*)(pamg_hier*)> H(new pamg_hier, pamg_hier_destroy);
     H->ctx = ctx;
     H->L = nlevels;
     H->rep = rep_level;
@@ -1001,7 +1049,7 @@ int pamg_hier_destroy(pamg_hier* H) {
     (void)hipSetDevice(H->ctx->device);
     (void)hipStreamSynchronize(H->ctx->s_comp);
     drop_graph(H);
-    for (int l = 0; l < H->L; ++l) {
+    for (size_t l = 0; l < H->t.size(); ++l) {
         if (l > 0) {
             dfree(H->x[l]);
             dfree(H->b[l]);
@@ -1233,6 +1281,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "tile_order" && (value == 0 || value == 1)) o.tile_order = (int)value;
     else if (k == "poison_ghosts" && (value == 0 || value == 1)) o.poison_ghosts = (int)value;
     else if (k == "col24" && (value == 0 || value == 1)) o.col24 = (int)value;
+    else if (k == "value_dict" && (value == 0 || value == 1)) o.value_dict = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -1266,6 +1315,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "tile_order") *value = o.tile_order;
     else if (k == "poison_ghosts") *value = o.poison_ghosts;
     else if (k == "col24") *value = o.col24;
+    else if (k == "value_dict") *value = o.value_dict;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

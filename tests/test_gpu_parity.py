@@ -19,7 +19,7 @@ def bits(a):
     return np.asarray(a, np.float64).view(np.int64)
 
 
-def random_csr(rng, lengths, ncols, square=False):
+def random_csr(rng, lengths, ncols, square=False, palette=None):
     rows, cols, vals = [0], [], []
     for i, m in enumerate(lengths):
         m = min(max(m, 1) if square else m, ncols)
@@ -27,7 +27,7 @@ def random_csr(rng, lengths, ncols, square=False):
         if square and m > 0 and i not in c:
             c[0] = i
         c = np.sort(c)
-        v = rng.standard_normal(m)
+        v = rng.standard_normal(m) if palette is None else rng.choice(palette, m)
         if square and m > 0:
             v[c == i] = 4.0 + abs(v[c == i]) + m
         cols.append(c)
@@ -53,19 +53,20 @@ LENGTHS = {
     "empty_rows": [0] * 100,
 }
 
-# (rows_kernel, tile_nnz, tile_rows, xcd_remap, jacobi_diag, stream_nt, tile_order, col24):
-# every tuning configuration must be bit-exact
-TILE_CONFIGS = [(0, 2048, 256, 0, 0, 0, 0, 1), (1, 2048, 256, 0, 0, 0, 0, 1), (1, 2048, 256, 1, 1, 0, 0, 1),
-                (1, 1024, 256, 0, 0, 0, 0, 1), (1, 1024, 256, 0, 0, 1, 1, 1), (1, 4096, 256, 0, 0, 1, 0, 1),
-                (1, 4096, 512, 1, 0, 0, 0, 1), (2, 256, 64, 0, 0, 0, 0, 1), (2, 512, 64, 0, 0, 0, 1, 1),
-                (2, 512, 64, 0, 1, 0, 0, 1), (2, 1024, 64, 0, 0, 0, 0, 1), (3, 1024, 256, 0, 0, 0, 1, 1),
-                (3, 2048, 256, 0, 0, 0, 0, 1), (1, 512, 128, 0, 0, 0, 1, 1), (1, 2048, 512, 0, 0, 0, 1, 1),
-                (1, 1024, 256, 0, 0, 0, 1, 0), (1, 1024, 256, 0, 1, 0, 1, 1)]
+# (rows_kernel, tile_nnz, tile_rows, xcd_remap, jacobi_diag, stream_nt, tile_order, col24,
+#  value_dict): every tuning configuration must be bit-exact
+TILE_CONFIGS = [(0, 2048, 256, 0, 0, 0, 0, 1, 0), (1, 2048, 256, 0, 0, 0, 0, 1, 0), (1, 2048, 256, 1, 1, 0, 0, 1, 0),
+                (1, 1024, 256, 0, 0, 0, 0, 1, 0), (1, 1024, 256, 0, 0, 1, 1, 1, 0), (1, 4096, 256, 0, 0, 1, 0, 1, 0),
+                (1, 4096, 512, 1, 0, 0, 0, 1, 0), (2, 256, 64, 0, 0, 0, 0, 1, 0), (2, 512, 64, 0, 0, 0, 1, 1, 0),
+                (2, 512, 64, 0, 1, 0, 0, 1, 0), (2, 1024, 64, 0, 0, 0, 0, 1, 0), (3, 1024, 256, 0, 0, 0, 1, 1, 0),
+                (3, 2048, 256, 0, 0, 0, 0, 1, 0), (1, 512, 128, 0, 0, 0, 1, 1, 0), (1, 2048, 512, 0, 0, 0, 1, 1, 0),
+                (1, 1024, 256, 0, 0, 0, 1, 0, 0), (1, 1024, 256, 0, 1, 0, 1, 1, 0), (1, 1024, 256, 0, 0, 0, 1, 1, 1),
+                (1, 1024, 256, 0, 1, 0, 1, 1, 1), (1, 2048, 256, 0, 0, 0, 1, 1, 1)]
 OPT_KEYS = ("rows_kernel", "tile_nnz", "tile_rows", "xcd_remap", "jacobi_diag", "stream_nt", "tile_order",
-            "col24")
+            "col24", "value_dict")
 
 
-@pytest.fixture(params=TILE_CONFIGS, ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}".format(*c))
+@pytest.fixture(params=TILE_CONFIGS, ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}".format(*c))
 def tile_cfg(request, built):
     import ctypes
     from parallel_amg_amd._lib import call
@@ -81,12 +82,19 @@ def tile_cfg(request, built):
         call("pamg_set_option", k.encode(), v)
 
 
+# value palettes: None = all distinct (no tile fits a value dictionary); a few repeated
+# values incl. +-0.0 (every tile fits one); 17 values (tiles straddle the 16-value limit)
+PALETTES = {"distinct": None, "few": [-1.0, 2.5, 0.0, -0.0, 6.0, 1e-300],
+            "seventeen": [float(v) for v in range(-8, 9)]}
+
+
+@pytest.mark.parametrize("palette", list(PALETTES))
 @pytest.mark.parametrize("case", list(LENGTHS))
-def test_spmv_residual_bit_exact(ctx, case, tile_cfg):
+def test_spmv_residual_bit_exact(ctx, case, palette, tile_cfg):
     rng = np.random.default_rng(11)
     lengths = LENGTHS[case]
     ncols = max(max(lengths) + 1, len(lengths) + 7)
-    M = random_csr(rng, lengths, ncols)
+    M = random_csr(rng, lengths, ncols, palette=PALETTES[palette])
     A, _h = upload(ctx, M)
     xh = rng.standard_normal(ncols)
     bh = rng.standard_normal(len(lengths))
@@ -109,13 +117,14 @@ def test_spmv_residual_bit_exact(ctx, case, tile_cfg):
     assert np.array_equal(bits(yy.own_values()), bits((bh + ref) + ref))
 
 
+@pytest.mark.parametrize("palette", ["distinct", "few"])
 @pytest.mark.parametrize("case", ["stencil7", "ragged", "long", "budget_edge", "one_row"])
-def test_jacobi_bit_exact(ctx, case, tile_cfg):
+def test_jacobi_bit_exact(ctx, case, palette, tile_cfg):
     rng = np.random.default_rng(5)
     lengths = LENGTHS[case]
     n = max(max(lengths) + 1, len(lengths))
     lengths = lengths + [3] * (n - len(lengths))
-    M = random_csr(rng, lengths, n, square=True)
+    M = random_csr(rng, lengths, n, square=True, palette=PALETTES[palette])
     A, _h = upload(ctx, M)
     xh, bh = rng.standard_normal(n), rng.standard_normal(n)
     x, b, t = PVector(ctx, n, 0, xh), PVector(ctx, n, 0, bh), PVector(ctx, n)
@@ -260,3 +269,9 @@ def test_stream_bytes_layout(ctx):
     nt, rem = divmod(got[0] - 12 * nnz - 4 * (n + 1), 16)
     assert rem == 0 and nt > 0
     assert got[1] == 11 * nnz + 4 * (n + 1) + 20 * nt
+    call("pamg_set_option", b"value_dict", 1)   # 2 distinct values: every tile fits
+    try:
+        A, _h = upload(ctx, M)
+    finally:
+        call("pamg_set_option", b"value_dict", 0)
+    assert A.stream_bytes == 3 * nnz + nnz // 2 + 4 * (n + 1) + (20 + 128) * nt
