@@ -991,7 +991,8 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
         if (!P[l] || !R[l]) return fail(PAMG_E_ARG, "hier_create: P/R[%d] is NULL", l);
         H->P[l] = P[l];
         H->R[l] = R[l];
-        if (!A[l]->d_diag) return fail(PAMG_E_SETUP, "hier_create: A[%d] lacks a nonzero diagonal", l);
+        if (!A[l]->d_diag && A[l]->nrows > 0)  // (a part may own no row of a coarse level)
+            return fail(PAMG_E_SETUP, "hier_create: A[%d] lacks a nonzero diagonal", l);
         const int64_t r_rows = (l + 1 == rep_level) ? rep_own : H->nown[l + 1];
         if (P[l]->nrows != A[l]->nrows || R[l]->nrows != r_rows)
             return fail(PAMG_E_ARG, "hier_create: level %d operator shapes inconsistent", l);

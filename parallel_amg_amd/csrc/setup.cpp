@@ -252,7 +252,7 @@ int pamg_setup_gershgorin(const pamg_hcsr* A, int64_t row0, double* rho) {
 // SPEC §S4.2-3: decoupled standard aggregation over own columns [row0, row0 + nr).
 int pamg_setup_aggregate(const pamg_hcsr* A, int64_t row0, double theta, int32_t* agg,
                          int64_t* n_agg) {
-    if (!valid(A) || !agg || !n_agg) return fail(PAMG_E_ARG, "aggregate: bad args");
+    if (!valid(A) || (!agg && A->nr > 0) || !n_agg) return fail(PAMG_E_ARG, "aggregate: bad args");
     const int64_t n = A->nr, hi = row0 + n;
     std::vector<double> dg(n);
 #pragma omp parallel for schedule(static)
@@ -313,7 +313,7 @@ int pamg_setup_aggregate(const pamg_hcsr* A, int64_t row0, double theta, int32_t
 // SPEC §S4.4.
 int pamg_setup_tentative(int64_t n, const int32_t* agg, int64_t n_agg, int64_t coarse0,
                          int64_t ncols_global, pamg_hcsr** out) {
-    if (!agg || !out || n < 0 || n_agg < 0) return fail(PAMG_E_ARG, "tentative: bad args");
+    if ((!agg && n > 0) || !out || n < 0 || n_agg < 0) return fail(PAMG_E_ARG, "tentative: bad args");
     std::vector<int64_t> cnt(n_agg, 0);
     for (int64_t i = 0; i < n; ++i)
         if (agg[i] >= 0) {

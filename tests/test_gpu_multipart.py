@@ -40,7 +40,10 @@ def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, poison
         call("pamg_set_option", b"poison_ghosts", int(poison))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         be = pa.DistributedBackend()
-        A, offs, xs = pa.generate_problem(be, kind, n)
+        if kind.startswith("mtx:"):
+            A, offs, xs = pa.load_problem(be, kind[4:])
+        else:
+            A, offs, xs = pa.generate_problem(be, kind, n)
         H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse, agglomerate=agglomerate))
         ndev = max(1, torch.cuda.device_count())
         # RCCL needs one device per rank; with fewer GPUs than ranks use the host transport
@@ -99,3 +102,44 @@ def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, agglomerate, poi
     assert np.array_equal(bits(x), bits(xo))
     for r in range(world):
         np.testing.assert_allclose(res[r][4], ho, rtol=1e-12)
+
+
+def test_multipart_with_an_empty_part(tmp_path, built):
+    """Part 1's rows are all isolated (diagonal only): it forms no aggregates, so it owns no
+    row of level 1 — exchanges, tiles and reductions must cope with an empty part."""
+    import scipy.io
+    import scipy.sparse as sp
+    from oracle import oracle as O
+    A = O.generate("poisson2d", 20, 20, 1).to_scipy().tolil()
+    for i in range(200, 400):
+        A[i, :] = 0
+        A[:, i] = 0
+        A[i, i] = 3.0 + (i % 7)
+    A = A.tocsr()
+    A.eliminate_zeros()
+    A.sort_indices()
+    path = str(tmp_path / "iso.mtx")
+    scipy.io.mmwrite(path, A.tocoo(), symmetry="symmetric")
+    world, ncycles = 2, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, "mtx:" + path, 0, 10, 0, ncycles, 1, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r = q.get(timeout=300)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+    assert all(res[r][1] == "ok" for r in range(world)), "\n".join(str(res[r][1]) for r in range(world))
+    Ao = O.CSR(A.indptr.astype(np.int64), A.indices.astype(np.int64), A.data.copy(), 400)
+    Ho = O.setup(Ao, nparts=2, max_coarse=10, agglomerate=0)
+    assert Ho.offsets[1][1] == Ho.offsets[1][2]     # part 1 owns no row of level 1
+    bo = O.spmv(Ao, O.xstar(400))
+    xo, ho = Ho.solve(bo, ncycles, res_hist=True)
+    bits = lambda a: np.asarray(a, np.float64).view(np.int64)
+    assert np.array_equal(bits(np.concatenate([res[r][2] for r in range(world)])), bits(bo))
+    assert np.array_equal(bits(np.concatenate([res[r][3] for r in range(world)])), bits(xo))
