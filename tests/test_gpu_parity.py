@@ -275,3 +275,27 @@ def test_stream_bytes_layout(ctx):
     finally:
         call("pamg_set_option", b"value_dict", 0)
     assert A.stream_bytes == 3 * nnz + nnz // 2 + 4 * (n + 1) + (20 + 128) * nt
+
+
+@pytest.mark.parametrize("seed,n,density,weak,iso", [(1, 3000, 0.003, 0.3, 0.02), (2, 5000, 0.001, 0.0, 0.0),
+                                                     (3, 2500, 0.01, 0.6, 0.05), (4, 4000, 0.002, 0.2, 0.1)])
+def test_vcycle_random_spd_bit_exact(ctx, seed, n, density, weak, iso):
+    """Irregular matrices (random patterns, weak couplings, isolated rows) through the whole
+    device path — GPU setup products, ragged tiles on every level, V-cycles — vs the oracle."""
+    from test_setup_random import random_spd
+    M = random_spd(seed, n, density, weak, iso)
+    A = {0: HCSR.from_arrays(M.indptr, M.indices.astype(np.int32), M.data, n)}
+    be = pa.SequentialBackend(1)
+    H = pa.build_hierarchy(be, A, np.array([0, n], np.int64), pa.SAParams(max_coarse=60), device=ctx)
+    S = AMGSolver(ctx, H)
+    rng = np.random.default_rng(seed)
+    bh = rng.standard_normal(n)
+    b = PVector(ctx, n, 0, bh)
+    Ao = O.CSR(M.indptr.astype(np.int64), M.indices.astype(np.int64), M.data.copy(), n)
+    Ho = O.setup(Ao, max_coarse=60)
+    assert Ho.nlevels == H.nlevels
+    xo, ho = Ho.solve(bh, 5, res_hist=True)
+    x = S.new_vector()
+    hist = S.vcycle(x, b, 5, res_hist=True)
+    assert np.array_equal(bits(x.own_values()), bits(xo))
+    np.testing.assert_allclose(hist, ho, rtol=1e-12)
