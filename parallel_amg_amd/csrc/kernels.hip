@@ -40,19 +40,51 @@ __device__ __forceinline__ void epilogue(int r, double s, const double* __restri
     }
 }
 
-// Sum of lp[kb..ke) left to right from +0.0 (SPEC §S3). The LDS loads go out 8 at a time
-// ahead of the dependent adds (one LDS latency per 8 products instead of per product — what
-// bounds the long rows of the coarse operators); slots past the row end contribute +0.0, which
-// leaves the sum's bits unchanged: a sum started at +0.0 is never -0.0, and s + (+0.0) == s
-// for every other s.
+// Sum of lp[kb..ke) left to right from +0.0 (SPEC §S3). The chain of dependent fp64 adds is
+// what bounds the long rows of the coarse operators, so nothing else may sit on it: full
+// batches of 8 are read unconditionally (no exec-masked branches) and software-pipelined —
+// batch m+1's LDS reads are in flight while batch m is added. The last, partial batch reads
+// 8 slots (callers pad lp by 8) and selects +0.0 past the row end, which leaves the sum's
+// bits unchanged: a sum started at +0.0 is never -0.0, and s + (+0.0) == s for every other s.
+__device__ __forceinline__ void lds_batch8(const double* __restrict__ lp, int k, double (&p)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = lp[k + j];
+}
+
 __device__ __forceinline__ double row_sum_lds(const double* __restrict__ lp, int kb, int ke,
                                               double s = 0.0) {
-    for (int k = kb; k < ke; k += 8) {
+    int k = kb;
+    if (k + 8 <= ke) {
+        // two register batches in alternation (no copies): p is added while q is read
+        double p[8], q[8];
+        lds_batch8(lp, k, p);
+        k += 8;
+        while (true) {
+            if (k + 8 > ke) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) s = s + p[j];
+                break;
+            }
+            lds_batch8(lp, k, q);
+            k += 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s = s + p[j];
+            if (k + 8 > ke) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) s = s + q[j];
+                break;
+            }
+            lds_batch8(lp, k, p);
+            k += 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s = s + q[j];
+        }
+    }
+    if (k < ke) {
         double p[8];
+        lds_batch8(lp, k, p);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) p[j] = (k + j < ke) ? lp[k + j] : 0.0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s = s + p[j];
+        for (int j = 0; j < 8; ++j) s = s + ((k + j < ke) ? p[j] : 0.0);
     }
     return s;
 }
@@ -560,32 +592,44 @@ __global__ void k_jacobi_zero(int64_t n, const double* __restrict__ b,
     }
 }
 
-// x[row0 + i] for the caller's rows: s = sum_j ainv[j*n + (row0+i)] * b[j] (SPEC §S5, §S3).
+// x[row0 + i] for the caller's rows: s = sum_j ainv[(row0+i)*n + j] * b[j], j left to right
+// (SPEC §S5, §S3). ainv is row-major on the device (transposed at upload), so one wave owns a
+// row: its lanes read the row in coalesced 64-wide strips (16 loads in flight per lane), the
+// products go to the wave's LDS slice, and lane 0 adds them in column order. The in-order add
+// chain (~n dependent fp64 adds) is the floor; the first version (one lane per row walking a
+// column-major A^-1, 4 loads in flight) was bound by n/4 serial L2 round trips (30 us at n=225).
+constexpr int kGemvChunk = 1024;
 __global__ __launch_bounds__(kBlock) void k_dense_gemv(int64_t n_rows, int64_t n,
                                                        int64_t row0,
                                                        const double* __restrict__ ainv,
                                                        const double* __restrict__ b,
                                                        double* __restrict__ y) {
-    const int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x;
-    if (i >= n_rows) return;
-    const double* a = ainv + row0 + i;
+    __shared__ __attribute__((aligned(16))) double lp_all[kBlock / 64][kGemvChunk + 8];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * (kBlock / 64) + w;
+    if (i >= n_rows) return;  // whole waves only: the hand-offs below are wave-local
+    const double* a = ainv + (row0 + i) * n;
+    double* lp = lp_all[w];
     double s = 0.0;
-    int64_t j = 0;
-    for (; j + 4 <= n; j += 4) {
-        const double p0 = a[(j + 0) * n] * b[j + 0];
-        const double p1 = a[(j + 1) * n] * b[j + 1];
-        const double p2 = a[(j + 2) * n] * b[j + 2];
-        const double p3 = a[(j + 3) * n] * b[j + 3];
-        s = s + p0;
-        s = s + p1;
-        s = s + p2;
-        s = s + p3;
+    for (int64_t c = 0; c < n; c += kGemvChunk) {
+        const int m = (int)((n - c) < kGemvChunk ? (n - c) : kGemvChunk);
+#pragma unroll
+        for (int q = 0; q < kGemvChunk / 64; ++q) {
+            const int j = lane + 64 * q;
+            if (j < m) {
+                const double p = a[c + j] * b[c + j];
+                lp[j] = p;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0) s = row_sum_lds(lp, 0, m, s);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    for (; j < n; ++j) {
-        const double p = a[j * n] * b[j];
-        s = s + p;
-    }
-    y[i] = s;
+    if (lane == 0) y[i] = s;
 }
 
 __global__ void k_pack(int64_t n, const int* __restrict__ idx, const double* __restrict__ x,
@@ -764,11 +808,12 @@ void launch_jacobi_zero(int64_t n, const double* b, const double* diag, double o
     if (n > 0) k_jacobi_zero<<<grid_for(n), kBlock, 0, s>>>(n, b, diag, omega, y);
 }
 
-void launch_dense_gemv(int64_t n_rows, int64_t n_cols, int64_t row0, const double* ainv_cm,
+void launch_dense_gemv(int64_t n_rows, int64_t n_cols, int64_t row0, const double* ainv_rm,
                        const double* b, double* y, hipStream_t s) {
+    constexpr int kRowsPerBlock = kBlock / 64;
     if (n_rows > 0)
-        k_dense_gemv<<<(int)((n_rows + kBlock - 1) / kBlock), kBlock, 0, s>>>(n_rows, n_cols,
-                                                                             row0, ainv_cm, b, y);
+        k_dense_gemv<<<(int)((n_rows + kRowsPerBlock - 1) / kRowsPerBlock), kBlock, 0, s>>>(n_rows, n_cols,
+                                                                             row0, ainv_rm, b, y);
 }
 
 void launch_pack(int64_t n, const int* idx, const double* x, double* out, hipStream_t s) {

@@ -123,7 +123,7 @@ void launch_rows(const pamg_mat& A, const TileSet& ts, int op, const double* x, 
                  const double* xold, double* y, double omega, hipStream_t s);
 void launch_jacobi_zero(int64_t n, const double* b, const double* diag, double omega, double* y,
                         hipStream_t s);
-void launch_dense_gemv(int64_t n_rows, int64_t n_cols, int64_t row0, const double* ainv_cm,
+void launch_dense_gemv(int64_t n_rows, int64_t n_cols, int64_t row0, const double* ainv_rm,
                        const double* b, double* y, hipStream_t s);
 void launch_pack(int64_t n, const int* idx, const double* x, double* out, hipStream_t s);
 void launch_fill(int64_t n, double v, double* y, hipStream_t s);

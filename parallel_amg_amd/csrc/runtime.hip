@@ -320,7 +320,7 @@ struct pamg_hier {
     std::vector<int64_t> nown;
     // coarsest level
     int64_t nc = 0;
-    double* d_ainv = nullptr;          // column-major nc x nc
+    double* d_ainv = nullptr;          // row-major nc x nc (the ABI hands it over column-major)
     // replicated tail (SPEC §S7 agglomeration): levels >= rep are held whole on every rank;
     // the restriction into level rep yields this rank's rows [coffs[me], coffs[me+1]), which
     // are all-gathered (in blocks of cmax) into the whole vector
@@ -1027,8 +1027,14 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
                     (long long)H->nown[L - 1], (long long)n_coarse);
     if (L == 1 && (n_rep != n_coarse || rep_own != A[0]->nrows))
         return fail(PAMG_E_ARG, "hier_create: rep_offsets inconsistent with the one-level hierarchy");
-    CHECK(dalloc(&H->d_ainv, n_coarse * n_coarse));
-    HIPC(hipMemcpy(H->d_ainv, ainv, sizeof(double) * n_coarse * n_coarse, hipMemcpyHostToDevice));
+    {
+        // row-major on the device: one wave reads a row of A^-1 coalesced (k_dense_gemv)
+        std::vector<double> rm((size_t)n_coarse * n_coarse);
+        for (int64_t j = 0; j < n_coarse; ++j)
+            for (int64_t i = 0; i < n_coarse; ++i) rm[(size_t)i * n_coarse + j] = ainv[(size_t)j * n_coarse + i];
+        CHECK(dalloc(&H->d_ainv, n_coarse * n_coarse));
+        HIPC(hipMemcpy(H->d_ainv, rm.data(), sizeof(double) * rm.size(), hipMemcpyHostToDevice));
+    }
     if (nr > 1) {
         CHECK(dalloc(&H->d_bgather, (int64_t)nr * H->cmax + n_rep + kVecPad));
         CHECK(dalloc(&H->d_bsend, H->cmax + kVecPad));
