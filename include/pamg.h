@@ -72,7 +72,8 @@ int pamg_comm_init_host(pamg_ctx* ctx, int nranks, int rank, pamg_host_comm_fn f
 /* ------------------------------------------------------------------ exchange plan */
 /* Replaces PRange / ExchangeGraph: ghosts [n_own, n_own+n_ghost) grouped by neighbour in
  * nbr order (recv_counts), and per neighbour the own indices sent to it (send_idx,
- * concatenated in nbr order, send_counts). */
+ * concatenated in nbr order, send_counts). A part may list its own rank (ghost copies of own
+ * entries, served by an RCCL send/recv to self; refused under the host debug transport). */
 int pamg_plan_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, int n_nbr,
                      const int32_t* nbr_rank, const int64_t* recv_counts,
                      const int64_t* send_counts, const int64_t* send_idx, pamg_plan** out);

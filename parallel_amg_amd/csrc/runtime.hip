@@ -591,7 +591,9 @@ int pamg_plan_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, int n_nbr,
     p->recv_off.assign(n_nbr + 1, 0);
     p->send_off.assign(n_nbr + 1, 0);
     for (int k = 0; k < n_nbr; ++k) {
-        if (nbr_rank[k] < 0 || nbr_rank[k] >= ctx->nranks || nbr_rank[k] == ctx->rank)
+        // a part may be its own neighbour (ghost copies of own entries, e.g. a periodic wrap
+        // on one part): RCCL serves that as a send/recv to self; the host transport does not
+        if (nbr_rank[k] < 0 || nbr_rank[k] >= ctx->nranks || (nbr_rank[k] == ctx->rank && ctx->host_fn))
             return fail(PAMG_E_ARG, "plan_create: bad neighbour rank %d", nbr_rank[k]);
         p->recv_off[k + 1] = p->recv_off[k] + recv_counts[k];
         p->send_off[k + 1] = p->send_off[k] + send_counts[k];
