@@ -164,7 +164,7 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
 
 /* Process-wide knobs. Applied to later pamg_mat_upload calls: "rows_kernel" (0..3, kernel
  * variant), "tile_nnz" / "tile_rows" (tile budget; the valid pairs per variant are checked),
- * "xcd_remap", "jacobi_diag", "stream_nt", "tile_order" (0 | 1). Applied at every exchange:
+ * "xcd_remap", "jacobi_diag", "stream_nt", "tile_order" (0 | 1 | 2 | 4 | 8 | 16). Applied at every exchange:
  * "poison_ghosts" (0 | 1, debug: NaN-fill the ghost slots before each exchange). */
 int pamg_set_option(const char* key, int64_t value);
 int pamg_get_option(const char* key, int64_t* value);

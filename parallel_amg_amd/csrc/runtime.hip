@@ -71,12 +71,20 @@ int set_device(const pamg_ctx* ctx) {
 // the k-th eighth of every super-row, and interleave the 8 sequences so block b (XCD b % 8,
 // as dispatch is observed to deal blocks) walks its eighth plane after plane. The x lines of
 // rows z-1, z, z+1 of one eighth then stay in that XCD's L2. Speed only: any order is correct.
-static std::vector<int4> xcd_band_order(const std::vector<int4>& tiles, int64_t band) {
+// split > 1: each XCD's eighth is cut again into `split` sub-slabs, and the XCD walks the
+// first sub-slab through all super-rows, then the second, ... so that the rows read again by
+// the next super-row (z+1) come back after 1/split of a plane eighth of stream instead of a
+// whole one (restriction rows read four fine planes; a plane eighth of R0 is ~2.9 MB of
+// stream, close to the 4 MB L2), at the price of a y-halo per sub-slab.
+static std::vector<int4> xcd_band_order(const std::vector<int4>& tiles, int64_t band, int split = 1) {
     std::vector<std::vector<int4>> bucket(8);
+    std::vector<std::vector<std::vector<int4>>> sub(8, std::vector<std::vector<int4>>(split));
     for (const auto& t : tiles) {
-        const int64_t k = ((int64_t)(t.x % band) * 8) / band;
-        bucket[k].push_back(t);
+        const int64_t q = ((int64_t)(t.x % band) * 8 * split) / band;
+        sub[q / split][q % split].push_back(t);
     }
+    for (int k = 0; k < 8; ++k)
+        for (auto& v : sub[k]) bucket[k].insert(bucket[k].end(), v.begin(), v.end());
     size_t m = 0;
     for (auto& b : bucket) m = std::max(m, b.size());
     std::vector<int4> out;
@@ -158,7 +166,8 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
         i = j;
     }
     for (int r : longr) ts->nnz_long += rp[r + 1] - rp[r];
-    if (opt.tile_order == 1 && band >= 64 && tiles.size() >= 64) tiles = xcd_band_order(tiles, band);
+    if (opt.tile_order >= 1 && band >= 64 && tiles.size() >= 64)
+        tiles = xcd_band_order(tiles, band, band >= 64 * opt.tile_order ? opt.tile_order : 1);
     ts->n_short = (int)tiles.size();
     ts->n_long = (int)longr.size();
     CHECK(dalloc(&ts->d_short, ts->n_short));
@@ -1287,7 +1296,8 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "xcd_remap" && (value == 0 || value == 1)) o.xcd_remap = (int)value;
     else if (k == "jacobi_diag" && (value == 0 || value == 1)) o.jacobi_diag = (int)value;
     else if (k == "stream_nt" && (value == 0 || value == 1)) o.stream_nt = (int)value;
-    else if (k == "tile_order" && (value == 0 || value == 1)) o.tile_order = (int)value;
+    else if (k == "tile_order" && (value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16))
+        o.tile_order = (int)value;  // 0 natural, 1 banded XCD-blocked, k > 1 banded with k sub-slabs per XCD
     else if (k == "poison_ghosts" && (value == 0 || value == 1)) o.poison_ghosts = (int)value;
     else if (k == "col24" && (value == 0 || value == 1)) o.col24 = (int)value;
     else if (k == "value_dict" && (value == 0 || value == 1)) o.value_dict = (int)value;
