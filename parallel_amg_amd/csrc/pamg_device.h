@@ -55,6 +55,7 @@ struct Options {
     int stream_nt = 0;         // 1: non-temporal loads for the matrix stream (variant 1)
     int tile_order = 1;        // 1: banded XCD-blocked tile order (see build_tiles)
     int col24 = 1;             // 1: 3-byte column stream where every tile's span fits 2^24
+    int long_tiles = 1;        // 1: 4096-nonzero tiles for operators averaging >= 48 nnz/row
     int value_dict = 0;        // 1 (opt-in): 4-bit per-tile value dictionaries where they fit
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };

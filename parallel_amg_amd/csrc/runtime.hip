@@ -135,7 +135,17 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
                 std::vector<uint16_t>* lo, std::vector<uint8_t>* hi, const double* val,
                 std::vector<uint8_t>* vidx) {
     const auto& opt = pamg::options();
-    const int tnnz = opt.tile_nnz, trows = opt.tile_rows;
+    int tnnz = opt.tile_nnz, trows = opt.tile_rows;
+    // long_tiles: operators with long rows (coarse A_l, R_l: >= 48 nonzeros per row on
+    // average) take 4096-nonzero tiles instead of the default 1024 — their time goes into the
+    // in-order add chain of each row (SPEC §S3), and a tile of 4x the rows runs 4x the chains
+    // side by side (512^3: A2 0.139 -> 0.110 ms, R1 0.458 -> 0.439 ms,
+    // profiles/r01_kbench_512_tnnz.jsonl); the 7- and 27-point levels keep 1024.
+    if (opt.long_tiles && opt.rows_kernel == 1 && tnnz == 1024 && trows == 256 && !rows.empty()) {
+        int64_t nz = 0;
+        for (int r : rows) nz += rp[r + 1] - rp[r];
+        if (nz >= 48 * (int64_t)rows.size()) tnnz = 4096;
+    }
     ts->tile_nnz = tnnz;
     ts->tile_rows = trows;
     std::vector<int4> tiles;
@@ -1300,6 +1310,7 @@ int pamg_set_option(const char* key, int64_t value) {
         o.tile_order = (int)value;  // 0 natural, 1 banded XCD-blocked, k > 1 banded with k sub-slabs per XCD
     else if (k == "poison_ghosts" && (value == 0 || value == 1)) o.poison_ghosts = (int)value;
     else if (k == "col24" && (value == 0 || value == 1)) o.col24 = (int)value;
+    else if (k == "long_tiles" && (value == 0 || value == 1)) o.long_tiles = (int)value;
     else if (k == "value_dict" && (value == 0 || value == 1)) o.value_dict = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
@@ -1332,6 +1343,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "jacobi_diag") *value = o.jacobi_diag;
     else if (k == "stream_nt") *value = o.stream_nt;
     else if (k == "tile_order") *value = o.tile_order;
+    else if (k == "long_tiles") *value = o.long_tiles;
     else if (k == "poison_ghosts") *value = o.poison_ghosts;
     else if (k == "col24") *value = o.col24;
     else if (k == "value_dict") *value = o.value_dict;

@@ -54,19 +54,20 @@ LENGTHS = {
 }
 
 # (rows_kernel, tile_nnz, tile_rows, xcd_remap, jacobi_diag, stream_nt, tile_order, col24,
-#  value_dict): every tuning configuration must be bit-exact
-TILE_CONFIGS = [(0, 2048, 256, 0, 0, 0, 0, 1, 0), (1, 2048, 256, 0, 0, 0, 0, 1, 0), (1, 2048, 256, 1, 1, 0, 0, 1, 0),
-                (1, 1024, 256, 0, 0, 0, 0, 1, 0), (1, 1024, 256, 0, 0, 1, 1, 1, 0), (1, 4096, 256, 0, 0, 1, 0, 1, 0),
-                (1, 4096, 512, 1, 0, 0, 0, 1, 0), (2, 256, 64, 0, 0, 0, 0, 1, 0), (2, 512, 64, 0, 0, 0, 1, 1, 0),
-                (2, 512, 64, 0, 1, 0, 0, 1, 0), (2, 1024, 64, 0, 0, 0, 0, 1, 0), (3, 1024, 256, 0, 0, 0, 1, 1, 0),
-                (3, 2048, 256, 0, 0, 0, 0, 1, 0), (1, 512, 128, 0, 0, 0, 1, 1, 0), (1, 2048, 512, 0, 0, 0, 1, 1, 0),
-                (1, 1024, 256, 0, 0, 0, 1, 0, 0), (1, 1024, 256, 0, 1, 0, 1, 1, 0), (1, 1024, 256, 0, 0, 0, 1, 1, 1),
-                (1, 1024, 256, 0, 1, 0, 1, 1, 1), (1, 2048, 256, 0, 0, 0, 1, 1, 1)]
+#  value_dict, long_tiles): every tuning configuration must be bit-exact
+TILE_CONFIGS = [(0, 2048, 256, 0, 0, 0, 0, 1, 0, 1), (1, 2048, 256, 0, 0, 0, 0, 1, 0, 1), (1, 2048, 256, 1, 1, 0, 0, 1, 0, 1),
+                (1, 1024, 256, 0, 0, 0, 0, 1, 0, 1), (1, 1024, 256, 0, 0, 1, 1, 1, 0, 1), (1, 4096, 256, 0, 0, 1, 0, 1, 0, 1),
+                (1, 4096, 512, 1, 0, 0, 0, 1, 0, 1), (2, 256, 64, 0, 0, 0, 0, 1, 0, 1), (2, 512, 64, 0, 0, 0, 1, 1, 0, 1),
+                (2, 512, 64, 0, 1, 0, 0, 1, 0, 1), (2, 1024, 64, 0, 0, 0, 0, 1, 0, 1), (3, 1024, 256, 0, 0, 0, 1, 1, 0, 1),
+                (3, 2048, 256, 0, 0, 0, 0, 1, 0, 1), (1, 512, 128, 0, 0, 0, 1, 1, 0, 1), (1, 2048, 512, 0, 0, 0, 1, 1, 0, 1),
+                (1, 1024, 256, 0, 0, 0, 1, 0, 0, 1), (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1), (1, 1024, 256, 0, 0, 0, 1, 1, 1, 1),
+                (1, 1024, 256, 0, 1, 0, 1, 1, 1, 1), (1, 2048, 256, 0, 0, 0, 1, 1, 1, 1),
+                (1, 1024, 256, 0, 0, 0, 1, 1, 0, 0), (1, 1024, 256, 0, 0, 0, 4, 1, 0, 1)]
 OPT_KEYS = ("rows_kernel", "tile_nnz", "tile_rows", "xcd_remap", "jacobi_diag", "stream_nt", "tile_order",
-            "col24", "value_dict")
+            "col24", "value_dict", "long_tiles")
 
 
-@pytest.fixture(params=TILE_CONFIGS, ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}".format(*c))
+@pytest.fixture(params=TILE_CONFIGS, ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}_lt{}".format(*c))
 def tile_cfg(request, built):
     import ctypes
     from parallel_amg_amd._lib import call

@@ -70,59 +70,81 @@ def _selfify(H, HostPlan):
     return replace(H, levels=levels)
 
 
-@pytest.fixture(scope="module")
-def rccl_ctx(built):
-    from parallel_amg_amd._lib import call
-    from parallel_amg_amd.partitioned import Context
-    c = Context(0)
-    uid = C.create_string_buffer(128)
-    call("pamg_comm_unique_id", uid)
-    call("pamg_comm_init", c.handle, 1, 0, uid.raw)
-    yield c  # released by reference counting, after the matrices and plans that use it
+def _run(kind, n, q):
+    """The test body, in a fresh process: RCCL (its bootstrap threads, proxy and shared-memory
+    state) then starts from a clean slate rather than after everything earlier tests did in
+    the pytest process, and a failure comes back as a message instead of ending the run."""
+    import os
+    import sys
+    import traceback
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        import parallel_amg_amd as pa
+        from parallel_amg_amd._lib import call
+        from parallel_amg_amd.hierarchy import HostPlan
+        from parallel_amg_amd.partitioned import Context, PVector, mul
+        from parallel_amg_amd.solver import AMGSolver
+
+        ctx = Context(0)
+        rccl_ctx = Context(0)
+        uid = C.create_string_buffer(128)
+        call("pamg_comm_unique_id", uid)
+        call("pamg_comm_init", rccl_ctx.handle, 1, 0, uid.raw)
+
+        be = pa.SequentialBackend(1)
+        A, offs, xs = pa.generate_problem(be, kind, n)
+        H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=40))
+        assert H.nlevels >= 3
+        Hs = _selfify(H, HostPlan)
+
+        # reference: the plain single-part path (no communicator)
+        S0 = AMGSolver(ctx, H, graph=False)
+        xst0 = PVector(ctx, S0.A[0].n_own_cols, S0.A[0].n_ghost, xs[0])
+        b0 = PVector(ctx, S0.A[0].nrows)
+        mul(b0, S0.A[0], xst0)
+        x0 = S0.new_vector()
+        h0 = S0.vcycle(x0, b0, 3, res_hist=True)
+        it0, ph0 = S0.pcg(S0.new_vector(), b0, rtol=1e-10, maxit=60)
+
+        for graph in (False, True):
+            S = AMGSolver(rccl_ctx, Hs, graph=graph)
+            assert S.A[0].n_ghost > 0 and S.R[0].n_ghost > 0
+            # SpMV through the self-exchange (overlapped interior/boundary split)
+            xst = PVector(rccl_ctx, S.A[0].n_own_cols, S.A[0].n_ghost, xs[0])
+            b = PVector(rccl_ctx, S.A[0].nrows)
+            mul(b, S.A[0], xst)
+            assert np.array_equal(b.own_values().view(np.int64), b0.own_values().view(np.int64))
+            x = S.new_vector()
+            S.vcycle(x, b, 2)  # first call captures the graph (when enabled)
+            S.vcycle(x, b, 1)
+            h = S.vcycle(S.new_vector(), b, 3, res_hist=True)
+            x3 = S.new_vector()
+            S.vcycle(x3, b, 3)
+            assert np.array_equal(x3.own_values().view(np.int64), x0.own_values().view(np.int64)), \
+                f"graph={graph}: V-cycles through RCCL self-exchange differ from the plain path"
+            np.testing.assert_allclose(h, h0, rtol=1e-12, atol=0)
+            st = S.graph_state()
+            assert st["captured"] == graph and not st["failed"], st
+            it, ph = S.pcg(S.new_vector(), b, rtol=1e-10, maxit=60)
+            assert it == it0
+            np.testing.assert_allclose(ph, ph0, rtol=1e-9, atol=0)
+            del S, xst, b, x, x3
+        q.put("ok")
+    except BaseException:
+        q.put(traceback.format_exc())
 
 
 @pytest.mark.parametrize("kind,n", [("poisson3d", 14), ("aniso3d", 12), ("poisson2d", 40)])
-def test_rccl_self_exchange_vcycle_bits(ctx, rccl_ctx, kind, n):
-    import parallel_amg_amd as pa
-    from parallel_amg_amd.hierarchy import HostPlan
-    from parallel_amg_amd.partitioned import PVector, mul
-    from parallel_amg_amd.solver import AMGSolver
-
-    be = pa.SequentialBackend(1)
-    A, offs, xs = pa.generate_problem(be, kind, n)
-    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=40))
-    assert H.nlevels >= 3
-    Hs = _selfify(H, HostPlan)
-
-    # reference: the plain single-part path (no communicator)
-    S0 = AMGSolver(ctx, H, graph=False)
-    xst0 = PVector(ctx, S0.A[0].n_own_cols, S0.A[0].n_ghost, xs[0])
-    b0 = PVector(ctx, S0.A[0].nrows)
-    mul(b0, S0.A[0], xst0)
-    x0 = S0.new_vector()
-    h0 = S0.vcycle(x0, b0, 3, res_hist=True)
-    it0, ph0 = S0.pcg(S0.new_vector(), b0, rtol=1e-10, maxit=60)
-
-    for graph in (False, True):
-        S = AMGSolver(rccl_ctx, Hs, graph=graph)
-        assert S.A[0].n_ghost > 0 and S.R[0].n_ghost > 0
-        # SpMV through the self-exchange (overlapped interior/boundary split)
-        xst = PVector(rccl_ctx, S.A[0].n_own_cols, S.A[0].n_ghost, xs[0])
-        b = PVector(rccl_ctx, S.A[0].nrows)
-        mul(b, S.A[0], xst)
-        assert np.array_equal(b.own_values().view(np.int64), b0.own_values().view(np.int64))
-        x = S.new_vector()
-        S.vcycle(x, b, 2)  # first call captures the graph (when enabled)
-        S.vcycle(x, b, 1)
-        h = S.vcycle(S.new_vector(), b, 3, res_hist=True)
-        x3 = S.new_vector()
-        S.vcycle(x3, b, 3)
-        assert np.array_equal(x3.own_values().view(np.int64), x0.own_values().view(np.int64)), \
-            f"graph={graph}: V-cycles through RCCL self-exchange differ from the plain path"
-        np.testing.assert_allclose(h, h0, rtol=1e-12, atol=0)
-        st = S.graph_state()
-        assert st["captured"] == graph and not st["failed"], st
-        it, ph = S.pcg(S.new_vector(), b, rtol=1e-10, maxit=60)
-        assert it == it0
-        np.testing.assert_allclose(ph, ph0, rtol=1e-9, atol=0)
-        del S
+def test_rccl_self_exchange_vcycle_bits(built, kind, n):
+    import multiprocessing as mp
+    import queue
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_run, args=(kind, n, q))
+    p.start()
+    try:
+        res = q.get(timeout=150)
+    except queue.Empty:
+        res = None
+    p.join(timeout=60)
+    assert res == "ok", res if res is not None else f"worker died (exit code {p.exitcode})"
