@@ -186,7 +186,9 @@ def main():
     # (only when the record was measured on the same column layout as this run)
     c24 = A0.stream_bytes < 12 * A0.nnz
     vd = A0.stream_bytes < 10 * A0.nnz
+    rl8 = c24 and not vd and A0.stream_bytes < 11 * A0.nnz + 4 * A0.nrows
     kname = ("k_rows_tile2<2, 1024, 256, false, false, 256, true, true>" if vd
+             else "k_rows_tile2<2, 1024, 256, false, false, 256, true, false, true>" if rl8
              else "k_rows_tile2<2, 1024, 256, false, false, 256, true>" if c24
              else "k_rows_tile2<2, 1024, 256, false, false>")
     traffic, traffic_src = None, None
@@ -229,7 +231,8 @@ def main():
             "roofline": {
                 "kernel": kname + " (level-0 post-smoothing Jacobi"
                           + (", value dictionaries" if vd else "")
-                          + (", 24-bit column stream)" if c24 else ")"),
+                          + (", 24-bit column stream" if c24 else "")
+                          + (", 8-bit row lengths)" if rl8 else ")"),
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic, "traffic_source": traffic_src,

@@ -159,14 +159,15 @@ __device__ __forceinline__ T stream_load(const T* p, std::false_type) {
 }
 
 template <int OP, int TNNZ, int TROWS, bool XCD, bool NT = false, int BS = kBlock, bool C24 = false,
-          bool VD = false>
+          bool VD = false, bool RL8 = false>
 __global__ __launch_bounds__(BS) void k_rows_tile2(
     const int4* __restrict__ tiles, int ntiles, const int* __restrict__ rowptr,
     const int* __restrict__ col, const double* __restrict__ val, const double* __restrict__ x,
     const double* __restrict__ b, double* __restrict__ y, double omega,
     const double* __restrict__ diag, const uint16_t* __restrict__ clo = nullptr,
     const uint8_t* __restrict__ chi = nullptr, const int* __restrict__ tbase = nullptr,
-    const uint8_t* __restrict__ vidx = nullptr, const double* __restrict__ vtab = nullptr) {
+    const uint8_t* __restrict__ vidx = nullptr, const double* __restrict__ vtab = nullptr,
+    const uint8_t* __restrict__ rlen = nullptr) {
     // C24: the column stream is 3 B/nonzero — per-tile base + 16-bit low part (8 B per lane)
     // + 8-bit high part (4 B per lane) instead of the 16-B int4 of 32-bit ids.
     // VD (opt-in): values are 4-bit indices (2 B per lane) into the tile's 16-value table,
@@ -178,6 +179,10 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
     __shared__ __attribute__((aligned(16))) double lprod[TNNZ + 8];
     __shared__ int lrp[TROWS + 1];
     __shared__ double ldiag[OP == OP_JACOBI ? TROWS : 1];
+    // RL8: row lengths are 8-bit (1 B/row instead of a 4-B row pointer); the row starts are
+    // rebuilt from the tile's first nonzero by a wave-level scan + the wave totals (lwt)
+    static_assert(!RL8 || TROWS <= BS, "8-bit row lengths: one row per lane");
+    __shared__ int lwt[RL8 ? BS / 64 : 1];
 
     int bid = blockIdx.x;
     if constexpr (XCD) {
@@ -218,7 +223,27 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
             vb[j] = stream_load(reinterpret_cast<const double2*>(val + gs + 2), nt{});
         }
     }
-    for (int i = tid; i <= nr; i += BS) lrp[i] = rowptr[r0 + i];
+    int rl_len = 0, rl_inc = 0;  // RL8: this lane's row length and wave-inclusive length sum
+    if constexpr (RL8) {
+        const int lane = tid & 63;
+        rl_len = tid < nr ? (int)rlen[r0 + tid] : 0;
+        rl_inc = rl_len;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int u = __shfl_up(rl_inc, off, 64);
+            if (lane >= off) rl_inc += u;
+        }
+        if (lane == 63) lwt[tid >> 6] = rl_inc;
+    } else {
+        for (int i = tid; i <= nr; i += BS) lrp[i] = rowptr[r0 + i];
+    }
+    // row start of this lane's row (RL8, after a barrier has published lwt)
+    auto rl_base = [&]() {
+        int pre = z0;
+#pragma unroll
+        for (int q = 0; q < BS / 64; ++q) pre += q < (tid >> 6) ? lwt[q] : 0;
+        return pre;
+    };
     // one row per lane: fetch the epilogue's own-row operands (b, old x, y, a_ii) now, so
     // their latency hides under the column stream instead of trailing the LDS phase
     constexpr bool ONE_ROW = TROWS <= BS;
@@ -235,7 +260,15 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
         }
     }
     if constexpr (OP == OP_JACOBI) {
-        if (!diag) __syncthreads();
+        if (!diag) {
+            __syncthreads();
+            if constexpr (RL8) {  // the in-tile diagonal search needs every row's bounds
+                const int base = rl_base();
+                if (tid == 0) lrp[0] = z0;
+                if (tid < TROWS) lrp[tid + 1] = base + rl_inc;
+                __syncthreads();
+            }
+        }
     }
 
     double xv[G][4];
@@ -282,7 +315,15 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
     __syncthreads();
     if constexpr (ONE_ROW) {
         if (tid < nr) {
-            const int kb = lrp[tid] - za, ke = lrp[tid + 1] - za;
+            int kb, ke;
+            if constexpr (RL8) {
+                const int base = rl_base();
+                kb = base + rl_inc - rl_len - za;
+                ke = base + rl_inc - za;
+            } else {
+                kb = lrp[tid] - za;
+                ke = lrp[tid + 1] - za;
+            }
             const double s = row_sum_lds(lprod, kb, ke);
             const int r = r0 + tid;
             if constexpr (OP == OP_SPMV) {
@@ -709,6 +750,12 @@ void launch_tile2(const pamg_mat& A, const TileSet& ts, const double* x, const d
         k_rows_tile2<OP, TNNZ, TROWS, false, false, kBlock, true, true><<<ts.n_short, kBlock, 0, s>>>(
             ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg, A.d_clo,
             A.d_chi, ts.d_base, A.d_vidx, ts.d_vtab);
+    } else if (ts.c24 && A.d_clo && ts.rl8 && A.d_rlen) {
+        if constexpr (TROWS <= kBlock) {
+            k_rows_tile2<OP, TNNZ, TROWS, false, false, kBlock, true, false, true><<<ts.n_short, kBlock, 0, s>>>(
+                ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg, A.d_clo,
+                A.d_chi, ts.d_base, nullptr, nullptr, A.d_rlen);
+        }
     } else if (ts.c24 && A.d_clo) {
         k_rows_tile2<OP, TNNZ, TROWS, false, false, kBlock, true><<<ts.n_short, kBlock, 0, s>>>(
             ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg, A.d_clo,

@@ -40,6 +40,11 @@ struct TileSet {
     // a value is a 4-bit index (pamg_mat::d_vidx) into the tile's 16-entry table
     double* d_vtab = nullptr;  // 16 per short tile
     bool vd = false;
+    // 8-bit row lengths (pamg_mat::d_rlen) instead of row pointers: every row of a short tile
+    // has <= 255 nonzeros (variant 1, one row per lane, 24-bit columns, plain values)
+    bool rl8 = false;
+    int max_short_len = 0;    // longest row in a short tile
+    int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
 };
 
@@ -56,6 +61,7 @@ struct Options {
     int tile_order = 1;        // 1: banded XCD-blocked tile order (see build_tiles)
     int col24 = 1;             // 1: 3-byte column stream where every tile's span fits 2^24
     int long_tiles = 1;        // 1: 4096-nonzero tiles for operators averaging >= 48 nnz/row
+    int row_len8 = 1;          // 1: 8-bit row lengths instead of 32-bit row pointers where they fit
     int value_dict = 0;        // 1 (opt-in): 4-bit per-tile value dictionaries where they fit
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };
@@ -105,6 +111,7 @@ struct pamg_mat {
     uint16_t* d_clo = nullptr;  // 24-bit column stream (TileSet::c24): low 16 bits
     uint8_t* d_chi = nullptr;   //   and high 8 bits of (column - tile base)
     uint8_t* d_vidx = nullptr;  // value dictionary indices, two per byte (TileSet::vd)
+    uint8_t* d_rlen = nullptr;  // row lengths, when a tile set uses them (TileSet::rl8)
     double* d_val = nullptr;
     double* d_diag = nullptr;  // a_ii for square matrices (zero-guess Jacobi), else null
     const pamg_plan* plan = nullptr;

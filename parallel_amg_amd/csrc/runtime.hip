@@ -173,6 +173,8 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
         }
         tiles.push_back(make_int4(r, end, (int)rp[r], (int)rp[end]));
         ts->nnz_short += rp[end] - rp[r];
+        ts->rows_short += end - r;
+        for (int q = r; q < end; ++q) ts->max_short_len = std::max(ts->max_short_len, (int)(rp[q + 1] - rp[q]));
         i = j;
     }
     for (int r : longr) ts->nnz_long += rp[r + 1] - rp[r];
@@ -218,6 +220,12 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
     ts->vd = false;
     if (opt.value_dict && ts->c24 && val)
         CHECK(build_value_dict(tiles, val, ts, vidx, (ci.size() + 1) / 2 + 8));
+    ts->rl8 = opt.row_len8 && opt.rows_kernel == 1 && ts->c24 && !ts->vd && tnnz >= 1024 && trows <= pamg::kBlock &&
+              ts->max_short_len <= 255 && !opt.xcd_remap && !opt.stream_nt && ts->n_short > 0 &&
+              ts->nnz_short <= 16 * ts->rows_short;
+    // ^ short rows only: the 3 B/row saved are 3-8 % of a 4-7-nonzero row (A0 SpMV -2 %, P0
+    //   -5..-8 %) but ~1 % of a 30-nonzero row, where the scan's latency costs more (R0, A1
+    //   +2..3 %; profiles/r01_kbench_512_rl8.jsonl)
     if (ts->n_short)
         HIPC(hipMemcpy(ts->d_short, tiles.data(), sizeof(int4) * tiles.size(), hipMemcpyHostToDevice));
     if (ts->n_long)
@@ -230,7 +238,9 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_long);
     dfree(ts.d_base);
     dfree(ts.d_vtab);
-    ts.c24 = ts.vd = false;
+    ts.c24 = ts.vd = ts.rl8 = false;
+    ts.max_short_len = 0;
+    ts.rows_short = 0;
     ts.n_short = ts.n_long = 0;
 }
 
@@ -847,13 +857,23 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     std::vector<uint8_t> hi, vidx;
     CHECK(build_tiles(rp, inner, &A->interior, band, ci, &lo, &hi, val, &vidx));
     CHECK(build_tiles(rp, bnd, &A->boundary, band, ci, &lo, &hi, val, &vidx));
+    if (A->interior.rl8 || A->boundary.rl8) {
+        std::vector<uint8_t> rl(nrows + kVecPad, 0);
+        for (int64_t i = 0; i < nrows; ++i) rl[i] = (uint8_t)std::min<int64_t>(255, rp[i + 1] - rp[i]);
+        CHECK(dalloc(&A->d_rlen, nrows + kVecPad));
+        HIPC(hipMemcpy(A->d_rlen, rl.data(), rl.size(), hipMemcpyHostToDevice));
+    }
     if (!vidx.empty()) {
         CHECK(dalloc(&A->d_vidx, (int64_t)vidx.size()));
         HIPC(hipMemcpy(A->d_vidx, vidx.data(), vidx.size(), hipMemcpyHostToDevice));
     }
     // the bytes one apply streams: values (8 B, or a 4-bit index + the tile's 128-B table),
     // columns (3 B in 24-bit tile sets), row pointers, tile descriptors (+ bases)
-    A->stream_bytes = 4 * (nrows + 1);
+    // row bounds: 1 B per row of an rl8 tile set, else 4 B per row pointer (+ the one that
+    // closes the last row)
+    A->stream_bytes = 4;
+    for (const pamg::TileSet* t : {&A->interior, &A->boundary})
+        A->stream_bytes += (t->rl8 ? 1 : 4) * t->rows_short + 4 * (int64_t)t->n_long;
     for (const pamg::TileSet* t : {&A->interior, &A->boundary})
         A->stream_bytes += (t->c24 ? 3 : 4) * t->nnz_short + 12 * t->nnz_long +
                            (t->vd ? t->nnz_short / 2 + 128 * (int64_t)t->n_short : 8 * t->nnz_short) +
@@ -877,6 +897,7 @@ int pamg_mat_destroy(pamg_mat* A) {
     dfree(A->d_rowptr);
     dfree(A->d_col);
     dfree(A->d_clo);
+    dfree(A->d_rlen);
     dfree(A->d_chi);
     dfree(A->d_vidx);
     dfree(A->d_val);
@@ -1311,6 +1332,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "poison_ghosts" && (value == 0 || value == 1)) o.poison_ghosts = (int)value;
     else if (k == "col24" && (value == 0 || value == 1)) o.col24 = (int)value;
     else if (k == "long_tiles" && (value == 0 || value == 1)) o.long_tiles = (int)value;
+    else if (k == "row_len8" && (value == 0 || value == 1)) o.row_len8 = (int)value;
     else if (k == "value_dict" && (value == 0 || value == 1)) o.value_dict = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
@@ -1344,6 +1366,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "stream_nt") *value = o.stream_nt;
     else if (k == "tile_order") *value = o.tile_order;
     else if (k == "long_tiles") *value = o.long_tiles;
+    else if (k == "row_len8") *value = o.row_len8;
     else if (k == "poison_ghosts") *value = o.poison_ghosts;
     else if (k == "col24") *value = o.col24;
     else if (k == "value_dict") *value = o.value_dict;

@@ -51,23 +51,28 @@ LENGTHS = {
     "budget_edge": [1021, 1022, 1023, 1024, 1, 2045, 2046, 2047, 2048, 3, 4093, 4094, 4095, 4096, 2, 511] * 3,
     "one_row": [13],
     "empty_rows": [0] * 100,
+    # short rows on average (8-bit row lengths in use) with the longest row at the limit...
+    "len8_edge": ([255, 254] + [1, 0, 3, 7] * 10) * 8,
+    # ... and one past it (32-bit row pointers)
+    "len8_over": ([256] + [2] * 40) * 4,
 }
 
 # (rows_kernel, tile_nnz, tile_rows, xcd_remap, jacobi_diag, stream_nt, tile_order, col24,
-#  value_dict, long_tiles): every tuning configuration must be bit-exact
-TILE_CONFIGS = [(0, 2048, 256, 0, 0, 0, 0, 1, 0, 1), (1, 2048, 256, 0, 0, 0, 0, 1, 0, 1), (1, 2048, 256, 1, 1, 0, 0, 1, 0, 1),
-                (1, 1024, 256, 0, 0, 0, 0, 1, 0, 1), (1, 1024, 256, 0, 0, 1, 1, 1, 0, 1), (1, 4096, 256, 0, 0, 1, 0, 1, 0, 1),
-                (1, 4096, 512, 1, 0, 0, 0, 1, 0, 1), (2, 256, 64, 0, 0, 0, 0, 1, 0, 1), (2, 512, 64, 0, 0, 0, 1, 1, 0, 1),
-                (2, 512, 64, 0, 1, 0, 0, 1, 0, 1), (2, 1024, 64, 0, 0, 0, 0, 1, 0, 1), (3, 1024, 256, 0, 0, 0, 1, 1, 0, 1),
-                (3, 2048, 256, 0, 0, 0, 0, 1, 0, 1), (1, 512, 128, 0, 0, 0, 1, 1, 0, 1), (1, 2048, 512, 0, 0, 0, 1, 1, 0, 1),
-                (1, 1024, 256, 0, 0, 0, 1, 0, 0, 1), (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1), (1, 1024, 256, 0, 0, 0, 1, 1, 1, 1),
-                (1, 1024, 256, 0, 1, 0, 1, 1, 1, 1), (1, 2048, 256, 0, 0, 0, 1, 1, 1, 1),
-                (1, 1024, 256, 0, 0, 0, 1, 1, 0, 0), (1, 1024, 256, 0, 0, 0, 4, 1, 0, 1)]
+#  value_dict, long_tiles, row_len8): every tuning configuration must be bit-exact
+TILE_CONFIGS = [(0, 2048, 256, 0, 0, 0, 0, 1, 0, 1, 1), (1, 2048, 256, 0, 0, 0, 0, 1, 0, 1, 1), (1, 2048, 256, 1, 1, 0, 0, 1, 0, 1, 1),
+                (1, 1024, 256, 0, 0, 0, 0, 1, 0, 1, 1), (1, 1024, 256, 0, 0, 1, 1, 1, 0, 1, 1), (1, 4096, 256, 0, 0, 1, 0, 1, 0, 1, 1),
+                (1, 4096, 512, 1, 0, 0, 0, 1, 0, 1, 1), (2, 256, 64, 0, 0, 0, 0, 1, 0, 1, 1), (2, 512, 64, 0, 0, 0, 1, 1, 0, 1, 1),
+                (2, 512, 64, 0, 1, 0, 0, 1, 0, 1, 1), (2, 1024, 64, 0, 0, 0, 0, 1, 0, 1, 1), (3, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1),
+                (3, 2048, 256, 0, 0, 0, 0, 1, 0, 1, 1), (1, 512, 128, 0, 0, 0, 1, 1, 0, 1, 1), (1, 2048, 512, 0, 0, 0, 1, 1, 0, 1, 1),
+                (1, 1024, 256, 0, 0, 0, 1, 0, 0, 1, 1), (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1), (1, 1024, 256, 0, 0, 0, 1, 1, 1, 1, 1),
+                (1, 1024, 256, 0, 1, 0, 1, 1, 1, 1, 1), (1, 2048, 256, 0, 0, 0, 1, 1, 1, 1, 1),
+                (1, 1024, 256, 0, 0, 0, 1, 1, 0, 0, 1), (1, 1024, 256, 0, 0, 0, 4, 1, 0, 1, 1),
+                (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 0), (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1)]
 OPT_KEYS = ("rows_kernel", "tile_nnz", "tile_rows", "xcd_remap", "jacobi_diag", "stream_nt", "tile_order",
-            "col24", "value_dict", "long_tiles")
+            "col24", "value_dict", "long_tiles", "row_len8")
 
 
-@pytest.fixture(params=TILE_CONFIGS, ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}_lt{}".format(*c))
+@pytest.fixture(params=TILE_CONFIGS, ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}_lt{}_rl{}".format(*c))
 def tile_cfg(request, built):
     import ctypes
     from parallel_amg_amd._lib import call
@@ -254,28 +259,29 @@ def test_vcycle_sweeps_bit_exact(ctx, nu1, nu2):
 
 def test_stream_bytes_layout(ctx):
     """pamg_mat_stream_bytes: 12 B/nnz + row pointers + 16-B tile descriptors in the 32-bit
-    layout; 3-B columns (+ a 4-B base per tile) in the 24-bit one (roofline byte model)."""
-    import ctypes
+    layout; 3-B columns (+ a 4-B base per tile) in the 24-bit one; 1 B per row instead of a
+    4-B row pointer with 8-bit row lengths (roofline byte model)."""
     from parallel_amg_amd._lib import call
     M = O.generate("poisson3d", 16, 16, 16)
     n, nnz = M.nrows, len(M.col)
-    got = {}
-    for c24 in (0, 1):
-        call("pamg_set_option", b"col24", c24)
+
+    def stream_bytes(**opts):
+        for k, v in opts.items():
+            call("pamg_set_option", k.encode(), v)
         try:
             A, _h = upload(ctx, M)
+            return A.stream_bytes
         finally:
-            call("pamg_set_option", b"col24", 1)
-        got[c24] = A.stream_bytes
-    nt, rem = divmod(got[0] - 12 * nnz - 4 * (n + 1), 16)
+            for k in opts:
+                call("pamg_set_option", k.encode(), 0 if k == "value_dict" else 1)
+
+    got0 = stream_bytes(col24=0, row_len8=0)
+    nt, rem = divmod(got0 - 12 * nnz - 4 * (n + 1), 16)
     assert rem == 0 and nt > 0
-    assert got[1] == 11 * nnz + 4 * (n + 1) + 20 * nt
-    call("pamg_set_option", b"value_dict", 1)   # 2 distinct values: every tile fits
-    try:
-        A, _h = upload(ctx, M)
-    finally:
-        call("pamg_set_option", b"value_dict", 0)
-    assert A.stream_bytes == 3 * nnz + nnz // 2 + 4 * (n + 1) + (20 + 128) * nt
+    assert stream_bytes(col24=1, row_len8=0) == 11 * nnz + 4 * (n + 1) + 20 * nt
+    assert stream_bytes(col24=1, row_len8=1) == 11 * nnz + n + 4 + 20 * nt
+    # 2 distinct values: every tile takes a value dictionary (which keeps the row pointers)
+    assert stream_bytes(value_dict=1) == 3 * nnz + nnz // 2 + 4 * (n + 1) + (20 + 128) * nt
 
 
 @pytest.mark.parametrize("seed,n,density,weak,iso", [(1, 3000, 0.003, 0.3, 0.02), (2, 5000, 0.001, 0.0, 0.0),
