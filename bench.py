@@ -199,6 +199,9 @@ def main():
         if rec:
             traffic, traffic_src = float(rec[0]["traffic_bytes"]), os.path.relpath(pmc, ROOT)
 
+    # fine-level nonzeros of the whole problem (every rank holds only its own rows)
+    nnz_fine = (sum(be.allgather({rank: int(H.levels[0][rank].A.nnz)})) if world > 1
+                else int(sum(H.levels[0][p].A.nnz for p in H.levels[0])))
     if rank == 0:
         gl_rows = int(H.offsets(0)[-1])
         out = {
@@ -217,8 +220,7 @@ def main():
             "config": {
                 "workload": f"{workload}, SA-AMG V({nu1},{nu2}) weighted-Jacobi, "
                             f"{world} part(s)",
-                "n": gl_rows, "nnz_fine": int(sum(H.levels[0][p].A.nnz for p in H.levels[0])) if world == 1
-                else None, "levels": S.L, "max_coarse": args.max_coarse,
+                "n": gl_rows, "nnz_fine": int(nnz_fine), "levels": S.L, "max_coarse": args.max_coarse,
                 "parallelism": f"row-slab partition p{world} (RCCL ghost exchange)",
                 "graph": S.graph_state(),
                 "transport": args.transport if world > 1 else None,
