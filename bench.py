@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--transport", choices=["rccl", "host"], default="rccl",
                     help="host = debug transport (ranks may share one GPU; not a perf mode)")
     ap.add_argument("--sweeps", default="1,1", help="nu1,nu2 of the V(nu1,nu2) cycle (SPEC S6)")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="libpamg tuning option for an A/B run (pamg_set_option; INTEGRATION.md table)")
     ap.add_argument("--value-dict", action="store_true",
                     help="opt-in per-tile 4-bit value dictionaries where a tile has <= 16 distinct "
                          "values (exact; not the default layout)")
@@ -79,6 +81,9 @@ def main():
 
     _lib.lib()  # fail loudly if libpamg.so is missing
     _lib.call("pamg_set_option", b"value_dict", int(args.value_dict))
+    for kv in args.set:
+        k, v = kv.split("=")
+        _lib.call("pamg_set_option", k.encode(), int(v))
     ndev = torch.cuda.device_count()
     dev = local % max(ndev, 1)
     torch.cuda.set_device(dev)
@@ -227,6 +232,7 @@ def main():
                 # levels >= this one are held whole on every rank (SPEC §S7 agglomeration)
                 "replicated_from_level": int(S.rep_level) if world > 1 else None,
                 "value_dict": bool(args.value_dict),
+                "options": list(args.set),
             },
             "fine_spmv_GBps": round(spmv_gbps, 1),
             "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
