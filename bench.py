@@ -10,12 +10,14 @@ exchanges ghosts over RCCL.
     python bench.py [--gpus N --steps K --warmup W]          # N=1
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line. Timed region: barrier + device sync, K V-cycles (hipGraph
-replay on one part), device sync + barrier; max over ranks. Inputs are resident in HBM.
+Rank 0 prints ONE JSON line. Timed region: device sync + barrier, K V-cycles (hipGraph
+replay), device sync + barrier; max over ranks. Inputs are resident in HBM. libpamg is loaded
+before torch, and torch stays off the GPU (gloo rendezvous only): see _lib.runtime_providers.
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -71,37 +73,36 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
 
-    import torch
-    import torch.distributed as dist
-
+    # libpamg first: it then binds to /opt/rocm's HIP 7.2 / RCCL 2.27.7 rather than the copies
+    # the torch wheel bundles (HIP 7.0 / RCCL 2.26.6, same sonames; _lib.runtime_providers).
+    # torch is only the process-group rendezvous here (gloo, CPU): it never touches the GPU,
+    # so libpamg's runtime is the only one driving the device (device sync = ctx.sync()).
     import parallel_amg_amd as pa
     from parallel_amg_amd import _lib
     from parallel_amg_amd.partitioned import Context, PVector, mul
     from parallel_amg_amd.solver import OPS, AMGSolver
 
     _lib.lib()  # fail loudly if libpamg.so is missing
+    import torch
+    import torch.distributed as dist
+
     _lib.call("pamg_set_option", b"value_dict", int(args.value_dict))
     for kv in args.set:
         k, v = kv.split("=")
         _lib.call("pamg_set_option", k.encode(), int(v))
-    ndev = torch.cuda.device_count()
-    dev = local % max(ndev, 1)
-    torch.cuda.set_device(dev)
+    nd = ctypes.c_int()
+    _lib.call("pamg_device_count", ctypes.byref(nd))
+    dev = local % max(nd.value, 1)
     if world > 1:
-        if args.transport == "rccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-        else:
-            dist.init_process_group("gloo")
+        dist.init_process_group("gloo")  # host messages; the device exchange is libpamg's RCCL
         be = pa.DistributedBackend()
     else:
         be = pa.SequentialBackend(1)
+    log(f"runtime: {_lib.runtime_providers()}")
 
     def barrier():
         if world > 1:
-            if args.transport == "rccl":
-                dist.barrier(device_ids=[dev])
-            else:
-                dist.barrier()
+            dist.barrier()
 
     ctx = Context(dev, be, transport=args.transport)
     t0 = time.time()
@@ -146,19 +147,16 @@ def main():
     # ---- warmup + timed region -------------------------------------------------------
     if args.warmup:
         S.vcycle(x, b, args.warmup)
+    ctx.sync()    # device sync: every GPU operation of this process is on libpamg's streams
     barrier()
-    ctx.sync()
-    torch.cuda.synchronize()
     ts = time.perf_counter()
     S.vcycle_async(x, b, args.steps)
     ctx.sync()
-    torch.cuda.synchronize()
     barrier()
     te = time.perf_counter()
     dt = te - ts
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64,
-                         device="cuda" if args.transport == "rccl" else "cpu")
+        t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     vps = args.steps / dt

@@ -52,6 +52,9 @@ const char* pamg_last_error(void);
 int pamg_ctx_create(int device, pamg_ctx** out);
 int pamg_ctx_destroy(pamg_ctx* ctx);
 int pamg_ctx_sync(pamg_ctx* ctx);
+/* Number of visible GPUs, through libpamg's own HIP runtime (a driver that must not
+ * initialise another runtime in the process asks here; see INTEGRATION.md, load order). */
+int pamg_device_count(int* n);
 /* RCCL communicator for multi-part runs: rank 0 calls pamg_comm_unique_id, the 128 bytes are
  * broadcast by the host layer (MPI / torch.distributed), then every rank calls pamg_comm_init. */
 int pamg_comm_unique_id(unsigned char id[128]);

@@ -37,6 +37,7 @@ SIGNATURES = {
     "pamg_ctx_create": [i32, pvp],
     "pamg_ctx_destroy": [vp],
     "pamg_ctx_sync": [vp],
+    "pamg_device_count": [C.POINTER(C.c_int)],
     "pamg_comm_unique_id": [C.c_char_p],
     "pamg_comm_init": [vp, i32, i32, C.c_char_p],
     "pamg_comm_rank": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
@@ -114,6 +115,37 @@ def lib():
             f.restype = _RESTYPE.get(name, C.c_int)
         _lib = L
     return _lib
+
+
+class _DlInfo(C.Structure):
+    _fields_ = [("dli_fname", C.c_char_p), ("dli_fbase", C.c_void_p),
+                ("dli_sname", C.c_char_p), ("dli_saddr", C.c_void_p)]
+
+
+def runtime_providers() -> dict:
+    """The files that serve libpamg's HIP and RCCL calls in this process.
+
+    Load order matters: the PyTorch wheel bundles its own ROCm (HIP 7.0, RCCL 2.26) under
+    torch/lib with the same sonames as /opt/rocm's (libamdhip64.so.7, librccl.so.1), so if
+    torch is imported first, libpamg binds to those copies; loaded first, libpamg binds to
+    /opt/rocm (HIP 7.2, RCCL 2.27.7) and torch maps its own copies beside them. Measured on the
+    MI355X box: RCCL 2.26.6 segfaults in tests/test_gpu_rccl_self.py where 2.27.7 passes, so
+    drivers that use libpamg's RCCL load it before torch and keep torch off the GPU (bench.py).
+    """
+    L = lib()
+    dl = C.CDLL(None)
+    dladdr = dl.dladdr
+    dladdr.argtypes = [C.c_void_p, C.POINTER(_DlInfo)]
+    out = {}
+    for key, sym in (("hip", "hipStreamCreateWithFlags"), ("rccl", "ncclCommInitRank")):
+        try:
+            addr = C.cast(getattr(L, sym), C.c_void_p).value
+        except AttributeError:
+            continue
+        info = _DlInfo()
+        if addr and dladdr(addr, C.byref(info)) and info.dli_fname:
+            out[key] = os.path.realpath(info.dli_fname.decode())
+    return out
 
 
 def call(name, *args):

@@ -557,6 +557,12 @@ int pamg_ctx_destroy(pamg_ctx* ctx) {
     return PAMG_OK;
 }
 
+int pamg_device_count(int* n) {
+    if (!n) return fail(PAMG_E_ARG, "device_count: NULL");
+    HIPC(hipGetDeviceCount(n));
+    return PAMG_OK;
+}
+
 int pamg_ctx_sync(pamg_ctx* ctx) {
     if (!ctx) return fail(PAMG_E_ARG, "ctx_sync: NULL");
     HIPC(hipStreamSynchronize(ctx->s_comm));

@@ -7,6 +7,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# Load libpamg before any test module imports torch: libpamg then binds to /opt/rocm's HIP and
+# RCCL instead of the copies bundled in the torch wheel (parallel_amg_amd/_lib.py,
+# runtime_providers). Not built yet (fresh CPU checkout): the `built` fixture builds it.
+if os.path.exists(os.path.join(ROOT, "parallel_amg_amd", "libpamg.so")):
+    from parallel_amg_amd import _lib as _pamg_lib
+    _pamg_lib.lib()
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libpamg's HIP path)")

@@ -87,3 +87,20 @@ def test_product_never_imports_the_oracle():
                 assert "import oracle" not in txt and "from oracle" not in txt, f
                 assert "libpamg_oracle" not in txt and not re.search(r"#include\s*[<\"].*oracle", txt), f
                 assert not re.search(r"\borc_\w+\(", txt), f
+
+
+def test_load_order_binds_opt_rocm_runtime(built):
+    """libpamg loaded before torch binds to /opt/rocm's HIP and RCCL, not to the copies in the
+    torch wheel (same sonames, older RCCL; _lib.runtime_providers). bench.py, conftest.py and
+    the multi-process workers rely on this order."""
+    import json
+    import subprocess
+    import sys
+    code = ("import json, parallel_amg_amd._lib as L; L.lib(); import torch; "
+            "print(json.dumps(L.runtime_providers()))")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                         check=True).stdout.strip().splitlines()[-1]
+    prov = json.loads(out)
+    assert set(prov) == {"hip", "rccl"}
+    for k, path in prov.items():
+        assert "/torch/" not in path and path.startswith("/opt/rocm"), (k, path)

@@ -28,13 +28,15 @@ def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, poison
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), OMP_NUM_THREADS="2")
-    import torch
-    import torch.distributed as dist
+    import ctypes
 
     import parallel_amg_amd as pa
-    from parallel_amg_amd.partitioned import Context, PVector, mul
+    from parallel_amg_amd import _lib
     from parallel_amg_amd._lib import call
+    from parallel_amg_amd.partitioned import Context, PVector, mul
     from parallel_amg_amd.solver import AMGSolver
+    _lib.lib()  # before torch: /opt/rocm's HIP/RCCL (see _lib.runtime_providers)
+    import torch.distributed as dist
     try:
         # SURVEY §5 race check: ghosts are NaN until their exchange lands
         call("pamg_set_option", b"poison_ghosts", int(poison))
@@ -45,7 +47,9 @@ def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, poison
         else:
             A, offs, xs = pa.generate_problem(be, kind, n)
         H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse, agglomerate=agglomerate))
-        ndev = max(1, torch.cuda.device_count())
+        nd = ctypes.c_int()
+        call("pamg_device_count", ctypes.byref(nd))
+        ndev = max(1, nd.value)
         # RCCL needs one device per rank; with fewer GPUs than ranks use the host transport
         ctx = Context(rank % ndev, be, transport="rccl" if ndev >= world else "host")
         S = AMGSolver(ctx, H, part=rank)

@@ -71,14 +71,18 @@ def _selfify(H, HostPlan):
 
 
 def _run(kind, n, q):
-    """The test body, in a fresh process: RCCL (its bootstrap threads, proxy and shared-memory
-    state) then starts from a clean slate rather than after everything earlier tests did in
-    the pytest process, and a failure comes back as a message instead of ending the run."""
+    """The test body, in a fresh process that loads libpamg before anything imports torch, so
+    libpamg's RCCL is /opt/rocm's 2.27.7 (in a process where torch came first it binds to the
+    wheel's RCCL 2.26.6, which segfaults on this self-exchange: _lib.runtime_providers); a
+    failure comes back as a message instead of ending the pytest run."""
     import os
     import sys
     import traceback
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     try:
+        from parallel_amg_amd import _lib
+        _lib.lib()
+        assert "/torch/" not in _lib.runtime_providers().get("rccl", ""), _lib.runtime_providers()
         import parallel_amg_amd as pa
         from parallel_amg_amd._lib import call
         from parallel_amg_amd.hierarchy import HostPlan
