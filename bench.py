@@ -147,11 +147,15 @@ def main():
     # ---- warmup + timed region -------------------------------------------------------
     if args.warmup:
         S.vcycle(x, b, args.warmup)
-    ctx.sync()    # device sync: every GPU operation of this process is on libpamg's streams
+    def device_sync():  # the context's streams, then hipDeviceSynchronize (every stream)
+        ctx.sync()
+        _lib.call("pamg_device_sync", dev)
+
+    device_sync()
     barrier()
     ts = time.perf_counter()
     S.vcycle_async(x, b, args.steps)
-    ctx.sync()
+    device_sync()
     barrier()
     te = time.perf_counter()
     dt = te - ts
@@ -164,12 +168,17 @@ def main():
     # ---- per-kernel timing (HIP events on the compute stream, eager) ------------------
     kprof = max(3, min(args.steps, 10))
     prof = S.profile(x, b, kprof) / kprof          # ms per V-cycle per (level, op)
-    obytes = S.op_bytes()                           # algorithmic bytes per (level, op)
+    # roofline numerator: SURVEY §8(d)'s algorithmic bytes (plain CSR, 32-bit indices: 12 B
+    # per nonzero + row pointers + x once + y [+ b]); the uploaded layout streams fewer
+    # (24-bit / dictionary columns, 8-bit row lengths), reported beside it as format bytes
+    obytes = S.op_bytes("csr")                      # algorithmic bytes per (level, op)
+    fbytes = S.op_bytes("format")                   # bytes the uploaded layout streams
     post_ms = float(prof[0, 4]) / nu2 if S.L > 1 else float(prof[0, 5])  # one sweep
     post_bytes = float(obytes[0, 4]) if S.L > 1 else float(obytes[0, 5])
+    post_fbytes = float(fbytes[0, 4]) if S.L > 1 else float(fbytes[0, 5])
     achieved = post_bytes / (post_ms * 1e-3) / 1e9
     spmv_ms = ctypes_bench_spmv(ctx, A0, x, S)
-    spmv_bytes = S.rowsum_bytes(A0, 0)
+    spmv_bytes = S.csr_bytes(A0, 0)
     spmv_gbps = spmv_bytes / (spmv_ms * 1e-3) / 1e9
     hist = S.vcycle(x, b, 1, res_hist=True)
 
@@ -187,10 +196,10 @@ def main():
     # HBM traffic of the dominant kernel from the committed rocprofv3 PMC passes of this exact
     # workload (tools/pmc_traffic.py; counters cannot be read from inside the process)
     # (only when the record was measured on the same column layout as this run)
-    c24 = A0.stream_bytes < 12 * A0.nnz
-    vd = A0.stream_bytes < 10 * A0.nnz
-    rl8 = c24 and not vd and A0.stream_bytes < 11 * A0.nnz + 4 * A0.nrows
-    kname = ("k_rows_tile2<2, 1024, 256, false, false, 256, true, true>" if vd
+    lay = _lib.layout_of(A0)
+    c24, vd, rl8, cd = lay["c24"], lay["vd"], lay["rl8"], lay["cd"]
+    kname = ("k_rows_tile2<2, 1024, 256, false, false, 256, false, false, true, %d>" % cd if cd
+             else "k_rows_tile2<2, 1024, 256, false, false, 256, true, true>" if vd
              else "k_rows_tile2<2, 1024, 256, false, false, 256, true, false, true>" if rl8
              else "k_rows_tile2<2, 1024, 256, false, false, 256, true>" if c24
              else "k_rows_tile2<2, 1024, 256, false, false>")
@@ -224,7 +233,9 @@ def main():
                 "workload": f"{workload}, SA-AMG V({nu1},{nu2}) weighted-Jacobi, "
                             f"{world} part(s)",
                 "n": gl_rows, "nnz_fine": int(nnz_fine), "levels": S.L, "max_coarse": args.max_coarse,
-                "parallelism": f"row-slab partition p{world} (RCCL ghost exchange)",
+                "parallelism": f"row-slab partition p{world}" + (
+                    "" if world == 1 else " (RCCL ghost exchange)" if args.transport == "rccl"
+                    else " (host debug transport)"),
                 "graph": S.graph_state(),
                 "transport": args.transport if world > 1 else None,
                 # levels >= this one are held whole on every rank (SPEC §S7 agglomeration)
@@ -236,13 +247,17 @@ def main():
             "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
             "roofline": {
                 "kernel": kname + " (level-0 post-smoothing Jacobi"
+                          + (f", {cd}-bit column dictionary" if cd else "")
                           + (", value dictionaries" if vd else "")
-                          + (", 24-bit column stream" if c24 else "")
+                          + (", 24-bit column stream" if c24 and not cd else "")
                           + (", 8-bit row lengths)" if rl8 else ")"),
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic, "traffic_source": traffic_src,
-                "bytes_per_launch": int(post_bytes), "ms_per_launch": round(post_ms, 4),
+                "bytes_per_launch": int(post_bytes), "bytes_model": "SURVEY 8(d) CSR (12 B/nnz)",
+                "format_bytes_per_launch": int(post_fbytes),
+                "format_GBps": round(post_fbytes / (post_ms * 1e-3) / 1e9, 1),
+                "ms_per_launch": round(post_ms, 4),
             },
             "cpu_baseline": cpu,
             "setup_s": round(t_setup, 1),

@@ -55,6 +55,9 @@ int pamg_ctx_sync(pamg_ctx* ctx);
 /* Number of visible GPUs, through libpamg's own HIP runtime (a driver that must not
  * initialise another runtime in the process asks here; see INTEGRATION.md, load order). */
 int pamg_device_count(int* n);
+/* hipDeviceSynchronize on `device`: waits for every stream of the process on that GPU (the
+ * benchmark's sync brackets; pamg_ctx_sync waits only for the context's own streams). */
+int pamg_device_sync(int device);
 /* RCCL communicator for multi-part runs: rank 0 calls pamg_comm_unique_id, the 128 bytes are
  * broadcast by the host layer (MPI / torch.distributed), then every rank calls pamg_comm_init. */
 int pamg_comm_unique_id(unsigned char id[128]);
@@ -107,9 +110,13 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols_local, const int
 int pamg_mat_destroy(pamg_mat* A);
 int pamg_mat_info(const pamg_mat* A, int64_t* nrows, int64_t* ncols_local, int64_t* nnz);
 /* Bytes of matrix data one row operation streams in the layout chosen at upload: 8 B values +
- * 4 B (or 3 B in 24-bit column tiles) columns per nonzero, 4 B row pointers, tile descriptors
- * (+ 4-B column bases). The algorithmic byte model of the roofline adds the vectors. */
+ * 4 B (3 B in 24-bit column tiles, 0.5 / 1 B with a column dictionary) columns per nonzero,
+ * 4 B row pointers (1 B with 8-bit row lengths), tile descriptors (+ 4-B column bases). */
 int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
+/* Layout the upload chose for the interior (set 0) or boundary (set 1) rows:
+ * out[0] 24-bit columns, out[1] value dictionary, out[2] 8-bit row lengths,
+ * out[3] column-dictionary index width (0, 4 or 8), out[4] column-dictionary offsets. */
+int pamg_mat_layout(const pamg_mat* A, int set, int out[5]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
 int pamg_spmv(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, pamg_vec* y);

@@ -38,6 +38,7 @@ SIGNATURES = {
     "pamg_ctx_destroy": [vp],
     "pamg_ctx_sync": [vp],
     "pamg_device_count": [C.POINTER(C.c_int)],
+    "pamg_device_sync": [i32],
     "pamg_comm_unique_id": [C.c_char_p],
     "pamg_comm_init": [vp, i32, i32, C.c_char_p],
     "pamg_comm_rank": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
@@ -60,6 +61,7 @@ SIGNATURES = {
     "pamg_mat_destroy": [vp],
     "pamg_mat_info": [vp, pi64, pi64, pi64],
     "pamg_mat_stream_bytes": [vp, pi64],
+    "pamg_mat_layout": [vp, i32, C.POINTER(C.c_int)],
     "pamg_spmv": [vp, vp, vp, vp],
     "pamg_residual": [vp, vp, vp, vp, vp, pdbl],
     "pamg_jacobi": [vp, vp, vp, vp, vp, dbl, i32],
@@ -156,6 +158,14 @@ def call(name, *args):
         msg = L.pamg_last_error().decode(errors="replace")
         raise PamgError(rc, name, msg)
     return rc
+
+
+def layout_of(M, part_set: int = 0) -> dict:
+    """The tile layout libpamg chose at upload for a device matrix (pamg_mat_layout)."""
+    out = (C.c_int * 5)()
+    call("pamg_mat_layout", M.handle, part_set, out)
+    return {"c24": bool(out[0]), "vd": bool(out[1]), "rl8": bool(out[2]), "cd": int(out[3]),
+            "cd_offsets": int(out[4])}
 
 
 def last_error() -> str:

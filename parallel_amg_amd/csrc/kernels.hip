@@ -159,7 +159,7 @@ __device__ __forceinline__ T stream_load(const T* p, std::false_type) {
 }
 
 template <int OP, int TNNZ, int TROWS, bool XCD, bool NT = false, int BS = kBlock, bool C24 = false,
-          bool VD = false, bool RL8 = false>
+          bool VD = false, bool RL8 = false, int CD = 0>
 __global__ __launch_bounds__(BS) void k_rows_tile2(
     const int4* __restrict__ tiles, int ntiles, const int* __restrict__ rowptr,
     const int* __restrict__ col, const double* __restrict__ val, const double* __restrict__ x,
@@ -167,7 +167,8 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
     const double* __restrict__ diag, const uint16_t* __restrict__ clo = nullptr,
     const uint8_t* __restrict__ chi = nullptr, const int* __restrict__ tbase = nullptr,
     const uint8_t* __restrict__ vidx = nullptr, const double* __restrict__ vtab = nullptr,
-    const uint8_t* __restrict__ rlen = nullptr) {
+    const uint8_t* __restrict__ rlen = nullptr, const uint8_t* __restrict__ cidx = nullptr,
+    const int* __restrict__ ctab = nullptr, int ctab_n = 0) {
     // C24: the column stream is 3 B/nonzero — per-tile base + 16-bit low part (8 B per lane)
     // + 8-bit high part (4 B per lane) instead of the 16-B int4 of 32-bit ids.
     // VD (opt-in): values are 4-bit indices (2 B per lane) into the tile's 16-value table,
@@ -183,6 +184,12 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
     // rebuilt from the tile's first nonzero by a wave-level scan + the wave totals (lwt)
     static_assert(!RL8 || TROWS <= BS, "8-bit row lengths: one row per lane");
     __shared__ int lwt[RL8 ? BS / 64 : 1];
+    // CD (column dictionary, 4 or 8 bits per nonzero): column = row + ctab[index], with the
+    // tile set's <= 16 / <= 256 distinct offsets (a stencil's 7 for A0) in LDS; every
+    // position's row (lrow, tile-local) is marked by the lane that owns the row (RL8 scan)
+    static_assert(CD == 0 || (RL8 && !C24 && !VD), "column dictionary: 8-bit rows, plain values");
+    __shared__ int ltab[CD == 8 ? 256 : 16];
+    __shared__ __attribute__((aligned(4))) uint8_t lrow[CD ? TNNZ + 8 : 4];
 
     int bid = blockIdx.x;
     if constexpr (XCD) {
@@ -198,6 +205,7 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
     int4 c4[G];
     double2 va[G], vb[G];
     uint16_t vn[G];  // VD: four 4-bit value indices per lane group
+    uint32_t cn[G];  // CD: four 4- or 8-bit column dictionary indices per lane group
 #pragma unroll
     for (int j = 0; j < G; ++j) {
         const int g = za + 4 * (tid + j * BS);
@@ -205,7 +213,11 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
         // NT: the once-read matrix stream goes non-temporal so the x lines (reused by the
         // z+-1 / y+-1 neighbour rows) keep their place in the XCD's L2
         using nt = std::integral_constant<bool, NT>;
-        if constexpr (C24) {
+        if constexpr (CD == 4) {
+            cn[j] = *reinterpret_cast<const uint16_t*>(cidx + (gs >> 1));
+        } else if constexpr (CD == 8) {
+            cn[j] = *reinterpret_cast<const uint32_t*>(cidx + gs);
+        } else if constexpr (C24) {
             const ushort4 lo = *reinterpret_cast<const ushort4*>(clo + gs);
             const uchar4 hi = *reinterpret_cast<const uchar4*>(chi + gs);
             const int cb = tbase[bid];
@@ -259,7 +271,27 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
             if constexpr (OP == OP_PROLONG) py = y[r];
         }
     }
-    if constexpr (OP == OP_JACOBI) {
+    if constexpr (CD != 0) {
+        if (tid < ctab_n) ltab[tid] = ctab[tid];
+        __syncthreads();  // lwt, ltab
+        if (tid < nr) {
+            const int e = rl_base() + rl_inc - za;
+            for (int p = e - rl_len; p < e; ++p) lrow[p] = (uint8_t)tid;
+        }
+        __syncthreads();  // lrow
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int q = 4 * (tid + j * BS);
+            const uint32_t rw = za + q < z1 ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
+            int cc[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int ix = CD == 4 ? (int)((cn[j] >> (4 * e)) & 15u) : (int)((cn[j] >> (8 * e)) & 255u);
+                cc[e] = r0 + (int)((rw >> (8 * e)) & 255u) + ltab[ix];
+            }
+            c4[j] = make_int4(cc[0], cc[1], cc[2], cc[3]);
+        }
+    } else if constexpr (OP == OP_JACOBI) {
         if (!diag) {
             __syncthreads();
             if constexpr (RL8) {  // the in-tile diagonal search needs every row's bounds
@@ -305,8 +337,13 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
             p[e] = ok ? vv[e] * xv[j][e] : 0.0;
             if constexpr (OP == OP_JACOBI) {
                 const int rl = cc[e] - r0;
-                if (!diag && ok && rl >= 0 && rl < nr && k >= lrp[rl] && k < lrp[rl + 1])
-                    ldiag[rl] = vv[e];
+                if constexpr (CD != 0) {
+                    // the diagonal is the entry whose column is its own row
+                    if (!diag && ok && rl == (int)lrow[k - za]) ldiag[rl] = vv[e];
+                } else {
+                    if (!diag && ok && rl >= 0 && rl < nr && k >= lrp[rl] && k < lrp[rl + 1])
+                        ldiag[rl] = vv[e];
+                }
             }
         }
         *reinterpret_cast<double2*>(&lprod[g - za]) = make_double2(p[0], p[1]);
@@ -746,6 +783,17 @@ void launch_tile2(const pamg_mat& A, const TileSet& ts, const double* x, const d
     } else if (A.stream_nt) {
         k_rows_tile2<OP, TNNZ, TROWS, false, true><<<ts.n_short, kBlock, 0, s>>>(
             ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg);
+    } else if (ts.cd && A.d_cidx && ts.rl8 && A.d_rlen) {
+        if constexpr (TROWS <= kBlock) {
+            if (ts.cd == 4)
+                k_rows_tile2<OP, TNNZ, TROWS, false, false, kBlock, false, false, true, 4><<<ts.n_short, kBlock, 0, s>>>(
+                    ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg, nullptr,
+                    nullptr, nullptr, nullptr, nullptr, A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n);
+            else
+                k_rows_tile2<OP, TNNZ, TROWS, false, false, kBlock, false, false, true, 8><<<ts.n_short, kBlock, 0, s>>>(
+                    ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg, nullptr,
+                    nullptr, nullptr, nullptr, nullptr, A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n);
+        }
     } else if (ts.c24 && A.d_clo && ts.vd && A.d_vidx) {
         k_rows_tile2<OP, TNNZ, TROWS, false, false, kBlock, true, true><<<ts.n_short, kBlock, 0, s>>>(
             ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg, A.d_clo,

@@ -43,6 +43,12 @@ struct TileSet {
     // 8-bit row lengths (pamg_mat::d_rlen) instead of row pointers: every row of a short tile
     // has <= 255 nonzeros (variant 1, one row per lane, 24-bit columns, plain values)
     bool rl8 = false;
+    // column dictionary (Options::col_dict; needs rl8): every nonzero of the short tiles has
+    // column = row + d_ctab[i] for one of the set's <= 16 (cd = 4 bits) / <= 256 (cd = 8)
+    // offsets; i is stored in pamg_mat::d_cidx (4 or 8 bits per nonzero)
+    int cd = 0;
+    int* d_ctab = nullptr;
+    int ctab_n = 0;
     int max_short_len = 0;    // longest row in a short tile
     int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
@@ -63,6 +69,7 @@ struct Options {
     int long_tiles = 1;        // 1: 4096-nonzero tiles for operators averaging >= 48 nnz/row
     int row_len8 = 1;          // 1: 8-bit row lengths instead of 32-bit row pointers where they fit
     int value_dict = 0;        // 1 (opt-in): 4-bit per-tile value dictionaries where they fit
+    int col_dict = 1;          // 1: row-relative column dictionaries (4/8-bit) where they fit
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };
 Options& options();
@@ -112,6 +119,7 @@ struct pamg_mat {
     uint8_t* d_chi = nullptr;   //   and high 8 bits of (column - tile base)
     uint8_t* d_vidx = nullptr;  // value dictionary indices, two per byte (TileSet::vd)
     uint8_t* d_rlen = nullptr;  // row lengths, when a tile set uses them (TileSet::rl8)
+    uint8_t* d_cidx = nullptr;  // column dictionary indices (TileSet::cd; 4 or 8 bits each)
     double* d_val = nullptr;
     double* d_diag = nullptr;  // a_ii for square matrices (zero-guess Jacobi), else null
     const pamg_plan* plan = nullptr;

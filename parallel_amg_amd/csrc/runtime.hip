@@ -133,7 +133,7 @@ int build_value_dict(const std::vector<int4>& tiles, const double* val, pamg::Ti
 int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
                 pamg::TileSet* ts, int64_t band, const std::vector<int>& ci,
                 std::vector<uint16_t>* lo, std::vector<uint8_t>* hi, const double* val,
-                std::vector<uint8_t>* vidx) {
+                std::vector<uint8_t>* vidx, std::vector<int4>* tiles_out) {
     const auto& opt = pamg::options();
     int tnnz = opt.tile_nnz, trows = opt.tile_rows;
     // long_tiles: operators with long rows (coarse A_l, R_l: >= 48 nonzeros per row on
@@ -230,6 +230,78 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
         HIPC(hipMemcpy(ts->d_short, tiles.data(), sizeof(int4) * tiles.size(), hipMemcpyHostToDevice));
     if (ts->n_long)
         HIPC(hipMemcpy(ts->d_long, longr.data(), sizeof(int) * longr.size(), hipMemcpyHostToDevice));
+    tiles_out->swap(tiles);
+    return PAMG_OK;
+}
+
+// Column dictionaries (Options::col_dict). A tile set whose short-tile nonzeros have at most
+// 256 distinct row-relative offsets col - row (the fine-grid stencils: 7 for the 7-point
+// Poisson, 5 in 2D, 99 for elastic3d) stores each column as an index into the set's offset
+// table: 4 bits where every such set of the matrix has <= 16 offsets, else 8 bits (one width
+// per matrix, so the interior and boundary sets share d_cidx). The kernel rebuilds the
+// column as row + table[index] (exact); its rows come from the 8-bit row lengths, so a
+// dictionary set also turns rl8 on. Against the 24-bit stream this saves 2.5 B/nonzero
+// (4-bit) or 2 B/nonzero (8-bit) of the 11-12 B a nonzero streams.
+int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci,
+                    const std::vector<int4>& t_in, const std::vector<int4>& t_bd) {
+    const auto& opt = pamg::options();
+    pamg::TileSet* sets[2] = {&A->interior, &A->boundary};
+    const std::vector<int4>* tl[2] = {&t_in, &t_bd};
+    std::vector<uint8_t> idx;  // 8-bit index per nonzero (packed to 4 bits below if they fit)
+    std::vector<int> tab[2];
+    for (int q = 0; q < 2; ++q) {
+        pamg::TileSet* ts = sets[q];
+        if (!opt.col_dict || opt.rows_kernel != 1 || opt.xcd_remap || opt.stream_nt || ts->vd ||
+            ts->n_short == 0 || ts->tile_rows > pamg::kBlock || ts->max_short_len > 255)
+            continue;
+        if (idx.empty()) idx.assign((size_t)A->nnz + kVecPad, 0);
+        // open-addressing map offset -> table slot (1024 cells for <= 256 keys)
+        constexpr int kCells = 1024;
+        int key[kCells], slot[kCells];
+        std::fill(slot, slot + kCells, -1);
+        bool ok = true;
+        for (const int4& t : *tl[q]) {
+            for (int r = t.x; r < t.y && ok; ++r) {
+                for (int64_t k = rp[r]; k < rp[r + 1]; ++k) {
+                    const int o = ci[k] - r;
+                    uint32_t h = ((uint32_t)o * 0x9E3779B1u) >> 22;
+                    while (slot[h] >= 0 && key[h] != o) h = (h + 1) & (kCells - 1);
+                    if (slot[h] < 0) {
+                        if (tab[q].size() == 256) {
+                            ok = false;
+                            break;
+                        }
+                        key[h] = o;
+                        slot[h] = (int)tab[q].size();
+                        tab[q].push_back(o);
+                    }
+                    idx[k] = (uint8_t)slot[h];
+                }
+            }
+            if (!ok) break;
+        }
+        if (!ok) tab[q].clear();
+    }
+    int width = 0;
+    for (int q = 0; q < 2; ++q)
+        if (!tab[q].empty()) width = std::max(width, tab[q].size() <= 16 ? 4 : 8);
+    if (width == 0) return PAMG_OK;
+    for (int q = 0; q < 2; ++q) {
+        if (tab[q].empty()) continue;
+        pamg::TileSet* ts = sets[q];
+        CHECK(dalloc(&ts->d_ctab, (int64_t)tab[q].size()));
+        HIPC(hipMemcpy(ts->d_ctab, tab[q].data(), sizeof(int) * tab[q].size(), hipMemcpyHostToDevice));
+        ts->ctab_n = (int)tab[q].size();
+        ts->cd = width;
+        ts->rl8 = true;
+    }
+    if (width == 4) {
+        std::vector<uint8_t> nib(((size_t)A->nnz + 1) / 2 + kVecPad, 0);
+        for (int64_t k = 0; k < A->nnz; ++k) nib[k >> 1] |= (uint8_t)((idx[k] & 15) << (4 * (k & 1)));
+        idx.swap(nib);
+    }
+    CHECK(dalloc(&A->d_cidx, (int64_t)idx.size()));
+    HIPC(hipMemcpy(A->d_cidx, idx.data(), idx.size(), hipMemcpyHostToDevice));
     return PAMG_OK;
 }
 
@@ -238,6 +310,8 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_long);
     dfree(ts.d_base);
     dfree(ts.d_vtab);
+    dfree(ts.d_ctab);
+    ts.cd = ts.ctab_n = 0;
     ts.c24 = ts.vd = ts.rl8 = false;
     ts.max_short_len = 0;
     ts.rows_short = 0;
@@ -570,6 +644,12 @@ int pamg_ctx_sync(pamg_ctx* ctx) {
     return PAMG_OK;
 }
 
+int pamg_device_sync(int device) {
+    HIPC(hipSetDevice(device));
+    HIPC(hipDeviceSynchronize());
+    return PAMG_OK;
+}
+
 int pamg_comm_unique_id(unsigned char id[128]) {
     static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
     ncclUniqueId u;
@@ -861,8 +941,12 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     }
     std::vector<uint16_t> lo;
     std::vector<uint8_t> hi, vidx;
-    CHECK(build_tiles(rp, inner, &A->interior, band, ci, &lo, &hi, val, &vidx));
-    CHECK(build_tiles(rp, bnd, &A->boundary, band, ci, &lo, &hi, val, &vidx));
+    {
+        std::vector<int4> t_in, t_bd;
+        CHECK(build_tiles(rp, inner, &A->interior, band, ci, &lo, &hi, val, &vidx, &t_in));
+        CHECK(build_tiles(rp, bnd, &A->boundary, band, ci, &lo, &hi, val, &vidx, &t_bd));
+        CHECK(build_col_dicts(A.get(), rp, ci, t_in, t_bd));
+    }
     if (A->interior.rl8 || A->boundary.rl8) {
         std::vector<uint8_t> rl(nrows + kVecPad, 0);
         for (int64_t i = 0; i < nrows; ++i) rl[i] = (uint8_t)std::min<int64_t>(255, rp[i + 1] - rp[i]);
@@ -880,6 +964,10 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     A->stream_bytes = 4;
     for (const pamg::TileSet* t : {&A->interior, &A->boundary})
         A->stream_bytes += (t->rl8 ? 1 : 4) * t->rows_short + 4 * (int64_t)t->n_long;
+    // columns: cd/8 B per nonzero of a dictionary set (+ its 4-B offsets, once)
+    for (const pamg::TileSet* t : {&A->interior, &A->boundary})
+        A->stream_bytes += (t->cd ? (t->cd * t->nnz_short + 7) / 8 + 4 * t->ctab_n - (t->c24 ? 3 : 4) * t->nnz_short : 0) -
+                           (t->cd && t->c24 ? 4 * (int64_t)t->n_short : 0);
     for (const pamg::TileSet* t : {&A->interior, &A->boundary})
         A->stream_bytes += (t->c24 ? 3 : 4) * t->nnz_short + 12 * t->nnz_long +
                            (t->vd ? t->nnz_short / 2 + 128 * (int64_t)t->n_short : 8 * t->nnz_short) +
@@ -906,6 +994,7 @@ int pamg_mat_destroy(pamg_mat* A) {
     dfree(A->d_rlen);
     dfree(A->d_chi);
     dfree(A->d_vidx);
+    dfree(A->d_cidx);
     dfree(A->d_val);
     dfree(A->d_diag);
     free_tiles(A->interior);
@@ -925,6 +1014,17 @@ int pamg_mat_info(const pamg_mat* A, int64_t* nrows, int64_t* ncols, int64_t* nn
 int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes) {
     if (!A || !bytes) return fail(PAMG_E_ARG, "mat_stream_bytes: bad args");
     *bytes = A->stream_bytes;
+    return PAMG_OK;
+}
+
+int pamg_mat_layout(const pamg_mat* A, int set, int out[5]) {
+    if (!A || !out || set < 0 || set > 1) return fail(PAMG_E_ARG, "mat_layout: bad args");
+    const pamg::TileSet& t = set == 0 ? A->interior : A->boundary;
+    out[0] = t.c24;
+    out[1] = t.vd;
+    out[2] = t.rl8;
+    out[3] = t.cd;
+    out[4] = t.ctab_n;
     return PAMG_OK;
 }
 
@@ -1340,6 +1440,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "long_tiles" && (value == 0 || value == 1)) o.long_tiles = (int)value;
     else if (k == "row_len8" && (value == 0 || value == 1)) o.row_len8 = (int)value;
     else if (k == "value_dict" && (value == 0 || value == 1)) o.value_dict = (int)value;
+    else if (k == "col_dict" && (value == 0 || value == 1)) o.col_dict = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -1376,6 +1477,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "poison_ghosts") *value = o.poison_ghosts;
     else if (k == "col24") *value = o.col24;
     else if (k == "value_dict") *value = o.value_dict;
+    else if (k == "col_dict") *value = o.col_dict;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

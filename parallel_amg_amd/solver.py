@@ -108,8 +108,20 @@ class AMGSolver:
         x entry read once + 8 B per output row + 8 B per extra own vector read or written."""
         return M.stream_bytes + 8 * (M.n_own_cols + M.n_ghost) + 8 * M.nrows + 8 * M.nrows * extra_vec_rw
 
-    def op_bytes(self) -> np.ndarray:
-        """Algorithmic bytes per (level, op) of one V-cycle on this part (L x 6)."""
+    @staticmethod
+    def csr_bytes(M, extra_vec_rw: int) -> int:
+        """SURVEY §8(d)'s algorithmic bytes of one row operation, independent of the device
+        layout: plain CSR with 32-bit indices (12 B per nonzero + 4 B per row pointer) + 8 B
+        per x entry read once + 8 B per output row + 8 B per extra own vector read or written
+        (b; the diagonal is read inline). The layouts libpamg uploads (24-bit columns, 8-bit
+        row lengths, column dictionaries) stream fewer bytes than this (rowsum_bytes)."""
+        return (12 * M.nnz + 4 * (M.nrows + 1) + 8 * (M.n_own_cols + M.n_ghost) + 8 * M.nrows
+                + 8 * M.nrows * extra_vec_rw)
+
+    def op_bytes(self, model: str = "format") -> np.ndarray:
+        """Bytes per (level, op) of one V-cycle on this part (L x 6): model "format" = what
+        the uploaded layout streams (rowsum_bytes), "csr" = SURVEY §8(d)'s CSR model."""
+        rb = self.rowsum_bytes if model == "format" else self.csr_bytes
         out = np.zeros((self.L, 6))
         for l in range(self.L):
             n = self.level_rows[l]
@@ -119,11 +131,11 @@ class AMGSolver:
                 continue
             A, P, R = self.A[l], self.P[l], self.R[l]
             # jacobi: x (read once), b, x' ; zero-guess form on l >= 1 reads b, diag, writes x'
-            out[l, 0] = self.rowsum_bytes(A, 1) if l == 0 else 24 * n
-            out[l, 1] = self.rowsum_bytes(A, 1)
-            out[l, 2] = self.rowsum_bytes(R, 0)
-            out[l, 3] = self.rowsum_bytes(P, 1)
-            out[l, 4] = self.rowsum_bytes(A, 1)
+            out[l, 0] = rb(A, 1) if l == 0 else 24 * n
+            out[l, 1] = rb(A, 1)
+            out[l, 2] = rb(R, 0)
+            out[l, 3] = rb(P, 1)
+            out[l, 4] = rb(A, 1)
         return out
 
     def __del__(self):

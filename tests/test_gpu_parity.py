@@ -68,11 +68,16 @@ TILE_CONFIGS = [(0, 2048, 256, 0, 0, 0, 0, 1, 0, 1, 1), (1, 2048, 256, 0, 0, 0, 
                 (1, 1024, 256, 0, 1, 0, 1, 1, 1, 1, 1), (1, 2048, 256, 0, 0, 0, 1, 1, 1, 1, 1),
                 (1, 1024, 256, 0, 0, 0, 1, 1, 0, 0, 1), (1, 1024, 256, 0, 0, 0, 4, 1, 0, 1, 1),
                 (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 0), (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1)]
+# + col_dict (last column): on for every configuration above (it engages only where its
+# conditions hold), plus the default layout and the stored-diagonal Jacobi without it
+TILE_CONFIGS = [c + (1,) for c in TILE_CONFIGS] + [(1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 0),
+                                                   (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1, 0)]
 OPT_KEYS = ("rows_kernel", "tile_nnz", "tile_rows", "xcd_remap", "jacobi_diag", "stream_nt", "tile_order",
-            "col24", "value_dict", "long_tiles", "row_len8")
+            "col24", "value_dict", "long_tiles", "row_len8", "col_dict")
 
 
-@pytest.fixture(params=TILE_CONFIGS, ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}_lt{}_rl{}".format(*c))
+@pytest.fixture(params=TILE_CONFIGS,
+                ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}_lt{}_rl{}_cd{}".format(*c))
 def tile_cfg(request, built):
     import ctypes
     from parallel_amg_amd._lib import call
@@ -139,6 +144,91 @@ def test_jacobi_bit_exact(ctx, case, palette, tile_cfg):
     for _ in range(3):
         ref = O.jacobi(M, ref, bh, 0.7)
     assert np.array_equal(bits(x.own_values()), bits(ref))
+
+
+def offset_csr(rng, n, offsets, lengths, palette=None):
+    """Square matrix whose row i holds the diagonal plus columns i + o for o drawn from
+    `offsets` (those inside [0, n)): at most len(offsets) + 1 distinct row-relative offsets,
+    the layout the column dictionaries (col_dict) compress."""
+    offsets = np.asarray(offsets, np.int64)
+    rows, cols, vals = [0], [], []
+    for i in range(n):
+        m = lengths[i % len(lengths)]
+        cand = i + offsets
+        cand = cand[(cand >= 0) & (cand < n) & (cand != i)]
+        c = np.sort(np.concatenate([[i], rng.choice(cand, size=min(max(m - 1, 0), len(cand)), replace=False)]))
+        v = rng.standard_normal(len(c)) if palette is None else rng.choice(palette, len(c))
+        v[c == i] = 4.0 + len(c) + abs(v[c == i])
+        cols.append(c)
+        vals.append(v)
+        rows.append(rows[-1] + len(c))
+    return O.CSR(np.asarray(rows, np.int64), np.concatenate(cols).astype(np.int64), np.concatenate(vals), n)
+
+
+# (name, number of distinct off-diagonal offsets, row lengths): 4-bit tables (<= 16 offsets
+# with the diagonal), 8-bit (17..256), no dictionary (> 256); ragged rows up to the 255 limit
+COLDICT_CASES = [("stencil7", None, [7]), ("d15", 15, [1, 16, 5, 9]), ("d16", 16, [17, 2]),
+                 ("d200", 200, [30, 1, 7, 255, 3]), ("d255", 255, [64, 9]), ("d256", 256, [40, 2]),
+                 ("ragged4", 12, [1, 2, 13, 1, 1, 9, 4])]
+
+
+@pytest.mark.parametrize("name,ndist,lengths", COLDICT_CASES, ids=[c[0] for c in COLDICT_CASES])
+@pytest.mark.parametrize("tnnz", [1024, 4096])
+def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
+    """col_dict: columns rebuilt as row + table[index] give the very bits of the oracle for
+    SpMV, residual, prolongate-add and Jacobi (in-tile diagonal and stored diagonal), and the
+    layout engages exactly when the matrix has <= 256 distinct row-relative offsets."""
+    import ctypes
+    from parallel_amg_amd._lib import call, layout_of
+    rng = np.random.default_rng(len(name) * 7 + tnnz)
+    n = 4000
+    if ndist is None:
+        offs = [-289, -17, -1, 1, 17, 289]
+    else:
+        offs = rng.choice(np.arange(-n // 2, n // 2), size=ndist + 1, replace=False)
+        offs = offs[offs != 0][:ndist]
+    M = offset_csr(rng, n, offs, lengths)
+    distinct = len(np.unique(M.col - np.repeat(np.arange(n), np.diff(M.rowptr))))
+    keys = ("col_dict", "tile_nnz", "jacobi_diag")
+    old = []
+    for k in keys:
+        v = ctypes.c_int64()
+        call("pamg_get_option", k.encode(), ctypes.byref(v))
+        old.append(v.value)
+    try:
+        call("pamg_set_option", b"tile_nnz", tnnz)
+        call("pamg_set_option", b"col_dict", 0)
+        plain = upload(ctx, M)[0].stream_bytes
+        for dg in (0, 1):
+            call("pamg_set_option", b"col_dict", 1)
+            call("pamg_set_option", b"jacobi_diag", dg)
+            A, _h = upload(ctx, M)
+            assert (A.stream_bytes < plain) == (distinct <= 256), (A.stream_bytes, plain, distinct)
+            lay = layout_of(A)
+            assert lay["cd"] == (4 if distinct <= 16 else 8 if distinct <= 256 else 0), (lay, distinct)
+            assert lay["cd_offsets"] == (distinct if distinct <= 256 else 0)
+            xh, bh = rng.standard_normal(n), rng.standard_normal(n)
+            x, b = PVector(ctx, n, 0, xh), PVector(ctx, n, 0, bh)
+            y = PVector(ctx, n)
+            mul(y, A, x)
+            ref = O.spmv(M, xh)
+            assert np.array_equal(bits(y.own_values()), bits(ref))
+            r = PVector(ctx, n)
+            residual(r, A, x, b)
+            assert np.array_equal(bits(r.own_values()), bits(O.residual(M, xh, bh)))
+            ms = ctypes.c_double()
+            yy = PVector(ctx, n, 0, bh)
+            call("pamg_bench_rowop", ctx.handle, A.handle, 3, x.handle, None, yy.handle, 0.0, 1, ctypes.byref(ms))
+            assert np.array_equal(bits(yy.own_values()), bits((bh + ref) + ref))
+            t = PVector(ctx, n)
+            jacobi(x, A, b, t, 0.7, 3)
+            rj = xh
+            for _ in range(3):
+                rj = O.jacobi(M, rj, bh, 0.7)
+            assert np.array_equal(bits(x.own_values()), bits(rj))
+    finally:
+        for k, v in zip(keys, old):
+            call("pamg_set_option", k.encode(), v)
 
 
 def test_blas1(ctx):
@@ -275,13 +365,16 @@ def test_stream_bytes_layout(ctx):
             for k in opts:
                 call("pamg_set_option", k.encode(), 0 if k == "value_dict" else 1)
 
-    got0 = stream_bytes(col24=0, row_len8=0)
+    got0 = stream_bytes(col24=0, row_len8=0, col_dict=0)
     nt, rem = divmod(got0 - 12 * nnz - 4 * (n + 1), 16)
     assert rem == 0 and nt > 0
-    assert stream_bytes(col24=1, row_len8=0) == 11 * nnz + 4 * (n + 1) + 20 * nt
-    assert stream_bytes(col24=1, row_len8=1) == 11 * nnz + n + 4 + 20 * nt
+    assert stream_bytes(col24=1, row_len8=0, col_dict=0) == 11 * nnz + 4 * (n + 1) + 20 * nt
+    assert stream_bytes(col24=1, row_len8=1, col_dict=0) == 11 * nnz + n + 4 + 20 * nt
     # 2 distinct values: every tile takes a value dictionary (which keeps the row pointers)
     assert stream_bytes(value_dict=1) == 3 * nnz + nnz // 2 + 4 * (n + 1) + (20 + 128) * nt
+    # column dictionary (default): 7 offsets -> 4-bit indices + the 28-B table, 8-bit row
+    # lengths, no per-tile base
+    assert stream_bytes() == 8 * nnz + (nnz + 1) // 2 + 4 * 7 + n + 4 + 16 * nt
 
 
 @pytest.mark.parametrize("seed,n,density,weak,iso", [(1, 3000, 0.003, 0.3, 0.02), (2, 5000, 0.001, 0.0, 0.0),

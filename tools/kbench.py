@@ -3,7 +3,8 @@
 
 For each tuning configuration (pamg_set_option) the level operators are re-uploaded and every
 row op is timed with HIP events (pamg_bench_rowop); prints one JSON line per measurement with
-the algorithmic bytes and the achieved GB/s. Dev tool, not part of the ABI.
+the algorithmic bytes (SURVEY.md §8d CSR model) and the achieved GB/s, plus the rate on the
+bytes the uploaded layout actually streams (format_GBps). Dev tool, not part of the ABI.
 
     python tools/kbench.py --n 512 --levels 1      # fine matrix only (no setup)
     python tools/kbench.py --n 256 --levels 3      # hierarchy levels 0..2 (A, R, P)
@@ -44,8 +45,7 @@ def bench(ctx, M, op, reps):
     call("pamg_bench_rowop", ctx.handle, M.handle, op, x.handle, b.handle, y.handle, 0.6, reps,
          C.byref(ms))
     extra = {0: 0, 1: 1, 2: 1, 3: 1}[op]
-    byt = AMGSolver.rowsum_bytes(M, extra)
-    return ms.value, byt
+    return ms.value, AMGSolver.csr_bytes(M, extra), AMGSolver.rowsum_bytes(M, extra)
 
 
 def main():
@@ -54,7 +54,7 @@ def main():
     ap.add_argument("--levels", type=int, default=1)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--configs", default="1:1024:256:0:0:0:1:1,1:1024:256:0:0:0:1:0",
-                    help="kern:tile_nnz:tile_rows:xcd:jacobi_diag:stream_nt:tile_order:col24:value_dict:long_tiles:row_len8,...")
+                    help="kern:tile_nnz:tile_rows:xcd:jacobi_diag:stream_nt:tile_order:col24:value_dict:long_tiles:row_len8:col_dict,...")
     ap.add_argument("--ops", default="0,2")
     args = ap.parse_args()
     ctx = Context(0)
@@ -73,10 +73,11 @@ def main():
     ops = [int(o) for o in args.ops.split(",")]
     for cfg in args.configs.split(","):
         given = [int(v) for v in cfg.split(":")]
-        vals = given + [1, 1024, 256, 0, 0, 0, 0, 1, 0, 1, 1][len(given):]  # defaults for missing fields
-        kern, tnnz, trows, xcd, jd, nt, order, c24, vd, lt, rl8 = vals[:11]
+        vals = given + [1, 1024, 256, 0, 0, 0, 0, 1, 0, 1, 1, 1][len(given):]  # defaults for missing fields
+        kern, tnnz, trows, xcd, jd, nt, order, c24, vd, lt, rl8, cd = vals[:12]
         set_opts(rows_kernel=kern, tile_nnz=tnnz, tile_rows=trows, xcd_remap=xcd, jacobi_diag=jd,
-                 stream_nt=nt, tile_order=order, col24=c24, value_dict=vd, long_tiles=lt, row_len8=rl8)
+                 stream_nt=nt, tile_order=order, col24=c24, value_dict=vd, long_tiles=lt, row_len8=rl8,
+                 col_dict=cd)
         for name, (M, plan) in mats.items():
             D = PSparseMatrix(ctx, M, plan)
             for op in ops:
@@ -84,9 +85,11 @@ def main():
                     continue
                 if op == 3 and not name.startswith("P"):
                     continue
-                ms, byt = bench(ctx, D, op, args.reps)
+                ms, byt, fbyt = bench(ctx, D, op, args.reps)
+                # GBps: SURVEY §8(d) CSR bytes; format_GBps: the bytes the uploaded layout streams
                 print(json.dumps({"cfg": cfg, "mat": name, "op": OPNAME[op], "rows": D.nrows, "nnz": D.nnz,
-                                  "ms": round(ms, 4), "GBps": round(byt / ms / 1e6, 1)}), flush=True)
+                                  "ms": round(ms, 4), "GBps": round(byt / ms / 1e6, 1),
+                                  "format_GBps": round(fbyt / ms / 1e6, 1)}), flush=True)
             del D
 
 

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Profiles of a round, run on the MI355X box (gpurun): the default bench line (with the CPU
+# baseline), a rocprofv3 kernel trace + stats of bench.py, and the two PMC passes
+# (FETCH_SIZE, WRITE_SIZE; separate runs, MI355X_MICROARCH.md §HBM) of the level-0 SpMV and
+# Jacobi kernels through tools/kbench.py. Every GPU step has its own time limit; the first
+# failure ends the script (set -e).
+#
+#   gpurun -- 'bash tools/profile_round.sh r01_v9'
+set -euo pipefail
+export TMPDIR=/tmp
+TAG=${1:-r01}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+timeout -k 10 300 python3 -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log"
+echo "bench done"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv \
+    -- python3 -u bench.py --steps 5 --cpu-baseline off > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.log"
+echo "kernel trace done"
+KB="tools/kbench.py --n 512 --levels 1 --ops 0,2 --reps 3 --configs 1:1024:256:0:0:0:1:1:0:1:1:1"
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o fetch --output-format csv \
+    -- python3 -u $KB > "$OUT/pmc_fetch.jsonl" 2> "$OUT/pmc_fetch.err"
+echo "fetch pass done"
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o write --output-format csv \
+    -- python3 -u $KB > "$OUT/pmc_write.jsonl" 2> "$OUT/pmc_write.err"
+echo "write pass done"
