@@ -197,8 +197,9 @@ def main():
     # workload (tools/pmc_traffic.py; counters cannot be read from inside the process)
     # (only when the record was measured on the same column layout as this run)
     lay = _lib.layout_of(A0)
-    c24, vd, rl8, cd = lay["c24"], lay["vd"], lay["rl8"], lay["cd"]
-    kname = ("k_rows_tile2<2, 1024, 256, false, false, 256, false, false, true, %d>" % cd if cd
+    c24, vd, rl8, cd, tm = lay["c24"], lay["vd"], lay["rl8"], lay["cd"], lay["tm"]
+    kname = ("k_rows_tm<2, 1024, %d>" % cd if tm
+             else "k_rows_tile2<2, 1024, 256, false, false, 256, false, false, true, %d>" % cd if cd
              else "k_rows_tile2<2, 1024, 256, false, false, 256, true, true>" if vd
              else "k_rows_tile2<2, 1024, 256, false, false, 256, true, false, true>" if rl8
              else "k_rows_tile2<2, 1024, 256, false, false, 256, true>" if c24
@@ -247,6 +248,7 @@ def main():
             "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
             "roofline": {
                 "kernel": kname + " (level-0 post-smoothing Jacobi"
+                          + (", tile-major slots" if tm else "")
                           + (f", {cd}-bit column dictionary" if cd else "")
                           + (", value dictionaries" if vd else "")
                           + (", 24-bit column stream" if c24 and not cd else "")

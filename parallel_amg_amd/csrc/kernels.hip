@@ -388,6 +388,147 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
     }
 }
 
+// Variant 4, tile-major (TileSet::tm): tile t's values, column stream and row lengths live at
+// fixed slots of padded per-set arrays — values/columns at t*TNNZ, row lengths at t*rs — so
+// every load a block needs before its x gathers is addressed from blockIdx alone and issued
+// at entry beside the descriptor load. Variant 1 has to wait for the descriptor (its nonzero
+// range) before it can issue the stream, one dependent memory round trip more per tile.
+// Columns: CD = 4 / 8, row + table[index] (column dictionary); CD = 0, tile base + 24-bit
+// (16-bit low + 8-bit high) offset. Rows: one per lane, starts by a wave scan of the lengths;
+// positions are tile-relative (no alignment head: a tile's slot starts at its first nonzero).
+// Summation order, epilogues and Jacobi's in-tile diagonal are variant 1's (SPEC §S3).
+template <int OP, int TNNZ, int CD>
+__global__ __launch_bounds__(kBlock) void k_rows_tm(
+    const int4* __restrict__ tiles, const double* __restrict__ tval,
+    const uint8_t* __restrict__ tcidx, const uint16_t* __restrict__ tclo,
+    const uint8_t* __restrict__ tchi, const int* __restrict__ tbase,
+    const uint8_t* __restrict__ trlen, int rs, const int* __restrict__ ctab, int ctab_n,
+    const double* __restrict__ x, const double* __restrict__ b, double* __restrict__ y,
+    double omega, const double* __restrict__ diag) {
+    constexpr int BS = kBlock;
+    constexpr int G = TNNZ / (4 * BS);
+    static_assert(G >= 1 && TNNZ % (4 * BS) == 0, "tile budget must be a multiple of 4 x block");
+    __shared__ __attribute__((aligned(16))) double lprod[TNNZ + 8];
+    __shared__ double ldiag[OP == OP_JACOBI ? BS : 1];
+    __shared__ int lwt[BS / 64];
+    __shared__ int ltab[CD == 8 ? 256 : 16];
+    __shared__ __attribute__((aligned(4))) uint8_t lrow[TNNZ + 8];
+
+    const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int4 d = tiles[t];
+    const size_t sb = (size_t)t * TNNZ;
+    double2 va[G], vb[G];
+    uint32_t cn[G];
+    ushort4 clo4[G];
+    int cb = 0;
+    if constexpr (CD == 0) cb = tbase[t];
+    // the whole slot is loaded at entry (padding included: a load that waits for the
+    // descriptor's nonzero count brings its round trip back — measured 2-15 % slower)
+    auto load = [&](int j) {
+        const size_t q = sb + 4 * (tid + j * BS);
+        va[j] = *reinterpret_cast<const double2*>(tval + q);
+        vb[j] = *reinterpret_cast<const double2*>(tval + q + 2);
+        if constexpr (CD == 4) {
+            cn[j] = *reinterpret_cast<const uint16_t*>(tcidx + (q >> 1));
+        } else if constexpr (CD == 8) {
+            cn[j] = *reinterpret_cast<const uint32_t*>(tcidx + q);
+        } else {  // 24-bit: low 16 bits per nonzero + the four high bytes packed in cn
+            clo4[j] = *reinterpret_cast<const ushort4*>(tclo + q);
+            cn[j] = *reinterpret_cast<const uint32_t*>(tchi + q);
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < G; ++j) load(j);
+    int rl_len = tid < rs ? (int)trlen[(size_t)t * rs + tid] : 0;
+    if constexpr (CD != 0) {
+        if (tid < ctab_n) ltab[tid] = ctab[tid];
+    }
+    int rl_inc = rl_len;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(rl_inc, off, 64);
+        if (lane >= off) rl_inc += u;
+    }
+    if (lane == 63) lwt[tid >> 6] = rl_inc;
+    const int r0 = d.x, nr = d.y - d.x, cnt = d.w - d.z;
+    double pb = 0.0, px = 0.0, py = 0.0, pd = 0.0;
+    if (tid < nr) {
+        const int r = r0 + tid;
+        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[r];
+        if constexpr (OP == OP_JACOBI) {
+            px = x[r];
+            if (diag) pd = diag[r];
+        }
+        if constexpr (OP == OP_PROLONG) py = y[r];
+    }
+    __syncthreads();  // lwt, ltab
+    int pre = 0;
+#pragma unroll
+    for (int q = 0; q < BS / 64; ++q) pre += q < (tid >> 6) ? lwt[q] : 0;
+    const int re = pre + rl_inc;  // end of this lane's row (tile-relative)
+    if (tid < nr)
+        for (int p = re - rl_len; p < re; ++p) lrow[p] = (uint8_t)tid;
+    __syncthreads();  // lrow
+
+    double xv[G][4];
+    int cc[G][4];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const int q = 4 * (tid + j * BS);
+        const uint32_t rw = q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
+        if constexpr (CD == 0) {
+            const uint16_t l4[4] = {clo4[j].x, clo4[j].y, clo4[j].z, clo4[j].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                cc[j][e] = cb + (int)((uint32_t)l4[e] | (((cn[j] >> (8 * e)) & 255u) << 16));
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int ix = CD == 4 ? (int)((cn[j] >> (4 * e)) & 15u) : (int)((cn[j] >> (8 * e)) & 255u);
+                cc[j][e] = r0 + (int)((rw >> (8 * e)) & 255u) + ltab[ix];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[j][e] = x[q + e < cnt ? cc[j][e] : 0];
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const int q = 4 * (tid + j * BS);
+        const uint32_t rw = q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
+        const double vv[4] = {va[j].x, va[j].y, vb[j].x, vb[j].y};
+        double p[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool ok = q + e < cnt;
+            p[e] = ok ? vv[e] * xv[j][e] : 0.0;
+            if constexpr (OP == OP_JACOBI) {
+                const int rl = (int)((rw >> (8 * e)) & 255u);
+                if (!diag && ok && cc[j][e] - r0 == rl) ldiag[rl] = vv[e];
+            }
+        }
+        *reinterpret_cast<double2*>(&lprod[q]) = make_double2(p[0], p[1]);
+        *reinterpret_cast<double2*>(&lprod[q + 2]) = make_double2(p[2], p[3]);
+    }
+    __syncthreads();
+    if (tid < nr) {
+        const double s = row_sum_lds(lprod, re - rl_len, re);
+        const int r = r0 + tid;
+        if constexpr (OP == OP_SPMV) {
+            y[r] = s;
+        } else if constexpr (OP == OP_RESID) {
+            y[r] = pb - s;
+        } else if constexpr (OP == OP_JACOBI) {
+            const double dd = diag ? pd : ldiag[tid];
+            const double u = pb - s;
+            const double v = omega * u;
+            const double w = v / dd;
+            y[r] = px + w;
+        } else {
+            y[r] = py + s;
+        }
+    }
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops (lgkmcnt), NOT for
 // its outstanding global loads (no vmcnt), so a prefetch issued before it stays in flight.
 __device__ __forceinline__ void lds_barrier() {
@@ -776,7 +917,22 @@ template <int OP, int TNNZ, int TROWS>
 void launch_tile2(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
                   double* y, double omega, hipStream_t s) {
     const double* dg = (OP == OP_JACOBI && A.jacobi_diag) ? A.d_diag : nullptr;
-    if (A.xcd_remap) {
+    if (ts.tm) {
+        if constexpr (TROWS <= kBlock) {
+            if (ts.cd == 4)
+                k_rows_tm<OP, TNNZ, 4><<<ts.n_short, kBlock, 0, s>>>(
+                    ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr, nullptr, ts.d_tm_rlen,
+                    ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y, omega, dg);
+            else if (ts.cd == 8)
+                k_rows_tm<OP, TNNZ, 8><<<ts.n_short, kBlock, 0, s>>>(
+                    ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr, nullptr, ts.d_tm_rlen,
+                    ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y, omega, dg);
+            else
+                k_rows_tm<OP, TNNZ, 0><<<ts.n_short, kBlock, 0, s>>>(
+                    ts.d_short, ts.d_tm_val, nullptr, ts.d_tm_clo, ts.d_tm_chi, ts.d_base, ts.d_tm_rlen,
+                    ts.tm_rs, nullptr, 0, x, b, y, omega, dg);
+        }
+    } else if (A.xcd_remap) {
         const int grid = ((ts.n_short + 7) / 8) * 8;
         k_rows_tile2<OP, TNNZ, TROWS, true><<<grid, kBlock, 0, s>>>(
             ts.d_short, ts.n_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, dg);

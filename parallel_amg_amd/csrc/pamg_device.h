@@ -49,6 +49,15 @@ struct TileSet {
     int cd = 0;
     int* d_ctab = nullptr;
     int ctab_n = 0;
+    // tile-major copies (Options::tile_major; kernels.hip k_rows_tm): tile t's values and
+    // column stream at t * tile_nnz, its row lengths at t * tm_rs, zero-padded
+    bool tm = false;
+    int tm_rs = 0;                 // row-length slot per tile (>= its rows, multiple of 4)
+    double* d_tm_val = nullptr;
+    uint8_t* d_tm_cidx = nullptr;  // column dictionary indices (cd bits each)
+    uint16_t* d_tm_clo = nullptr;  // or 24-bit columns: low 16 bits
+    uint8_t* d_tm_chi = nullptr;   //   high 8 bits
+    uint8_t* d_tm_rlen = nullptr;
     int max_short_len = 0;    // longest row in a short tile
     int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
@@ -70,6 +79,7 @@ struct Options {
     int row_len8 = 1;          // 1: 8-bit row lengths instead of 32-bit row pointers where they fit
     int value_dict = 0;        // 1 (opt-in): 4-bit per-tile value dictionaries where they fit
     int col_dict = 1;          // 1: row-relative column dictionaries (4/8-bit) where they fit
+    int tile_major = 1;        // tile-major padded copies (variant 4): 1 where measured faster, 2 all eligible
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };
 Options& options();

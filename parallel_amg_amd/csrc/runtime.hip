@@ -243,7 +243,8 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
 // dictionary set also turns rl8 on. Against the 24-bit stream this saves 2.5 B/nonzero
 // (4-bit) or 2 B/nonzero (8-bit) of the 11-12 B a nonzero streams.
 int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci,
-                    const std::vector<int4>& t_in, const std::vector<int4>& t_bd) {
+                    const std::vector<int4>& t_in, const std::vector<int4>& t_bd,
+                    std::vector<uint8_t>* idx8) {
     const auto& opt = pamg::options();
     pamg::TileSet* sets[2] = {&A->interior, &A->boundary};
     const std::vector<int4>* tl[2] = {&t_in, &t_bd};
@@ -298,10 +299,86 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
     if (width == 4) {
         std::vector<uint8_t> nib(((size_t)A->nnz + 1) / 2 + kVecPad, 0);
         for (int64_t k = 0; k < A->nnz; ++k) nib[k >> 1] |= (uint8_t)((idx[k] & 15) << (4 * (k & 1)));
-        idx.swap(nib);
+        CHECK(dalloc(&A->d_cidx, (int64_t)nib.size()));
+        HIPC(hipMemcpy(A->d_cidx, nib.data(), nib.size(), hipMemcpyHostToDevice));
+    } else {
+        CHECK(dalloc(&A->d_cidx, (int64_t)idx.size()));
+        HIPC(hipMemcpy(A->d_cidx, idx.data(), idx.size(), hipMemcpyHostToDevice));
     }
-    CHECK(dalloc(&A->d_cidx, (int64_t)idx.size()));
-    HIPC(hipMemcpy(A->d_cidx, idx.data(), idx.size(), hipMemcpyHostToDevice));
+    idx8->swap(idx);
+    return PAMG_OK;
+}
+
+// Tile-major copies (Options::tile_major, kernel variant 4 k_rows_tm): for a tile set with
+// one row per lane (<= 256 rows per tile, rows <= 255 nonzeros) and 24-bit or dictionary
+// columns, tile t's values, column stream and row lengths are copied to fixed, zero-padded
+// slots (t * tile_nnz, t * tm_rs), so the kernel addresses every pre-gather load from its
+// block index. The CSR arrays stay resident for the other variants and the long rows.
+int build_tile_major(pamg_mat* A, const std::vector<int64_t>& rp, const double* val,
+                     const std::vector<int4>& t_in, const std::vector<int4>& t_bd,
+                     const std::vector<uint16_t>& lo, const std::vector<uint8_t>& hi,
+                     const std::vector<uint8_t>& idx8) {
+    const auto& opt = pamg::options();
+    pamg::TileSet* sets[2] = {&A->interior, &A->boundary};
+    const std::vector<int4>* tl[2] = {&t_in, &t_bd};
+    for (int q = 0; q < 2; ++q) {
+        pamg::TileSet* ts = sets[q];
+        ts->tm = false;
+        if (!opt.tile_major || opt.rows_kernel != 1 || opt.xcd_remap || opt.stream_nt || ts->vd ||
+            ts->n_short == 0 || ts->tile_rows > pamg::kBlock || ts->max_short_len > 255 ||
+            !(ts->cd || (ts->c24 && !lo.empty())) || (ts->cd && idx8.empty()) || !val)
+            continue;
+        // tile_major 1 (default): the sets where it measured faster at 512^3 — column
+        // dictionary sets (A0: Jacobi -6.5 %, residual -4.6 %, SpMV -3.1 %) and wide operators
+        // (restrictions, ncols >= 2 nrows: R0 -4..-6 %); prolongations (P0 +3..8 %: row-limited
+        // tiles leave ~8 % of each slot as padding) and the coarse A1 (+1..2 %) keep variant 1.
+        // tile_major 2: every eligible set (A/B, tests).
+        if (opt.tile_major == 1 && !ts->cd && A->ncols < 2 * A->nrows) continue;
+        const std::vector<int4>& tiles = *tl[q];
+        const int64_t nt = (int64_t)tiles.size(), tn = ts->tile_nnz;
+        int rs = 0;
+        for (const int4& t : tiles) rs = std::max(rs, t.y - t.x);
+        rs = (rs + 3) & ~3;
+        std::vector<double> tv((size_t)(nt * tn + kVecPad), 0.0);
+        std::vector<uint8_t> trl((size_t)(nt * rs + kVecPad), 0);
+        std::vector<uint8_t> tci, tch;
+        std::vector<uint16_t> tcl;
+        if (ts->cd == 4) tci.assign((size_t)(nt * tn / 2 + kVecPad), 0);
+        else if (ts->cd == 8) tci.assign((size_t)(nt * tn + kVecPad), 0);
+        else {
+            tcl.assign((size_t)(nt * tn + kVecPad), 0);
+            tch.assign((size_t)(nt * tn + kVecPad), 0);
+        }
+        for (int64_t i = 0; i < nt; ++i) {
+            const int4 t = tiles[i];
+            for (int r = t.x; r < t.y; ++r) trl[i * rs + (r - t.x)] = (uint8_t)(rp[r + 1] - rp[r]);
+            for (int k = t.z; k < t.w; ++k) {
+                const int64_t p = i * tn + (k - t.z);
+                tv[p] = val[k];
+                if (ts->cd == 4) tci[p >> 1] |= (uint8_t)((idx8[k] & 15) << (4 * (p & 1)));
+                else if (ts->cd == 8) tci[p] = idx8[k];
+                else {
+                    tcl[p] = lo[k];
+                    tch[p] = hi[k];
+                }
+            }
+        }
+        CHECK(dalloc(&ts->d_tm_val, (int64_t)tv.size()));
+        HIPC(hipMemcpy(ts->d_tm_val, tv.data(), sizeof(double) * tv.size(), hipMemcpyHostToDevice));
+        CHECK(dalloc(&ts->d_tm_rlen, (int64_t)trl.size()));
+        HIPC(hipMemcpy(ts->d_tm_rlen, trl.data(), trl.size(), hipMemcpyHostToDevice));
+        if (!tci.empty()) {
+            CHECK(dalloc(&ts->d_tm_cidx, (int64_t)tci.size()));
+            HIPC(hipMemcpy(ts->d_tm_cidx, tci.data(), tci.size(), hipMemcpyHostToDevice));
+        } else {
+            CHECK(dalloc(&ts->d_tm_clo, (int64_t)tcl.size()));
+            CHECK(dalloc(&ts->d_tm_chi, (int64_t)tch.size()));
+            HIPC(hipMemcpy(ts->d_tm_clo, tcl.data(), sizeof(uint16_t) * tcl.size(), hipMemcpyHostToDevice));
+            HIPC(hipMemcpy(ts->d_tm_chi, tch.data(), tch.size(), hipMemcpyHostToDevice));
+        }
+        ts->tm_rs = rs;
+        ts->tm = true;
+    }
     return PAMG_OK;
 }
 
@@ -312,6 +389,13 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_vtab);
     dfree(ts.d_ctab);
     ts.cd = ts.ctab_n = 0;
+    dfree(ts.d_tm_val);
+    dfree(ts.d_tm_cidx);
+    dfree(ts.d_tm_clo);
+    dfree(ts.d_tm_chi);
+    dfree(ts.d_tm_rlen);
+    ts.tm = false;
+    ts.tm_rs = 0;
     ts.c24 = ts.vd = ts.rl8 = false;
     ts.max_short_len = 0;
     ts.rows_short = 0;
@@ -945,7 +1029,9 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         std::vector<int4> t_in, t_bd;
         CHECK(build_tiles(rp, inner, &A->interior, band, ci, &lo, &hi, val, &vidx, &t_in));
         CHECK(build_tiles(rp, bnd, &A->boundary, band, ci, &lo, &hi, val, &vidx, &t_bd));
-        CHECK(build_col_dicts(A.get(), rp, ci, t_in, t_bd));
+        std::vector<uint8_t> idx8;
+        CHECK(build_col_dicts(A.get(), rp, ci, t_in, t_bd, &idx8));
+        CHECK(build_tile_major(A.get(), rp, val, t_in, t_bd, lo, hi, idx8));
     }
     if (A->interior.rl8 || A->boundary.rl8) {
         std::vector<uint8_t> rl(nrows + kVecPad, 0);
@@ -957,21 +1043,29 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         CHECK(dalloc(&A->d_vidx, (int64_t)vidx.size()));
         HIPC(hipMemcpy(A->d_vidx, vidx.data(), vidx.size(), hipMemcpyHostToDevice));
     }
-    // the bytes one apply streams: values (8 B, or a 4-bit index + the tile's 128-B table),
-    // columns (3 B in 24-bit tile sets), row pointers, tile descriptors (+ bases)
-    // row bounds: 1 B per row of an rl8 tile set, else 4 B per row pointer (+ the one that
-    // closes the last row)
+    // the bytes one apply streams, per tile set: long rows (row pointer, 12 B/nonzero, list
+    // entry) + short tiles in their layout — row bounds (1 B/row with 8-bit lengths, else 4-B
+    // row pointers), columns (4 B; 3 B 24-bit; cd/8 B with a dictionary + its 4-B offsets),
+    // values (8 B; or a 4-bit index + the tile's 128-B table), 16-B descriptors (+ a 4-B
+    // column base with 24-bit columns); a tile-major set streams whole padded slots
+    // (tile_nnz values and column entries, tm_rs row lengths per tile). + the closing pointer.
     A->stream_bytes = 4;
-    for (const pamg::TileSet* t : {&A->interior, &A->boundary})
-        A->stream_bytes += (t->rl8 ? 1 : 4) * t->rows_short + 4 * (int64_t)t->n_long;
-    // columns: cd/8 B per nonzero of a dictionary set (+ its 4-B offsets, once)
-    for (const pamg::TileSet* t : {&A->interior, &A->boundary})
-        A->stream_bytes += (t->cd ? (t->cd * t->nnz_short + 7) / 8 + 4 * t->ctab_n - (t->c24 ? 3 : 4) * t->nnz_short : 0) -
-                           (t->cd && t->c24 ? 4 * (int64_t)t->n_short : 0);
-    for (const pamg::TileSet* t : {&A->interior, &A->boundary})
-        A->stream_bytes += (t->c24 ? 3 : 4) * t->nnz_short + 12 * t->nnz_long +
-                           (t->vd ? t->nnz_short / 2 + 128 * (int64_t)t->n_short : 8 * t->nnz_short) +
-                           (16 + (t->c24 ? 4 : 0)) * (int64_t)t->n_short + 4 * (int64_t)t->n_long;
+    for (const pamg::TileSet* t : {&A->interior, &A->boundary}) {
+        const int64_t ns = t->n_short, nz = t->nnz_short;
+        int64_t b = 8 * (int64_t)t->n_long + 12 * t->nnz_long;
+        const bool base = t->c24 && !t->cd;
+        if (t->tm) {  // whole padded slots: tile_nnz values + column entries, tm_rs lengths
+            const int64_t tn = t->tile_nnz;
+            b += ns * (t->tm_rs + 8 * tn + (t->cd ? t->cd * tn / 8 : 3 * tn) + 16 + (base ? 4 : 0)) +
+                 (t->cd ? 4 * t->ctab_n : 0);
+        } else {
+            b += (t->rl8 ? 1 : 4) * t->rows_short;
+            b += t->cd ? (t->cd * nz + 7) / 8 + 4 * t->ctab_n : (t->c24 ? 3 : 4) * nz;
+            b += t->vd ? nz / 2 + 128 * ns : 8 * nz;
+            b += (16 + (base ? 4 : 0)) * ns;
+        }
+        A->stream_bytes += b;
+    }
     if (!lo.empty()) {  // padded like d_col
         lo.resize(nnz + kVecPad, 0);
         hi.resize(nnz + kVecPad, 0);
@@ -1017,7 +1111,7 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes) {
     return PAMG_OK;
 }
 
-int pamg_mat_layout(const pamg_mat* A, int set, int out[5]) {
+int pamg_mat_layout(const pamg_mat* A, int set, int out[7]) {
     if (!A || !out || set < 0 || set > 1) return fail(PAMG_E_ARG, "mat_layout: bad args");
     const pamg::TileSet& t = set == 0 ? A->interior : A->boundary;
     out[0] = t.c24;
@@ -1025,6 +1119,8 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[5]) {
     out[2] = t.rl8;
     out[3] = t.cd;
     out[4] = t.ctab_n;
+    out[5] = t.tm;
+    out[6] = t.tm_rs;
     return PAMG_OK;
 }
 
@@ -1441,6 +1537,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "row_len8" && (value == 0 || value == 1)) o.row_len8 = (int)value;
     else if (k == "value_dict" && (value == 0 || value == 1)) o.value_dict = (int)value;
     else if (k == "col_dict" && (value == 0 || value == 1)) o.col_dict = (int)value;
+    else if (k == "tile_major" && value >= 0 && value <= 2) o.tile_major = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -1478,6 +1575,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "col24") *value = o.col24;
     else if (k == "value_dict") *value = o.value_dict;
     else if (k == "col_dict") *value = o.col_dict;
+    else if (k == "tile_major") *value = o.tile_major;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

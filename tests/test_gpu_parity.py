@@ -70,14 +70,20 @@ TILE_CONFIGS = [(0, 2048, 256, 0, 0, 0, 0, 1, 0, 1, 1), (1, 2048, 256, 0, 0, 0, 
                 (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 0), (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1)]
 # + col_dict (last column): on for every configuration above (it engages only where its
 # conditions hold), plus the default layout and the stored-diagonal Jacobi without it
-TILE_CONFIGS = [c + (1,) for c in TILE_CONFIGS] + [(1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 0),
-                                                   (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1, 0)]
+# + tile_major (last column): on wherever its conditions hold, plus variant 1 without it
+# (1 = where measured faster, 2 = every eligible set: 24-bit tile-major on every operator)
+TILE_CONFIGS = [c + (1, 1) for c in TILE_CONFIGS] + [(1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 0, 2),
+                                                      (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1, 0, 2),
+                                                      (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 0),
+                                                      (1, 1024, 256, 0, 1, 0, 1, 0, 0, 1, 1, 1, 0),
+                                                      (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2),
+                                                      (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1, 0, 2)]
 OPT_KEYS = ("rows_kernel", "tile_nnz", "tile_rows", "xcd_remap", "jacobi_diag", "stream_nt", "tile_order",
-            "col24", "value_dict", "long_tiles", "row_len8", "col_dict")
+            "col24", "value_dict", "long_tiles", "row_len8", "col_dict", "tile_major")
 
 
 @pytest.fixture(params=TILE_CONFIGS,
-                ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}_lt{}_rl{}_cd{}".format(*c))
+                ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}_lt{}_rl{}_cd{}_tm{}".format(*c))
 def tile_cfg(request, built):
     import ctypes
     from parallel_amg_amd._lib import call
@@ -189,7 +195,7 @@ def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
         offs = offs[offs != 0][:ndist]
     M = offset_csr(rng, n, offs, lengths)
     distinct = len(np.unique(M.col - np.repeat(np.arange(n), np.diff(M.rowptr))))
-    keys = ("col_dict", "tile_nnz", "jacobi_diag")
+    keys = ("col_dict", "tile_nnz", "jacobi_diag", "tile_major")
     old = []
     for k in keys:
         v = ctypes.c_int64()
@@ -198,13 +204,17 @@ def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
     try:
         call("pamg_set_option", b"tile_nnz", tnnz)
         call("pamg_set_option", b"col_dict", 0)
+        call("pamg_set_option", b"tile_major", 0)
         plain = upload(ctx, M)[0].stream_bytes
-        for dg in (0, 1):
+        for dg, tm in ((0, 0), (1, 0), (0, 2), (1, 2)):
             call("pamg_set_option", b"col_dict", 1)
             call("pamg_set_option", b"jacobi_diag", dg)
+            call("pamg_set_option", b"tile_major", tm)
             A, _h = upload(ctx, M)
-            assert (A.stream_bytes < plain) == (distinct <= 256), (A.stream_bytes, plain, distinct)
+            if not tm:
+                assert (A.stream_bytes < plain) == (distinct <= 256), (A.stream_bytes, plain, distinct)
             lay = layout_of(A)
+            assert lay["tm"] == bool(tm)
             assert lay["cd"] == (4 if distinct <= 16 else 8 if distinct <= 256 else 0), (lay, distinct)
             assert lay["cd_offsets"] == (distinct if distinct <= 256 else 0)
             xh, bh = rng.standard_normal(n), rng.standard_normal(n)
@@ -365,16 +375,23 @@ def test_stream_bytes_layout(ctx):
             for k in opts:
                 call("pamg_set_option", k.encode(), 0 if k == "value_dict" else 1)
 
-    got0 = stream_bytes(col24=0, row_len8=0, col_dict=0)
+    got0 = stream_bytes(col24=0, row_len8=0, col_dict=0, tile_major=0)
     nt, rem = divmod(got0 - 12 * nnz - 4 * (n + 1), 16)
     assert rem == 0 and nt > 0
-    assert stream_bytes(col24=1, row_len8=0, col_dict=0) == 11 * nnz + 4 * (n + 1) + 20 * nt
-    assert stream_bytes(col24=1, row_len8=1, col_dict=0) == 11 * nnz + n + 4 + 20 * nt
+    assert stream_bytes(col24=1, row_len8=0, col_dict=0, tile_major=0) == 11 * nnz + 4 * (n + 1) + 20 * nt
+    assert stream_bytes(col24=1, row_len8=1, col_dict=0, tile_major=0) == 11 * nnz + n + 4 + 20 * nt
     # 2 distinct values: every tile takes a value dictionary (which keeps the row pointers)
     assert stream_bytes(value_dict=1) == 3 * nnz + nnz // 2 + 4 * (n + 1) + (20 + 128) * nt
-    # column dictionary (default): 7 offsets -> 4-bit indices + the 28-B table, 8-bit row
-    # lengths, no per-tile base
-    assert stream_bytes() == 8 * nnz + (nnz + 1) // 2 + 4 * 7 + n + 4 + 16 * nt
+    # column dictionary: 7 offsets -> 4-bit indices + the 28-B table, 8-bit row lengths, no
+    # per-tile base
+    assert stream_bytes(tile_major=0) == 8 * nnz + (nnz + 1) // 2 + 4 * 7 + n + 4 + 16 * nt
+    # tile-major (default): whole padded slots of 1024 values + 512 B of indices + the
+    # row-length slot per tile
+    from parallel_amg_amd._lib import layout_of
+    A, _h = upload(ctx, M)
+    lay = layout_of(A)
+    assert lay["tm"] and lay["cd"] == 4 and 0 < lay["tm_rs"] <= 256 and lay["tm_rs"] % 4 == 0
+    assert A.stream_bytes == nt * (lay["tm_rs"] + 8 * 1024 + 512 + 16) + 4 * 7 + 4
 
 
 @pytest.mark.parametrize("seed,n,density,weak,iso", [(1, 3000, 0.003, 0.3, 0.02), (2, 5000, 0.001, 0.0, 0.0),
