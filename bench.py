@@ -54,7 +54,8 @@ def main():
                     help="levels >= 1 with <= this many rows are one part, replicated (0: off)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    ap.add_argument("--cpu-cycles", type=int, default=1)
+    ap.add_argument("--cpu-cycles", type=int, default=10,
+                    help="V-cycles of the CPU baseline sample (~1 s each at 512^3 on 16 threads)")
     ap.add_argument("--transport", choices=["rccl", "host"], default="rccl",
                     help="host = debug transport (ranks may share one GPU; not a perf mode)")
     ap.add_argument("--sweeps", default="1,1", help="nu1,nu2 of the V(nu1,nu2) cycle (SPEC S6)")
@@ -198,12 +199,13 @@ def main():
     # (only when the record was measured on the same column layout as this run)
     lay = _lib.layout_of(A0)
     c24, vd, rl8, cd, tm = lay["c24"], lay["vd"], lay["rl8"], lay["cd"], lay["tm"]
-    kname = ("k_rows_tm<2, 1024, %d>" % cd if tm
-             else "k_rows_tile2<2, 1024, 256, false, false, 256, false, false, true, %d>" % cd if cd
-             else "k_rows_tile2<2, 1024, 256, false, false, 256, true, true>" if vd
-             else "k_rows_tile2<2, 1024, 256, false, false, 256, true, false, true>" if rl8
-             else "k_rows_tile2<2, 1024, 256, false, false, 256, true>" if c24
-             else "k_rows_tile2<2, 1024, 256, false, false>")
+    tn = lay["tile_nnz"]
+    kname = (f"k_rows_tm<2, {tn}, {cd}>" if tm
+             else f"k_rows_tile2<2, {tn}, 256, false, false, 256, false, false, true, {cd}>" if cd
+             else f"k_rows_tile2<2, {tn}, 256, false, false, 256, true, true>" if vd
+             else f"k_rows_tile2<2, {tn}, 256, false, false, 256, true, false, true>" if rl8
+             else f"k_rows_tile2<2, {tn}, 256, false, false, 256, true>" if c24
+             else f"k_rows_tile2<2, {tn}, 256, false, false>")
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "r01_pmc", "traffic_jacobi_512.json")
     if (not args.matrix and args.kind == "poisson3d" and args.grid == 512 and world == 1

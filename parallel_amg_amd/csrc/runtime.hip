@@ -1111,7 +1111,7 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes) {
     return PAMG_OK;
 }
 
-int pamg_mat_layout(const pamg_mat* A, int set, int out[7]) {
+int pamg_mat_layout(const pamg_mat* A, int set, int out[8]) {
     if (!A || !out || set < 0 || set > 1) return fail(PAMG_E_ARG, "mat_layout: bad args");
     const pamg::TileSet& t = set == 0 ? A->interior : A->boundary;
     out[0] = t.c24;
@@ -1121,6 +1121,7 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[7]) {
     out[4] = t.ctab_n;
     out[5] = t.tm;
     out[6] = t.tm_rs;
+    out[7] = t.tile_nnz;
     return PAMG_OK;
 }
 

@@ -1,7 +1,8 @@
 """Full-size checks (BASELINE.json sizes) through properties that need no oracle run:
 
 * 512^3 fine matrix (the metric's workload): A*1 on the GPU equals the exact integer row sums
-  6 - (#neighbours) for all 134M rows; A*x* matches the host's SPEC §S3 row sums on sampled rows.
+  6 - (#neighbours) for all 134M rows; A*x* matches the host's SPEC §S3 row sums on sampled rows;
+  one Jacobi sweep gives the same bits in all four upload layouts.
 * 256^3 hierarchy: a V-cycle is linear and scaling by 2 is exact in binary floating point, so
   V(2x, 2b) must equal 2 V(x, b) bit for bit; two runs are bit-identical (determinism); the
   residual falls every cycle; graph replay equals eager launches.
@@ -44,6 +45,51 @@ def test_fine_512_rowsums(ctx):
         for k in range(A0.rowptr[i], A0.rowptr[i + 1]):
             s = s + A0.val[k] * xs[0][A0.col[k]]
         assert got[i] == s
+
+
+def test_fine_512_layouts_agree(ctx):
+    """The metric's level-0 Jacobi gives the same bits in every upload layout at full size:
+    tile-major slots + 4-bit column dictionary (default), variant 1 with the dictionary,
+    24-bit columns + 8-bit row lengths, and plain 32-bit CSR tiles."""
+    import ctypes
+    from parallel_amg_amd._lib import call, layout_of
+    from parallel_amg_amd.partitioned import jacobi
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 512)
+    A0 = A[0]
+    N = A0.nrows
+    rng = np.random.default_rng(3)
+    xh = rng.standard_normal(N)
+    bh = rng.standard_normal(N)
+    b = PVector(ctx, N, 0, bh)
+    layouts = [{}, {"tile_major": 0}, {"tile_major": 0, "col_dict": 0},
+               {"tile_major": 0, "col_dict": 0, "col24": 0, "row_len8": 0}]
+    keys = ("tile_major", "col_dict", "col24", "row_len8")
+    old = []
+    for k in keys:
+        v = ctypes.c_int64()
+        call("pamg_get_option", k.encode(), ctypes.byref(v))
+        old.append(v.value)
+    ref, seen = None, []
+    try:
+        for lay in layouts:
+            for k, v in zip(keys, old):
+                call("pamg_set_option", k.encode(), lay.get(k, v))
+            D = PSparseMatrix(ctx, A0)
+            seen.append(layout_of(D))
+            x, t = PVector(ctx, N, 0, xh), PVector(ctx, N)
+            jacobi(x, D, b, t, 2.0 / 3.0, 1)
+            got = bits(x.own_values())
+            del D, x, t
+            if ref is None:
+                ref = got
+            else:
+                assert np.array_equal(got, ref), lay
+    finally:
+        for k, v in zip(keys, old):
+            call("pamg_set_option", k.encode(), v)
+    assert seen[0]["tm"] and seen[0]["cd"] == 4 and not seen[1]["tm"] and seen[1]["cd"] == 4
+    assert seen[2]["cd"] == 0 and seen[2]["c24"] and not seen[3]["c24"]
 
 
 @pytest.fixture(scope="module")
