@@ -461,21 +461,33 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
         }
         if constexpr (OP == OP_PROLONG) py = y[r];
     }
-    __syncthreads();  // lwt, ltab
-    int pre = 0;
+    // end of this lane's row (tile-relative): the wave's inclusive sum + the earlier waves'
+    // totals, readable after the next barrier
+    auto row_end = [&]() {
+        int pre = 0;
 #pragma unroll
-    for (int q = 0; q < BS / 64; ++q) pre += q < (tid >> 6) ? lwt[q] : 0;
-    const int re = pre + rl_inc;  // end of this lane's row (tile-relative)
-    if (tid < nr)
-        for (int p = re - rl_len; p < re; ++p) lrow[p] = (uint8_t)tid;
-    __syncthreads();  // lrow
+        for (int q = 0; q < BS / 64; ++q) pre += q < (tid >> 6) ? lwt[q] : 0;
+        return pre + rl_inc;
+    };
+    // Per-position row ids are needed for dictionary columns (row + offset) and for Jacobi's
+    // in-tile diagonal; 24-bit SpMV / residual / prolongate-add skip them, so their gathers
+    // follow the stream loads with no barrier in between.
+    constexpr bool NEED_ROWS = CD != 0 || OP == OP_JACOBI;
+    int re = 0;
+    if constexpr (NEED_ROWS) {
+        __syncthreads();  // lwt, ltab
+        re = row_end();
+        if (tid < nr)
+            for (int p = re - rl_len; p < re; ++p) lrow[p] = (uint8_t)tid;
+        __syncthreads();  // lrow
+    }
 
     double xv[G][4];
     int cc[G][4];
 #pragma unroll
     for (int j = 0; j < G; ++j) {
         const int q = 4 * (tid + j * BS);
-        const uint32_t rw = q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
+        const uint32_t rw = NEED_ROWS && q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
         if constexpr (CD == 0) {
             const uint16_t l4[4] = {clo4[j].x, clo4[j].y, clo4[j].z, clo4[j].w};
 #pragma unroll
@@ -494,7 +506,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
 #pragma unroll
     for (int j = 0; j < G; ++j) {
         const int q = 4 * (tid + j * BS);
-        const uint32_t rw = q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
+        const uint32_t rw = NEED_ROWS && q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
         const double vv[4] = {va[j].x, va[j].y, vb[j].x, vb[j].y};
         double p[4];
 #pragma unroll
@@ -510,6 +522,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
         *reinterpret_cast<double2*>(&lprod[q + 2]) = make_double2(p[2], p[3]);
     }
     __syncthreads();
+    if constexpr (!NEED_ROWS) re = row_end();
     if (tid < nr) {
         const double s = row_sum_lds(lprod, re - rl_len, re);
         const int r = r0 + tid;

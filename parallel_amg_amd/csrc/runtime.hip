@@ -314,7 +314,7 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
 // columns, tile t's values, column stream and row lengths are copied to fixed, zero-padded
 // slots (t * tile_nnz, t * tm_rs), so the kernel addresses every pre-gather load from its
 // block index. The CSR arrays stay resident for the other variants and the long rows.
-int build_tile_major(pamg_mat* A, const std::vector<int64_t>& rp, const double* val,
+int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>& rp, const double* val,
                      const std::vector<int4>& t_in, const std::vector<int4>& t_bd,
                      const std::vector<uint16_t>& lo, const std::vector<uint8_t>& hi,
                      const std::vector<uint8_t>& idx8) {
@@ -328,12 +328,16 @@ int build_tile_major(pamg_mat* A, const std::vector<int64_t>& rp, const double* 
             ts->n_short == 0 || ts->tile_rows > pamg::kBlock || ts->max_short_len > 255 ||
             !(ts->cd || (ts->c24 && !lo.empty())) || (ts->cd && idx8.empty()) || !val)
             continue;
-        // tile_major 1 (default): the sets where it measured faster at 512^3 — column
-        // dictionary sets (A0: Jacobi -6.5 %, residual -4.6 %, SpMV -3.1 %) and wide operators
-        // (restrictions, ncols >= 2 nrows: R0 -4..-6 %); prolongations (P0 +3..8 %: row-limited
-        // tiles leave ~8 % of each slot as padding) and the coarse A1 (+1..2 %) keep variant 1.
+        // tile_major 1 (default): the sets where it measured faster at 512^3
+        // (profiles/r01_kbench_512_tm_*.jsonl) — column-dictionary sets (A0: Jacobi -9 %,
+        // residual -7 %, SpMV -5 %) and the non-square operators whose tiles fill >= 97 % of
+        // their slots (R0 -5..-7 %, P1 -3 %); P0's row-limited tiles leave ~8 % of each slot as
+        // padding (+5 %) and the square coarse A1 gains nothing (Jacobi +3 %): variant 1.
         // tile_major 2: every eligible set (A/B, tests).
-        if (opt.tile_major == 1 && !ts->cd && A->ncols < 2 * A->nrows) continue;
+        if (opt.tile_major == 1 && !ts->cd) {
+            const double fill = (double)ts->nnz_short / ((double)ts->n_short * (double)ts->tile_nnz);
+            if (n_own_cols == A->nrows || fill < 0.97) continue;
+        }
         const std::vector<int4>& tiles = *tl[q];
         const int64_t nt = (int64_t)tiles.size(), tn = ts->tile_nnz;
         int rs = 0;
@@ -1031,7 +1035,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         CHECK(build_tiles(rp, bnd, &A->boundary, band, ci, &lo, &hi, val, &vidx, &t_bd));
         std::vector<uint8_t> idx8;
         CHECK(build_col_dicts(A.get(), rp, ci, t_in, t_bd, &idx8));
-        CHECK(build_tile_major(A.get(), rp, val, t_in, t_bd, lo, hi, idx8));
+        CHECK(build_tile_major(A.get(), n_own_cols, rp, val, t_in, t_bd, lo, hi, idx8));
     }
     if (A->interior.rl8 || A->boundary.rl8) {
         std::vector<uint8_t> rl(nrows + kVecPad, 0);
