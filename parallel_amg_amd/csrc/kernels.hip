@@ -548,6 +548,201 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Variant 4p (Options::tm_persist): variant 4's tile body in a persistent grid. Block b walks
+// tiles b, b+G, b+2G, ... (G a multiple of 8: the block stays on its XCD's slice of the banded
+// order). Tile-major slots are addressed by tile index alone, so the NEXT tile's values,
+// column stream and row lengths are issued right after the current tile's x gathers into a
+// second register set (two sets in alternation, no copies: a copy would wait for the loads)
+// and stay in flight through the current tile's LDS sums, epilogue and stores. Barriers are
+// LDS-only (lds_barrier), so no __syncthreads() drains the prefetch.
+template <int OP, int TNNZ, int CD>
+struct TmSlot {
+    static constexpr int G = TNNZ / (4 * kBlock);
+    double2 va[G], vb[G];
+    uint32_t cn[G];
+    ushort4 clo4[G];
+    int rl;
+};
+
+template <int OP, int TNNZ, int CD>
+__device__ __forceinline__ void tm_load(int t, TmSlot<OP, TNNZ, CD>& S, int tid,
+                                        const double* __restrict__ tval,
+                                        const uint8_t* __restrict__ tcidx,
+                                        const uint16_t* __restrict__ tclo,
+                                        const uint8_t* __restrict__ tchi,
+                                        const uint8_t* __restrict__ trlen, int rs) {
+    constexpr int G = TmSlot<OP, TNNZ, CD>::G;
+    const size_t sb = (size_t)t * TNNZ;
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const size_t q = sb + 4 * (tid + j * kBlock);
+        S.va[j] = *reinterpret_cast<const double2*>(tval + q);
+        S.vb[j] = *reinterpret_cast<const double2*>(tval + q + 2);
+        if constexpr (CD == 4) {
+            S.cn[j] = *reinterpret_cast<const uint16_t*>(tcidx + (q >> 1));
+        } else if constexpr (CD == 8) {
+            S.cn[j] = *reinterpret_cast<const uint32_t*>(tcidx + q);
+        } else {
+            S.clo4[j] = *reinterpret_cast<const ushort4*>(tclo + q);
+            S.cn[j] = *reinterpret_cast<const uint32_t*>(tchi + q);
+        }
+    }
+    S.rl = tid < rs ? (int)trlen[(size_t)t * rs + tid] : 0;
+}
+
+struct TmArgs {
+    const int4* tiles;
+    const double* tval;
+    const uint8_t* tcidx;
+    const uint16_t* tclo;
+    const uint8_t* tchi;
+    const int* tbase;
+    const uint8_t* trlen;
+    int rs;
+    const double* x;
+    const double* b;
+    double* y;
+    double omega;
+    const double* diag;
+};
+
+// One tile of variant 4p from slot C; prefetches tile tn into N behind the x gathers.
+template <int OP, int TNNZ, int CD>
+__device__ __forceinline__ void tm_tile(const TmArgs& a, int t, TmSlot<OP, TNNZ, CD>& C, int tn,
+                                        TmSlot<OP, TNNZ, CD>& N, double* lprod, double* ldiag,
+                                        int* lwt, const int* ltab, uint8_t* lrow) {
+    constexpr int BS = kBlock;
+    constexpr int G = TmSlot<OP, TNNZ, CD>::G;
+    constexpr bool NEED_ROWS = CD != 0 || OP == OP_JACOBI;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int4 d = a.tiles[t];
+    int cb = 0;
+    if constexpr (CD == 0) cb = a.tbase[t];
+    const int rl_len = C.rl;
+    int rl_inc = rl_len;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(rl_inc, off, 64);
+        if (lane >= off) rl_inc += u;
+    }
+    if (lane == 63) lwt[tid >> 6] = rl_inc;
+    const int r0 = d.x, nr = d.y - d.x, cnt = d.w - d.z;
+    double pb = 0.0, px = 0.0, py = 0.0, pd = 0.0;
+    if (tid < nr) {
+        const int r = r0 + tid;
+        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = a.b[r];
+        if constexpr (OP == OP_JACOBI) {
+            px = a.x[r];
+            if (a.diag) pd = a.diag[r];
+        }
+        if constexpr (OP == OP_PROLONG) py = a.y[r];
+    }
+    auto row_end = [&]() {
+        int pre = 0;
+#pragma unroll
+        for (int q = 0; q < BS / 64; ++q) pre += q < (tid >> 6) ? lwt[q] : 0;
+        return pre + rl_inc;
+    };
+    int re = 0;
+    if constexpr (NEED_ROWS) {
+        lds_barrier();  // lwt (and ltab on the first tile)
+        re = row_end();
+        if (tid < nr)
+            for (int p = re - rl_len; p < re; ++p) lrow[p] = (uint8_t)tid;
+        lds_barrier();  // lrow
+    }
+    double xv[G][4];
+    int cc[G][4];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const int q = 4 * (tid + j * BS);
+        const uint32_t rw = NEED_ROWS && q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
+        if constexpr (CD == 0) {
+            const uint16_t l4[4] = {C.clo4[j].x, C.clo4[j].y, C.clo4[j].z, C.clo4[j].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                cc[j][e] = cb + (int)((uint32_t)l4[e] | (((C.cn[j] >> (8 * e)) & 255u) << 16));
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int ix = CD == 4 ? (int)((C.cn[j] >> (4 * e)) & 15u) : (int)((C.cn[j] >> (8 * e)) & 255u);
+                cc[j][e] = r0 + (int)((rw >> (8 * e)) & 255u) + ltab[ix];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[j][e] = a.x[q + e < cnt ? cc[j][e] : 0];
+    }
+    tm_load<OP, TNNZ, CD>(tn, N, tid, a.tval, a.tcidx, a.tclo, a.tchi, a.trlen, a.rs);
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const int q = 4 * (tid + j * BS);
+        const uint32_t rw = NEED_ROWS && q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
+        const double vv[4] = {C.va[j].x, C.va[j].y, C.vb[j].x, C.vb[j].y};
+        double p[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool ok = q + e < cnt;
+            p[e] = ok ? vv[e] * xv[j][e] : 0.0;
+            if constexpr (OP == OP_JACOBI) {
+                const int rl = (int)((rw >> (8 * e)) & 255u);
+                if (!a.diag && ok && cc[j][e] - r0 == rl) ldiag[rl] = vv[e];
+            }
+        }
+        *reinterpret_cast<double2*>(&lprod[q]) = make_double2(p[0], p[1]);
+        *reinterpret_cast<double2*>(&lprod[q + 2]) = make_double2(p[2], p[3]);
+    }
+    lds_barrier();  // lprod, ldiag (and lwt for the 24-bit ops)
+    if constexpr (!NEED_ROWS) re = row_end();
+    if (tid < nr) {
+        const double s = row_sum_lds(lprod, re - rl_len, re);
+        const int r = r0 + tid;
+        if constexpr (OP == OP_SPMV) {
+            a.y[r] = s;
+        } else if constexpr (OP == OP_RESID) {
+            a.y[r] = pb - s;
+        } else if constexpr (OP == OP_JACOBI) {
+            const double dd = a.diag ? pd : ldiag[tid];
+            const double u = pb - s;
+            const double v = a.omega * u;
+            const double w = v / dd;
+            a.y[r] = px + w;
+        } else {
+            a.y[r] = py + s;
+        }
+    }
+    lds_barrier();  // every lane is done with this tile's lwt / lrow / lprod / ldiag
+}
+
+template <int OP, int TNNZ, int CD>
+__global__ __launch_bounds__(kBlock) void k_rows_tmp(TmArgs a, int ntiles, const int* __restrict__ ctab,
+                                                     int ctab_n) {
+    __shared__ __attribute__((aligned(16))) double lprod[TNNZ + 8];
+    __shared__ double ldiag[OP == OP_JACOBI ? kBlock : 1];
+    __shared__ int lwt[kBlock / 64];
+    __shared__ int ltab[CD == 8 ? 256 : 16];
+    __shared__ __attribute__((aligned(4))) uint8_t lrow[TNNZ + 8];
+    const int tid = threadIdx.x;
+    int t = blockIdx.x;
+    if (t >= ntiles) return;
+    if constexpr (CD != 0) {
+        if (tid < ctab_n) ltab[tid] = ctab[tid];
+        lds_barrier();
+    }
+    TmSlot<OP, TNNZ, CD> A, B;
+    tm_load<OP, TNNZ, CD>(t, A, tid, a.tval, a.tcidx, a.tclo, a.tchi, a.trlen, a.rs);
+    const int step = gridDim.x;
+    while (true) {  // two slots in alternation: A holds tile t, B receives the next one
+        int tn = t + step;
+        tm_tile<OP, TNNZ, CD>(a, t, A, tn < ntiles ? tn : t, B, lprod, ldiag, lwt, ltab, lrow);
+        if (tn >= ntiles) break;
+        t = tn;
+        tn = t + step;
+        tm_tile<OP, TNNZ, CD>(a, t, B, tn < ntiles ? tn : t, A, lprod, ldiag, lwt, ltab, lrow);
+        if (tn >= ntiles) break;
+        t = tn;
+    }
+}
+
 // Variant 3: variant 1's tile body in a persistent grid. Block b walks tiles b, b+G, b+2G, ...
 // (G = grid, a multiple of 8, so a block stays on one XCD's slice of the banded tile order)
 // and issues the NEXT tile's descriptor-driven column/value stream right after the current
@@ -926,11 +1121,36 @@ inline int grid_for(int64_t n, int cap = 8192) {
     return (int)(g < cap ? g : cap);
 }
 
+// Variant 4p launch: a persistent grid of the resident blocks (a multiple of 8, the XCDs).
+template <int OP, int TNNZ, int CD>
+void launch_tmp(const TileSet& ts, const double* x, const double* b, double* y, double omega,
+                const double* dg, hipStream_t s) {
+    static int grid_cap = 0;
+    if (grid_cap == 0) {
+        int nb = 0, dev = 0, ncu = 256;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rows_tmp<OP, TNNZ, CD>, kBlock, 0);
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        grid_cap = ((nb > 0 ? nb : 1) * ncu) & ~7;
+        if (grid_cap < 8) grid_cap = 8;
+    }
+    const int grid = ts.n_short < grid_cap ? ts.n_short : grid_cap;
+    TmArgs a{ts.d_short, ts.d_tm_val, ts.d_tm_cidx, ts.d_tm_clo, ts.d_tm_chi, ts.d_base,
+             ts.d_tm_rlen, ts.tm_rs, x, b, y, omega, dg};
+    k_rows_tmp<OP, TNNZ, CD><<<grid, kBlock, 0, s>>>(a, ts.n_short, ts.d_ctab, ts.ctab_n);
+}
+
 template <int OP, int TNNZ, int TROWS>
 void launch_tile2(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
                   double* y, double omega, hipStream_t s) {
     const double* dg = (OP == OP_JACOBI && A.jacobi_diag) ? A.d_diag : nullptr;
-    if (ts.tm) {
+    if (ts.tm && A.tm_persist) {
+        if constexpr (TROWS <= kBlock) {
+            if (ts.cd == 4) launch_tmp<OP, TNNZ, 4>(ts, x, b, y, omega, dg, s);
+            else if (ts.cd == 8) launch_tmp<OP, TNNZ, 8>(ts, x, b, y, omega, dg, s);
+            else launch_tmp<OP, TNNZ, 0>(ts, x, b, y, omega, dg, s);
+        }
+    } else if (ts.tm) {
         if constexpr (TROWS <= kBlock) {
             if (ts.cd == 4)
                 k_rows_tm<OP, TNNZ, 4><<<ts.n_short, kBlock, 0, s>>>(

@@ -80,6 +80,7 @@ struct Options {
     int value_dict = 0;        // 1 (opt-in): 4-bit per-tile value dictionaries where they fit
     int col_dict = 1;          // 1: row-relative column dictionaries (4/8-bit) where they fit
     int tile_major = 1;        // tile-major padded copies (variant 4): 1 where measured faster, 2 all eligible
+    int tm_persist = 0;        // 1: tile-major sets run the persistent prefetching variant 4p
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };
 Options& options();
@@ -140,6 +141,7 @@ struct pamg_mat {
     int xcd_remap = 0;
     int jacobi_diag = 0;
     int stream_nt = 0;
+    int tm_persist = 0;
 };
 
 namespace pamg {

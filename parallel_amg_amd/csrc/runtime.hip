@@ -974,6 +974,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     A->xcd_remap = pamg::options().xcd_remap;
     A->jacobi_diag = pamg::options().jacobi_diag;
     A->stream_nt = pamg::options().stream_nt;
+    A->tm_persist = pamg::options().tm_persist;
     A->nrows = nrows;
     A->ncols = ncols;
     A->nnz = nnz;
@@ -1543,6 +1544,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "value_dict" && (value == 0 || value == 1)) o.value_dict = (int)value;
     else if (k == "col_dict" && (value == 0 || value == 1)) o.col_dict = (int)value;
     else if (k == "tile_major" && value >= 0 && value <= 2) o.tile_major = (int)value;
+    else if (k == "tm_persist" && (value == 0 || value == 1)) o.tm_persist = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -1581,6 +1583,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "value_dict") *value = o.value_dict;
     else if (k == "col_dict") *value = o.col_dict;
     else if (k == "tile_major") *value = o.tile_major;
+    else if (k == "tm_persist") *value = o.tm_persist;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }
