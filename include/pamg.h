@@ -117,8 +117,8 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * out[0] 24-bit columns, out[1] value dictionary, out[2] 8-bit row lengths,
  * out[3] column-dictionary index width (0, 4 or 8), out[4] column-dictionary offsets,
  * out[5] tile-major padded copy, out[6] its row-length slot per tile, out[7] the tile
- * budget (nonzeros per tile) the set was cut with. */
-int pamg_mat_layout(const pamg_mat* A, int set, int out[8]);
+ * budget (nonzeros per tile) the set was cut with, out[8] row-start flags (variant 4f). */
+int pamg_mat_layout(const pamg_mat* A, int set, int out[9]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
 int pamg_spmv(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, pamg_vec* y);

@@ -162,11 +162,11 @@ def call(name, *args):
 
 def layout_of(M, part_set: int = 0) -> dict:
     """The tile layout libpamg chose at upload for a device matrix (pamg_mat_layout)."""
-    out = (C.c_int * 8)()
+    out = (C.c_int * 9)()
     call("pamg_mat_layout", M.handle, part_set, out)
     return {"c24": bool(out[0]), "vd": bool(out[1]), "rl8": bool(out[2]), "cd": int(out[3]),
             "cd_offsets": int(out[4]), "tm": bool(out[5]), "tm_rs": int(out[6]),
-            "tile_nnz": int(out[7])}
+            "tile_nnz": int(out[7]), "tm_flags": bool(out[8])}
 
 
 def last_error() -> str:

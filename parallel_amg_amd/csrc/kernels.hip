@@ -542,6 +542,133 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     }
 }
 
+// Variant 4f (TileSet::tm_flags): variant 4 with row-start flags instead of row lengths, so a
+// tile has ONE barrier. Every nonzero of the slot carries a "first of its row" bit (tflag, 4
+// bits per lane) and every wave chunk of the slot the number of rows begun before it (twb, 16
+// bits per wave and lane group: a tile may hold 256 rows). A lane finds the row of each of its four nonzeros inside its
+// wave — ballots of the four flag bits, counts below the lane, plus the chunk's base — so
+// columns (row + table[index], the table read through L1) and x gathers follow the stream
+// loads with no barrier, no scan and no LDS row map. The lane holding a row's first nonzero
+// publishes the row's start in LDS with the products; after the one barrier each row's lane
+// sums [start, next start) in order (SPEC §S3). Needs every row of the set non-empty.
+template <int OP, int TNNZ, int CD>
+__global__ __launch_bounds__(kBlock) void k_rows_tmf(
+    const int4* __restrict__ tiles, const double* __restrict__ tval,
+    const uint8_t* __restrict__ tcidx, const uint16_t* __restrict__ tclo,
+    const uint8_t* __restrict__ tchi, const int* __restrict__ tbase,
+    const uint8_t* __restrict__ tflag, const uint16_t* __restrict__ twb,
+    const int* __restrict__ ctab, const double* __restrict__ x, const double* __restrict__ b,
+    double* __restrict__ y, double omega, const double* __restrict__ diag) {
+    constexpr int BS = kBlock;
+    constexpr int G = TNNZ / (4 * BS);
+    static_assert(G >= 1 && TNNZ % (4 * BS) == 0, "tile budget must be a multiple of 4 x block");
+    __shared__ __attribute__((aligned(16))) double lprod[TNNZ + 8];
+    __shared__ double ldiag[OP == OP_JACOBI ? BS : 1];
+    __shared__ int lstart[BS + 1];
+
+    const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int4 d = tiles[t];
+    const size_t sb = (size_t)t * TNNZ;
+    double2 va[G], vb[G];
+    uint32_t cn[G], fl[G];
+    ushort4 clo4[G];
+    int wb[G];
+    int cb = 0;
+    if constexpr (CD == 0) cb = tbase[t];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const int q = 4 * (tid + j * BS);
+        const size_t g = sb + q;
+        va[j] = *reinterpret_cast<const double2*>(tval + g);
+        vb[j] = *reinterpret_cast<const double2*>(tval + g + 2);
+        if constexpr (CD == 4) {
+            cn[j] = *reinterpret_cast<const uint16_t*>(tcidx + (g >> 1));
+        } else if constexpr (CD == 8) {
+            cn[j] = *reinterpret_cast<const uint32_t*>(tcidx + g);
+        } else {
+            clo4[j] = *reinterpret_cast<const ushort4*>(tclo + g);
+            cn[j] = *reinterpret_cast<const uint32_t*>(tchi + g);
+        }
+        fl[j] = (uint32_t)(tflag[g >> 3] >> (4 * ((q >> 2) & 1))) & 15u;
+        wb[j] = twb[(size_t)t * (4 * G) + j * 4 + w];
+    }
+    const int r0 = d.x, nr = d.y - d.x, cnt = d.w - d.z;
+    double pb = 0.0, px = 0.0, py = 0.0, pd = 0.0;
+    if (tid < nr) {
+        const int r = r0 + tid;
+        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[r];
+        if constexpr (OP == OP_JACOBI) {
+            px = x[r];
+            if (diag) pd = diag[r];
+        }
+        if constexpr (OP == OP_PROLONG) py = y[r];
+    }
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    double xv[G][4];
+    int cc[G][4], rw[G][4];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        // rows begun before this lane's first nonzero inside the wave chunk
+        int excl = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) excl += __popcll(__ballot((fl[j] >> e) & 1u) & below);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            rw[j][e] = wb[j] + excl + __popc(fl[j] & ((2u << e) - 1u)) - 1;
+        if constexpr (CD == 0) {
+            const uint16_t l4[4] = {clo4[j].x, clo4[j].y, clo4[j].z, clo4[j].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                cc[j][e] = cb + (int)((uint32_t)l4[e] | (((cn[j] >> (8 * e)) & 255u) << 16));
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int ix = CD == 4 ? (int)((cn[j] >> (4 * e)) & 15u) : (int)((cn[j] >> (8 * e)) & 255u);
+                cc[j][e] = r0 + rw[j][e] + ctab[ix];
+            }
+        }
+        const int q = 4 * (tid + j * BS);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[j][e] = x[q + e < cnt ? cc[j][e] : 0];
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const int q = 4 * (tid + j * BS);
+        const double vv[4] = {va[j].x, va[j].y, vb[j].x, vb[j].y};
+        double p[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool ok = q + e < cnt;
+            p[e] = ok ? vv[e] * xv[j][e] : 0.0;
+            if (ok && ((fl[j] >> e) & 1u)) lstart[rw[j][e]] = q + e;
+            if constexpr (OP == OP_JACOBI) {
+                if (!diag && ok && cc[j][e] - r0 == rw[j][e]) ldiag[rw[j][e]] = vv[e];
+            }
+        }
+        *reinterpret_cast<double2*>(&lprod[q]) = make_double2(p[0], p[1]);
+        *reinterpret_cast<double2*>(&lprod[q + 2]) = make_double2(p[2], p[3]);
+    }
+    if (tid == 0) lstart[nr] = cnt;
+    __syncthreads();
+    if (tid < nr) {
+        const double s = row_sum_lds(lprod, lstart[tid], lstart[tid + 1]);
+        const int r = r0 + tid;
+        if constexpr (OP == OP_SPMV) {
+            y[r] = s;
+        } else if constexpr (OP == OP_RESID) {
+            y[r] = pb - s;
+        } else if constexpr (OP == OP_JACOBI) {
+            const double dd = diag ? pd : ldiag[tid];
+            const double u = pb - s;
+            const double v = omega * u;
+            const double ww = v / dd;
+            y[r] = px + ww;
+        } else {
+            y[r] = py + s;
+        }
+    }
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops (lgkmcnt), NOT for
 // its outstanding global loads (no vmcnt), so a prefetch issued before it stays in flight.
 __device__ __forceinline__ void lds_barrier() {
@@ -1149,6 +1276,21 @@ void launch_tile2(const pamg_mat& A, const TileSet& ts, const double* x, const d
             if (ts.cd == 4) launch_tmp<OP, TNNZ, 4>(ts, x, b, y, omega, dg, s);
             else if (ts.cd == 8) launch_tmp<OP, TNNZ, 8>(ts, x, b, y, omega, dg, s);
             else launch_tmp<OP, TNNZ, 0>(ts, x, b, y, omega, dg, s);
+        }
+    } else if (ts.tm && ts.tm_flags) {
+        if constexpr (TROWS <= kBlock) {
+            if (ts.cd == 4)
+                k_rows_tmf<OP, TNNZ, 4><<<ts.n_short, kBlock, 0, s>>>(
+                    ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr, nullptr, ts.d_tm_flag,
+                    ts.d_tm_wb, ts.d_ctab, x, b, y, omega, dg);
+            else if (ts.cd == 8)
+                k_rows_tmf<OP, TNNZ, 8><<<ts.n_short, kBlock, 0, s>>>(
+                    ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr, nullptr, ts.d_tm_flag,
+                    ts.d_tm_wb, ts.d_ctab, x, b, y, omega, dg);
+            else
+                k_rows_tmf<OP, TNNZ, 0><<<ts.n_short, kBlock, 0, s>>>(
+                    ts.d_short, ts.d_tm_val, nullptr, ts.d_tm_clo, ts.d_tm_chi, ts.d_base, ts.d_tm_flag,
+                    ts.d_tm_wb, nullptr, x, b, y, omega, dg);
         }
     } else if (ts.tm) {
         if constexpr (TROWS <= kBlock) {

@@ -58,6 +58,9 @@ struct TileSet {
     uint16_t* d_tm_clo = nullptr;  // or 24-bit columns: low 16 bits
     uint8_t* d_tm_chi = nullptr;   //   high 8 bits
     uint8_t* d_tm_rlen = nullptr;
+    bool tm_flags = false;         // variant 4f: row-start bits + per-chunk row bases
+    uint8_t* d_tm_flag = nullptr;  // tile_nnz / 8 bytes per tile
+    uint16_t* d_tm_wb = nullptr;   // tile_nnz / 256 entries per tile (rows begun before a chunk)
     int max_short_len = 0;    // longest row in a short tile
     int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
@@ -81,6 +84,7 @@ struct Options {
     int col_dict = 1;          // 1: row-relative column dictionaries (4/8-bit) where they fit
     int tile_major = 1;        // tile-major padded copies (variant 4): 1 where measured faster, 2 all eligible
     int tm_persist = 0;        // 1: tile-major sets run the persistent prefetching variant 4p
+    int tm_flags = 0;          // 1: row-start flags (one-barrier variant 4f; measured slower, A/B)
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };
 Options& options();

@@ -290,8 +290,10 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
     for (int q = 0; q < 2; ++q) {
         if (tab[q].empty()) continue;
         pamg::TileSet* ts = sets[q];
-        CHECK(dalloc(&ts->d_ctab, (int64_t)tab[q].size()));
-        HIPC(hipMemcpy(ts->d_ctab, tab[q].data(), sizeof(int) * tab[q].size(), hipMemcpyHostToDevice));
+        std::vector<int> tab256(256, 0);  // any 8-bit index stays inside the allocation
+        std::copy(tab[q].begin(), tab[q].end(), tab256.begin());
+        CHECK(dalloc(&ts->d_ctab, (int64_t)tab256.size()));
+        HIPC(hipMemcpy(ts->d_ctab, tab256.data(), sizeof(int) * tab256.size(), hipMemcpyHostToDevice));
         ts->ctab_n = (int)tab[q].size();
         ts->cd = width;
         ts->rl8 = true;
@@ -382,6 +384,39 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
         }
         ts->tm_rs = rs;
         ts->tm = true;
+        // variant 4f: row-start flags (1 bit per slot position) + rows begun before every
+        // wave chunk (2 B per chunk of 256 positions), where no row of the set is empty
+        ts->tm_flags = false;
+        bool nonempty = opt.tm_flags != 0;
+        for (int64_t i = 0; i < nt && nonempty; ++i)
+            for (int r = tiles[i].x; r < tiles[i].y; ++r)
+                if (rp[r + 1] == rp[r]) {
+                    nonempty = false;
+                    break;
+                }
+        if (nonempty) {
+            const int nch = (int)(tn / 256);  // wave chunks per slot (4 per 1024 positions)
+            std::vector<uint8_t> tf((size_t)(nt * tn / 8 + kVecPad), 0);
+            std::vector<uint16_t> twb((size_t)(nt * nch + kVecPad), 0);  // 0..256 rows
+            for (int64_t i = 0; i < nt; ++i) {
+                const int4 t = tiles[i];
+                int64_t pos = 0;
+                int row = 0, ch = 0;
+                for (int r = t.x; r < t.y; ++r, ++row) {
+                    // chunks that begin at or before this row's start count the rows before it
+                    while (ch < nch && 256 * ch <= pos) twb[i * nch + ch++] = (uint16_t)row;
+                    const int64_t p = i * tn + pos;
+                    tf[p >> 3] |= (uint8_t)(1u << (p & 7));
+                    pos += rp[r + 1] - rp[r];
+                }
+                while (ch < nch) twb[i * nch + ch++] = (uint16_t)(t.y - t.x);
+            }
+            CHECK(dalloc(&ts->d_tm_flag, (int64_t)tf.size()));
+            HIPC(hipMemcpy(ts->d_tm_flag, tf.data(), tf.size(), hipMemcpyHostToDevice));
+            CHECK(dalloc(&ts->d_tm_wb, (int64_t)twb.size()));
+            HIPC(hipMemcpy(ts->d_tm_wb, twb.data(), sizeof(uint16_t) * twb.size(), hipMemcpyHostToDevice));
+            ts->tm_flags = true;
+        }
     }
     return PAMG_OK;
 }
@@ -398,6 +433,9 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_tm_clo);
     dfree(ts.d_tm_chi);
     dfree(ts.d_tm_rlen);
+    dfree(ts.d_tm_flag);
+    dfree(ts.d_tm_wb);
+    ts.tm_flags = false;
     ts.tm = false;
     ts.tm_rs = 0;
     ts.c24 = ts.vd = ts.rl8 = false;
@@ -1059,9 +1097,11 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         const int64_t ns = t->n_short, nz = t->nnz_short;
         int64_t b = 8 * (int64_t)t->n_long + 12 * t->nnz_long;
         const bool base = t->c24 && !t->cd;
-        if (t->tm) {  // whole padded slots: tile_nnz values + column entries, tm_rs lengths
+        if (t->tm) {  // whole padded slots: tile_nnz values + column entries + row bounds
+            // (tm_rs lengths, or tile_nnz/8 flag bytes + one byte per 256-position chunk)
             const int64_t tn = t->tile_nnz;
-            b += ns * (t->tm_rs + 8 * tn + (t->cd ? t->cd * tn / 8 : 3 * tn) + 16 + (base ? 4 : 0)) +
+            const int64_t rowb = t->tm_flags ? tn / 8 + 2 * (tn / 256) : t->tm_rs;
+            b += ns * (rowb + 8 * tn + (t->cd ? t->cd * tn / 8 : 3 * tn) + 16 + (base ? 4 : 0)) +
                  (t->cd ? 4 * t->ctab_n : 0);
         } else {
             b += (t->rl8 ? 1 : 4) * t->rows_short;
@@ -1116,7 +1156,7 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes) {
     return PAMG_OK;
 }
 
-int pamg_mat_layout(const pamg_mat* A, int set, int out[8]) {
+int pamg_mat_layout(const pamg_mat* A, int set, int out[9]) {
     if (!A || !out || set < 0 || set > 1) return fail(PAMG_E_ARG, "mat_layout: bad args");
     const pamg::TileSet& t = set == 0 ? A->interior : A->boundary;
     out[0] = t.c24;
@@ -1127,6 +1167,7 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[8]) {
     out[5] = t.tm;
     out[6] = t.tm_rs;
     out[7] = t.tile_nnz;
+    out[8] = t.tm_flags;
     return PAMG_OK;
 }
 
@@ -1545,6 +1586,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "col_dict" && (value == 0 || value == 1)) o.col_dict = (int)value;
     else if (k == "tile_major" && value >= 0 && value <= 2) o.tile_major = (int)value;
     else if (k == "tm_persist" && (value == 0 || value == 1)) o.tm_persist = (int)value;
+    else if (k == "tm_flags" && (value == 0 || value == 1)) o.tm_flags = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -1584,6 +1626,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "col_dict") *value = o.col_dict;
     else if (k == "tile_major") *value = o.tile_major;
     else if (k == "tm_persist") *value = o.tm_persist;
+    else if (k == "tm_flags") *value = o.tm_flags;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

@@ -82,12 +82,17 @@ TILE_CONFIGS = [c + (1, 1) for c in TILE_CONFIGS] + [(1, 1024, 256, 0, 0, 0, 1, 
 TILE_CONFIGS = [c + (0,) for c in TILE_CONFIGS] + [(1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 1),
                                                    (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1, 1, 2, 1),
                                                    (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 1)]
+# + tm_flags (last column): row lengths (variant 4) by default, row-start flags (variant 4f)
+TILE_CONFIGS = [c + (0,) for c in TILE_CONFIGS] + [(1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 0, 1),
+                                                   (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1, 1, 2, 0, 1),
+                                                   (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 0, 1),
+                                                   (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 0, 2, 0, 1)]
 OPT_KEYS = ("rows_kernel", "tile_nnz", "tile_rows", "xcd_remap", "jacobi_diag", "stream_nt", "tile_order",
-            "col24", "value_dict", "long_tiles", "row_len8", "col_dict", "tile_major", "tm_persist")
+            "col24", "value_dict", "long_tiles", "row_len8", "col_dict", "tile_major", "tm_persist", "tm_flags")
 
 
 @pytest.fixture(params=TILE_CONFIGS,
-                ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}_lt{}_rl{}_cd{}_tm{}_tp{}".format(*c))
+                ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}_lt{}_rl{}_cd{}_tm{}_tp{}_tf{}".format(*c))
 def tile_cfg(request, built):
     import ctypes
     from parallel_amg_amd._lib import call
@@ -179,7 +184,7 @@ def offset_csr(rng, n, offsets, lengths, palette=None):
 # with the diagonal), 8-bit (17..256), no dictionary (> 256); ragged rows up to the 255 limit
 COLDICT_CASES = [("stencil7", None, [7]), ("d15", 15, [1, 16, 5, 9]), ("d16", 16, [17, 2]),
                  ("d200", 200, [30, 1, 7, 255, 3]), ("d255", 255, [64, 9]), ("d256", 256, [40, 2]),
-                 ("ragged4", 12, [1, 2, 13, 1, 1, 9, 4])]
+                 ("ragged4", 12, [1, 2, 13, 1, 1, 9, 4]), ("rows256", 3, [1, 1, 1, 4, 1, 1, 1, 2])]
 
 
 @pytest.mark.parametrize("name,ndist,lengths", COLDICT_CASES, ids=[c[0] for c in COLDICT_CASES])
@@ -199,7 +204,7 @@ def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
         offs = offs[offs != 0][:ndist]
     M = offset_csr(rng, n, offs, lengths)
     distinct = len(np.unique(M.col - np.repeat(np.arange(n), np.diff(M.rowptr))))
-    keys = ("col_dict", "tile_nnz", "jacobi_diag", "tile_major", "tm_persist")
+    keys = ("col_dict", "tile_nnz", "jacobi_diag", "tile_major", "tm_persist", "tm_flags")
     old = []
     for k in keys:
         v = ctypes.c_int64()
@@ -210,16 +215,18 @@ def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
         call("pamg_set_option", b"col_dict", 0)
         call("pamg_set_option", b"tile_major", 0)
         plain = upload(ctx, M)[0].stream_bytes
-        for dg, tm, tp in ((0, 0, 0), (1, 0, 0), (0, 2, 0), (1, 2, 0), (0, 2, 1), (1, 2, 1)):
+        for dg, tm, tp, tf in ((0, 0, 0, 1), (1, 0, 0, 1), (0, 2, 0, 0), (1, 2, 0, 0), (0, 2, 1, 0),
+                               (1, 2, 1, 0), (0, 2, 0, 1), (1, 2, 0, 1)):
             call("pamg_set_option", b"col_dict", 1)
             call("pamg_set_option", b"jacobi_diag", dg)
             call("pamg_set_option", b"tile_major", tm)
             call("pamg_set_option", b"tm_persist", tp)
+            call("pamg_set_option", b"tm_flags", tf)
             A, _h = upload(ctx, M)
             if not tm:
                 assert (A.stream_bytes < plain) == (distinct <= 256), (A.stream_bytes, plain, distinct)
             lay = layout_of(A)
-            assert lay["tm"] == bool(tm)
+            assert lay["tm"] == bool(tm) and lay["tm_flags"] == bool(tm and tf)
             assert lay["cd"] == (4 if distinct <= 16 else 8 if distinct <= 256 else 0), (lay, distinct)
             assert lay["cd_offsets"] == (distinct if distinct <= 256 else 0)
             xh, bh = rng.standard_normal(n), rng.standard_normal(n)
@@ -396,7 +403,16 @@ def test_stream_bytes_layout(ctx):
     A, _h = upload(ctx, M)
     lay = layout_of(A)
     assert lay["tm"] and lay["cd"] == 4 and 0 < lay["tm_rs"] <= 256 and lay["tm_rs"] % 4 == 0
+    assert not lay["tm_flags"]
     assert A.stream_bytes == nt * (lay["tm_rs"] + 8 * 1024 + 512 + 16) + 4 * 7 + 4
+    # variant 4f: row bounds as 128 flag bytes + 4 two-byte chunk bases per 1024-position slot
+    call("pamg_set_option", b"tm_flags", 1)
+    try:
+        A, _h = upload(ctx, M)
+    finally:
+        call("pamg_set_option", b"tm_flags", 0)
+    assert layout_of(A)["tm_flags"]  # every row of the grid operator is non-empty
+    assert A.stream_bytes == nt * (128 + 8 + 8 * 1024 + 512 + 16) + 4 * 7 + 4
 
 
 @pytest.mark.parametrize("seed,n,density,weak,iso", [(1, 3000, 0.003, 0.3, 0.02), (2, 5000, 0.001, 0.0, 0.0),
