@@ -213,6 +213,15 @@ def main():
         rec = [r for r in json.load(open(pmc)) if r["kernel"] == kname]
         if rec:
             traffic, traffic_src = float(rec[0]["traffic_bytes"]), os.path.relpath(pmc, ROOT)
+    # the fine SpMV's HBM rate from its committed PMC record (same workload and layout)
+    spmv_traffic_gbps = None
+    pmc_s = os.path.join(ROOT, "profiles", "r01_pmc", "traffic_spmv_512.json")
+    if (not args.matrix and args.kind == "poisson3d" and args.grid == 512 and world == 1
+            and os.path.exists(pmc_s)):
+        sname = kname.replace("<2,", "<0,", 1)
+        rec = [r for r in json.load(open(pmc_s)) if r["kernel"] == sname]
+        if rec:
+            spmv_traffic_gbps = round(float(rec[0]["traffic_bytes"]) / (spmv_ms * 1e-3) / 1e9, 1)
 
     # fine-level nonzeros of the whole problem (every rank holds only its own rows)
     nnz_fine = (sum(be.allgather({rank: int(H.levels[0][rank].A.nnz)})) if world > 1
@@ -248,6 +257,8 @@ def main():
             },
             "fine_spmv_GBps": round(spmv_gbps, 1),
             "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
+            # HBM bytes actually moved (PMC, profiles/r01_pmc) per second of the same launch
+            "fine_spmv_traffic_GBps": spmv_traffic_gbps,
             "roofline": {
                 "kernel": kname + " (level-0 post-smoothing Jacobi"
                           + (", tile-major slots" if tm else "")
