@@ -397,14 +397,23 @@ __global__ __launch_bounds__(BS) void k_rows_tile2(
 // (16-bit low + 8-bit high) offset. Rows: one per lane, starts by a wave scan of the lengths;
 // positions are tile-relative (no alignment head: a tile's slot starts at its first nonzero).
 // Summation order, epilogues and Jacobi's in-tile diagonal are variant 1's (SPEC §S3).
-template <int OP, int TNNZ, int CD>
+// x prefetch (dictionary sets, pf_lo/pf_hi != 0): the tile's rows read x at row + offset for
+// the set's offsets, so the lines of its farthest neighbours — [r0 + pf_lo, r0 + pf_lo + nr)
+// and [r0 + pf_hi, ...), the grid planes below and above — are known from the descriptor.
+// A few lanes load one word per 128-B line of both ranges at entry, beside the stream: the
+// first touch of the plane above (a compulsory HBM miss) and the re-read of the plane below
+// (evicted from L2 two plane slices ago) then overlap the stream instead of following it in
+// the gather phase. The loaded words feed a never-taken store (poison is NaN) so the loads
+// are kept; any index is clamped into [0, xlen).
+template <int OP, int TNNZ, int CD, bool TR = false>
 __global__ __launch_bounds__(kBlock) void k_rows_tm(
     const int4* __restrict__ tiles, const double* __restrict__ tval,
     const uint8_t* __restrict__ tcidx, const uint16_t* __restrict__ tclo,
     const uint8_t* __restrict__ tchi, const int* __restrict__ tbase,
     const uint8_t* __restrict__ trlen, int rs, const int* __restrict__ ctab, int ctab_n,
     const double* __restrict__ x, const double* __restrict__ b, double* __restrict__ y,
-    double omega, const double* __restrict__ diag) {
+    double omega, const double* __restrict__ diag, int pf_lo = 0, int pf_hi = 0, int xlen = 0,
+    double poison = 0.0) {
     constexpr int BS = kBlock;
     constexpr int G = TNNZ / (4 * BS);
     static_assert(G >= 1 && TNNZ % (4 * BS) == 0, "tile budget must be a multiple of 4 x block");
@@ -415,6 +424,12 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     __shared__ __attribute__((aligned(4))) uint8_t lrow[TNNZ + 8];
 
     const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    // slot position of this lane's e-th nonzero in group j: four consecutive positions per
+    // lane (16-B loads), or TR: lane-consecutive positions per gather instruction (8-B loads;
+    // an instruction's 64 gathers then come from ~9 rows instead of ~36: fewer x lines)
+    auto pos = [&](int j, int e) {
+        return TR ? 4 * (j * BS + 64 * (tid >> 6)) + 64 * e + lane : 4 * (tid + j * BS) + e;
+    };
     const int4 d = tiles[t];
     const size_t sb = (size_t)t * TNNZ;
     double2 va[G], vb[G];
@@ -425,6 +440,29 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     // the whole slot is loaded at entry (padding included: a load that waits for the
     // descriptor's nonzero count brings its round trip back — measured 2-15 % slower)
     auto load = [&](int j) {
+        if constexpr (TR) {
+            double v[4];
+            uint32_t c = 0;
+            uint16_t l[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const size_t g = sb + pos(j, e);
+                v[e] = tval[g];
+                if constexpr (CD == 4) {
+                    c |= (uint32_t)((tcidx[g >> 1] >> (4 * (g & 1))) & 15u) << (4 * e);
+                } else if constexpr (CD == 8) {
+                    c |= (uint32_t)tcidx[g] << (8 * e);
+                } else {
+                    l[e] = tclo[g];
+                    c |= (uint32_t)tchi[g] << (8 * e);
+                }
+            }
+            va[j] = make_double2(v[0], v[1]);
+            vb[j] = make_double2(v[2], v[3]);
+            cn[j] = c;
+            clo4[j] = make_ushort4(l[0], l[1], l[2], l[3]);
+            return;
+        }
         const size_t q = sb + 4 * (tid + j * BS);
         va[j] = *reinterpret_cast<const double2*>(tval + q);
         vb[j] = *reinterpret_cast<const double2*>(tval + q + 2);
@@ -451,6 +489,18 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     }
     if (lane == 63) lwt[tid >> 6] = rl_inc;
     const int r0 = d.x, nr = d.y - d.x, cnt = d.w - d.z;
+    double touch = 0.0;
+    if constexpr (CD != 0) {
+        if (pf_hi != 0) {
+            const int nl = (nr + 15) / 16 + 1;  // 128-B lines of one nr-row range
+            if (tid < 2 * nl) {
+                const int base = r0 + (tid < nl ? pf_lo : pf_hi);
+                int i = base + 16 * (tid < nl ? tid : tid - nl);
+                i = i < 0 ? 0 : (i >= xlen ? xlen - 1 : i);
+                touch = x[i];
+            }
+        }
+    }
     double pb = 0.0, px = 0.0, py = 0.0, pd = 0.0;
     if (tid < nr) {
         const int r = r0 + tid;
@@ -487,7 +537,15 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
 #pragma unroll
     for (int j = 0; j < G; ++j) {
         const int q = 4 * (tid + j * BS);
-        const uint32_t rw = NEED_ROWS && q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
+        uint32_t rw = 0u;
+        if constexpr (NEED_ROWS) {
+            if constexpr (TR) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) rw |= (uint32_t)lrow[pos(j, e)] << (8 * e);
+            } else {
+                rw = q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
+            }
+        }
         if constexpr (CD == 0) {
             const uint16_t l4[4] = {clo4[j].x, clo4[j].y, clo4[j].z, clo4[j].w};
 #pragma unroll
@@ -501,25 +559,38 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
             }
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) xv[j][e] = x[q + e < cnt ? cc[j][e] : 0];
+        for (int e = 0; e < 4; ++e) xv[j][e] = x[pos(j, e) < cnt ? cc[j][e] : 0];
     }
 #pragma unroll
     for (int j = 0; j < G; ++j) {
         const int q = 4 * (tid + j * BS);
-        const uint32_t rw = NEED_ROWS && q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
+        uint32_t rw = 0u;
+        if constexpr (NEED_ROWS) {
+            if constexpr (TR) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) rw |= (uint32_t)lrow[pos(j, e)] << (8 * e);
+            } else {
+                rw = q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
+            }
+        }
         const double vv[4] = {va[j].x, va[j].y, vb[j].x, vb[j].y};
         double p[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const bool ok = q + e < cnt;
+            const bool ok = pos(j, e) < cnt;
             p[e] = ok ? vv[e] * xv[j][e] : 0.0;
             if constexpr (OP == OP_JACOBI) {
                 const int rl = (int)((rw >> (8 * e)) & 255u);
                 if (!diag && ok && cc[j][e] - r0 == rl) ldiag[rl] = vv[e];
             }
         }
-        *reinterpret_cast<double2*>(&lprod[q]) = make_double2(p[0], p[1]);
-        *reinterpret_cast<double2*>(&lprod[q + 2]) = make_double2(p[2], p[3]);
+        if constexpr (TR) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) lprod[pos(j, e)] = p[e];
+        } else {
+            *reinterpret_cast<double2*>(&lprod[q]) = make_double2(p[0], p[1]);
+            *reinterpret_cast<double2*>(&lprod[q + 2]) = make_double2(p[2], p[3]);
+        }
     }
     __syncthreads();
     if constexpr (!NEED_ROWS) re = row_end();
@@ -539,6 +610,9 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
         } else {
             y[r] = py + s;
         }
+    }
+    if constexpr (CD != 0) {
+        if (touch == poison) y[0] = touch;  // never: poison is NaN (keeps the prefetch loads)
     }
 }
 
@@ -1294,14 +1368,30 @@ void launch_tile2(const pamg_mat& A, const TileSet& ts, const double* x, const d
         }
     } else if (ts.tm) {
         if constexpr (TROWS <= kBlock) {
-            if (ts.cd == 4)
+            const int plo = A.x_prefetch ? ts.cd_min : 0, phi = A.x_prefetch ? ts.cd_max : 0;
+            const int xl = (int)A.ncols;
+            const double nan = __builtin_nan("");
+            if (A.tm_transpose) {
+                if (ts.cd == 4)
+                    k_rows_tm<OP, TNNZ, 4, true><<<ts.n_short, kBlock, 0, s>>>(
+                        ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr, nullptr, ts.d_tm_rlen,
+                        ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y, omega, dg, plo, phi, xl, nan);
+                else if (ts.cd == 8)
+                    k_rows_tm<OP, TNNZ, 8, true><<<ts.n_short, kBlock, 0, s>>>(
+                        ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr, nullptr, ts.d_tm_rlen,
+                        ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y, omega, dg, plo, phi, xl, nan);
+                else
+                    k_rows_tm<OP, TNNZ, 0, true><<<ts.n_short, kBlock, 0, s>>>(
+                        ts.d_short, ts.d_tm_val, nullptr, ts.d_tm_clo, ts.d_tm_chi, ts.d_base, ts.d_tm_rlen,
+                        ts.tm_rs, nullptr, 0, x, b, y, omega, dg);
+            } else if (ts.cd == 4)
                 k_rows_tm<OP, TNNZ, 4><<<ts.n_short, kBlock, 0, s>>>(
                     ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr, nullptr, ts.d_tm_rlen,
-                    ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y, omega, dg);
+                    ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y, omega, dg, plo, phi, xl, nan);
             else if (ts.cd == 8)
                 k_rows_tm<OP, TNNZ, 8><<<ts.n_short, kBlock, 0, s>>>(
                     ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr, nullptr, ts.d_tm_rlen,
-                    ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y, omega, dg);
+                    ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y, omega, dg, plo, phi, xl, nan);
             else
                 k_rows_tm<OP, TNNZ, 0><<<ts.n_short, kBlock, 0, s>>>(
                     ts.d_short, ts.d_tm_val, nullptr, ts.d_tm_clo, ts.d_tm_chi, ts.d_base, ts.d_tm_rlen,

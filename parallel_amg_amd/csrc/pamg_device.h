@@ -49,6 +49,7 @@ struct TileSet {
     int cd = 0;
     int* d_ctab = nullptr;
     int ctab_n = 0;
+    int cd_min = 0, cd_max = 0;  // smallest / largest offset of the table (x prefetch ranges)
     // tile-major copies (Options::tile_major; kernels.hip k_rows_tm): tile t's values and
     // column stream at t * tile_nnz, its row lengths at t * tm_rs, zero-padded
     bool tm = false;
@@ -85,6 +86,8 @@ struct Options {
     int tile_major = 1;        // tile-major padded copies (variant 4): 1 where measured faster, 2 all eligible
     int tm_persist = 0;        // 1: tile-major sets run the persistent prefetching variant 4p
     int tm_flags = 0;          // 1: row-start flags (one-barrier variant 4f; measured slower, A/B)
+    int x_prefetch = 0;        // 1: dictionary tile-major tiles touch their far x lines at entry (A/B: no gain)
+    int tm_transpose = 0;      // 1: tile-major gathers in lane-consecutive positions (fewer x lines each)
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };
 Options& options();
@@ -146,6 +149,8 @@ struct pamg_mat {
     int jacobi_diag = 0;
     int stream_nt = 0;
     int tm_persist = 0;
+    int x_prefetch = 0;
+    int tm_transpose = 0;
 };
 
 namespace pamg {

@@ -295,6 +295,8 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
         CHECK(dalloc(&ts->d_ctab, (int64_t)tab256.size()));
         HIPC(hipMemcpy(ts->d_ctab, tab256.data(), sizeof(int) * tab256.size(), hipMemcpyHostToDevice));
         ts->ctab_n = (int)tab[q].size();
+        ts->cd_min = *std::min_element(tab[q].begin(), tab[q].end());
+        ts->cd_max = *std::max_element(tab[q].begin(), tab[q].end());
         ts->cd = width;
         ts->rl8 = true;
     }
@@ -427,7 +429,7 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_base);
     dfree(ts.d_vtab);
     dfree(ts.d_ctab);
-    ts.cd = ts.ctab_n = 0;
+    ts.cd = ts.ctab_n = ts.cd_min = ts.cd_max = 0;
     dfree(ts.d_tm_val);
     dfree(ts.d_tm_cidx);
     dfree(ts.d_tm_clo);
@@ -1013,6 +1015,8 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     A->jacobi_diag = pamg::options().jacobi_diag;
     A->stream_nt = pamg::options().stream_nt;
     A->tm_persist = pamg::options().tm_persist;
+    A->x_prefetch = pamg::options().x_prefetch;
+    A->tm_transpose = pamg::options().tm_transpose;
     A->nrows = nrows;
     A->ncols = ncols;
     A->nnz = nnz;
@@ -1587,6 +1591,8 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "tile_major" && value >= 0 && value <= 2) o.tile_major = (int)value;
     else if (k == "tm_persist" && (value == 0 || value == 1)) o.tm_persist = (int)value;
     else if (k == "tm_flags" && (value == 0 || value == 1)) o.tm_flags = (int)value;
+    else if (k == "x_prefetch" && (value == 0 || value == 1)) o.x_prefetch = (int)value;
+    else if (k == "tm_transpose" && (value == 0 || value == 1)) o.tm_transpose = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -1627,6 +1633,8 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "tile_major") *value = o.tile_major;
     else if (k == "tm_persist") *value = o.tm_persist;
     else if (k == "tm_flags") *value = o.tm_flags;
+    else if (k == "x_prefetch") *value = o.x_prefetch;
+    else if (k == "tm_transpose") *value = o.tm_transpose;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

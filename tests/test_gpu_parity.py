@@ -87,12 +87,18 @@ TILE_CONFIGS = [c + (0,) for c in TILE_CONFIGS] + [(1, 1024, 256, 0, 0, 0, 1, 1,
                                                    (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1, 1, 2, 0, 1),
                                                    (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 0, 1),
                                                    (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 0, 2, 0, 1)]
+# + x_prefetch, tm_transpose (last two columns): the variant 4 A/B forms
+TILE_CONFIGS = [c + (0, 0) for c in TILE_CONFIGS] + [(1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 0, 0, 1, 1),
+                                                      (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1, 1, 2, 0, 0, 0, 1),
+                                                      (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 0, 0, 1, 1),
+                                                      (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 0, 2, 0, 0, 0, 1)]
 OPT_KEYS = ("rows_kernel", "tile_nnz", "tile_rows", "xcd_remap", "jacobi_diag", "stream_nt", "tile_order",
-            "col24", "value_dict", "long_tiles", "row_len8", "col_dict", "tile_major", "tm_persist", "tm_flags")
+            "col24", "value_dict", "long_tiles", "row_len8", "col_dict", "tile_major", "tm_persist", "tm_flags",
+            "x_prefetch", "tm_transpose")
 
 
 @pytest.fixture(params=TILE_CONFIGS,
-                ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}_lt{}_rl{}_cd{}_tm{}_tp{}_tf{}".format(*c))
+                ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}_lt{}_rl{}_cd{}_tm{}_tp{}_tf{}_xp{}_tt{}".format(*c))
 def tile_cfg(request, built):
     import ctypes
     from parallel_amg_amd._lib import call
@@ -204,7 +210,7 @@ def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
         offs = offs[offs != 0][:ndist]
     M = offset_csr(rng, n, offs, lengths)
     distinct = len(np.unique(M.col - np.repeat(np.arange(n), np.diff(M.rowptr))))
-    keys = ("col_dict", "tile_nnz", "jacobi_diag", "tile_major", "tm_persist", "tm_flags")
+    keys = ("col_dict", "tile_nnz", "jacobi_diag", "tile_major", "tm_persist", "tm_flags", "tm_transpose")
     old = []
     for k in keys:
         v = ctypes.c_int64()
@@ -215,13 +221,15 @@ def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
         call("pamg_set_option", b"col_dict", 0)
         call("pamg_set_option", b"tile_major", 0)
         plain = upload(ctx, M)[0].stream_bytes
-        for dg, tm, tp, tf in ((0, 0, 0, 1), (1, 0, 0, 1), (0, 2, 0, 0), (1, 2, 0, 0), (0, 2, 1, 0),
-                               (1, 2, 1, 0), (0, 2, 0, 1), (1, 2, 0, 1)):
+        for dg, tm, tp, tf, tt in ((0, 0, 0, 1, 0), (1, 0, 0, 1, 0), (0, 2, 0, 0, 0), (1, 2, 0, 0, 0),
+                                   (0, 2, 1, 0, 0), (1, 2, 1, 0, 0), (0, 2, 0, 1, 0), (1, 2, 0, 1, 0),
+                                   (0, 2, 0, 0, 1), (1, 2, 0, 0, 1)):
             call("pamg_set_option", b"col_dict", 1)
             call("pamg_set_option", b"jacobi_diag", dg)
             call("pamg_set_option", b"tile_major", tm)
             call("pamg_set_option", b"tm_persist", tp)
             call("pamg_set_option", b"tm_flags", tf)
+            call("pamg_set_option", b"tm_transpose", tt)
             A, _h = upload(ctx, M)
             if not tm:
                 assert (A.stream_bytes < plain) == (distinct <= 256), (A.stream_bytes, plain, distinct)
