@@ -15,6 +15,16 @@
 //   phase 2  one lane per row adds its products from LDS in storage order and applies the
 //            epilogue (SpMV / residual / Jacobi / prolongate-add), coalesced stores.
 // Rows longer than the tile budget go to k_rows_long (one workgroup per row, chunked).
+//
+// Variants of that tile body (pamg_set_option; the upload fixes the layout per tile set,
+// launch_tile2 picks the kernel; every variant is bit-identical, tests/test_gpu_parity.py):
+//   0  k_rows_tile    row pointers first, then the stream (first version)
+//   1  k_rows_tile2   descriptor-driven: the stream is issued at entry from the tile's nonzero
+//                     range; 24-bit columns, 8-bit row lengths, column / value dictionaries
+//   4  k_rows_tm      tile-major slots: every pre-gather load addressed by tile index alone
+//                     (default for dictionary sets and slot-filling non-square operators)
+//   2, 3, 4p, 4f      wave tiles, persistent grids, one-barrier row flags: measured slower,
+//                     kept for A/B ("Measured and rejected")
 #include <type_traits>
 
 #include "pamg_device.h"
