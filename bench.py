@@ -200,7 +200,7 @@ def main():
     lay = _lib.layout_of(A0)
     c24, vd, rl8, cd, tm = lay["c24"], lay["vd"], lay["rl8"], lay["cd"], lay["tm"]
     tn = lay["tile_nnz"]
-    kname = (f"k_rows_tm<2, {tn}, {cd}>" if tm
+    kname = (f"k_rows_tm<2, {tn}, {cd}, false>" if tm
              else f"k_rows_tile2<2, {tn}, 256, false, false, 256, false, false, true, {cd}>" if cd
              else f"k_rows_tile2<2, {tn}, 256, false, false, 256, true, true>" if vd
              else f"k_rows_tile2<2, {tn}, 256, false, false, 256, true, false, true>" if rl8
