@@ -423,7 +423,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     const uint8_t* __restrict__ trlen, int rs, const int* __restrict__ ctab, int ctab_n,
     const double* __restrict__ x, const double* __restrict__ b, double* __restrict__ y,
     double omega, const double* __restrict__ diag, int pf_lo = 0, int pf_hi = 0, int xlen = 0,
-    double poison = 0.0) {
+    double poison = __builtin_nan("")) {
     constexpr int BS = kBlock;
     constexpr int G = TNNZ / (4 * BS);
     static_assert(G >= 1 && TNNZ % (4 * BS) == 0, "tile budget must be a multiple of 4 x block");
