@@ -61,7 +61,13 @@ int pamg_device_sync(int device);
 /* RCCL communicator for multi-part runs: rank 0 calls pamg_comm_unique_id, the 128 bytes are
  * broadcast by the host layer (MPI / torch.distributed), then every rank calls pamg_comm_init. */
 int pamg_comm_unique_id(unsigned char id[128]);
+/* Fails with PAMG_E_RCCL (message names the library file) when the RCCL the process bound
+ * is older than the one libpamg was built against — e.g. a host that loaded the torch
+ * wheel's bundled RCCL 2.26 before libpamg. */
 int pamg_comm_init(pamg_ctx* ctx, int nranks, int rank, const unsigned char id[128]);
+/* HIP runtime / RCCL versions this process resolved, beside the versions libpamg was built
+ * against (HIP_VERSION, NCCL_VERSION_CODE). Any pointer may be NULL. */
+int pamg_runtime_versions(int* hip_runtime, int* hip_built, int* rccl_runtime, int* rccl_built);
 int pamg_comm_rank(const pamg_ctx* ctx, int* rank, int* nranks);
 /* Debug transport (PartitionedArrays' debug-backend role): instead of RCCL, every exchange is
  * staged through host buffers and handed to `fn` (synchronously, no overlap). Lets several
@@ -117,7 +123,8 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * out[0] 24-bit columns, out[1] value dictionary, out[2] 8-bit row lengths,
  * out[3] column-dictionary index width (0, 4 or 8), out[4] column-dictionary offsets,
  * out[5] tile-major padded copy, out[6] its row-length slot per tile, out[7] the tile
- * budget (nonzeros per tile) the set was cut with, out[8] row-start flags (variant 4f). */
+ * budget (nonzeros per tile) the set was cut with, out[8] the number of short tiles (the
+ * grid of the set's tile kernel). */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[9]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
@@ -174,9 +181,10 @@ int pamg_hier_profile_read(pamg_hier* H, double* ms_per_level_op /* nlevels*6 */
 int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, const pamg_vec* b,
                      pamg_vec* y, double omega, int reps, double* avg_ms);
 
-/* Process-wide knobs. Applied to later pamg_mat_upload calls: "rows_kernel" (0..3, kernel
- * variant), "tile_nnz" / "tile_rows" (tile budget; the valid pairs per variant are checked),
- * "xcd_remap", "jacobi_diag", "stream_nt", "tile_order" (0 | 1 | 2 | 4 | 8 | 16). Applied at every exchange:
+/* Process-wide knobs. Applied to later pamg_mat_upload calls: "tile_nnz" (1024 | 2048 | 4096,
+ * nonzero budget of a 256-row tile), "tile_order" (0 natural | 1 banded XCD-blocked), "col24",
+ * "long_tiles", "row_len8", "value_dict", "col_dict" (0 | 1 layout features), "tile_major"
+ * (0 | 1 where measured faster | 2 every eligible set). Applied at every exchange:
  * "poison_ghosts" (0 | 1, debug: NaN-fill the ghost slots before each exchange). */
 int pamg_set_option(const char* key, int64_t value);
 int pamg_get_option(const char* key, int64_t* value);

@@ -42,6 +42,7 @@ SIGNATURES = {
     "pamg_comm_unique_id": [C.c_char_p],
     "pamg_comm_init": [vp, i32, i32, C.c_char_p],
     "pamg_comm_rank": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
+    "pamg_runtime_versions": [C.POINTER(C.c_int)] * 4,
     "pamg_comm_init_host": [vp, i32, i32, vp, vp],
     "pamg_plan_create": [vp, i64, i64, i32, vp, vp, vp, vp, pvp],
     "pamg_plan_destroy": [vp],
@@ -166,7 +167,7 @@ def layout_of(M, part_set: int = 0) -> dict:
     call("pamg_mat_layout", M.handle, part_set, out)
     return {"c24": bool(out[0]), "vd": bool(out[1]), "rl8": bool(out[2]), "cd": int(out[3]),
             "cd_offsets": int(out[4]), "tm": bool(out[5]), "tm_rs": int(out[6]),
-            "tile_nnz": int(out[7]), "tm_flags": bool(out[8])}
+            "tile_nnz": int(out[7]), "tiles": int(out[8])}
 
 
 def last_error() -> str:

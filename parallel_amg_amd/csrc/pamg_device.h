@@ -12,12 +12,11 @@
 
 namespace pamg {
 
-// Row tiles of the LDS-staged CSR kernel (kernels.hip): each tile is a run of <= kTileRows
-// consecutive rows holding <= kTileNnz nonzeros; a row longer than kTileNnz is a tile of its
-// own in the "long" list.
+// Row tiles of the LDS-staged CSR kernels (kernels.hip): each tile is a run of <= kTileRows
+// consecutive rows (one per lane of the 256-thread workgroup) holding <= tile_nnz nonzeros;
+// a row longer than the budget is a tile of its own in the "long" list.
 constexpr int kBlock = 256;
 constexpr int kTileRows = 256;
-constexpr int kTileNnz = 2048;
 
 enum RowOp : int {
     OP_SPMV = 0,     // y = A x
@@ -31,7 +30,7 @@ struct TileSet {
     int n_short = 0;
     int* d_long = nullptr;  // single rows
     int n_long = 0;
-    int tile_nnz = kTileNnz, tile_rows = kTileRows;  // budget the tiles were cut with
+    int tile_nnz = 1024;  // nonzero budget the tiles were cut with
     // 24-bit column stream: every tile's columns lie in [base, base + 2^24), so a column is
     // stored as base (per tile) + 16-bit low part (pamg_mat::d_clo) + 8-bit high part (d_chi)
     int* d_base = nullptr;  // per short tile (same order as d_short), when c24
@@ -41,7 +40,7 @@ struct TileSet {
     double* d_vtab = nullptr;  // 16 per short tile
     bool vd = false;
     // 8-bit row lengths (pamg_mat::d_rlen) instead of row pointers: every row of a short tile
-    // has <= 255 nonzeros (variant 1, one row per lane, 24-bit columns, plain values)
+    // has <= 255 nonzeros (one row per lane, 24-bit columns, plain values)
     bool rl8 = false;
     // column dictionary (Options::col_dict; needs rl8): every nonzero of the short tiles has
     // column = row + d_ctab[i] for one of the set's <= 16 (cd = 4 bits) / <= 256 (cd = 8)
@@ -49,7 +48,6 @@ struct TileSet {
     int cd = 0;
     int* d_ctab = nullptr;
     int ctab_n = 0;
-    int cd_min = 0, cd_max = 0;  // smallest / largest offset of the table (x prefetch ranges)
     // tile-major copies (Options::tile_major; kernels.hip k_rows_tm): tile t's values and
     // column stream at t * tile_nnz, its row lengths at t * tm_rs, zero-padded
     bool tm = false;
@@ -59,9 +57,6 @@ struct TileSet {
     uint16_t* d_tm_clo = nullptr;  // or 24-bit columns: low 16 bits
     uint8_t* d_tm_chi = nullptr;   //   high 8 bits
     uint8_t* d_tm_rlen = nullptr;
-    bool tm_flags = false;         // variant 4f: row-start bits + per-chunk row bases
-    uint8_t* d_tm_flag = nullptr;  // tile_nnz / 8 bytes per tile
-    uint16_t* d_tm_wb = nullptr;   // tile_nnz / 256 entries per tile (rows begun before a chunk)
     int max_short_len = 0;    // longest row in a short tile
     int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
@@ -70,13 +65,8 @@ struct TileSet {
 // Tuning knobs (pamg_set_option): kernel variant and tile budget used by later uploads.
 struct Options {
     // defaults = fastest measured on MI355X at 512^3 (profiles/r01_kbench_*.jsonl):
-    // variant 1 with 1024-nonzero / 256-row tiles
-    int rows_kernel = 1;       // 0: rowptr-first tile, 1: descriptor-driven tile, 2: wave tiles
-    int tile_nnz = 1024;       // 256 / 512 / 1024 / 2048 / 4096
-    int tile_rows = kTileRows; // 64 / 256 / 512
-    int xcd_remap = 0;         // 1: contiguous tile chunks per XCD
-    int jacobi_diag = 0;       // 1: Jacobi reads the stored diagonal (no in-tile detection)
-    int stream_nt = 0;         // 1: non-temporal loads for the matrix stream (variant 1)
+    // 1024-nonzero / 256-row tiles
+    int tile_nnz = 1024;       // 1024 / 2048 / 4096 (tiles always hold <= kTileRows rows)
     int tile_order = 1;        // 1: banded XCD-blocked tile order (see build_tiles)
     int col24 = 1;             // 1: 3-byte column stream where every tile's span fits 2^24
     int long_tiles = 1;        // 1: 4096-nonzero tiles for operators averaging >= 48 nnz/row
@@ -84,10 +74,6 @@ struct Options {
     int value_dict = 0;        // 1 (opt-in): 4-bit per-tile value dictionaries where they fit
     int col_dict = 1;          // 1: row-relative column dictionaries (4/8-bit) where they fit
     int tile_major = 1;        // tile-major padded copies (variant 4): 1 where measured faster, 2 all eligible
-    int tm_persist = 0;        // 1: tile-major sets run the persistent prefetching variant 4p
-    int tm_flags = 0;          // 1: row-start flags (one-barrier variant 4f; measured slower, A/B)
-    int x_prefetch = 0;        // 1: dictionary tile-major tiles touch their far x lines at entry (A/B: no gain)
-    int tm_transpose = 0;      // 1: tile-major gathers in lane-consecutive positions (fewer x lines each)
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };
 Options& options();
@@ -144,13 +130,6 @@ struct pamg_mat {
     pamg::TileSet interior;  // rows with own columns only (overlap with the exchange)
     pamg::TileSet boundary;  // rows with >= 1 ghost column
     int64_t stream_bytes = 0;  // matrix bytes one apply reads (values, columns, row pointers, tiles)
-    int rows_kernel = 1;     // variant fixed at upload (pamg::Options)
-    int xcd_remap = 0;
-    int jacobi_diag = 0;
-    int stream_nt = 0;
-    int tm_persist = 0;
-    int x_prefetch = 0;
-    int tm_transpose = 0;
 };
 
 namespace pamg {

@@ -3,6 +3,8 @@
 // layout), device vectors and matrices, mul!/residual/Jacobi with the ghost exchange
 // overlapped with the interior rows, and the V-cycle driver (SPEC.md §S6) replayed as a
 // captured hipGraph.
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cstring>
 #include <map>
@@ -65,26 +67,17 @@ int set_device(const pamg_ctx* ctx) {
 }
 
 // Greedy tiling of the rows listed in `rows` (ascending) into runs of consecutive rows with
-// <= kTileRows rows and <= kTileNnz nonzeros; rows above the budget become "long" rows.
+// <= kTileRows rows and <= tile_nnz nonzeros; rows above the budget become "long" rows.
 // tile_order 1 (banded XCD-blocked order) for a square matrix of half-bandwidth `band`:
 // cut the rows into super-rows of `band` rows (one grid plane for the stencils), give XCD k
 // the k-th eighth of every super-row, and interleave the 8 sequences so block b (XCD b % 8,
 // as dispatch is observed to deal blocks) walks its eighth plane after plane. The x lines of
 // rows z-1, z, z+1 of one eighth then stay in that XCD's L2. Speed only: any order is correct.
-// split > 1: each XCD's eighth is cut again into `split` sub-slabs, and the XCD walks the
-// first sub-slab through all super-rows, then the second, ... so that the rows read again by
-// the next super-row (z+1) come back after 1/split of a plane eighth of stream instead of a
-// whole one (restriction rows read four fine planes; a plane eighth of R0 is ~2.9 MB of
-// stream, close to the 4 MB L2), at the price of a y-halo per sub-slab.
-static std::vector<int4> xcd_band_order(const std::vector<int4>& tiles, int64_t band, int split = 1) {
+// (Cutting each eighth into sub-slabs walked one after another was measured slower on every
+// operator and removed: DESIGN.md "Measured and rejected".)
+static std::vector<int4> xcd_band_order(const std::vector<int4>& tiles, int64_t band) {
     std::vector<std::vector<int4>> bucket(8);
-    std::vector<std::vector<std::vector<int4>>> sub(8, std::vector<std::vector<int4>>(split));
-    for (const auto& t : tiles) {
-        const int64_t q = ((int64_t)(t.x % band) * 8 * split) / band;
-        sub[q / split][q % split].push_back(t);
-    }
-    for (int k = 0; k < 8; ++k)
-        for (auto& v : sub[k]) bucket[k].insert(bucket[k].end(), v.begin(), v.end());
+    for (const auto& t : tiles) bucket[((int64_t)(t.x % band) * 8) / band].push_back(t);
     size_t m = 0;
     for (auto& b : bucket) m = std::max(m, b.size());
     std::vector<int4> out;
@@ -135,19 +128,19 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
                 std::vector<uint16_t>* lo, std::vector<uint8_t>* hi, const double* val,
                 std::vector<uint8_t>* vidx, std::vector<int4>* tiles_out) {
     const auto& opt = pamg::options();
-    int tnnz = opt.tile_nnz, trows = opt.tile_rows;
+    int tnnz = opt.tile_nnz;
+    const int trows = pamg::kTileRows;
     // long_tiles: operators with long rows (coarse A_l, R_l: >= 48 nonzeros per row on
     // average) take 4096-nonzero tiles instead of the default 1024 — their time goes into the
     // in-order add chain of each row (SPEC §S3), and a tile of 4x the rows runs 4x the chains
     // side by side (512^3: A2 0.139 -> 0.110 ms, R1 0.458 -> 0.439 ms,
     // profiles/r01_kbench_512_tnnz.jsonl); the 7- and 27-point levels keep 1024.
-    if (opt.long_tiles && opt.rows_kernel == 1 && tnnz == 1024 && trows == 256 && !rows.empty()) {
+    if (opt.long_tiles && tnnz == 1024 && !rows.empty()) {
         int64_t nz = 0;
         for (int r : rows) nz += rp[r + 1] - rp[r];
         if (nz >= 48 * (int64_t)rows.size()) tnnz = 4096;
     }
     ts->tile_nnz = tnnz;
-    ts->tile_rows = trows;
     std::vector<int4> tiles;
     std::vector<int> longr;
     size_t i = 0;
@@ -178,8 +171,7 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
         i = j;
     }
     for (int r : longr) ts->nnz_long += rp[r + 1] - rp[r];
-    if (opt.tile_order >= 1 && band >= 64 && tiles.size() >= 64)
-        tiles = xcd_band_order(tiles, band, band >= 64 * opt.tile_order ? opt.tile_order : 1);
+    if (opt.tile_order == 1 && band >= 64 && tiles.size() >= 64) tiles = xcd_band_order(tiles, band);
     ts->n_short = (int)tiles.size();
     ts->n_long = (int)longr.size();
     CHECK(dalloc(&ts->d_short, ts->n_short));
@@ -220,8 +212,7 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
     ts->vd = false;
     if (opt.value_dict && ts->c24 && val)
         CHECK(build_value_dict(tiles, val, ts, vidx, (ci.size() + 1) / 2 + 8));
-    ts->rl8 = opt.row_len8 && opt.rows_kernel == 1 && ts->c24 && !ts->vd && tnnz >= 1024 && trows <= pamg::kBlock &&
-              ts->max_short_len <= 255 && !opt.xcd_remap && !opt.stream_nt && ts->n_short > 0 &&
+    ts->rl8 = opt.row_len8 && ts->c24 && !ts->vd && ts->max_short_len <= 255 && ts->n_short > 0 &&
               ts->nnz_short <= 16 * ts->rows_short;
     // ^ short rows only: the 3 B/row saved are 3-8 % of a 4-7-nonzero row (A0 SpMV -2 %, P0
     //   -5..-8 %) but ~1 % of a 30-nonzero row, where the scan's latency costs more (R0, A1
@@ -252,8 +243,7 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
     std::vector<int> tab[2];
     for (int q = 0; q < 2; ++q) {
         pamg::TileSet* ts = sets[q];
-        if (!opt.col_dict || opt.rows_kernel != 1 || opt.xcd_remap || opt.stream_nt || ts->vd ||
-            ts->n_short == 0 || ts->tile_rows > pamg::kBlock || ts->max_short_len > 255)
+        if (!opt.col_dict || ts->vd || ts->n_short == 0 || ts->max_short_len > 255)
             continue;
         if (idx.empty()) idx.assign((size_t)A->nnz + kVecPad, 0);
         // open-addressing map offset -> table slot (1024 cells for <= 256 keys)
@@ -295,8 +285,6 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
         CHECK(dalloc(&ts->d_ctab, (int64_t)tab256.size()));
         HIPC(hipMemcpy(ts->d_ctab, tab256.data(), sizeof(int) * tab256.size(), hipMemcpyHostToDevice));
         ts->ctab_n = (int)tab[q].size();
-        ts->cd_min = *std::min_element(tab[q].begin(), tab[q].end());
-        ts->cd_max = *std::max_element(tab[q].begin(), tab[q].end());
         ts->cd = width;
         ts->rl8 = true;
     }
@@ -328,8 +316,7 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
     for (int q = 0; q < 2; ++q) {
         pamg::TileSet* ts = sets[q];
         ts->tm = false;
-        if (!opt.tile_major || opt.rows_kernel != 1 || opt.xcd_remap || opt.stream_nt || ts->vd ||
-            ts->n_short == 0 || ts->tile_rows > pamg::kBlock || ts->max_short_len > 255 ||
+        if (!opt.tile_major || ts->vd || ts->n_short == 0 || ts->max_short_len > 255 ||
             !(ts->cd || (ts->c24 && !lo.empty())) || (ts->cd && idx8.empty()) || !val)
             continue;
         // tile_major 1 (default): the sets where it measured faster at 512^3
@@ -386,39 +373,6 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
         }
         ts->tm_rs = rs;
         ts->tm = true;
-        // variant 4f: row-start flags (1 bit per slot position) + rows begun before every
-        // wave chunk (2 B per chunk of 256 positions), where no row of the set is empty
-        ts->tm_flags = false;
-        bool nonempty = opt.tm_flags != 0;
-        for (int64_t i = 0; i < nt && nonempty; ++i)
-            for (int r = tiles[i].x; r < tiles[i].y; ++r)
-                if (rp[r + 1] == rp[r]) {
-                    nonempty = false;
-                    break;
-                }
-        if (nonempty) {
-            const int nch = (int)(tn / 256);  // wave chunks per slot (4 per 1024 positions)
-            std::vector<uint8_t> tf((size_t)(nt * tn / 8 + kVecPad), 0);
-            std::vector<uint16_t> twb((size_t)(nt * nch + kVecPad), 0);  // 0..256 rows
-            for (int64_t i = 0; i < nt; ++i) {
-                const int4 t = tiles[i];
-                int64_t pos = 0;
-                int row = 0, ch = 0;
-                for (int r = t.x; r < t.y; ++r, ++row) {
-                    // chunks that begin at or before this row's start count the rows before it
-                    while (ch < nch && 256 * ch <= pos) twb[i * nch + ch++] = (uint16_t)row;
-                    const int64_t p = i * tn + pos;
-                    tf[p >> 3] |= (uint8_t)(1u << (p & 7));
-                    pos += rp[r + 1] - rp[r];
-                }
-                while (ch < nch) twb[i * nch + ch++] = (uint16_t)(t.y - t.x);
-            }
-            CHECK(dalloc(&ts->d_tm_flag, (int64_t)tf.size()));
-            HIPC(hipMemcpy(ts->d_tm_flag, tf.data(), tf.size(), hipMemcpyHostToDevice));
-            CHECK(dalloc(&ts->d_tm_wb, (int64_t)twb.size()));
-            HIPC(hipMemcpy(ts->d_tm_wb, twb.data(), sizeof(uint16_t) * twb.size(), hipMemcpyHostToDevice));
-            ts->tm_flags = true;
-        }
     }
     return PAMG_OK;
 }
@@ -429,15 +383,12 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_base);
     dfree(ts.d_vtab);
     dfree(ts.d_ctab);
-    ts.cd = ts.ctab_n = ts.cd_min = ts.cd_max = 0;
+    ts.cd = ts.ctab_n = 0;
     dfree(ts.d_tm_val);
     dfree(ts.d_tm_cidx);
     dfree(ts.d_tm_clo);
     dfree(ts.d_tm_chi);
     dfree(ts.d_tm_rlen);
-    dfree(ts.d_tm_flag);
-    dfree(ts.d_tm_wb);
-    ts.tm_flags = false;
     ts.tm = false;
     ts.tm_rs = 0;
     ts.c24 = ts.vd = ts.rl8 = false;
@@ -719,8 +670,6 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false)
 
 // ------------------------------------------------------------------ C-ABI
 
-static int check_tile_options(const pamg::Options& o);
-
 extern "C" {
 
 
@@ -786,9 +735,38 @@ int pamg_comm_unique_id(unsigned char id[128]) {
     return PAMG_OK;
 }
 
+int pamg_runtime_versions(int* hip_runtime, int* hip_built, int* rccl_runtime, int* rccl_built) {
+    int hv = 0, rv = 0;
+    HIPC(hipRuntimeGetVersion(&hv));
+    NCCLC(ncclGetVersion(&rv));
+    if (hip_runtime) *hip_runtime = hv;
+    if (hip_built) *hip_built = HIP_VERSION;
+    if (rccl_runtime) *rccl_runtime = rv;
+    if (rccl_built) *rccl_built = NCCL_VERSION_CODE;
+    return PAMG_OK;
+}
+
 int pamg_comm_init(pamg_ctx* ctx, int nranks, int rank, const unsigned char id[128]) {
     if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks)
         return fail(PAMG_E_ARG, "comm_init: bad args");
+    // The RCCL this process resolved librccl.so.1 to must be the one libpamg was compiled
+    // against or newer. A host that loaded another ROCm copy first (the torch wheel bundles
+    // HIP 7.0 + RCCL 2.26.6 under the same sonames) binds libpamg's RCCL calls to that older
+    // library and its HIP runtime; round 1 saw that combination segfault inside the first
+    // captured V-cycle ("Library load order"). Refuse it with an error instead.
+    {
+        int rv = 0;
+        NCCLC(ncclGetVersion(&rv));
+        if (rv < NCCL_VERSION_CODE) {
+            Dl_info di{};
+            const char* path = dladdr(reinterpret_cast<void*>(&ncclGetVersion), &di) && di.dli_fname
+                                   ? di.dli_fname : "?";
+            return fail(PAMG_E_RCCL,
+                        "comm_init: RCCL %d loaded from %s is older than the RCCL %d libpamg was built "
+                        "against; load libpamg before any other ROCm copy (e.g. before importing torch)",
+                        rv, path, NCCL_VERSION_CODE);
+        }
+    }
     CHECK(set_device(ctx));
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
@@ -993,7 +971,6 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     if (plan && plan->n_own + plan->n_ghost != ncols)
         return fail(PAMG_E_ARG, "mat_upload: ncols %lld != plan own+ghost %lld", (long long)ncols,
                     (long long)(plan->n_own + plan->n_ghost));
-    CHECK(check_tile_options(pamg::options()));
     CHECK(set_device(ctx));
     std::vector<int64_t> rp(nrows + 1);
     std::vector<int> ci(nnz + kVecPad, 0);
@@ -1010,13 +987,6 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     // released through pamg_mat_destroy on every error path (no device memory leaks)
     std::unique_ptr<pamg_mat, int (*)(pamg_mat*)> A(new pamg_mat, pamg_mat_destroy);
     A->ctx = ctx;
-    A->rows_kernel = pamg::options().rows_kernel;
-    A->xcd_remap = pamg::options().xcd_remap;
-    A->jacobi_diag = pamg::options().jacobi_diag;
-    A->stream_nt = pamg::options().stream_nt;
-    A->tm_persist = pamg::options().tm_persist;
-    A->x_prefetch = pamg::options().x_prefetch;
-    A->tm_transpose = pamg::options().tm_transpose;
     A->nrows = nrows;
     A->ncols = ncols;
     A->nnz = nnz;
@@ -1101,10 +1071,9 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         const int64_t ns = t->n_short, nz = t->nnz_short;
         int64_t b = 8 * (int64_t)t->n_long + 12 * t->nnz_long;
         const bool base = t->c24 && !t->cd;
-        if (t->tm) {  // whole padded slots: tile_nnz values + column entries + row bounds
-            // (tm_rs lengths, or tile_nnz/8 flag bytes + one byte per 256-position chunk)
+        if (t->tm) {  // whole padded slots: tile_nnz values + column entries + tm_rs lengths
             const int64_t tn = t->tile_nnz;
-            const int64_t rowb = t->tm_flags ? tn / 8 + 2 * (tn / 256) : t->tm_rs;
+            const int64_t rowb = t->tm_rs;
             b += ns * (rowb + 8 * tn + (t->cd ? t->cd * tn / 8 : 3 * tn) + 16 + (base ? 4 : 0)) +
                  (t->cd ? 4 * t->ctab_n : 0);
         } else {
@@ -1171,7 +1140,7 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[9]) {
     out[5] = t.tm;
     out[6] = t.tm_rs;
     out[7] = t.tile_nnz;
-    out[8] = t.tm_flags;
+    out[8] = t.n_short;
     return PAMG_OK;
 }
 
@@ -1573,15 +1542,8 @@ int pamg_set_option(const char* key, int64_t value) {
     if (!key) return fail(PAMG_E_ARG, "set_option: NULL key");
     auto& o = pamg::options();
     const std::string k(key);
-    if (k == "rows_kernel" && value >= 0 && value <= 3) o.rows_kernel = (int)value;
-    else if (k == "tile_nnz" && (value == 256 || value == 512 || value == 1024 || value == 2048 || value == 4096))
-        o.tile_nnz = (int)value;
-    else if (k == "tile_rows" && (value == 64 || value == 128 || value == 256 || value == 512)) o.tile_rows = (int)value;
-    else if (k == "xcd_remap" && (value == 0 || value == 1)) o.xcd_remap = (int)value;
-    else if (k == "jacobi_diag" && (value == 0 || value == 1)) o.jacobi_diag = (int)value;
-    else if (k == "stream_nt" && (value == 0 || value == 1)) o.stream_nt = (int)value;
-    else if (k == "tile_order" && (value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16))
-        o.tile_order = (int)value;  // 0 natural, 1 banded XCD-blocked, k > 1 banded with k sub-slabs per XCD
+    if (k == "tile_nnz" && (value == 1024 || value == 2048 || value == 4096)) o.tile_nnz = (int)value;
+    else if (k == "tile_order" && (value == 0 || value == 1)) o.tile_order = (int)value;  // 0 natural, 1 banded XCD-blocked
     else if (k == "poison_ghosts" && (value == 0 || value == 1)) o.poison_ghosts = (int)value;
     else if (k == "col24" && (value == 0 || value == 1)) o.col24 = (int)value;
     else if (k == "long_tiles" && (value == 0 || value == 1)) o.long_tiles = (int)value;
@@ -1589,27 +1551,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "value_dict" && (value == 0 || value == 1)) o.value_dict = (int)value;
     else if (k == "col_dict" && (value == 0 || value == 1)) o.col_dict = (int)value;
     else if (k == "tile_major" && value >= 0 && value <= 2) o.tile_major = (int)value;
-    else if (k == "tm_persist" && (value == 0 || value == 1)) o.tm_persist = (int)value;
-    else if (k == "tm_flags" && (value == 0 || value == 1)) o.tm_flags = (int)value;
-    else if (k == "x_prefetch" && (value == 0 || value == 1)) o.x_prefetch = (int)value;
-    else if (k == "tm_transpose" && (value == 0 || value == 1)) o.tm_transpose = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
-    return PAMG_OK;
-}
-
-// Kernel variants and the tile shapes they are instantiated for (kernels.hip dispatch).
-static int check_tile_options(const pamg::Options& o) {
-    const int k = o.rows_kernel, n = o.tile_nnz, r = o.tile_rows;
-    bool ok = false;
-    if (k == 0) ok = (n == 2048 && r == 256);
-    if (k == 1)
-        ok = (r == 256 && (n == 1024 || n == 2048 || n == 4096)) || (r == 512 && (n == 2048 || n == 4096)) ||
-             (r == 128 && n == 512);
-    if (k == 2) ok = (r == 64 && (n == 256 || n == 512 || n == 1024));
-    if (k == 3) ok = (r == 256 && (n == 1024 || n == 2048));
-    if (!ok)
-        return fail(PAMG_E_ARG, "options: rows_kernel %d has no instance for tile_nnz %d / tile_rows %d",
-                    k, n, r);
     return PAMG_OK;
 }
 
@@ -1617,12 +1559,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     if (!key || !value) return fail(PAMG_E_ARG, "get_option: bad args");
     const auto& o = pamg::options();
     const std::string k(key);
-    if (k == "rows_kernel") *value = o.rows_kernel;
-    else if (k == "tile_nnz") *value = o.tile_nnz;
-    else if (k == "tile_rows") *value = o.tile_rows;
-    else if (k == "xcd_remap") *value = o.xcd_remap;
-    else if (k == "jacobi_diag") *value = o.jacobi_diag;
-    else if (k == "stream_nt") *value = o.stream_nt;
+    if (k == "tile_nnz") *value = o.tile_nnz;
     else if (k == "tile_order") *value = o.tile_order;
     else if (k == "long_tiles") *value = o.long_tiles;
     else if (k == "row_len8") *value = o.row_len8;
@@ -1631,10 +1568,6 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "value_dict") *value = o.value_dict;
     else if (k == "col_dict") *value = o.col_dict;
     else if (k == "tile_major") *value = o.tile_major;
-    else if (k == "tm_persist") *value = o.tm_persist;
-    else if (k == "tm_flags") *value = o.tm_flags;
-    else if (k == "x_prefetch") *value = o.x_prefetch;
-    else if (k == "tm_transpose") *value = o.tm_transpose;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

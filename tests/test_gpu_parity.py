@@ -57,48 +57,31 @@ LENGTHS = {
     "len8_over": ([256] + [2] * 40) * 4,
 }
 
-# (rows_kernel, tile_nnz, tile_rows, xcd_remap, jacobi_diag, stream_nt, tile_order, col24,
-#  value_dict, long_tiles, row_len8): every tuning configuration must be bit-exact
-TILE_CONFIGS = [(0, 2048, 256, 0, 0, 0, 0, 1, 0, 1, 1), (1, 2048, 256, 0, 0, 0, 0, 1, 0, 1, 1), (1, 2048, 256, 1, 1, 0, 0, 1, 0, 1, 1),
-                (1, 1024, 256, 0, 0, 0, 0, 1, 0, 1, 1), (1, 1024, 256, 0, 0, 1, 1, 1, 0, 1, 1), (1, 4096, 256, 0, 0, 1, 0, 1, 0, 1, 1),
-                (1, 4096, 512, 1, 0, 0, 0, 1, 0, 1, 1), (2, 256, 64, 0, 0, 0, 0, 1, 0, 1, 1), (2, 512, 64, 0, 0, 0, 1, 1, 0, 1, 1),
-                (2, 512, 64, 0, 1, 0, 0, 1, 0, 1, 1), (2, 1024, 64, 0, 0, 0, 0, 1, 0, 1, 1), (3, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1),
-                (3, 2048, 256, 0, 0, 0, 0, 1, 0, 1, 1), (1, 512, 128, 0, 0, 0, 1, 1, 0, 1, 1), (1, 2048, 512, 0, 0, 0, 1, 1, 0, 1, 1),
-                (1, 1024, 256, 0, 0, 0, 1, 0, 0, 1, 1), (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1), (1, 1024, 256, 0, 0, 0, 1, 1, 1, 1, 1),
-                (1, 1024, 256, 0, 1, 0, 1, 1, 1, 1, 1), (1, 2048, 256, 0, 0, 0, 1, 1, 1, 1, 1),
-                (1, 1024, 256, 0, 0, 0, 1, 1, 0, 0, 1), (1, 1024, 256, 0, 0, 0, 4, 1, 0, 1, 1),
-                (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 0), (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1)]
-# + col_dict (last column): on for every configuration above (it engages only where its
-# conditions hold), plus the default layout and the stored-diagonal Jacobi without it
-# + tile_major (last column): on wherever its conditions hold, plus variant 1 without it
-# (1 = where measured faster, 2 = every eligible set: 24-bit tile-major on every operator)
-TILE_CONFIGS = [c + (1, 1) for c in TILE_CONFIGS] + [(1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 0, 2),
-                                                      (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1, 0, 2),
-                                                      (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 0),
-                                                      (1, 1024, 256, 0, 1, 0, 1, 0, 0, 1, 1, 1, 0),
-                                                      (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2),
-                                                      (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1, 0, 2)]
-# + tm_persist (last column): the persistent prefetching variant 4p on every tile-major set
-TILE_CONFIGS = [c + (0,) for c in TILE_CONFIGS] + [(1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 1),
-                                                   (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1, 1, 2, 1),
-                                                   (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 1)]
-# + tm_flags (last column): row lengths (variant 4) by default, row-start flags (variant 4f)
-TILE_CONFIGS = [c + (0,) for c in TILE_CONFIGS] + [(1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 0, 1),
-                                                   (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1, 1, 2, 0, 1),
-                                                   (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 0, 1),
-                                                   (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 0, 2, 0, 1)]
-# + x_prefetch, tm_transpose (last two columns): the variant 4 A/B forms
-TILE_CONFIGS = [c + (0, 0) for c in TILE_CONFIGS] + [(1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 0, 0, 1, 1),
-                                                      (1, 1024, 256, 0, 1, 0, 1, 1, 0, 1, 1, 1, 2, 0, 0, 0, 1),
-                                                      (1, 4096, 256, 0, 0, 0, 1, 1, 0, 1, 1, 1, 2, 0, 0, 1, 1),
-                                                      (1, 1024, 256, 0, 0, 0, 1, 1, 0, 1, 1, 0, 2, 0, 0, 0, 1)]
-OPT_KEYS = ("rows_kernel", "tile_nnz", "tile_rows", "xcd_remap", "jacobi_diag", "stream_nt", "tile_order",
-            "col24", "value_dict", "long_tiles", "row_len8", "col_dict", "tile_major", "tm_persist", "tm_flags",
-            "x_prefetch", "tm_transpose")
+# (tile_nnz, tile_order, col24, value_dict, long_tiles, row_len8, col_dict, tile_major): every
+# layout the upload can produce and the kernel that runs it (kernels.hip launch_tile):
+TILE_CONFIGS = [
+    (1024, 1, 0, 0, 1, 0, 0, 0),  # k_rows_tile2, 32-bit columns + row pointers
+    (2048, 1, 0, 0, 1, 0, 0, 0),
+    (4096, 0, 0, 0, 0, 0, 0, 0),  #   natural tile order, 4096-nonzero tiles everywhere
+    (1024, 1, 1, 0, 1, 0, 0, 0),  # k_rows_tile2 <C24>
+    (1024, 1, 1, 0, 1, 1, 0, 0),  # k_rows_tile2 <C24, RL8>
+    (1024, 1, 1, 1, 1, 0, 0, 0),  # k_rows_tile2 <C24, VD> (opt-in value dictionaries)
+    (2048, 1, 1, 1, 1, 1, 0, 0),
+    (1024, 1, 1, 0, 1, 1, 1, 0),  # k_rows_tile2 <RL8, CD 4/8>
+    (1024, 1, 0, 0, 1, 0, 1, 0),  #   column dictionaries without the 24-bit stream
+    (1024, 1, 1, 0, 1, 1, 1, 1),  # default: k_rows_tm on dictionary / slot-filling sets
+    (1024, 0, 1, 0, 0, 1, 1, 1),  #   natural order, no long tiles
+    (2048, 1, 1, 0, 1, 1, 1, 1),
+    (4096, 1, 1, 0, 1, 1, 1, 1),
+    (1024, 1, 1, 0, 1, 1, 1, 2),  # k_rows_tm on every eligible set (24-bit tile-major too)
+    (1024, 1, 1, 0, 1, 0, 0, 2),  #   24-bit tile-major only
+    (4096, 1, 1, 0, 1, 1, 1, 2),
+]
+OPT_KEYS = ("tile_nnz", "tile_order", "col24", "value_dict", "long_tiles", "row_len8", "col_dict", "tile_major")
 
 
 @pytest.fixture(params=TILE_CONFIGS,
-                ids=lambda c: "k{}_{}x{}_xcd{}_dg{}_nt{}_ord{}_c24{}_vd{}_lt{}_rl{}_cd{}_tm{}_tp{}_tf{}_xp{}_tt{}".format(*c))
+                ids=lambda c: "t{}_ord{}_c24{}_vd{}_lt{}_rl{}_cd{}_tm{}".format(*c))
 def tile_cfg(request, built):
     import ctypes
     from parallel_amg_amd._lib import call
@@ -210,7 +193,7 @@ def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
         offs = offs[offs != 0][:ndist]
     M = offset_csr(rng, n, offs, lengths)
     distinct = len(np.unique(M.col - np.repeat(np.arange(n), np.diff(M.rowptr))))
-    keys = ("col_dict", "tile_nnz", "jacobi_diag", "tile_major", "tm_persist", "tm_flags", "tm_transpose")
+    keys = ("col_dict", "tile_nnz", "tile_major")
     old = []
     for k in keys:
         v = ctypes.c_int64()
@@ -221,20 +204,14 @@ def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
         call("pamg_set_option", b"col_dict", 0)
         call("pamg_set_option", b"tile_major", 0)
         plain = upload(ctx, M)[0].stream_bytes
-        for dg, tm, tp, tf, tt in ((0, 0, 0, 1, 0), (1, 0, 0, 1, 0), (0, 2, 0, 0, 0), (1, 2, 0, 0, 0),
-                                   (0, 2, 1, 0, 0), (1, 2, 1, 0, 0), (0, 2, 0, 1, 0), (1, 2, 0, 1, 0),
-                                   (0, 2, 0, 0, 1), (1, 2, 0, 0, 1)):
+        for tm in (0, 2):
             call("pamg_set_option", b"col_dict", 1)
-            call("pamg_set_option", b"jacobi_diag", dg)
             call("pamg_set_option", b"tile_major", tm)
-            call("pamg_set_option", b"tm_persist", tp)
-            call("pamg_set_option", b"tm_flags", tf)
-            call("pamg_set_option", b"tm_transpose", tt)
             A, _h = upload(ctx, M)
             if not tm:
                 assert (A.stream_bytes < plain) == (distinct <= 256), (A.stream_bytes, plain, distinct)
             lay = layout_of(A)
-            assert lay["tm"] == bool(tm) and lay["tm_flags"] == bool(tm and tf)
+            assert lay["tm"] == bool(tm)
             assert lay["cd"] == (4 if distinct <= 16 else 8 if distinct <= 256 else 0), (lay, distinct)
             assert lay["cd_offsets"] == (distinct if distinct <= 256 else 0)
             xh, bh = rng.standard_normal(n), rng.standard_normal(n)
@@ -411,16 +388,7 @@ def test_stream_bytes_layout(ctx):
     A, _h = upload(ctx, M)
     lay = layout_of(A)
     assert lay["tm"] and lay["cd"] == 4 and 0 < lay["tm_rs"] <= 256 and lay["tm_rs"] % 4 == 0
-    assert not lay["tm_flags"]
     assert A.stream_bytes == nt * (lay["tm_rs"] + 8 * 1024 + 512 + 16) + 4 * 7 + 4
-    # variant 4f: row bounds as 128 flag bytes + 4 two-byte chunk bases per 1024-position slot
-    call("pamg_set_option", b"tm_flags", 1)
-    try:
-        A, _h = upload(ctx, M)
-    finally:
-        call("pamg_set_option", b"tm_flags", 0)
-    assert layout_of(A)["tm_flags"]  # every row of the grid operator is non-empty
-    assert A.stream_bytes == nt * (128 + 8 + 8 * 1024 + 512 + 16) + 4 * 7 + 4
 
 
 @pytest.mark.parametrize("seed,n,density,weak,iso", [(1, 3000, 0.003, 0.3, 0.02), (2, 5000, 0.001, 0.0, 0.0),

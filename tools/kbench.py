@@ -53,8 +53,8 @@ def main():
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--levels", type=int, default=1)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--configs", default="1:1024:256:0:0:0:1:1,1:1024:256:0:0:0:1:0",
-                    help="kern:tile_nnz:tile_rows:xcd:jacobi_diag:stream_nt:tile_order:col24:value_dict:long_tiles:row_len8:col_dict:tile_major:tm_persist:tm_flags:x_prefetch:tm_transpose,...")
+    ap.add_argument("--configs", default="1024:1,1024:0",
+                    help="tile_nnz:tile_order:col24:value_dict:long_tiles:row_len8:col_dict:tile_major,...")
     ap.add_argument("--ops", default="0,2")
     args = ap.parse_args()
     ctx = Context(0)
@@ -73,12 +73,10 @@ def main():
     ops = [int(o) for o in args.ops.split(",")]
     for cfg in args.configs.split(","):
         given = [int(v) for v in cfg.split(":")]
-        vals = given + [1, 1024, 256, 0, 0, 0, 0, 1, 0, 1, 1, 1, 1, 0, 0, 0, 0][len(given):]  # defaults for missing fields
-        kern, tnnz, trows, xcd, jd, nt, order, c24, vd, lt, rl8, cd, tm, tp, tf, xp, tt = vals[:17]
-        set_opts(rows_kernel=kern, tile_nnz=tnnz, tile_rows=trows, xcd_remap=xcd, jacobi_diag=jd,
-                 stream_nt=nt, tile_order=order, col24=c24, value_dict=vd, long_tiles=lt, row_len8=rl8,
-                 col_dict=cd, tile_major=tm, tm_persist=tp, tm_flags=tf, x_prefetch=xp,
-                 tm_transpose=tt)
+        vals = given + [1024, 1, 1, 0, 1, 1, 1, 1][len(given):]  # defaults for missing fields
+        tnnz, order, c24, vd, lt, rl8, cd, tm = vals[:8]
+        set_opts(tile_nnz=tnnz, tile_order=order, col24=c24, value_dict=vd, long_tiles=lt, row_len8=rl8,
+                 col_dict=cd, tile_major=tm)
         for name, (M, plan) in mats.items():
             D = PSparseMatrix(ctx, M, plan)
             for op in ops:
