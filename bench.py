@@ -41,6 +41,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--samples", type=int, default=5,
+                    help="timed regions of exactly --steps V-cycles each; value = the median")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--grid", type=int, default=512, help="grid points per side")
     ap.add_argument("--kind", default="poisson3d",
@@ -66,6 +68,12 @@ def main():
                          "values (exact; not the default layout)")
     ap.add_argument("--setup", choices=["gpu", "host"], default="gpu",
                     help="where the Galerkin products of the setup run (same bits either way)")
+    ap.add_argument("--permute", type=int, default=None, metavar="SEED",
+                    help="apply a seeded random symmetric permutation to the problem before setup "
+                         "(destroys the grid numbering, as an FE mesh ordering would; 1 part only)")
+    ap.add_argument("--pcg-rtol", type=float, default=1e-8,
+                    help="time-to-solution leg: PCG with the V-cycle preconditioner to this "
+                         "relative residual from x = 0 (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,6 +121,11 @@ def main():
     else:
         A, offs, xs = pa.generate_problem(be, args.kind, args.grid)
         workload = f"{args.kind} {args.grid}^{2 if args.kind == 'poisson2d' else 3} fp64"
+    if args.permute is not None:
+        if world > 1:
+            raise SystemExit("--permute: one part only")
+        A, xs = pa.permute_problem(A, xs, args.permute)
+        workload += f", randomly permuted (seed {args.permute})"
     H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=args.max_coarse, agglomerate=args.agglomerate), log=log,
                            device=ctx if args.setup == "gpu" else None)
     t_setup = time.time() - t0
@@ -133,17 +146,25 @@ def main():
     log(f"upload {t_upload:.1f}s")
 
     # ---- multi-part graph self-check: graph replay (RCCL captured) and eager launches must
-    # give the same bits on every rank, else the timed run uses eager launches
+    # give the same bits on every rank. A mismatch is a correctness bug of the captured
+    # multi-rank cycle, so the run stops there with an invalid line naming the ranks.
     if use_graph and world > 1:
         xa, xb = S.new_vector(), S.new_vector()
         S.vcycle(xa, b, 2)
         S.set_graph(False)
         S.vcycle(xb, b, 2)
         same = bool(np.array_equal(xa.own_values().view(np.int64), xb.own_values().view(np.int64)))
-        ok = be.allreduce_max({rank: 0.0 if same else 1.0}) == 0.0
-        S.set_graph(ok)
+        bad = [r for r, v in enumerate(be.allgather({rank: 0 if same else 1})) if v]
+        S.set_graph(True)
         del xa, xb
-        log(f"multi-part graph self-check: {'ok' if ok else 'MISMATCH -> eager'}")
+        log(f"multi-part graph self-check: {'ok' if not bad else f'MISMATCH on ranks {bad}'}")
+        if bad:
+            if rank == 0:
+                print(json.dumps({"metric": METRIC, "value": None, "unit": "V-cycles/s", "n_gpus": world,
+                                  "invalid": "hipGraph replay differs from eager launches",
+                                  "graph_mismatch": True, "mismatch_ranks": bad}), flush=True)
+            dist.destroy_process_group()
+            sys.exit(3)
 
     # ---- warmup + timed region -------------------------------------------------------
     if args.warmup:
@@ -152,19 +173,45 @@ def main():
         ctx.sync()
         _lib.call("pamg_device_sync", dev)
 
-    device_sync()
-    barrier()
-    ts = time.perf_counter()
-    S.vcycle_async(x, b, args.steps)
-    device_sync()
-    barrier()
-    te = time.perf_counter()
-    dt = te - ts
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    times = []
+    for _ in range(max(1, args.samples)):
+        device_sync()
+        barrier()
+        ts = time.perf_counter()
+        S.vcycle_async(x, b, args.steps)
+        device_sync()
+        barrier()
+        dt = time.perf_counter() - ts
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        times.append(dt)
+    dt = float(np.median(times))
     vps = args.steps / dt
+    log(f"timed samples ({args.steps} V-cycles each, max over ranks): "
+        + ", ".join(f"{t * 1e3:.1f} ms" for t in times))
+
+    # ---- time to solution: PCG (V-cycle preconditioner) from x = 0 to --pcg-rtol ----------
+    pcg = None
+    if args.pcg_rtol > 0:
+        xp = S.new_vector()
+        device_sync()
+        barrier()
+        ts = time.perf_counter()
+        its, phist = S.pcg(xp, b, rtol=args.pcg_rtol, maxit=200)
+        device_sync()
+        barrier()
+        tp = time.perf_counter() - ts
+        if world > 1:
+            t = torch.tensor([tp], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            tp = float(t.item())
+        pcg = {"rtol": args.pcg_rtol, "iterations": int(its), "seconds": round(tp, 4),
+               "final_rel_residual": float(phist[-1] / phist[0]) if phist[0] else 0.0,
+               "converged": bool(phist[-1] <= args.pcg_rtol * phist[0])}
+        log(f"pcg: {its} iterations, {tp:.3f} s to rtol {args.pcg_rtol:g}")
+        del xp
 
     # ---- per-kernel timing (HIP events on the compute stream, eager) ------------------
     kprof = max(3, min(args.steps, 10))
@@ -195,33 +242,23 @@ def main():
         cpu = cpu_baseline(H, xs[0], args.cpu_cycles, log, (nu1, nu2))
 
     # HBM traffic of the dominant kernel from the committed rocprofv3 PMC passes of this exact
-    # workload (tools/pmc_traffic.py; counters cannot be read from inside the process)
-    # (only when the record was measured on the same column layout as this run)
+    # workload (tools/pmc_traffic.py; counters cannot be read from inside the process). A
+    # record is used only when it was measured on the same kernel instance, the same tile
+    # count (the uploaded layout) and the same kernels.hip source as this run.
     lay = _lib.layout_of(A0)
-    c24, vd, rl8, cd, tm = lay["c24"], lay["vd"], lay["rl8"], lay["cd"], lay["tm"]
-    tn = lay["tile_nnz"]
-    kname = (f"k_rows_tm<2, {tn}, {cd}, false>" if tm
-             else f"k_rows_tile2<2, {tn}, 256, false, false, 256, false, false, true, {cd}>" if cd
-             else f"k_rows_tile2<2, {tn}, 256, false, false, 256, true, true>" if vd
-             else f"k_rows_tile2<2, {tn}, 256, false, false, 256, true, false, true>" if rl8
-             else f"k_rows_tile2<2, {tn}, 256, false, false, 256, true>" if c24
-             else f"k_rows_tile2<2, {tn}, 256, false, false>")
-    traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "r01_pmc", "traffic_jacobi_512.json")
-    if (not args.matrix and args.kind == "poisson3d" and args.grid == 512 and world == 1
-            and os.path.exists(pmc)):
-        rec = [r for r in json.load(open(pmc)) if r["kernel"] == kname]
-        if rec:
-            traffic, traffic_src = float(rec[0]["traffic_bytes"]), os.path.relpath(pmc, ROOT)
-    # the fine SpMV's HBM rate from its committed PMC record (same workload and layout)
-    spmv_traffic_gbps = None
-    pmc_s = os.path.join(ROOT, "profiles", "r01_pmc", "traffic_spmv_512.json")
-    if (not args.matrix and args.kind == "poisson3d" and args.grid == 512 and world == 1
-            and os.path.exists(pmc_s)):
-        sname = kname.replace("<2,", "<0,", 1)
-        rec = [r for r in json.load(open(pmc_s)) if r["kernel"] == sname]
-        if rec:
-            spmv_traffic_gbps = round(float(rec[0]["traffic_bytes"]) / (spmv_ms * 1e-3) / 1e9, 1)
+    cd, tm, tn = lay["cd"], lay["tm"], lay["tile_nnz"]
+    kname = (f"k_rows_tm<2, {tn}, {cd}>" if tm
+             else f"k_rows_tile2<2, {tn}, false, false, true, {cd}>" if cd
+             else f"k_rows_tile2<2, {tn}, true, true>" if lay["vd"]
+             else f"k_rows_tile2<2, {tn}, true, false, true>" if lay["rl8"]
+             else f"k_rows_tile2<2, {tn}, true>" if lay["c24"]
+             else f"k_rows_tile2<2, {tn}>")
+    workload_key = f"{args.matrix or args.kind}:{args.grid}:p{world}:perm{args.permute}"
+    src = kernel_source_sha()
+    traffic = pmc_lookup("traffic_jacobi.json", kname, lay["tiles"], workload_key, src)
+    spmv_traffic = pmc_lookup("traffic_spmv.json", kname.replace("<2,", "<0,", 1), lay["tiles"], workload_key, src)
+    spmv_traffic_gbps = (round(spmv_traffic["traffic_bytes"] / (spmv_ms * 1e-3) / 1e9, 1)
+                         if spmv_traffic else None)
 
     # fine-level nonzeros of the whole problem (every rank holds only its own rows)
     nnz_fine = (sum(be.allgather({rank: int(H.levels[0][rank].A.nnz)})) if world > 1
@@ -257,24 +294,31 @@ def main():
             },
             "fine_spmv_GBps": round(spmv_gbps, 1),
             "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
-            # HBM bytes actually moved (PMC, profiles/r01_pmc) per second of the same launch
+            # HBM bytes actually moved (PMC record of this kernel/layout/source) per second
             "fine_spmv_traffic_GBps": spmv_traffic_gbps,
+            "samples_ms_per_step": [round(t / args.steps * 1e3, 4) for t in times],
             "roofline": {
                 "kernel": kname + " (level-0 post-smoothing Jacobi"
                           + (", tile-major slots" if tm else "")
                           + (f", {cd}-bit column dictionary" if cd else "")
-                          + (", value dictionaries" if vd else "")
-                          + (", 24-bit column stream" if c24 and not cd else "")
-                          + (", 8-bit row lengths)" if rl8 else ")"),
+                          + (", value dictionaries" if lay["vd"] else "")
+                          + (", 24-bit column stream" if lay["c24"] and not cd else "")
+                          + (", 8-bit row lengths)" if lay["rl8"] else ")"),
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic, "traffic_source": traffic_src,
+                "frac_basis": "algorithmic bytes (SURVEY 8(d) plain CSR, 12 B/nnz) / launch time / peak",
+                "traffic": traffic["traffic_bytes"] if traffic else None,
+                "traffic_source": traffic["source"] if traffic else None,
+                # HBM bytes the launch actually moved (PMC) / launch time / peak
+                "hbm_frac": (round(traffic["traffic_bytes"] / (post_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+                             if traffic else None),
                 "bytes_per_launch": int(post_bytes), "bytes_model": "SURVEY 8(d) CSR (12 B/nnz)",
                 "format_bytes_per_launch": int(post_fbytes),
                 "format_GBps": round(post_fbytes / (post_ms * 1e-3) / 1e9, 1),
                 "ms_per_launch": round(post_ms, 4),
             },
             "cpu_baseline": cpu,
+            "time_to_solution": pcg,
             "setup_s": round(t_setup, 1),
             "setup_products": args.setup,
             "final_residual": float(hist[0]),
@@ -282,6 +326,25 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def kernel_source_sha() -> str:
+    import hashlib
+    with open(os.path.join(ROOT, "parallel_amg_amd", "csrc", "kernels.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def pmc_lookup(fname, kname, tiles, workload_key, src):
+    """The committed PMC traffic record (profiles/pmc/<fname>, tools/pmc_traffic.py) of this
+    kernel instance on this workload, tile count and kernels.hip source; None otherwise."""
+    path = os.path.join(ROOT, "profiles", "pmc", fname)
+    if not os.path.exists(path):
+        return None
+    for r in json.load(open(path)):
+        if (r.get("kernel") == kname and r.get("blocks") == tiles and r.get("workload") == workload_key
+                and r.get("kernels_hip_sha16") == src):
+            return {"traffic_bytes": float(r["traffic_bytes"]), "source": os.path.relpath(path, ROOT)}
+    return None
 
 
 def ctypes_bench_spmv(ctx, A0, x, S, reps=20) -> float:
@@ -310,8 +373,15 @@ def cpu_baseline(H, xstar, ncycles, log, sweeps=(1, 1)):
     O.lib().orc_solve(Ho._h, x, rhs, ncycles, None)
     dt = time.perf_counter() - t
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    log(f"cpu baseline: {ncycles} V-cycle(s) in {dt:.2f}s on {cores} threads")
+    model = "?"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    log(f"cpu baseline: {ncycles} V-cycle(s) in {dt:.2f}s on {cores} threads ({model})")
     return {"value": round(ncycles / dt, 5), "unit": "V-cycles/s", "cores": cores, "kind": "port",
+            "nproc": os.cpu_count(), "cpu_model": model,
             "sample": f"{ncycles} full V-cycle(s) of the same {A0.nrows}-row hierarchy by the C "
                       f"oracle (oracle/pamg_oracle.c, OpenMP, int64 indices); reference "
                       f"(Julia/PartitionedArrays) not runnable: no code in /root/reference"}

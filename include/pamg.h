@@ -97,6 +97,8 @@ int pamg_vec_destroy(pamg_vec* v);
 int pamg_vec_size(const pamg_vec* v, int64_t* n_own, int64_t* n_ghost);
 int pamg_vec_upload(pamg_ctx* ctx, pamg_vec* v, const double* own);     /* own_values(v) .= */
 int pamg_vec_download(pamg_ctx* ctx, const pamg_vec* v, double* own);
+/* ghost_values(x): the n_ghost ghost slots as last exchanged (debugging, tests). */
+int pamg_vec_download_ghosts(pamg_ctx* ctx, const pamg_vec* v, double* ghost);
 int pamg_vec_device_ptr(pamg_vec* v, double** dptr);                    /* zero-copy interop */
 int pamg_vec_fill(pamg_ctx* ctx, pamg_vec* v, double value);            /* fill!(v, a) */
 int pamg_vec_copy(pamg_ctx* ctx, const pamg_vec* src, pamg_vec* dst);   /* copy!(dst, src) */
@@ -105,6 +107,13 @@ int pamg_vec_dot(pamg_ctx* ctx, const pamg_vec* x, const pamg_vec* y, double* ou
 int pamg_vec_nrm2(pamg_ctx* ctx, const pamg_vec* x, double* out);                      /* norm */
 /* consistent!(x) |> wait : owners' values into the ghost slots described by plan. */
 int pamg_exchange(pamg_ctx* ctx, const pamg_plan* plan, pamg_vec* x);
+/* t = consistent!(x) ... wait(t), split: _begin enqueues the exchange on the context's comm
+ * stream behind the work already enqueued and returns at once; _end joins it (later calls see
+ * the ghosts) and waits. Work between the two overlaps the exchange; it must not read x's
+ * ghost slots or write x's own entries. One exchange in flight per plan (PAMG_E_STATE
+ * otherwise). The host debug transport completes the exchange inside _begin. */
+int pamg_exchange_begin(pamg_ctx* ctx, pamg_plan* plan, pamg_vec* x);
+int pamg_exchange_end(pamg_ctx* ctx, pamg_plan* plan, pamg_vec* x);
 
 /* ------------------------------------------------------------------ matrices (PSparseMatrix) */
 /* One part's own rows; columns already local (own 0..n_own-1 of the column space, then the

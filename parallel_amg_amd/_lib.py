@@ -51,6 +51,7 @@ SIGNATURES = {
     "pamg_vec_size": [vp, pi64, pi64],
     "pamg_vec_upload": [vp, vp, vp],
     "pamg_vec_download": [vp, vp, vp],
+    "pamg_vec_download_ghosts": [vp, vp, vp],
     "pamg_vec_device_ptr": [vp, pvp],
     "pamg_vec_fill": [vp, vp, dbl],
     "pamg_vec_copy": [vp, vp, vp],
@@ -58,6 +59,8 @@ SIGNATURES = {
     "pamg_vec_dot": [vp, vp, vp, pdbl],
     "pamg_vec_nrm2": [vp, vp, pdbl],
     "pamg_exchange": [vp, vp, vp],
+    "pamg_exchange_begin": [vp, vp, vp],
+    "pamg_exchange_end": [vp, vp, vp],
     "pamg_mat_upload": [vp, i64, i64, vp, vp, i32, vp, i32, vp, pvp],
     "pamg_mat_destroy": [vp],
     "pamg_mat_info": [vp, pi64, pi64, pi64],

@@ -106,6 +106,9 @@ struct pamg_plan {
     // planes of a slab partition), else -1; all_contig: no pack kernel is needed at all
     std::vector<int64_t> send_run;
     bool all_contig = false;
+    // split exchange (pamg_exchange_begin / _end): completion event on the comm stream
+    hipEvent_t ev_done = nullptr;
+    const void* in_flight = nullptr;  // the vector of the exchange begun and not yet ended
 };
 
 struct pamg_vec {

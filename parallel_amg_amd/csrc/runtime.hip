@@ -848,6 +848,8 @@ int pamg_plan_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, int n_nbr,
 int pamg_plan_destroy(pamg_plan* p) {
     if (!p) return PAMG_OK;
     (void)hipSetDevice(p->ctx->device);
+    if (p->in_flight) (void)hipStreamSynchronize(p->ctx->s_comm);
+    if (p->ev_done) (void)hipEventDestroy(p->ev_done);
     dfree(p->d_send_idx);
     dfree(p->d_sendbuf);
     delete p;
@@ -896,6 +898,16 @@ int pamg_vec_download(pamg_ctx* ctx, const pamg_vec* v, double* own) {
     if (!ctx || !v || (!own && v->n_own)) return fail(PAMG_E_ARG, "vec_download: bad args");
     CHECK(set_device(ctx));
     if (v->n_own) HIPC(hipMemcpyAsync(own, v->d, sizeof(double) * v->n_own, hipMemcpyDeviceToHost, ctx->s_comp));
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_vec_download_ghosts(pamg_ctx* ctx, const pamg_vec* v, double* ghost) {
+    if (!ctx || !v || (!ghost && v->n_ghost)) return fail(PAMG_E_ARG, "vec_download_ghosts: bad args");
+    CHECK(set_device(ctx));
+    if (v->n_ghost)
+        HIPC(hipMemcpyAsync(ghost, v->d + v->n_own, sizeof(double) * v->n_ghost, hipMemcpyDeviceToHost,
+                            ctx->s_comp));
     HIPC(hipStreamSynchronize(ctx->s_comp));
     return PAMG_OK;
 }
@@ -954,6 +966,44 @@ int pamg_exchange(pamg_ctx* ctx, const pamg_plan* plan, pamg_vec* x) {
         return fail(PAMG_E_ARG, "exchange: vector does not fit the plan");
     CHECK(set_device(ctx));
     CHECK(exchange_on(plan, x->d, ctx->s_comp));
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+// consistent!(x) split in two (PartitionedArrays returns a task to wait on): begin forks the
+// exchange onto the comm stream behind everything already enqueued on the compute stream and
+// returns; end joins it back (later compute-stream work sees the ghosts) and waits for it.
+// Between the two the caller may run anything that does not touch x's ghost slots or write
+// its send entries. The host debug transport has nothing to overlap: begin does it all.
+int pamg_exchange_begin(pamg_ctx* ctx, pamg_plan* plan, pamg_vec* x) {
+    if (!ctx || !plan || !x) return fail(PAMG_E_ARG, "exchange_begin: bad args");
+    if (x->n_own != plan->n_own || x->n_ghost < plan->n_ghost)
+        return fail(PAMG_E_ARG, "exchange_begin: vector does not fit the plan");
+    if (plan->in_flight) return fail(PAMG_E_STATE, "exchange_begin: the plan has an exchange in flight");
+    CHECK(set_device(ctx));
+    if (ctx->host_fn) {
+        CHECK(exchange_on(plan, x->d, ctx->s_comp));
+        plan->in_flight = x;
+        return PAMG_OK;
+    }
+    if (!plan->ev_done) HIPC(hipEventCreateWithFlags(&plan->ev_done, hipEventDisableTiming));
+    HIPC(hipEventRecord(ctx->ev_fork, ctx->s_comp));
+    HIPC(hipStreamWaitEvent(ctx->s_comm, ctx->ev_fork, 0));
+    CHECK(exchange_on(plan, x->d, ctx->s_comm));
+    HIPC(hipEventRecord(plan->ev_done, ctx->s_comm));
+    plan->in_flight = x;
+    return PAMG_OK;
+}
+
+int pamg_exchange_end(pamg_ctx* ctx, pamg_plan* plan, pamg_vec* x) {
+    if (!ctx || !plan || !x) return fail(PAMG_E_ARG, "exchange_end: bad args");
+    if (plan->in_flight != x) return fail(PAMG_E_STATE, "exchange_end: no exchange of this vector in flight");
+    CHECK(set_device(ctx));
+    plan->in_flight = nullptr;
+    if (!ctx->host_fn) {
+        HIPC(hipStreamWaitEvent(ctx->s_comp, plan->ev_done, 0));
+        HIPC(hipEventSynchronize(plan->ev_done));
+    }
     HIPC(hipStreamSynchronize(ctx->s_comp));
     return PAMG_OK;
 }

@@ -179,6 +179,37 @@ def generate_problem(backend, kind: str, n: int, eps: float = 1e-3):
     return A, offs, xs
 
 
+def permutation(n: int, seed: int) -> np.ndarray:
+    """The seeded random permutation ``permute_problem`` applies: new row i is old row perm[i]."""
+    return np.random.default_rng(seed).permutation(n).astype(np.int64)
+
+
+def permute_problem(A: dict, xs: dict, seed: int):
+    """Symmetric permutation Q A Q^T of a one-part problem, x* permuted alike (bench
+    ``--permute``). A grid operator renumbered at random keeps its values and nonzero counts
+    but loses the banded, row-relative column pattern that the column dictionaries and the
+    banded tile order exploit, as an FE mesh numbering would (a Flan_1565 proxy).
+    Rows keep their columns sorted ascending (SPEC §S1)."""
+    if set(A) != {0}:
+        raise ValueError("permute_problem: one part only")
+    M = A[0]
+    n = M.nrows
+    perm = permutation(n, seed)
+    inv = np.empty(n, np.int64)
+    inv[perm] = np.arange(n, dtype=np.int64)
+    lens = np.diff(M.rowptr)[perm]
+    rp = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=rp[1:])
+    src = np.repeat(M.rowptr[perm], lens) + (np.arange(rp[-1], dtype=np.int64) - np.repeat(rp[:-1], lens))
+    col = inv[M.col[src]]
+    val = M.val[src]
+    # sort each row's columns: one global stable sort on (row, col)
+    row = np.repeat(np.arange(n, dtype=np.int64), lens)
+    order = np.lexsort((col, row))
+    P = HCSR.from_arrays(rp, col[order].astype(np.int32), val[order], M.ncols)
+    return {0: P}, {0: np.ascontiguousarray(xs[0][perm])}
+
+
 def balanced_offsets(row_counts: np.ndarray, nparts: int) -> np.ndarray:
     """SPEC §S7 nnz-balanced partition: o_p = first row r with sum_{i<r} len_i >= floor(p*nnz/P)."""
     pre = np.zeros(len(row_counts) + 1, np.int64)

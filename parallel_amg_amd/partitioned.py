@@ -8,6 +8,7 @@ PartitionedArrays.jl names → this module:
 ``PSparseMatrix`` part                     ``PSparseMatrix`` (own rows, local columns)
 ``mul!(y, A, x)``                          ``mul(y, A, x)``
 ``consistent!(x) |> wait``                 ``consistent(x, plan)``
+``t = consistent!(x); …; wait(t)``         ``t = consistent_async(x, plan); …; t.wait()``
 ``own_values(x)``                          ``x.own_values()``
 ``dot(x, y)`` / ``norm(x)``                ``dot(x, y)`` / ``norm(x)``
 ``axpy!`` / ``copy!`` / ``fill!``          ``axpby`` / ``copy`` / ``fill``
@@ -204,6 +205,12 @@ class PVector:
         call("pamg_vec_download", self.ctx.handle, self._h, ptr(out))
         return out
 
+    def ghost_values(self) -> np.ndarray:
+        """PartitionedArrays ``ghost_values(x)``: the ghost slots, as last exchanged."""
+        out = np.empty(self.n_ghost)
+        call("pamg_vec_download_ghosts", self.ctx.handle, self._h, ptr(out))
+        return out
+
     def device_ptr(self) -> int:
         p = C.c_void_p()
         call("pamg_vec_device_ptr", self._h, C.byref(p))
@@ -278,6 +285,26 @@ def consistent(x: PVector, plan: DevicePlan) -> PVector:
     """``consistent!(x) |> wait``: owners' values into x's ghost slots."""
     call("pamg_exchange", x.ctx.handle, plan.handle, x.handle)
     return x
+
+
+class ExchangeTask:
+    """``t = consistent!(x)`` ... ``wait(t)``: the exchange runs on the comm stream until
+    ``wait`` (pamg_exchange_begin / pamg_exchange_end)."""
+
+    def __init__(self, x: PVector, plan: DevicePlan):
+        self.x, self.plan, self.done = x, plan, False
+        call("pamg_exchange_begin", x.ctx.handle, plan.handle, x.handle)
+
+    def wait(self) -> PVector:
+        if not self.done:
+            call("pamg_exchange_end", self.x.ctx.handle, self.plan.handle, self.x.handle)
+            self.done = True
+        return self.x
+
+
+def consistent_async(x: PVector, plan: DevicePlan) -> ExchangeTask:
+    """``consistent!(x)`` returning the task to ``wait`` on (overlap your own work with it)."""
+    return ExchangeTask(x, plan)
 
 
 def dot(x: PVector, y: PVector) -> float:

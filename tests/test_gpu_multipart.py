@@ -59,11 +59,24 @@ def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, poison
         mul(b, A0, xst)
         x = S.new_vector()
         hist = S.vcycle(x, b, ncycles, res_hist=True)
-        out = (rank, "ok", b.own_values(), x.own_values(), hist)
+        # consistent!(x) split (exchange_begin/_end) == the synchronous exchange == the
+        # owners' values at the ghost ids
+        ghosts = None
+        pl = H.levels[0][rank].planA
+        if S.A[0].plan is not None:
+            from parallel_amg_amd.partitioned import consistent, consistent_async
+            va = PVector(ctx, pl.n_own, pl.n_ghost, x.own_values())
+            vb = PVector(ctx, pl.n_own, pl.n_ghost, x.own_values())
+            consistent(va, S.A[0].plan)
+            consistent_async(vb, S.A[0].plan).wait()
+            ga, gb = va.ghost_values(), vb.ghost_values()
+            assert np.array_equal(ga.view(np.int64), gb.view(np.int64))
+            ghosts = (np.asarray(pl.ghost_ids, np.int64), ga)
+        out = (rank, "ok", b.own_values(), x.own_values(), hist, ghosts)
         q.put(out)
     except Exception:
         import traceback
-        q.put((rank, traceback.format_exc(), None, None, None))
+        q.put((rank, traceback.format_exc(), None, None, None, None))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
@@ -106,6 +119,9 @@ def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, agglomerate, poi
     assert np.array_equal(bits(x), bits(xo))
     for r in range(world):
         np.testing.assert_allclose(res[r][4], ho, rtol=1e-12)
+        if res[r][5] is not None:
+            gid, gv = res[r][5]
+            assert len(gid) > 0 and np.array_equal(bits(gv), bits(x[gid]))
 
 
 def test_multipart_with_an_empty_part(tmp_path, built):

@@ -110,6 +110,33 @@ def _run(kind, n, q):
         h0 = S0.vcycle(x0, b0, 3, res_hist=True)
         it0, ph0 = S0.pcg(S0.new_vector(), b0, rtol=1e-10, maxit=60)
 
+        # consistent!(x) split (pamg_exchange_begin / _end) vs the synchronous exchange: same
+        # ghost bits, with an SpMV of another vector overlapping the exchange in flight
+        from parallel_amg_amd.partitioned import DevicePlan, consistent, consistent_async
+        pl = Hs.levels[0][0].planA
+        dp = DevicePlan(rccl_ctx, pl)
+        own = np.random.default_rng(3).standard_normal(pl.n_own)
+        va = PVector(rccl_ctx, pl.n_own, pl.n_ghost, own)
+        vb = PVector(rccl_ctx, pl.n_own, pl.n_ghost, own)
+        consistent(va, dp)
+        S1 = AMGSolver(rccl_ctx, Hs, graph=False)
+        u = PVector(rccl_ctx, S1.A[0].n_own_cols, S1.A[0].n_ghost, xs[0])
+        yu = PVector(rccl_ctx, S1.A[0].nrows)
+        t = consistent_async(vb, dp)
+        mul(yu, S1.A[0], u)
+        assert t.wait() is vb
+        ga, gb = va.ghost_values(), vb.ghost_values()
+        assert len(ga) == pl.n_ghost > 0 and np.array_equal(ga.view(np.int64), gb.view(np.int64))
+        assert np.array_equal(ga, own[pl.send_idx])  # self-plan ghosts are copies of own entries
+        assert np.array_equal(yu.own_values().view(np.int64), b0.own_values().view(np.int64))
+        t2 = consistent_async(vb, dp)
+        try:
+            consistent_async(va, dp)  # one exchange in flight per plan
+            raise AssertionError("second begin on a busy plan was accepted")
+        except _lib.PamgError as e:
+            assert e.code == -6, e
+        t2.wait()
+        del S1, u, yu
         for graph in (False, True):
             S = AMGSolver(rccl_ctx, Hs, graph=graph)
             assert S.A[0].n_ghost > 0 and S.R[0].n_ghost > 0

@@ -7,16 +7,31 @@ is traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024. Our row kernels mix 16-B/lane
 (columns, values) with 8-B/lane x gathers (uncalibrated width), so the corrected figure is
 an upper bound; the raw counters are kept next to it.
 
-    python tools/pmc_traffic.py FETCH.csv WRITE.csv --kernel 'k_rows_tile2<2' > traffic.json
+    python tools/pmc_traffic.py FETCH.csv WRITE.csv --kernel 'k_rows_tm<2' \
+        --workload poisson3d:512:p1:permNone > profiles/pmc/traffic_jacobi.json
+
+Each record carries the workload key and the sha256 (16 hex digits) of the kernels.hip it was
+measured with; bench.py uses a record only when kernel name, tile count (blocks), workload and
+source hash all match its own run.
 """
 import argparse
 import collections
 import csv
+import hashlib
 import json
+import os
 import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def load(path, counter):
+    if os.path.isdir(path):  # a rocprofv3 -d directory: its (only) counter_collection csv
+        import glob
+        hits = sorted(glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True))
+        if not hits:
+            raise SystemExit(f"no counter_collection.csv under {path}")
+        path = hits[0]
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
@@ -32,8 +47,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch")
     ap.add_argument("write")
-    ap.add_argument("--kernel", default="k_rows_tile2<2")
+    ap.add_argument("--kernel", default="k_rows_tm<2")
+    ap.add_argument("--workload", default="poisson3d:512:p1:permNone",
+                    help="bench.py workload key: kind-or-matrix:grid:p<parts>:perm<seed>")
     a = ap.parse_args()
+    with open(os.path.join(ROOT, "parallel_amg_amd", "csrc", "kernels.hip"), "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
     F, W = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
     out = []
     for (name, blocks), fv in sorted(F.items(), key=lambda kv: -kv[0][1]):
@@ -41,7 +60,8 @@ def main():
             continue
         f = sum(fv) / len(fv)
         w = sum(W[(name, blocks)]) / len(W[(name, blocks)])
-        out.append({"kernel": name, "blocks": blocks, "fetch_kib": f, "write_kib": w,
+        out.append({"kernel": name, "blocks": blocks, "workload": a.workload, "kernels_hip_sha16": sha,
+                    "fetch_kib": f, "write_kib": w,
                     "traffic_bytes": (2 * f + w) * 1024.0,
                     "note": "(2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md §HBM; "
                             "upper bound: 8-B/lane x gathers are doubled too"})

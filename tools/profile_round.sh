@@ -16,10 +16,14 @@ echo "bench done"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv \
     -- python3 -u bench.py --steps 5 --cpu-baseline off > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.log"
 echo "kernel trace done"
-KB="tools/kbench.py --n 512 --levels 1 --ops 0,2 --reps 3 --configs 1:1024:256:0:0:0:1:1:0:1:1:1"
+KB="tools/kbench.py --n 512 --levels 1 --ops 0,2 --reps 3 --configs 1024"
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o fetch --output-format csv \
     -- python3 -u $KB > "$OUT/pmc_fetch.jsonl" 2> "$OUT/pmc_fetch.err"
 echo "fetch pass done"
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o write --output-format csv \
     -- python3 -u $KB > "$OUT/pmc_write.jsonl" 2> "$OUT/pmc_write.err"
 echo "write pass done"
+mkdir -p "$OUT/pmc"
+python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --kernel "k_rows_tm<2" > "$OUT/pmc/traffic_jacobi.json"
+python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --kernel "k_rows_tm<0" > "$OUT/pmc/traffic_spmv.json"
+echo "traffic records in $OUT/pmc (copy to profiles/pmc/ to let bench.py report them)"
