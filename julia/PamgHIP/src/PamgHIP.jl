@@ -20,7 +20,15 @@ using SparseArrays
 
 export Context, ExchangePlan, DeviceVector, DeviceMatrix, HostCSR, VCycle, ExchangeTask, PamgError,
        own_values, ghost_values, consistent!, residual!, jacobi!, vcycle!, pcg!, set_sweeps!,
-       setup_hierarchy, gen_grid, gen_xstar, read_mtx, unique_id, comm_init!, runtime_versions
+       setup_hierarchy, gen_grid, gen_xstar, read_mtx, unique_id, comm_init!, runtime_versions, hip
+
+"""
+    hip(ctxs, A::PSparseMatrix) / hip(ctxs, x::PVector)
+
+Move PartitionedArrays parts onto the GPU(s); methods live in the PartitionedArrays package
+extension (ext/PamgHIPPartitionedArraysExt.jl), loaded when PartitionedArrays is.
+"""
+function hip end
 
 const libpamg = get(ENV, "PAMG_LIB",
                     normpath(joinpath(@__DIR__, "..", "..", "..", "parallel_amg_amd", "libpamg.so")))
@@ -504,6 +512,99 @@ function setup_hierarchy(ctx::Context, A0::HostCSR; theta::Real = 0.02, max_coar
     dP = [DeviceMatrix(ctx, M) for M in P]
     dR = [DeviceMatrix(ctx, M) for M in R]
     VCycle(ctx, dA, dP, dR, omega, ainv; ncycles = ncycles)
+end
+
+# ------------------------------------------------------------------ setup entry points (multi-part)
+# The per-part building blocks of SPEC §S4 with ghost rows, for a distributed setup driven by
+# the caller (parallel_amg_amd/hierarchy.py is the Python version of that driver). Row ids are
+# global and 0-based, as in the C-ABI.
+function gershgorin(A::HostCSR, row0::Integer)
+    rho = Ref{Cdouble}(0.0)
+    check(ccall((:pamg_setup_gershgorin, libpamg), Cint, (Ptr{Cvoid}, Int64, Ptr{Cdouble}), A.h, row0, rho))
+    rho[]
+end
+function aggregate(A::HostCSR, row0::Integer, theta::Real)
+    n = size(A, 1)
+    agg, nagg = Vector{Int32}(undef, n + 1), Ref{Int64}(0)
+    check(ccall((:pamg_setup_aggregate, libpamg), Cint, (Ptr{Cvoid}, Int64, Cdouble, Ptr{Int32}, Ptr{Int64}),
+                A.h, row0, theta, agg, nagg))
+    (agg[1:n], Int(nagg[]))
+end
+function tentative(agg::Vector{Int32}, nagg::Integer, coarse0::Integer, ncols_global::Integer)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:pamg_setup_tentative, libpamg), Cint, (Int64, Ptr{Int32}, Int64, Int64, Int64, Ptr{Ptr{Cvoid}}),
+                length(agg), agg, nagg, coarse0, ncols_global, h))
+    HostCSR(h[])
+end
+"C = X * Y with Y's own rows from y0 and its ghost rows `Yghost` (global ids `ghost_ids`, ascending)."
+function spgemm(X::HostCSR, y0::Integer, Yown::HostCSR, ghost_ids::Vector{Int64} = Int64[],
+                Yghost::Union{Nothing,HostCSR} = nothing; ctx::Union{Nothing,Context} = nothing)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    yg = Yghost === nothing ? C_NULL : Yghost.h
+    if ctx === nothing
+        check(ccall((:pamg_setup_spgemm, libpamg), Cint,
+                    (Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Int64}, Int64, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
+                    X.h, y0, Yown.h, ghost_ids, length(ghost_ids), yg, h))
+    else
+        check(ccall((:pamg_dev_spgemm, libpamg), Cint,
+                    (Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Int64}, Int64, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
+                    ctx.h, X.h, y0, Yown.h, ghost_ids, length(ghost_ids), yg, h))
+    end
+    HostCSR(h[])
+end
+smooth!(AT::HostCSR, A::HostCSR, row0::Integer, T::HostCSR, omega::Real) =
+    (check(ccall((:pamg_setup_smooth, libpamg), Cint, (Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Cvoid}, Cdouble),
+                 A.h, row0, T.h, AT.h, omega)); AT)
+function transpose_piece(P::HostCSR, row0::Integer, c0::Integer, c1::Integer; ctx::Union{Nothing,Context} = nothing)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    if ctx === nothing
+        check(ccall((:pamg_setup_transpose, libpamg), Cint, (Ptr{Cvoid}, Int64, Int64, Int64, Ptr{Ptr{Cvoid}}),
+                    P.h, row0, c0, c1, h))
+    else
+        check(ccall((:pamg_dev_transpose, libpamg), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Int64, Int64, Int64, Ptr{Ptr{Cvoid}}),
+                    ctx.h, P.h, row0, c0, c1, h))
+    end
+    HostCSR(h[])
+end
+function hstack_rows(pieces::Vector{HostCSR})
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    ps = Ptr{Cvoid}[p.h for p in pieces]
+    check(ccall((:pamg_setup_hstack_rows, libpamg), Cint, (Cint, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}), length(ps), ps, h))
+    HostCSR(h[])
+end
+function cholinv(A::HostCSR)
+    n = size(A, 1)
+    ainv = Matrix{Float64}(undef, n, n)
+    check(ccall((:pamg_setup_cholinv, libpamg), Cint, (Ptr{Cvoid}, Ptr{Float64}), A.h, ainv))
+    ainv
+end
+
+# ------------------------------------------------------------------ profiling / micro-benchmarks
+function vec_size(v::DeviceVector)
+    o, g = Ref{Int64}(0), Ref{Int64}(0)
+    check(ccall((:pamg_vec_size, libpamg), Cint, (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int64}), v.h, o, g))
+    (Int(o[]), Int(g[]))
+end
+"ms per (level, op) of `ncycles` eagerly launched V-cycles (HIP events; columns: jacobi_pre, residual, restrict, prolong, jacobi_post, coarse)."
+function profile(x::DeviceVector, M::VCycle, b::DeviceVector, ncycles::Integer)
+    check(ccall((:pamg_hier_profile, libpamg), Cint, (Ptr{Cvoid}, Cint), M.h, 1))
+    try
+        vcycle_async!(x, M, b, ncycles)
+        out = zeros(6 * length(M.A))
+        check(ccall((:pamg_hier_profile_read, libpamg), Cint, (Ptr{Cvoid}, Ptr{Float64}), M.h, out))
+        permutedims(reshape(out, 6, length(M.A)))
+    finally
+        check(ccall((:pamg_hier_profile, libpamg), Cint, (Ptr{Cvoid}, Cint), M.h, 0))
+    end
+end
+"Average ms of `reps` launches of one row operation (0 SpMV, 1 residual, 2 Jacobi, 3 prolongate-add)."
+function bench_rowop(A::DeviceMatrix, op::Integer, x::DeviceVector, b::Union{Nothing,DeviceVector},
+                     y::DeviceVector; omega::Real = 0.0, reps::Integer = 20)
+    ms = Ref{Cdouble}(0.0)
+    check(ccall((:pamg_bench_rowop, libpamg), Cint,
+                (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cdouble, Cint, Ptr{Cdouble}),
+                A.ctx.h, A.h, op, x.h, b === nothing ? C_NULL : b.h, y.h, omega, reps, ms))
+    ms[]
 end
 
 # ------------------------------------------------------------------ knobs

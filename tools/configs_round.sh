@@ -20,3 +20,6 @@ run a256 --kind aniso3d --grid 256
 run a256_tm0 --kind aniso3d --grid 256 --set tile_major=0
 run e80 --kind elastic3d --grid 80
 run e80_tm0 --kind elastic3d --grid 80 --set tile_major=0
+# the Flan_1565 proxy: elastic3d renumbered at random (no column dictionary, no banded order)
+run e80_perm --kind elastic3d --grid 80 --permute 1
+run p128_perm --grid 128 --permute 1
