@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--configs", default="1024:1,1024:0",
                     help="tile_nnz:tile_order:col24:value_dict:long_tiles:row_len8:col_dict:tile_major,...")
     ap.add_argument("--ops", default="0,2")
+    ap.add_argument("--mats", default=None, help="comma list of level matrices to run (e.g. R0,A1); default all")
     args = ap.parse_args()
     ctx = Context(0)
     be = pa.SequentialBackend(1)
@@ -78,6 +79,8 @@ def main():
         set_opts(tile_nnz=tnnz, tile_order=order, col24=c24, value_dict=vd, long_tiles=lt, row_len8=rl8,
                  col_dict=cd, tile_major=tm)
         for name, (M, plan) in mats.items():
+            if args.mats and name not in args.mats.split(","):
+                continue
             D = PSparseMatrix(ctx, M, plan)
             for op in ops:
                 if op == 2 and not name.startswith("A"):
