@@ -3,8 +3,13 @@ skip setup"). The parts a process holds (all of them for SequentialBackend, its 
 DistributedBackend) go to one ``.npz`` of plain arrays — no pickle — and load back into a
 HostHierarchy that AMGSolver uploads exactly like a freshly built one.
 
-    save_hierarchy(H, "h512.npz")          # every rank its own file under DistributedBackend
-    H = load_hierarchy("h512.npz")
+    save_hierarchy(H, "h512.npz")                        # SequentialBackend: every part in one file
+    save_hierarchy(H, "h512_{rank}.npz")                 # DistributedBackend: one file per rank
+    H = load_hierarchy("h512_{rank}.npz", backend=be)    # checks the parts match be.parts
+
+A hierarchy that holds only some of its parts (DistributedBackend) must be saved under a path
+with a ``{rank}`` placeholder (filled with the first part it holds), so ranks on a shared
+filesystem never overwrite each other's file.
 """
 from __future__ import annotations
 
@@ -56,7 +61,18 @@ def _get_plan(z, key):
     return P
 
 
+def _resolve(path: str, parts) -> str:
+    if "{rank}" in path:
+        return path.replace("{rank}", str(min(parts)))
+    return path
+
+
 def save_hierarchy(H: HostHierarchy, path: str) -> None:
+    parts = sorted(H.levels[0])
+    if len(parts) < H.nparts and "{rank}" not in path:
+        raise ValueError(f"{path}: this hierarchy holds parts {parts} of {H.nparts}; save it under a "
+                         "path with a '{rank}' placeholder so every rank writes its own file")
+    path = _resolve(path, parts)
     d = {"version": np.int64(_VERSION), "nparts": np.int64(H.nparts), "nlevels": np.int64(H.nlevels),
          "parts": np.asarray(sorted(H.levels[0]), np.int64), "ainv": np.asarray(H.ainv, np.float64),
          "n_coarse": np.int64(H.n_coarse), "rep_level": np.int64(H.rep_level),
@@ -76,11 +92,19 @@ def save_hierarchy(H: HostHierarchy, path: str) -> None:
         np.savez(f, **d)
 
 
-def load_hierarchy(path: str) -> HostHierarchy:
+def load_hierarchy(path: str, backend=None) -> HostHierarchy:
+    """Load a saved hierarchy; with ``backend`` the file must hold exactly ``backend.parts``
+    (and ``{rank}`` in the path is filled with the backend's first part)."""
+    if backend is not None:
+        path = _resolve(path, backend.parts)
+    elif "{rank}" in path:
+        raise ValueError(f"{path}: a '{{rank}}' path needs the backend to resolve it")
     with np.load(path, allow_pickle=False) as z:
         if int(z["version"]) != _VERSION:
             raise ValueError(f"{path}: hierarchy file version {int(z['version'])} != {_VERSION}")
         parts = [int(p) for p in z["parts"]]
+        if backend is not None and sorted(backend.parts) != parts:
+            raise ValueError(f"{path}: holds parts {parts}, the backend has {sorted(backend.parts)}")
         levels = []
         for l in range(int(z["nlevels"])):
             lev = {}

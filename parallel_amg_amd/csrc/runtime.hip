@@ -6,10 +6,16 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pamg_device.h"
@@ -65,6 +71,86 @@ int set_device(const pamg_ctx* ctx) {
     HIPC(hipSetDevice(ctx->device));
     return PAMG_OK;
 }
+
+// ---- host side of the upload: threads for the per-nonzero passes, pinned staging for copies
+// Threads: OMP_NUM_THREADS if set (16 on the GPU box), else the hardware count, at most 64.
+int host_threads() {
+    static const int n = [] {
+        const char* e = std::getenv("OMP_NUM_THREADS");
+        int v = e ? std::atoi(e) : 0;
+        if (v <= 0) v = (int)std::thread::hardware_concurrency();
+        return std::max(1, std::min(v, 64));
+    }();
+    return n;
+}
+
+// f(begin, end) over [0, n) in contiguous chunks, one per thread (each chunk's work is
+// independent of the others; results are the same for any thread count)
+template <class F>
+void par_for(int64_t n, F&& f) {
+    const int nt = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, n / 16384));
+    if (nt <= 1) {
+        if (n > 0) f((int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(nt);
+    for (int t = 0; t < nt; ++t) {
+        const int64_t a = n * t / nt, b = n * (t + 1) / nt;
+        th.emplace_back([&f, a, b] { f(a, b); });
+    }
+    for (auto& x : th) x.join();
+}
+
+// Host-to-device copy of a large pageable buffer through two pinned 64 MiB staging buffers:
+// threads copy chunk k into one while the DMA engine moves chunk k-1 out of the other.
+int h2d(pamg_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    constexpr size_t kChunk = size_t(64) << 20;
+    if (bytes == 0) return PAMG_OK;
+    if (bytes < (size_t(4) << 20)) {
+        HIPC(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+        return PAMG_OK;
+    }
+    static std::mutex mu;
+    static char* stage[2] = {nullptr, nullptr};
+    static hipEvent_t done[2] = {nullptr, nullptr};
+    std::lock_guard<std::mutex> lock(mu);
+    for (int k = 0; k < 2; ++k) {
+        if (!stage[k]) HIPC(hipHostMalloc(reinterpret_cast<void**>(&stage[k]), kChunk, hipHostMallocPortable));
+        if (!done[k]) HIPC(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
+    }
+    hipStream_t s = ctx->s_comp;
+    size_t off = 0;
+    for (int k = 0; off < bytes; k ^= 1) {
+        const size_t m = std::min(kChunk, bytes - off);
+        HIPC(hipEventSynchronize(done[k]));  // the DMA out of this buffer has finished
+        const char* from = static_cast<const char*>(src) + off;
+        char* to = stage[k];
+        par_for((int64_t)((m + 4095) / 4096), [&](int64_t a, int64_t b) {
+            const size_t lo = (size_t)a * 4096, hi = std::min(m, (size_t)b * 4096);
+            std::memcpy(to + lo, from + lo, hi - lo);
+        });
+        HIPC(hipMemcpyAsync(static_cast<char*>(dst) + off, to, m, hipMemcpyHostToDevice, s));
+        HIPC(hipEventRecord(done[k], s));
+        off += m;
+    }
+    HIPC(hipStreamSynchronize(s));
+    return PAMG_OK;
+}
+
+// PAMG_TRACE_UPLOAD=1: per-phase host times of each matrix upload on stderr
+struct UploadTrace {
+    bool on = std::getenv("PAMG_TRACE_UPLOAD") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    int64_t nnz = 0;
+    void mark(const char* what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[pamg upload nnz=%lld] %-14s %8.3f s\n", (long long)nnz, what,
+                     std::chrono::duration<double>(now - t).count());
+        t = now;
+    }
+};
 
 // Greedy tiling of the rows listed in `rows` (ascending) into runs of consecutive rows with
 // <= kTileRows rows and <= tile_nnz nonzeros; rows above the budget become "long" rows.
@@ -180,30 +266,35 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
     // not for tiles that reach the ghost columns of a large part)
     ts->c24 = false;
     if (opt.col24 && !tiles.empty()) {
-        std::vector<int> base(tiles.size(), 0);
-        bool fits = true;
-        for (size_t t = 0; t < tiles.size() && fits; ++t) {
-            const int4 d = tiles[t];
-            int mn = INT32_MAX, mx = 0;
-            for (int k = d.z; k < d.w; ++k) {
-                mn = std::min(mn, ci[k]);
-                mx = std::max(mx, ci[k]);
+        const int64_t nt = (int64_t)tiles.size();
+        std::vector<int> base(nt, 0);
+        std::vector<char> fit(nt, 1);
+        par_for(nt, [&](int64_t a, int64_t b) {
+            for (int64_t t = a; t < b; ++t) {
+                const int4 d = tiles[t];
+                int mn = INT32_MAX, mx = 0;
+                for (int k = d.z; k < d.w; ++k) {
+                    mn = std::min(mn, ci[k]);
+                    mx = std::max(mx, ci[k]);
+                }
+                if (d.w == d.z) mn = mx = 0;
+                base[t] = mn;
+                fit[t] = (int64_t)mx - mn < (int64_t(1) << 24);
             }
-            if (d.w == d.z) mn = mx = 0;
-            base[t] = mn;
-            fits = (int64_t)mx - mn < (int64_t(1) << 24);
-        }
-        if (fits) {
+        });
+        if (std::all_of(fit.begin(), fit.end(), [](char f) { return f != 0; })) {
             if (lo->empty()) {
                 lo->assign(ci.size(), 0);
                 hi->assign(ci.size(), 0);
             }
-            for (size_t t = 0; t < tiles.size(); ++t)
-                for (int k = tiles[t].z; k < tiles[t].w; ++k) {
-                    const uint32_t dlt = (uint32_t)(ci[k] - base[t]);
-                    (*lo)[k] = (uint16_t)(dlt & 0xffffu);
-                    (*hi)[k] = (uint8_t)(dlt >> 16);
-                }
+            par_for(nt, [&](int64_t a, int64_t b) {
+                for (int64_t t = a; t < b; ++t)
+                    for (int k = tiles[t].z; k < tiles[t].w; ++k) {
+                        const uint32_t dlt = (uint32_t)(ci[k] - base[t]);
+                        (*lo)[k] = (uint16_t)(dlt & 0xffffu);
+                        (*hi)[k] = (uint8_t)(dlt >> 16);
+                    }
+            });
             CHECK(dalloc(&ts->d_base, (int64_t)tiles.size()));
             HIPC(hipMemcpy(ts->d_base, base.data(), sizeof(int) * base.size(), hipMemcpyHostToDevice));
             ts->c24 = true;
@@ -246,32 +337,67 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
         if (!opt.col_dict || ts->vd || ts->n_short == 0 || ts->max_short_len > 255)
             continue;
         if (idx.empty()) idx.assign((size_t)A->nnz + kVecPad, 0);
-        // open-addressing map offset -> table slot (1024 cells for <= 256 keys)
+        // Distinct offsets in first-occurrence order (tile order, then storage order): every
+        // chunk of tiles lists its own (<= 257) in parallel, the lists are merged in chunk
+        // order — the same table a single sequential pass builds.
+        const std::vector<int4>& tiles = *tl[q];
+        const int64_t nt = (int64_t)tiles.size();
+        const int nch = std::max(1, std::min<int>(host_threads(), (int)(nt / 64)));
+        std::vector<std::vector<int>> firsts(nch);
+        auto scan = [&](int64_t a, int64_t b, std::vector<int>& out) {
+            constexpr int kCells = 1024;  // open addressing: offset -> seen
+            int key[kCells];
+            bool used[kCells] = {};
+            for (int64_t t = a; t < b && out.size() <= 256; ++t)
+                for (int r = tiles[t].x; r < tiles[t].y; ++r)
+                    for (int64_t k = rp[r]; k < rp[r + 1]; ++k) {
+                        const int o = ci[k] - r;
+                        uint32_t h = ((uint32_t)o * 0x9E3779B1u) >> 22;
+                        while (used[h] && key[h] != o) h = (h + 1) & (kCells - 1);
+                        if (!used[h]) {
+                            used[h] = true;
+                            key[h] = o;
+                            out.push_back(o);
+                            if (out.size() > 256) return;
+                        }
+                    }
+        };
+        {
+            std::vector<std::thread> th;
+            for (int c = 0; c < nch; ++c)
+                th.emplace_back([&, c] { scan(nt * c / nch, nt * (c + 1) / nch, firsts[c]); });
+            for (auto& x : th) x.join();
+        }
         constexpr int kCells = 1024;
         int key[kCells], slot[kCells];
         std::fill(slot, slot + kCells, -1);
+        auto find = [&](int o) {
+            uint32_t h = ((uint32_t)o * 0x9E3779B1u) >> 22;
+            while (slot[h] >= 0 && key[h] != o) h = (h + 1) & (kCells - 1);
+            return h;
+        };
         bool ok = true;
-        for (const int4& t : *tl[q]) {
-            for (int r = t.x; r < t.y && ok; ++r) {
-                for (int64_t k = rp[r]; k < rp[r + 1]; ++k) {
-                    const int o = ci[k] - r;
-                    uint32_t h = ((uint32_t)o * 0x9E3779B1u) >> 22;
-                    while (slot[h] >= 0 && key[h] != o) h = (h + 1) & (kCells - 1);
-                    if (slot[h] < 0) {
-                        if (tab[q].size() == 256) {
-                            ok = false;
-                            break;
-                        }
-                        key[h] = o;
-                        slot[h] = (int)tab[q].size();
-                        tab[q].push_back(o);
-                    }
-                    idx[k] = (uint8_t)slot[h];
+        for (int c = 0; c < nch && ok; ++c)
+            for (int o : firsts[c]) {
+                const uint32_t h = find(o);
+                if (slot[h] >= 0) continue;
+                if (tab[q].size() == 256) {
+                    ok = false;
+                    break;
                 }
+                key[h] = o;
+                slot[h] = (int)tab[q].size();
+                tab[q].push_back(o);
             }
-            if (!ok) break;
+        if (!ok) {
+            tab[q].clear();
+            continue;
         }
-        if (!ok) tab[q].clear();
+        par_for(nt, [&](int64_t a, int64_t b) {
+            for (int64_t t = a; t < b; ++t)
+                for (int r = tiles[t].x; r < tiles[t].y; ++r)
+                    for (int64_t k = rp[r]; k < rp[r + 1]; ++k) idx[k] = (uint8_t)slot[find(ci[k] - r)];
+        });
     }
     int width = 0;
     for (int q = 0; q < 2; ++q)
@@ -290,12 +416,18 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
     }
     if (width == 4) {
         std::vector<uint8_t> nib(((size_t)A->nnz + 1) / 2 + kVecPad, 0);
-        for (int64_t k = 0; k < A->nnz; ++k) nib[k >> 1] |= (uint8_t)((idx[k] & 15) << (4 * (k & 1)));
+        const int64_t nb = (A->nnz + 1) / 2;
+        par_for(nb, [&](int64_t a, int64_t b) {
+            for (int64_t j = a; j < b; ++j) {
+                const int64_t k = 2 * j;
+                nib[j] = (uint8_t)((idx[k] & 15) | (k + 1 < A->nnz ? (idx[k + 1] & 15) << 4 : 0));
+            }
+        });
         CHECK(dalloc(&A->d_cidx, (int64_t)nib.size()));
-        HIPC(hipMemcpy(A->d_cidx, nib.data(), nib.size(), hipMemcpyHostToDevice));
+        CHECK(h2d(A->ctx, A->d_cidx, nib.data(), nib.size()));
     } else {
         CHECK(dalloc(&A->d_cidx, (int64_t)idx.size()));
-        HIPC(hipMemcpy(A->d_cidx, idx.data(), idx.size(), hipMemcpyHostToDevice));
+        CHECK(h2d(A->ctx, A->d_cidx, idx.data(), idx.size()));
     }
     idx8->swap(idx);
     return PAMG_OK;
@@ -334,42 +466,55 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
         int rs = 0;
         for (const int4& t : tiles) rs = std::max(rs, t.y - t.x);
         rs = (rs + 3) & ~3;
-        std::vector<double> tv((size_t)(nt * tn + kVecPad), 0.0);
-        std::vector<uint8_t> trl((size_t)(nt * rs + kVecPad), 0);
-        std::vector<uint8_t> tci, tch;
-        std::vector<uint16_t> tcl;
-        if (ts->cd == 4) tci.assign((size_t)(nt * tn / 2 + kVecPad), 0);
-        else if (ts->cd == 8) tci.assign((size_t)(nt * tn + kVecPad), 0);
-        else {
-            tcl.assign((size_t)(nt * tn + kVecPad), 0);
-            tch.assign((size_t)(nt * tn + kVecPad), 0);
-        }
-        for (int64_t i = 0; i < nt; ++i) {
-            const int4 t = tiles[i];
-            for (int r = t.x; r < t.y; ++r) trl[i * rs + (r - t.x)] = (uint8_t)(rp[r + 1] - rp[r]);
-            for (int k = t.z; k < t.w; ++k) {
-                const int64_t p = i * tn + (k - t.z);
-                tv[p] = val[k];
-                if (ts->cd == 4) tci[p >> 1] |= (uint8_t)((idx8[k] & 15) << (4 * (p & 1)));
-                else if (ts->cd == 8) tci[p] = idx8[k];
-                else {
-                    tcl[p] = lo[k];
-                    tch[p] = hi[k];
+        // every slot is written whole (nonzeros, then zero padding) by the thread that owns its
+        // tile, so the buffers need no serial zero fill
+        const int cdw = ts->cd;
+        std::unique_ptr<double[]> tv(new double[nt * tn + kVecPad]);
+        std::unique_ptr<uint8_t[]> trl(new uint8_t[nt * rs + kVecPad]);
+        const int64_t ncb = cdw == 4 ? tn / 2 : tn;  // column-stream bytes per slot (cd / chi)
+        std::unique_ptr<uint8_t[]> tci(new uint8_t[nt * ncb + kVecPad]);
+        std::unique_ptr<uint16_t[]> tcl(cdw ? nullptr : new uint16_t[nt * tn + kVecPad]);
+        par_for(nt, [&](int64_t a, int64_t b) {
+            for (int64_t i = a; i < b; ++i) {
+                const int4 t = tiles[i];
+                const int cnt = t.w - t.z;
+                uint8_t* rl = &trl[i * rs];
+                for (int r = 0; r < rs; ++r) rl[r] = t.x + r < t.y ? (uint8_t)(rp[t.x + r + 1] - rp[t.x + r]) : 0;
+                double* v = &tv[i * tn];
+                std::memcpy(v, val + t.z, sizeof(double) * cnt);
+                std::fill(v + cnt, v + tn, 0.0);
+                uint8_t* c = &tci[i * ncb];
+                if (cdw == 4) {
+                    std::fill(c, c + ncb, (uint8_t)0);
+                    for (int k = 0; k < cnt; ++k) c[k >> 1] |= (uint8_t)((idx8[t.z + k] & 15) << (4 * (k & 1)));
+                } else if (cdw == 8) {
+                    std::memcpy(c, &idx8[t.z], cnt);
+                    std::fill(c + cnt, c + tn, (uint8_t)0);
+                } else {
+                    uint16_t* l = &tcl[i * tn];
+                    std::memcpy(l, &lo[t.z], sizeof(uint16_t) * cnt);
+                    std::fill(l + cnt, l + tn, (uint16_t)0);
+                    std::memcpy(c, &hi[t.z], cnt);
+                    std::fill(c + cnt, c + tn, (uint8_t)0);
                 }
             }
-        }
-        CHECK(dalloc(&ts->d_tm_val, (int64_t)tv.size()));
-        HIPC(hipMemcpy(ts->d_tm_val, tv.data(), sizeof(double) * tv.size(), hipMemcpyHostToDevice));
-        CHECK(dalloc(&ts->d_tm_rlen, (int64_t)trl.size()));
-        HIPC(hipMemcpy(ts->d_tm_rlen, trl.data(), trl.size(), hipMemcpyHostToDevice));
-        if (!tci.empty()) {
-            CHECK(dalloc(&ts->d_tm_cidx, (int64_t)tci.size()));
-            HIPC(hipMemcpy(ts->d_tm_cidx, tci.data(), tci.size(), hipMemcpyHostToDevice));
+        });
+        std::fill(&tv[nt * tn], &tv[nt * tn] + kVecPad, 0.0);
+        std::fill(&trl[nt * rs], &trl[nt * rs] + kVecPad, (uint8_t)0);
+        std::fill(&tci[nt * ncb], &tci[nt * ncb] + kVecPad, (uint8_t)0);
+        if (tcl) std::fill(&tcl[nt * tn], &tcl[nt * tn] + kVecPad, (uint16_t)0);
+        CHECK(dalloc(&ts->d_tm_val, nt * tn + kVecPad));
+        CHECK(h2d(A->ctx, ts->d_tm_val, tv.get(), sizeof(double) * (nt * tn + kVecPad)));
+        CHECK(dalloc(&ts->d_tm_rlen, nt * rs + kVecPad));
+        CHECK(h2d(A->ctx, ts->d_tm_rlen, trl.get(), nt * rs + kVecPad));
+        if (cdw) {
+            CHECK(dalloc(&ts->d_tm_cidx, nt * ncb + kVecPad));
+            CHECK(h2d(A->ctx, ts->d_tm_cidx, tci.get(), nt * ncb + kVecPad));
         } else {
-            CHECK(dalloc(&ts->d_tm_clo, (int64_t)tcl.size()));
-            CHECK(dalloc(&ts->d_tm_chi, (int64_t)tch.size()));
-            HIPC(hipMemcpy(ts->d_tm_clo, tcl.data(), sizeof(uint16_t) * tcl.size(), hipMemcpyHostToDevice));
-            HIPC(hipMemcpy(ts->d_tm_chi, tch.data(), tch.size(), hipMemcpyHostToDevice));
+            CHECK(dalloc(&ts->d_tm_clo, nt * tn + kVecPad));
+            CHECK(dalloc(&ts->d_tm_chi, nt * tn + kVecPad));
+            CHECK(h2d(A->ctx, ts->d_tm_clo, tcl.get(), sizeof(uint16_t) * (nt * tn + kVecPad)));
+            CHECK(h2d(A->ctx, ts->d_tm_chi, tci.get(), nt * tn + kVecPad));
         }
         ts->tm_rs = rs;
         ts->tm = true;
@@ -1022,18 +1167,37 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         return fail(PAMG_E_ARG, "mat_upload: ncols %lld != plan own+ghost %lld", (long long)ncols,
                     (long long)(plan->n_own + plan->n_ghost));
     CHECK(set_device(ctx));
+    UploadTrace tr;
+    tr.nnz = nnz;
     std::vector<int64_t> rp(nrows + 1);
     std::vector<int> ci(nnz + kVecPad, 0);
     for (int64_t i = 0; i <= nrows; ++i) rp[i] = rowptr[i] - index_base;
     for (int64_t i = 0; i < nrows; ++i)
         if (rp[i + 1] < rp[i]) return fail(PAMG_E_ARG, "mat_upload: rowptr not monotone at %lld", (long long)i);
     if (rp[0] != 0) return fail(PAMG_E_ARG, "mat_upload: rowptr[0] != index_base");
-    for (int64_t k = 0; k < nnz; ++k) {
-        const int64_t c = (col_is_64 ? static_cast<const int64_t*>(col)[k]
-                                     : (int64_t) static_cast<const int32_t*>(col)[k]) - index_base;
-        if (c < 0 || c >= ncols) return fail(PAMG_E_ARG, "mat_upload: column %lld out of range", (long long)c);
-        ci[k] = (int)c;
+    {
+        std::atomic<int64_t> bad_at{INT64_MAX};
+        par_for(nnz, [&](int64_t a, int64_t b) {
+            for (int64_t k = a; k < b; ++k) {
+                const int64_t c = (col_is_64 ? static_cast<const int64_t*>(col)[k]
+                                             : (int64_t) static_cast<const int32_t*>(col)[k]) - index_base;
+                if (c < 0 || c >= ncols) {
+                    int64_t cur = bad_at.load();
+                    while (k < cur && !bad_at.compare_exchange_weak(cur, k)) {
+                    }
+                    return;
+                }
+                ci[k] = (int)c;
+            }
+        });
+        if (bad_at.load() != INT64_MAX) {
+            const int64_t k = bad_at.load();
+            const int64_t c = (col_is_64 ? static_cast<const int64_t*>(col)[k]
+                                         : (int64_t) static_cast<const int32_t*>(col)[k]) - index_base;
+            return fail(PAMG_E_ARG, "mat_upload: column %lld out of range", (long long)c);
+        }
     }
+    tr.mark("columns");
     // released through pamg_mat_destroy on every error path (no device memory leaks)
     std::unique_ptr<pamg_mat, int (*)(pamg_mat*)> A(new pamg_mat, pamg_mat_destroy);
     A->ctx = ctx;
@@ -1041,33 +1205,47 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     A->ncols = ncols;
     A->nnz = nnz;
     A->plan = plan;
-    // classify rows: interior (own columns only) or boundary (>= 1 ghost column). Also the
-    // row distance at which rows share x entries, for the banded tile order: per own column
-    // the largest gap between consecutive rows that read it (one grid plane for a stencil,
-    // one aggregate layer for a restriction); band = its 90th percentile over the columns.
+    // classify rows: interior (own columns only) or boundary (>= 1 ghost column), and find
+    // the diagonal (threads over row ranges)
     std::vector<int> inner, bnd;
     std::vector<double> diag(nrows, 0.0);
-    bool has_all_diag = (n_own_cols == nrows);
-    std::vector<int> last_row(n_own_cols, -1), max_gap(n_own_cols, 0);
-    for (int64_t i = 0; i < nrows; ++i) {
-        bool g = false, d = false;
-        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-            const int c = ci[k];
-            g |= c >= n_own_cols;
-            if (c < n_own_cols) {
-                if (last_row[c] >= 0) max_gap[c] = std::max(max_gap[c], (int)i - last_row[c]);
-                last_row[c] = (int)i;
+    std::vector<char> ghost_row(nrows, 0);
+    std::atomic<bool> has_all_diag{n_own_cols == nrows};
+    par_for(nrows, [&](int64_t a, int64_t b) {
+        bool all = true;
+        for (int64_t i = a; i < b; ++i) {
+            bool g = false, d = false;
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                const int c = ci[k];
+                g |= c >= n_own_cols;
+                if (c == i && n_own_cols == nrows) {
+                    diag[i] = val[k];
+                    d = true;
+                }
             }
-            if (c == i && n_own_cols == nrows) {
-                diag[i] = val[k];
-                d = true;
-            }
+            if (!d || diag[i] == 0.0) all = false;
+            ghost_row[i] = g;
         }
-        if (!d || diag[i] == 0.0) has_all_diag = false;
-        (g ? bnd : inner).push_back((int)i);
-    }
+        if (!all) has_all_diag = false;
+    });
+    for (int64_t i = 0; i < nrows; ++i) (ghost_row[i] ? bnd : inner).push_back((int)i);
+    std::vector<char>().swap(ghost_row);
+    tr.mark("classify");
+    // The row distance at which rows share x entries, for the banded tile order: per own
+    // column the largest gap between consecutive rows that read it (one grid plane for a
+    // stencil, one aggregate layer for a restriction); band = its 90th percentile over the
+    // columns. (Sequential: the gaps depend on the row order.)
     int64_t band = 0;
     {
+        std::vector<int> last_row(n_own_cols, -1), max_gap(n_own_cols, 0);
+        for (int64_t i = 0; i < nrows; ++i)
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                const int c = ci[k];
+                if (c < n_own_cols) {
+                    if (last_row[c] >= 0) max_gap[c] = std::max(max_gap[c], (int)i - last_row[c]);
+                    last_row[c] = (int)i;
+                }
+            }
         std::vector<int>().swap(last_row);
         auto end = std::remove(max_gap.begin(), max_gap.end(), 0);
         const size_t m = (size_t)(end - max_gap.begin());
@@ -1077,38 +1255,45 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
             band = *q;
         }
     }
+    tr.mark("band");
     std::vector<int> rp32(nrows + 1);
     for (int64_t i = 0; i <= nrows; ++i) rp32[i] = (int)rp[i];
     CHECK(dalloc(&A->d_rowptr, nrows + 1));
     CHECK(dalloc(&A->d_col, nnz + kVecPad));
     CHECK(dalloc(&A->d_val, nnz + kVecPad));
-    HIPC(hipMemcpy(A->d_rowptr, rp32.data(), sizeof(int) * (nrows + 1), hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(A->d_col, ci.data(), sizeof(int) * (nnz + kVecPad), hipMemcpyHostToDevice));
+    CHECK(h2d(ctx, A->d_rowptr, rp32.data(), sizeof(int) * (nrows + 1)));
+    CHECK(h2d(ctx, A->d_col, ci.data(), sizeof(int) * (nnz + kVecPad)));
     HIPC(hipMemset(A->d_val, 0, sizeof(double) * (nnz + kVecPad)));
-    if (nnz) HIPC(hipMemcpy(A->d_val, val, sizeof(double) * nnz, hipMemcpyHostToDevice));
+    if (nnz) CHECK(h2d(ctx, A->d_val, val, sizeof(double) * nnz));
     if (has_all_diag && nrows > 0) {
         CHECK(dalloc(&A->d_diag, nrows));
-        HIPC(hipMemcpy(A->d_diag, diag.data(), sizeof(double) * nrows, hipMemcpyHostToDevice));
+        CHECK(h2d(ctx, A->d_diag, diag.data(), sizeof(double) * nrows));
     }
+    tr.mark("csr copies");
     std::vector<uint16_t> lo;
     std::vector<uint8_t> hi, vidx;
     {
         std::vector<int4> t_in, t_bd;
         CHECK(build_tiles(rp, inner, &A->interior, band, ci, &lo, &hi, val, &vidx, &t_in));
         CHECK(build_tiles(rp, bnd, &A->boundary, band, ci, &lo, &hi, val, &vidx, &t_bd));
+        tr.mark("tiles");
         std::vector<uint8_t> idx8;
         CHECK(build_col_dicts(A.get(), rp, ci, t_in, t_bd, &idx8));
+        tr.mark("col dicts");
         CHECK(build_tile_major(A.get(), n_own_cols, rp, val, t_in, t_bd, lo, hi, idx8));
+        tr.mark("tile-major");
     }
     if (A->interior.rl8 || A->boundary.rl8) {
         std::vector<uint8_t> rl(nrows + kVecPad, 0);
-        for (int64_t i = 0; i < nrows; ++i) rl[i] = (uint8_t)std::min<int64_t>(255, rp[i + 1] - rp[i]);
+        par_for(nrows, [&](int64_t a, int64_t b) {
+            for (int64_t i = a; i < b; ++i) rl[i] = (uint8_t)std::min<int64_t>(255, rp[i + 1] - rp[i]);
+        });
         CHECK(dalloc(&A->d_rlen, nrows + kVecPad));
-        HIPC(hipMemcpy(A->d_rlen, rl.data(), rl.size(), hipMemcpyHostToDevice));
+        CHECK(h2d(ctx, A->d_rlen, rl.data(), rl.size()));
     }
     if (!vidx.empty()) {
         CHECK(dalloc(&A->d_vidx, (int64_t)vidx.size()));
-        HIPC(hipMemcpy(A->d_vidx, vidx.data(), vidx.size(), hipMemcpyHostToDevice));
+        CHECK(h2d(ctx, A->d_vidx, vidx.data(), vidx.size()));
     }
     // the bytes one apply streams, per tile set: long rows (row pointer, 12 B/nonzero, list
     // entry) + short tiles in their layout — row bounds (1 B/row with 8-bit lengths, else 4-B
@@ -1139,9 +1324,10 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         hi.resize(nnz + kVecPad, 0);
         CHECK(dalloc(&A->d_clo, nnz + kVecPad));
         CHECK(dalloc(&A->d_chi, nnz + kVecPad));
-        HIPC(hipMemcpy(A->d_clo, lo.data(), sizeof(uint16_t) * lo.size(), hipMemcpyHostToDevice));
-        HIPC(hipMemcpy(A->d_chi, hi.data(), sizeof(uint8_t) * hi.size(), hipMemcpyHostToDevice));
+        CHECK(h2d(ctx, A->d_clo, lo.data(), sizeof(uint16_t) * lo.size()));
+        CHECK(h2d(ctx, A->d_chi, hi.data(), sizeof(uint8_t) * hi.size()));
     }
+    tr.mark("rest");
     *out = A.release();
     return PAMG_OK;
 }

@@ -71,3 +71,63 @@ def test_reloaded_hierarchy_solves_identically(tmp_path, ctx):
         S.vcycle(x, b, 5)
         out.append(x.own_values())
     assert np.array_equal(bits(out[0]), bits(out[1]))
+
+
+def _ckpt_worker(rank, world, port, path, q):
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import parallel_amg_amd as pa
+        be = pa.DistributedBackend()
+        A, offs, _ = pa.generate_problem(be, "poisson3d", 12)
+        H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=40))
+        try:  # a partial hierarchy needs the {rank} placeholder
+            pa.save_hierarchy(H, path.replace("{rank}", "shared"))
+            raise AssertionError("saved a partial hierarchy to a shared path")
+        except ValueError:
+            pass
+        pa.save_hierarchy(H, path)
+        dist.barrier()
+        G = pa.load_hierarchy(path, backend=be)
+        assert sorted(G.levels[0]) == [rank] and G.nlevels == H.nlevels
+        for l in range(H.nlevels):
+            same_csr(H.levels[l][rank].A, G.levels[l][rank].A)
+            same_plan(H.levels[l][rank].planA, G.levels[l][rank].planA)
+        other = pa.SequentialBackend(world)  # holds every part: the file of one rank must not load
+        try:
+            pa.load_hierarchy(path, backend=other)
+            raise AssertionError("loaded one rank's file for all parts")
+        except ValueError:
+            pass
+        q.put((rank, "ok"))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_distributed_roundtrip_one_file_per_rank(tmp_path, built):
+    """DistributedBackend (gloo, 2 ranks): each rank saves its own part under a '{rank}' path and
+    loads it back; a shared path or a mismatching backend is refused."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    path = str(tmp_path / "h_{rank}.npz")
+    procs = [ctx.Process(target=_ckpt_worker, args=(r, 2, port, path, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}, res
+    assert sorted(f.name for f in tmp_path.iterdir()) == ["h_0.npz", "h_1.npz"]

@@ -57,6 +57,8 @@ def main():
                     help="tile_nnz:tile_order:col24:value_dict:long_tiles:row_len8:col_dict:tile_major,...")
     ap.add_argument("--ops", default="0,2")
     ap.add_argument("--mats", default=None, help="comma list of level matrices to run (e.g. R0,A1); default all")
+    ap.add_argument("--ab", default=None,
+                    help="launch-time option to A/B on the same upload (e.g. stream_nt): runs 0,1,0,1")
     args = ap.parse_args()
     ctx = Context(0)
     be = pa.SequentialBackend(1)
@@ -87,11 +89,19 @@ def main():
                     continue
                 if op == 3 and not name.startswith("P"):
                     continue
-                ms, byt, fbyt = bench(ctx, D, op, args.reps)
-                # GBps: SURVEY §8(d) CSR bytes; format_GBps: the bytes the uploaded layout streams
-                print(json.dumps({"cfg": cfg, "mat": name, "op": OPNAME[op], "rows": D.nrows, "nnz": D.nnz,
-                                  "ms": round(ms, 4), "GBps": round(byt / ms / 1e6, 1),
-                                  "format_GBps": round(fbyt / ms / 1e6, 1)}), flush=True)
+                for abv in ((0, 1, 0, 1) if args.ab else (None,)):
+                    if abv is not None:
+                        set_opts(**{args.ab: abv})
+                    ms, byt, fbyt = bench(ctx, D, op, args.reps)
+                    # GBps: SURVEY §8(d) CSR bytes; format_GBps: the bytes the uploaded layout streams
+                    rec = {"cfg": cfg, "mat": name, "op": OPNAME[op], "rows": D.nrows, "nnz": D.nnz,
+                           "ms": round(ms, 4), "GBps": round(byt / ms / 1e6, 1),
+                           "format_GBps": round(fbyt / ms / 1e6, 1)}
+                    if abv is not None:
+                        rec[args.ab] = abv
+                    print(json.dumps(rec), flush=True)
+                if args.ab:
+                    set_opts(**{args.ab: 0})
             del D
 
 
