@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpamg.so")
+# PAMG_LIB (dev A/B only): load another build of the same ABI, e.g. gpurun_ab/libpamg_a.so
+LIB_PATH = os.environ.get("PAMG_LIB") or os.path.join(_HERE, "libpamg.so")
 
 PAMG_OK = 0
 ERRORS = {-1: "PAMG_E_ARG", -2: "PAMG_E_HIP", -3: "PAMG_E_RCCL", -4: "PAMG_E_OVERFLOW",
@@ -166,11 +167,11 @@ def call(name, *args):
 
 def layout_of(M, part_set: int = 0) -> dict:
     """The tile layout libpamg chose at upload for a device matrix (pamg_mat_layout)."""
-    out = (C.c_int * 9)()
+    out = (C.c_int * 10)()
     call("pamg_mat_layout", M.handle, part_set, out)
     return {"c24": bool(out[0]), "vd": bool(out[1]), "rl8": bool(out[2]), "cd": int(out[3]),
             "cd_offsets": int(out[4]), "tm": bool(out[5]), "tm_rs": int(out[6]),
-            "tile_nnz": int(out[7]), "tiles": int(out[8])}
+            "tile_nnz": int(out[7]), "tiles": int(out[8]), "anchored": bool(out[9])}
 
 
 def last_error() -> str:

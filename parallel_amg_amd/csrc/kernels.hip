@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     // tile set's <= 16 / <= 256 distinct offsets (a stencil's 7 for A0) in LDS; every
     // position's row (lrow, tile-local) is marked by the lane that owns the row (RL8 scan)
     static_assert(CD == 0 || (RL8 && !C24 && !VD), "column dictionary: 8-bit rows, plain values");
-    __shared__ int ltab[CD == 8 ? 256 : 16];
+    __shared__ int ltab[CD != 0 ? BS : 1];
     __shared__ __attribute__((aligned(4))) uint8_t lrow[CD ? TNNZ + 8 : 4];
 
     const int bid = blockIdx.x;
@@ -141,6 +141,17 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     const int r0 = t.x, nr = t.y - t.x, z0 = t.z, z1 = t.w;
     const int za = z0 & ~3;
 
+    // Load order (vmcnt retires loads in issue order; see k_rows_tm): row bounds, table,
+    // column stream and the epilogue operands first, branch-free; the values last.
+    const int lr = tid < nr ? tid : (nr > 0 ? nr - 1 : 0);  // clamped own row
+    int rlv = 0, rpa = 0, rpb = 0, tabv = 0;
+    if constexpr (RL8) {
+        rlv = (int)rlen[r0 + lr];
+    } else {
+        rpa = rowptr[r0 + (tid < nr ? tid : nr)];
+        rpb = rowptr[r0 + nr];
+    }
+    if constexpr (CD != 0) tabv = ctab[tid];  // the table is allocated with 256 entries
     int4 c4[G];
     double2 va[G], vb[G];
     uint16_t vn[G];  // VD: four 4-bit value indices per lane group
@@ -164,9 +175,23 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
         } else {
             c4[j] = *reinterpret_cast<const int4*>(col + gs);
         }
-        if constexpr (VD) {
-            vn[j] = *reinterpret_cast<const uint16_t*>(vidx + (gs >> 1));
-        } else {
+        if constexpr (VD) vn[j] = *reinterpret_cast<const uint16_t*>(vidx + (gs >> 1));
+    }
+    // one row per lane: the epilogue's own-row operands (b, old x, y), so their latency
+    // hides under the stream instead of trailing the LDS phase
+    double pb = 0.0, px = 0.0, py = 0.0;
+    {
+        const int r = r0 + lr;
+        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[r];
+        if constexpr (OP == OP_JACOBI) px = x[r];
+        if constexpr (OP == OP_PROLONG) py = y[r];
+    }
+    asm volatile("" ::: "memory");  // keep the loads above ahead of the value stream
+    if constexpr (!VD) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int g = za + 4 * (tid + j * BS);
+            const int gs = g < z1 ? g : za;
             va[j] = *reinterpret_cast<const double2*>(val + gs);
             vb[j] = *reinterpret_cast<const double2*>(val + gs + 2);
         }
@@ -174,7 +199,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     int rl_len = 0, rl_inc = 0;  // RL8: this lane's row length and wave-inclusive length sum
     if constexpr (RL8) {
         const int lane = tid & 63;
-        rl_len = tid < nr ? (int)rlen[r0 + tid] : 0;
+        rl_len = tid < nr ? rlv : 0;
         rl_inc = rl_len;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -183,7 +208,10 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
         }
         if (lane == 63) lwt[tid >> 6] = rl_inc;
     } else {
-        for (int i = tid; i <= nr; i += BS) lrp[i] = rowptr[r0 + i];
+        // unconditional stores (lanes past the tile's rows rewrite lrp[nr] with its own value):
+        // a conditional store would let the compiler sink the loads behind the values
+        lrp[tid < nr ? tid : nr] = rpa;
+        lrp[nr] = rpb;
     }
     // row start of this lane's row (RL8, after a barrier has published lwt)
     auto rl_base = [&]() {
@@ -192,17 +220,8 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
         for (int q = 0; q < BS / 64; ++q) pre += q < (tid >> 6) ? lwt[q] : 0;
         return pre;
     };
-    // one row per lane: fetch the epilogue's own-row operands (b, old x, y) now, so their
-    // latency hides under the column stream instead of trailing the LDS phase
-    double pb = 0.0, px = 0.0, py = 0.0;
-    if (tid < nr) {
-        const int r = r0 + tid;
-        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[r];
-        if constexpr (OP == OP_JACOBI) px = x[r];
-        if constexpr (OP == OP_PROLONG) py = y[r];
-    }
     if constexpr (CD != 0) {
-        if (tid < ctab_n) ltab[tid] = ctab[tid];
+        ltab[tid] = tabv;
         __syncthreads();  // lwt, ltab
         if (tid < nr) {
             const int e = rl_base() + rl_inc - za;
@@ -277,31 +296,33 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
         *reinterpret_cast<double2*>(&lprod[g - za + 2]) = make_double2(p[2], p[3]);
     }
     __syncthreads();
-    if (tid < nr) {
-        int kb, ke;
-        if constexpr (RL8) {
-            const int base = rl_base();
-            kb = base + rl_inc - rl_len - za;
-            ke = base + rl_inc - za;
-        } else {
-            kb = lrp[tid] - za;
-            ke = lrp[tid + 1] - za;
-        }
-        const double s = row_sum_lds(lprod, kb, ke);
-        const int r = r0 + tid;
-        if constexpr (OP == OP_SPMV) {
-            y[r] = s;
-        } else if constexpr (OP == OP_RESID) {
-            y[r] = pb - s;
-        } else if constexpr (OP == OP_JACOBI) {
-            const double u = pb - s;
-            const double v = omega * u;
-            const double w = v / ldiag[tid];
-            y[r] = px + w;
-        } else {
-            y[r] = py + s;
-        }
+    // every lane computes (lanes past the tile's rows sum an empty range) and only the
+    // tile's rows store: with the epilogue unconditional, the compiler keeps the operand
+    // loads at entry instead of sinking them into the store branch
+    int kb = 0, ke = 0;
+    if constexpr (RL8) {
+        const int base = rl_base();
+        kb = base + rl_inc - rl_len - za;
+        ke = base + rl_inc - za;
+    } else if (tid < nr) {
+        kb = lrp[tid] - za;
+        ke = lrp[tid + 1] - za;
     }
+    const double s = row_sum_lds(lprod, kb, ke);
+    double out;
+    if constexpr (OP == OP_SPMV) {
+        out = s;
+    } else if constexpr (OP == OP_RESID) {
+        out = pb - s;
+    } else if constexpr (OP == OP_JACOBI) {
+        const double u = pb - s;
+        const double v = omega * u;
+        const double w = v / ldiag[tid < nr ? tid : 0];
+        out = px + w;
+    } else {
+        out = py + s;
+    }
+    if (tid < nr) y[r0 + tid] = out;
 }
 
 // k_rows_tm, tile-major (TileSet::tm): tile t's values, column stream and row lengths live at
@@ -314,38 +335,51 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
 // lengths; positions are tile-relative (no alignment head: a tile's slot starts at its first
 // nonzero). Summation order, epilogues and Jacobi's in-tile diagonal are k_rows_tile2's
 // (SPEC §S3).
-template <int OP, int TNNZ, int CD>
+template <int OP, int TNNZ, int CD, bool ANC = false>
 __global__ __launch_bounds__(kBlock) void k_rows_tm(
     const int4* __restrict__ tiles, const double* __restrict__ tval,
     const uint8_t* __restrict__ tcidx, const uint16_t* __restrict__ tclo,
     const uint8_t* __restrict__ tchi, const int* __restrict__ tbase,
     const uint8_t* __restrict__ trlen, int rs, const int* __restrict__ ctab, int ctab_n,
     const double* __restrict__ x, const double* __restrict__ b, double* __restrict__ y,
-    double omega) {
+    double omega, const int* __restrict__ tanc = nullptr) {
+    // ANC (anchored dictionary): column = the row's first column (slot anchors, tanc) +
+    // table[index] instead of row + table[index]
+    static_assert(!ANC || CD != 0, "anchored columns are dictionary columns");
     constexpr int BS = kBlock;
     constexpr int G = TNNZ / (4 * BS);
     static_assert(G >= 1 && TNNZ % (4 * BS) == 0, "tile budget must be a multiple of 4 x block");
     __shared__ __attribute__((aligned(16))) double lprod[TNNZ + 8];
     __shared__ double ldiag[OP == OP_JACOBI ? BS : 1];
     __shared__ int lwt[BS / 64];
-    __shared__ int ltab[CD == 8 ? 256 : 16];
+    __shared__ int ltab[CD != 0 ? BS : 1];
     __shared__ __attribute__((aligned(4))) uint8_t lrow[TNNZ + 8];
+    __shared__ int lanc[ANC ? BS : 1];
 
     const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int4 d = tiles[t];
     const size_t sb = (size_t)t * TNNZ;
+    const int r0 = d.x, nr = d.y - d.x, cnt = d.w - d.z;
+    // Load order matters: vmcnt retires loads in issue order, so a wait for a load also waits
+    // for every load issued before it. The small loads the dependent phases need first —
+    // dictionary table and row anchors, row lengths (scan), column stream (gathers), the
+    // epilogue's own-row operands — go out first, branch-free (clamped addresses), and the
+    // value stream last: the scan, the row map and the x gathers then proceed while the
+    // values are still in flight (previously the scan's wait on the row lengths also waited
+    // for the whole value stream, and the gathers' wait on the columns for b / x).
+    int tabv = 0, ancv = 0;
+    if constexpr (CD != 0) tabv = ctab[tid];  // the table is allocated with 256 entries
+    const size_t rsl = (size_t)t * rs + (tid < rs ? tid : rs - 1);
+    if constexpr (ANC) ancv = tanc[rsl];
+    const int rlv = (int)trlen[rsl];
     double2 va[G], vb[G];
     uint32_t cn[G];
     ushort4 clo4[G];
     int cb = 0;
     if constexpr (CD == 0) cb = tbase[t];
-    // the whole slot is loaded at entry (padding included: a load that waits for the
-    // descriptor's nonzero count brings its round trip back — measured 2-15 % slower)
 #pragma unroll
     for (int j = 0; j < G; ++j) {
         const size_t q = sb + 4 * (tid + j * BS);
-        va[j] = *reinterpret_cast<const double2*>(tval + q);
-        vb[j] = *reinterpret_cast<const double2*>(tval + q + 2);
         if constexpr (CD == 4) {
             cn[j] = *reinterpret_cast<const uint16_t*>(tcidx + (q >> 1));
         } else if constexpr (CD == 8) {
@@ -355,10 +389,27 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
             cn[j] = *reinterpret_cast<const uint32_t*>(tchi + q);
         }
     }
-    int rl_len = tid < rs ? (int)trlen[(size_t)t * rs + tid] : 0;
-    if constexpr (CD != 0) {
-        if (tid < ctab_n) ltab[tid] = ctab[tid];
+    double pb = 0.0, px = 0.0, py = 0.0;
+    {
+        const int r = r0 + (tid < nr ? tid : 0);  // padding tiles are (0, 0, 0, 0): row 0
+        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[r];
+        if constexpr (OP == OP_JACOBI) px = x[r];
+        if constexpr (OP == OP_PROLONG) py = y[r];
     }
+    asm volatile("" ::: "memory");  // keep the loads above ahead of the value stream
+    // the whole value slot is loaded at entry (padding included: a load that waits for the
+    // descriptor's nonzero count brings its round trip back — measured 2-15 % slower)
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const size_t q = sb + 4 * (tid + j * BS);
+        va[j] = *reinterpret_cast<const double2*>(tval + q);
+        vb[j] = *reinterpret_cast<const double2*>(tval + q + 2);
+    }
+    int rl_len = tid < rs ? rlv : 0;
+    // every lane stores its entry (unconditionally: a conditional store lets the compiler sink
+    // the table load into the branch, behind the value stream)
+    if constexpr (CD != 0) ltab[tid] = tabv;
+    if constexpr (ANC) lanc[tid] = tid < rs ? ancv : 0;
     int rl_inc = rl_len;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -366,14 +417,6 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
         if (lane >= off) rl_inc += u;
     }
     if (lane == 63) lwt[tid >> 6] = rl_inc;
-    const int r0 = d.x, nr = d.y - d.x, cnt = d.w - d.z;
-    double pb = 0.0, px = 0.0, py = 0.0;
-    if (tid < nr) {
-        const int r = r0 + tid;
-        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[r];
-        if constexpr (OP == OP_JACOBI) px = x[r];
-        if constexpr (OP == OP_PROLONG) py = y[r];
-    }
     // end of this lane's row (tile-relative): the wave's inclusive sum + the earlier waves'
     // totals, readable after the next barrier
     auto row_end = [&]() {
@@ -411,7 +454,9 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int ix = CD == 4 ? (int)((cn[j] >> (4 * e)) & 15u) : (int)((cn[j] >> (8 * e)) & 255u);
-                cc[j][e] = r0 + (int)((rw >> (8 * e)) & 255u) + ltab[ix];
+                const int rid = (int)((rw >> (8 * e)) & 255u);
+                if constexpr (ANC) cc[j][e] = lanc[rid] + ltab[ix];
+                else cc[j][e] = r0 + rid + ltab[ix];
             }
         }
 #pragma unroll
@@ -438,22 +483,23 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     }
     __syncthreads();
     if constexpr (!NEED_ROWS) re = row_end();
-    if (tid < nr) {
-        const double s = row_sum_lds(lprod, re - rl_len, re);
-        const int r = r0 + tid;
-        if constexpr (OP == OP_SPMV) {
-            y[r] = s;
-        } else if constexpr (OP == OP_RESID) {
-            y[r] = pb - s;
-        } else if constexpr (OP == OP_JACOBI) {
-            const double u = pb - s;
-            const double v = omega * u;
-            const double w = v / ldiag[tid];
-            y[r] = px + w;
-        } else {
-            y[r] = py + s;
-        }
+    // unconditional epilogue, conditional store (see k_rows_tile2); lanes past the tile's
+    // rows have rl_len = 0 and sum an empty range
+    const double s = row_sum_lds(lprod, re - rl_len, re);
+    double out;
+    if constexpr (OP == OP_SPMV) {
+        out = s;
+    } else if constexpr (OP == OP_RESID) {
+        out = pb - s;
+    } else if constexpr (OP == OP_JACOBI) {
+        const double u = pb - s;
+        const double v = omega * u;
+        const double w = v / ldiag[tid < nr ? tid : 0];
+        out = px + w;
+    } else {
+        out = py + s;
     }
+    if (tid < nr) y[r0 + tid] = out;
 }
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_rows_long(
@@ -604,7 +650,15 @@ void launch_tile(const pamg_mat& A, const TileSet& ts, const double* x, const do
                  double* y, double omega, hipStream_t s) {
     const int n = ts.n_short;
     if (ts.tm) {
-        if (ts.cd == 4)
+        if (ts.anc && ts.cd == 4)
+            k_rows_tm<OP, TNNZ, 4, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
+                                                             nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n,
+                                                             x, b, y, omega, ts.d_tm_anc);
+        else if (ts.anc)
+            k_rows_tm<OP, TNNZ, 8, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
+                                                             nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n,
+                                                             x, b, y, omega, ts.d_tm_anc);
+        else if (ts.cd == 4)
             k_rows_tm<OP, TNNZ, 4><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
                                                        nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n, x,
                                                        b, y, omega);

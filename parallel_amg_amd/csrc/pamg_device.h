@@ -48,6 +48,9 @@ struct TileSet {
     int cd = 0;
     int* d_ctab = nullptr;
     int ctab_n = 0;
+    // anchored dictionary (Options::col_dict_anchor; tile-major sets only): column = the row's
+    // first column + d_ctab[i]; the row anchors sit in the tile-major slots (d_tm_anc)
+    bool anc = false;
     // tile-major copies (Options::tile_major; kernels.hip k_rows_tm): tile t's values and
     // column stream at t * tile_nnz, its row lengths at t * tm_rs, zero-padded
     bool tm = false;
@@ -57,6 +60,7 @@ struct TileSet {
     uint16_t* d_tm_clo = nullptr;  // or 24-bit columns: low 16 bits
     uint8_t* d_tm_chi = nullptr;   //   high 8 bits
     uint8_t* d_tm_rlen = nullptr;
+    int* d_tm_anc = nullptr;       // anchored dictionary: each row's first column (tm_rs per tile)
     int max_short_len = 0;    // longest row in a short tile
     int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
@@ -74,6 +78,7 @@ struct Options {
     int value_dict = 0;        // 1 (opt-in): 4-bit per-tile value dictionaries where they fit
     int col_dict = 1;          // 1: row-relative column dictionaries (4/8-bit) where they fit
     int tile_major = 1;        // tile-major padded copies (variant 4): 1 where measured faster, 2 all eligible
+    int col_dict_anchor = 1;   // 1: anchored column dictionaries (col - row's first column) where row-relative ones do not fit
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };
 Options& options();

@@ -337,67 +337,78 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
         if (!opt.col_dict || ts->vd || ts->n_short == 0 || ts->max_short_len > 255)
             continue;
         if (idx.empty()) idx.assign((size_t)A->nnz + kVecPad, 0);
-        // Distinct offsets in first-occurrence order (tile order, then storage order): every
-        // chunk of tiles lists its own (<= 257) in parallel, the lists are merged in chunk
-        // order — the same table a single sequential pass builds.
         const std::vector<int4>& tiles = *tl[q];
         const int64_t nt = (int64_t)tiles.size();
-        const int nch = std::max(1, std::min<int>(host_threads(), (int)(nt / 64)));
-        std::vector<std::vector<int>> firsts(nch);
-        auto scan = [&](int64_t a, int64_t b, std::vector<int>& out) {
-            constexpr int kCells = 1024;  // open addressing: offset -> seen
-            int key[kCells];
-            bool used[kCells] = {};
-            for (int64_t t = a; t < b && out.size() <= 256; ++t)
-                for (int r = tiles[t].x; r < tiles[t].y; ++r)
-                    for (int64_t k = rp[r]; k < rp[r + 1]; ++k) {
-                        const int o = ci[k] - r;
-                        uint32_t h = ((uint32_t)o * 0x9E3779B1u) >> 22;
-                        while (used[h] && key[h] != o) h = (h + 1) & (kCells - 1);
-                        if (!used[h]) {
-                            used[h] = true;
-                            key[h] = o;
-                            out.push_back(o);
-                            if (out.size() > 256) return;
+        // Offset of a nonzero: col - row (row-relative: stencils), or col - the row's first
+        // column (anchored: rows of a repeated shape whose columns do not follow the row
+        // index, e.g. a restriction's 5x5x5 neighbourhoods of an aggregate root: 75 offsets).
+        // Anchored sets are read only by the tile-major kernel (the row anchors live in its
+        // slots), so they need tile_major on.
+        auto try_dict = [&](bool anchored) -> bool {
+            auto anchor = [&](int r) { return anchored ? (rp[r + 1] > rp[r] ? ci[rp[r]] : 0) : r; };
+            // Distinct offsets in first-occurrence order (tile order, then storage order):
+            // every chunk of tiles lists its own (<= 257) in parallel, the lists are merged in
+            // chunk order — the same table a single sequential pass builds.
+            const int nch = std::max(1, std::min<int>(host_threads(), (int)(nt / 64)));
+            std::vector<std::vector<int>> firsts(nch);
+            auto scan = [&](int64_t a, int64_t b, std::vector<int>& out) {
+                constexpr int kCells = 1024;  // open addressing: offset -> seen
+                int key[kCells];
+                bool used[kCells] = {};
+                for (int64_t t = a; t < b && out.size() <= 256; ++t)
+                    for (int r = tiles[t].x; r < tiles[t].y; ++r) {
+                        const int an = anchor(r);
+                        for (int64_t k = rp[r]; k < rp[r + 1]; ++k) {
+                            const int o = ci[k] - an;
+                            uint32_t h = ((uint32_t)o * 0x9E3779B1u) >> 22;
+                            while (used[h] && key[h] != o) h = (h + 1) & (kCells - 1);
+                            if (!used[h]) {
+                                used[h] = true;
+                                key[h] = o;
+                                out.push_back(o);
+                                if (out.size() > 256) return;
+                            }
                         }
                     }
-        };
-        {
-            std::vector<std::thread> th;
-            for (int c = 0; c < nch; ++c)
-                th.emplace_back([&, c] { scan(nt * c / nch, nt * (c + 1) / nch, firsts[c]); });
-            for (auto& x : th) x.join();
-        }
-        constexpr int kCells = 1024;
-        int key[kCells], slot[kCells];
-        std::fill(slot, slot + kCells, -1);
-        auto find = [&](int o) {
-            uint32_t h = ((uint32_t)o * 0x9E3779B1u) >> 22;
-            while (slot[h] >= 0 && key[h] != o) h = (h + 1) & (kCells - 1);
-            return h;
-        };
-        bool ok = true;
-        for (int c = 0; c < nch && ok; ++c)
-            for (int o : firsts[c]) {
-                const uint32_t h = find(o);
-                if (slot[h] >= 0) continue;
-                if (tab[q].size() == 256) {
-                    ok = false;
-                    break;
-                }
-                key[h] = o;
-                slot[h] = (int)tab[q].size();
-                tab[q].push_back(o);
+            };
+            {
+                std::vector<std::thread> th;
+                for (int c = 0; c < nch; ++c)
+                    th.emplace_back([&, c] { scan(nt * c / nch, nt * (c + 1) / nch, firsts[c]); });
+                for (auto& x : th) x.join();
             }
-        if (!ok) {
+            constexpr int kCells = 1024;
+            int key[kCells], slot[kCells];
+            std::fill(slot, slot + kCells, -1);
+            auto find = [&](int o) {
+                uint32_t h = ((uint32_t)o * 0x9E3779B1u) >> 22;
+                while (slot[h] >= 0 && key[h] != o) h = (h + 1) & (kCells - 1);
+                return h;
+            };
             tab[q].clear();
-            continue;
-        }
-        par_for(nt, [&](int64_t a, int64_t b) {
-            for (int64_t t = a; t < b; ++t)
-                for (int r = tiles[t].x; r < tiles[t].y; ++r)
-                    for (int64_t k = rp[r]; k < rp[r + 1]; ++k) idx[k] = (uint8_t)slot[find(ci[k] - r)];
-        });
+            for (int c = 0; c < nch; ++c)
+                for (int o : firsts[c]) {
+                    const uint32_t h = find(o);
+                    if (slot[h] >= 0) continue;
+                    if (tab[q].size() == 256) {
+                        tab[q].clear();
+                        return false;
+                    }
+                    key[h] = o;
+                    slot[h] = (int)tab[q].size();
+                    tab[q].push_back(o);
+                }
+            par_for(nt, [&](int64_t a, int64_t b) {
+                for (int64_t t = a; t < b; ++t)
+                    for (int r = tiles[t].x; r < tiles[t].y; ++r) {
+                        const int an = anchor(r);
+                        for (int64_t k = rp[r]; k < rp[r + 1]; ++k) idx[k] = (uint8_t)slot[find(ci[k] - an)];
+                    }
+            });
+            return true;
+        };
+        ts->anc = false;
+        if (!try_dict(false) && opt.col_dict_anchor && opt.tile_major) ts->anc = try_dict(true);
     }
     int width = 0;
     for (int q = 0; q < 2; ++q)
@@ -438,7 +449,8 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
 // columns, tile t's values, column stream and row lengths are copied to fixed, zero-padded
 // slots (t * tile_nnz, t * tm_rs), so the kernel addresses every pre-gather load from its
 // block index. The CSR arrays stay resident for the other variants and the long rows.
-int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>& rp, const double* val,
+int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>& rp,
+                     const std::vector<int>& ci, const double* val,
                      const std::vector<int4>& t_in, const std::vector<int4>& t_bd,
                      const std::vector<uint16_t>& lo, const std::vector<uint8_t>& hi,
                      const std::vector<uint8_t>& idx8) {
@@ -449,8 +461,10 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
         pamg::TileSet* ts = sets[q];
         ts->tm = false;
         if (!opt.tile_major || ts->vd || ts->n_short == 0 || ts->max_short_len > 255 ||
-            !(ts->cd || (ts->c24 && !lo.empty())) || (ts->cd && idx8.empty()) || !val)
+            !(ts->cd || (ts->c24 && !lo.empty())) || (ts->cd && idx8.empty()) || !val) {
+            if (ts->anc) return fail(PAMG_E_STATE, "upload: anchored column dictionary without tile-major slots");
             continue;
+        }
         // tile_major 1 (default): the sets where it measured faster at 512^3
         // (profiles/r01_kbench_512_tm_*.jsonl) — column-dictionary sets (A0: Jacobi -9 %,
         // residual -7 %, SpMV -5 %) and the non-square operators whose tiles fill >= 97 % of
@@ -474,12 +488,18 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
         const int64_t ncb = cdw == 4 ? tn / 2 : tn;  // column-stream bytes per slot (cd / chi)
         std::unique_ptr<uint8_t[]> tci(new uint8_t[nt * ncb + kVecPad]);
         std::unique_ptr<uint16_t[]> tcl(cdw ? nullptr : new uint16_t[nt * tn + kVecPad]);
+        std::unique_ptr<int[]> tan(ts->anc ? new int[nt * rs + kVecPad] : nullptr);
         par_for(nt, [&](int64_t a, int64_t b) {
             for (int64_t i = a; i < b; ++i) {
                 const int4 t = tiles[i];
                 const int cnt = t.w - t.z;
                 uint8_t* rl = &trl[i * rs];
                 for (int r = 0; r < rs; ++r) rl[r] = t.x + r < t.y ? (uint8_t)(rp[t.x + r + 1] - rp[t.x + r]) : 0;
+                if (tan)  // row anchors: each row's first column (anchored column dictionary)
+                    for (int r = 0; r < rs; ++r) {
+                        const int row = t.x + r;
+                        tan[i * rs + r] = row < t.y && rp[row + 1] > rp[row] ? ci[rp[row]] : 0;
+                    }
                 double* v = &tv[i * tn];
                 std::memcpy(v, val + t.z, sizeof(double) * cnt);
                 std::fill(v + cnt, v + tn, 0.0);
@@ -503,6 +523,11 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
         std::fill(&trl[nt * rs], &trl[nt * rs] + kVecPad, (uint8_t)0);
         std::fill(&tci[nt * ncb], &tci[nt * ncb] + kVecPad, (uint8_t)0);
         if (tcl) std::fill(&tcl[nt * tn], &tcl[nt * tn] + kVecPad, (uint16_t)0);
+        if (tan) {
+            std::fill(&tan[nt * rs], &tan[nt * rs] + kVecPad, 0);
+            CHECK(dalloc(&ts->d_tm_anc, nt * rs + kVecPad));
+            CHECK(h2d(A->ctx, ts->d_tm_anc, tan.get(), sizeof(int) * (nt * rs + kVecPad)));
+        }
         CHECK(dalloc(&ts->d_tm_val, nt * tn + kVecPad));
         CHECK(h2d(A->ctx, ts->d_tm_val, tv.get(), sizeof(double) * (nt * tn + kVecPad)));
         CHECK(dalloc(&ts->d_tm_rlen, nt * rs + kVecPad));
@@ -534,6 +559,8 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_tm_clo);
     dfree(ts.d_tm_chi);
     dfree(ts.d_tm_rlen);
+    dfree(ts.d_tm_anc);
+    ts.anc = false;
     ts.tm = false;
     ts.tm_rs = 0;
     ts.c24 = ts.vd = ts.rl8 = false;
@@ -1280,7 +1307,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         std::vector<uint8_t> idx8;
         CHECK(build_col_dicts(A.get(), rp, ci, t_in, t_bd, &idx8));
         tr.mark("col dicts");
-        CHECK(build_tile_major(A.get(), n_own_cols, rp, val, t_in, t_bd, lo, hi, idx8));
+        CHECK(build_tile_major(A.get(), n_own_cols, rp, ci, val, t_in, t_bd, lo, hi, idx8));
         tr.mark("tile-major");
     }
     if (A->interior.rl8 || A->boundary.rl8) {
@@ -1309,7 +1336,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         if (t->tm) {  // whole padded slots: tile_nnz values + column entries + tm_rs lengths
             const int64_t tn = t->tile_nnz;
             const int64_t rowb = t->tm_rs;
-            b += ns * (rowb + 8 * tn + (t->cd ? t->cd * tn / 8 : 3 * tn) + 16 + (base ? 4 : 0)) +
+            b += ns * (rowb * (t->anc ? 5 : 1) + 8 * tn + (t->cd ? t->cd * tn / 8 : 3 * tn) + 16 + (base ? 4 : 0)) +
                  (t->cd ? 4 * t->ctab_n : 0);
         } else {
             b += (t->rl8 ? 1 : 4) * t->rows_short;
@@ -1365,7 +1392,7 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes) {
     return PAMG_OK;
 }
 
-int pamg_mat_layout(const pamg_mat* A, int set, int out[9]) {
+int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     if (!A || !out || set < 0 || set > 1) return fail(PAMG_E_ARG, "mat_layout: bad args");
     const pamg::TileSet& t = set == 0 ? A->interior : A->boundary;
     out[0] = t.c24;
@@ -1377,6 +1404,7 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[9]) {
     out[6] = t.tm_rs;
     out[7] = t.tile_nnz;
     out[8] = t.n_short;
+    out[9] = t.anc;
     return PAMG_OK;
 }
 
@@ -1787,6 +1815,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "value_dict" && (value == 0 || value == 1)) o.value_dict = (int)value;
     else if (k == "col_dict" && (value == 0 || value == 1)) o.col_dict = (int)value;
     else if (k == "tile_major" && value >= 0 && value <= 2) o.tile_major = (int)value;
+    else if (k == "col_dict_anchor" && (value == 0 || value == 1)) o.col_dict_anchor = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -1804,6 +1833,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "value_dict") *value = o.value_dict;
     else if (k == "col_dict") *value = o.col_dict;
     else if (k == "tile_major") *value = o.tile_major;
+    else if (k == "col_dict_anchor") *value = o.col_dict_anchor;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

@@ -192,14 +192,17 @@ def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
         offs = rng.choice(np.arange(-n // 2, n // 2), size=ndist + 1, replace=False)
         offs = offs[offs != 0][:ndist]
     M = offset_csr(rng, n, offs, lengths)
-    distinct = len(np.unique(M.col - np.repeat(np.arange(n), np.diff(M.rowptr))))
-    keys = ("col_dict", "tile_nnz", "tile_major")
+    rows = np.repeat(np.arange(n), np.diff(M.rowptr))
+    distinct = len(np.unique(M.col - rows))
+    dist_anc = len(np.unique(M.col - np.repeat(M.col[np.minimum(M.rowptr[:-1], max(M.nnz - 1, 0))], np.diff(M.rowptr))))
+    keys = ("col_dict", "tile_nnz", "tile_major", "col_dict_anchor")
     old = []
     for k in keys:
         v = ctypes.c_int64()
         call("pamg_get_option", k.encode(), ctypes.byref(v))
         old.append(v.value)
     try:
+        call("pamg_set_option", b"col_dict_anchor", 1)
         call("pamg_set_option", b"tile_nnz", tnnz)
         call("pamg_set_option", b"col_dict", 0)
         call("pamg_set_option", b"tile_major", 0)
@@ -212,8 +215,11 @@ def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
                 assert (A.stream_bytes < plain) == (distinct <= 256), (A.stream_bytes, plain, distinct)
             lay = layout_of(A)
             assert lay["tm"] == bool(tm)
-            assert lay["cd"] == (4 if distinct <= 16 else 8 if distinct <= 256 else 0), (lay, distinct)
-            assert lay["cd_offsets"] == (distinct if distinct <= 256 else 0)
+            # row-relative where <= 256 offsets; else (tile-major only) anchored where <= 256
+            nd = distinct if distinct <= 256 else (dist_anc if tm and dist_anc <= 256 else 0)
+            assert lay["anchored"] == (distinct > 256 and nd > 0), (lay, distinct, dist_anc)
+            assert lay["cd"] == (4 if 0 < nd <= 16 else 8 if nd else 0), (lay, distinct, dist_anc)
+            assert lay["cd_offsets"] == nd
             xh, bh = rng.standard_normal(n), rng.standard_normal(n)
             x, b = PVector(ctx, n, 0, xh), PVector(ctx, n, 0, bh)
             y = PVector(ctx, n)
@@ -389,6 +395,71 @@ def test_stream_bytes_layout(ctx):
     lay = layout_of(A)
     assert lay["tm"] and lay["cd"] == 4 and 0 < lay["tm_rs"] <= 256 and lay["tm_rs"] % 4 == 0
     assert A.stream_bytes == nt * (lay["tm_rs"] + 8 * 1024 + 512 + 16) + 4 * 7 + 4
+
+
+def anchored_csr(rng, nrows, ncols, nshape, maxlen):
+    """A restriction-shaped matrix: row i reads anchor_i + a subset (always holding 0) of one
+    set of nshape offsets; anchors are unrelated to the row index (sorted, random gaps), so
+    no row-relative dictionary fits but an anchored one does."""
+    shape = np.concatenate([[0], np.sort(rng.choice(np.arange(1, 3000), nshape - 1, replace=False))])
+    anchors = np.sort(rng.integers(0, ncols - 3001, nrows))
+    rows, cols = [0], []
+    for i in range(nrows):
+        m = int(rng.integers(1, min(nshape, maxlen) + 1))
+        sub = np.concatenate([[0], rng.choice(shape[1:], m - 1, replace=False)]) if m > 1 else np.array([0])
+        cols.append(anchors[i] + np.sort(sub))
+        rows.append(rows[-1] + m)
+    col = np.concatenate(cols).astype(np.int64)
+    return O.CSR(np.asarray(rows, np.int64), col, rng.standard_normal(len(col)), ncols)
+
+
+@pytest.mark.parametrize("nshape,maxlen,tnnz", [(12, 12, 1024), (75, 40, 1024), (75, 255, 1024),
+                                                (256, 60, 4096), (257, 60, 1024)])
+def test_anchored_dictionary_bit_exact(ctx, nshape, maxlen, tnnz):
+    """Anchored column dictionaries (column = the row's first column + table[index], anchors in
+    the tile-major slots; the layout of the level-0 restriction): SpMV, residual and
+    prolongate-add give the oracle's bits; 257 offsets fall back to 24-bit columns."""
+    import ctypes
+    from parallel_amg_amd._lib import call, layout_of
+    rng = np.random.default_rng(nshape * 31 + maxlen)
+    nr, nc = 3000, 60000
+    M = anchored_csr(rng, nr, nc, nshape, maxlen)
+    old = ctypes.c_int64()
+    call("pamg_get_option", b"tile_nnz", ctypes.byref(old))
+    try:
+        call("pamg_set_option", b"tile_nnz", tnnz)
+        A, _h = upload(ctx, M)
+    finally:
+        call("pamg_set_option", b"tile_nnz", old.value)
+    lay = layout_of(A)
+    used = len(np.unique(M.col - np.repeat(M.col[M.rowptr[:-1]], np.diff(M.rowptr))))
+    assert lay["anchored"] == (used <= 256) and (lay["tm"] or used > 256)
+    assert lay["cd"] == (4 if used <= 16 else 8 if used <= 256 else 0), (lay, used)
+    xh, bh = rng.standard_normal(nc), rng.standard_normal(nr)
+    x, b = PVector(ctx, nc, 0, xh), PVector(ctx, nr, 0, bh)
+    y = PVector(ctx, nr)
+    mul(y, A, x)
+    ref = O.spmv(M, xh)
+    assert np.array_equal(bits(y.own_values()), bits(ref))
+    r = PVector(ctx, nr)
+    residual(r, A, x, b)
+    assert np.array_equal(bits(r.own_values()), bits(O.residual(M, xh, bh)))
+    ms = ctypes.c_double()
+    yy = PVector(ctx, nr, 0, bh)
+    call("pamg_bench_rowop", ctx.handle, A.handle, 3, x.handle, None, yy.handle, 0.0, 1, ctypes.byref(ms))
+    assert np.array_equal(bits(yy.own_values()), bits((bh + ref) + ref))
+
+
+def test_restriction_takes_anchored_dictionary(ctx):
+    """The level-0 restriction of the 7-point Poisson hierarchy (5x5x5 neighbourhoods of the
+    aggregate roots) is uploaded with an anchored 8-bit dictionary in tile-major slots."""
+    from parallel_amg_amd._lib import layout_of
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 24)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=100), device=ctx)
+    S = AMGSolver(ctx, H)
+    lay = layout_of(S.R[0])
+    assert lay["anchored"] and lay["tm"] and lay["cd"] == 8 and lay["cd_offsets"] <= 256, lay
 
 
 @pytest.mark.parametrize("seed,n,density,weak,iso", [(1, 3000, 0.003, 0.3, 0.02), (2, 5000, 0.001, 0.0, 0.0),
