@@ -32,6 +32,28 @@
 namespace pamg {
 namespace {
 
+// Inclusive prefix sum over the 64 lanes of a wave with DPP lane moves (row_shr 1/2/4/8 inside
+// each 16-lane row, then row_bcast 15 / 31 across rows): VALU-side, where __shfl_up's
+// ds_bpermute costs an LDS round trip per step. The explicit lane predicates make the result
+// independent of what DPP reads for out-of-row sources.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = threadIdx.x & 63, rl = lane & 15;
+    int t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    if (rl >= 1) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    if (rl >= 2) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    if (rl >= 4) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    if (rl >= 8) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x142, 0xf, 0xf, false);  // row_bcast:15
+    if (lane & 16) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x143, 0xf, 0xf, false);  // row_bcast:31
+    if (lane >= 32) v += t;
+    return v;
+}
+
 template <int OP>
 __device__ __forceinline__ void epilogue(int r, double s, const double* __restrict__ x,
                                          const double* __restrict__ b, double* __restrict__ y,
@@ -200,12 +222,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     if constexpr (RL8) {
         const int lane = tid & 63;
         rl_len = tid < nr ? rlv : 0;
-        rl_inc = rl_len;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int u = __shfl_up(rl_inc, off, 64);
-            if (lane >= off) rl_inc += u;
-        }
+        rl_inc = wave_incl_scan(rl_len);
         if (lane == 63) lwt[tid >> 6] = rl_inc;
     } else {
         // unconditional stores (lanes past the tile's rows rewrite lrp[nr] with its own value):
@@ -410,12 +427,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     // the table load into the branch, behind the value stream)
     if constexpr (CD != 0) ltab[tid] = tabv;
     if constexpr (ANC) lanc[tid] = tid < rs ? ancv : 0;
-    int rl_inc = rl_len;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int u = __shfl_up(rl_inc, off, 64);
-        if (lane >= off) rl_inc += u;
-    }
+    const int rl_inc = wave_incl_scan(rl_len);
     if (lane == 63) lwt[tid >> 6] = rl_inc;
     // end of this lane's row (tile-relative): the wave's inclusive sum + the earlier waves'
     // totals, readable after the next barrier
