@@ -49,8 +49,12 @@ def main():
                     choices=["poisson2d", "poisson3d", "aniso3d", "elastic3d"])
     ap.add_argument("--matrix", default=None,
                     help="Matrix Market file (e.g. SuiteSparse Flan_1565.mtx) instead of --kind")
-    ap.add_argument("--partition", choices=["uniform", "nnz"], default="uniform",
-                    help="row partition of a --matrix over N GPUs (SPEC §S7)")
+    ap.add_argument("--partition", choices=["uniform", "nnz", "rcm"], default="uniform",
+                    help="row partition of a --matrix over N GPUs (SPEC §S7; rcm: graph partitioner = "
+                         "reverse Cuthill-McKee renumbering + nnz-balanced blocks)")
+    ap.add_argument("--rcm", action="store_true",
+                    help="renumber a generated (and --permute'd) problem with the graph partitioner before "
+                         "the nnz-balanced split")
     ap.add_argument("--max-coarse", type=int, default=1000)
     ap.add_argument("--agglomerate", type=int, default=32768,
                     help="levels >= 1 with <= this many rows are one part, replicated (0: off)")
@@ -121,11 +125,19 @@ def main():
     else:
         A, offs, xs = pa.generate_problem(be, args.kind, args.grid)
         workload = f"{args.kind} {args.grid}^{2 if args.kind == 'poisson2d' else 3} fp64"
-    if args.permute is not None:
-        if world > 1:
-            raise SystemExit("--permute: one part only")
-        A, xs = pa.permute_problem(A, xs, args.permute)
-        workload += f", randomly permuted (seed {args.permute})"
+    if args.permute is not None or args.rcm:
+        if args.matrix:
+            raise SystemExit("--permute / --rcm: generated problems only (use --partition rcm for --matrix)")
+        if world > 1:  # every rank builds the whole problem, reorders it identically, keeps its block
+            A, offs, xs = pa.generate_problem(pa.SequentialBackend(1), args.kind, args.grid)
+        if args.permute is not None:
+            A, xs = pa.permute_problem(A, xs, args.permute)
+            workload += f", randomly permuted (seed {args.permute})"
+        if args.rcm:
+            A, xs, _perm = pa.rcm_problem(A, xs)
+            workload += ", RCM-renumbered"
+        if world > 1 or args.rcm:
+            A, offs, xs = pa.split_problem(be, A, xs, "nnz")
     H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=args.max_coarse, agglomerate=args.agglomerate), log=log,
                            device=ctx if args.setup == "gpu" else None)
     t_setup = time.time() - t0
@@ -253,7 +265,7 @@ def main():
              else f"k_rows_tile2<2, {tn}, true, false, true>" if lay["rl8"]
              else f"k_rows_tile2<2, {tn}, true>" if lay["c24"]
              else f"k_rows_tile2<2, {tn}>")
-    workload_key = f"{args.matrix or args.kind}:{args.grid}:p{world}:perm{args.permute}"
+    workload_key = f"{args.matrix or args.kind}:{args.grid}:p{world}:perm{args.permute}" + (":rcm" if args.rcm else "")
     src = kernel_source_sha()
     traffic = pmc_lookup("traffic_jacobi.json", kname, lay["tiles"], workload_key, src)
     spmv_traffic = pmc_lookup("traffic_spmv.json", kname.replace("<2,", "<0,", 1), lay["tiles"], workload_key, src)

@@ -217,6 +217,11 @@ int pamg_read_mtx(const char* path, int64_t r0, int64_t r1, int64_t* n_global, p
 /* Entries per row of a Matrix Market file (symmetric mirrored): weights for the nnz-balanced
  * row partition (SPEC §S7). counts may be NULL to query *n_global only. */
 int pamg_mtx_row_counts(const char* path, int64_t* n_global, int64_t* counts);
+/* Reverse Cuthill-McKee order of a square matrix's (symmetrised) graph: order[k] = the old
+ * row that becomes row k. The graph partitioner for irregularly numbered matrices (SURVEY
+ * §8(f)-3): renumber with it, then cut contiguous nnz-balanced row blocks (SPEC §S7).
+ * Deterministic (pseudo-peripheral start, neighbours by degree then index). */
+int pamg_rcm_order(const pamg_hcsr* A, int64_t* order);
 /* Gershgorin bound over own rows; A's rows are global rows row0.. (diagonal at col row0+i). */
 int pamg_setup_gershgorin(const pamg_hcsr* A, int64_t row0, double* rho);
 /* Decoupled standard aggregation (SPEC §S4.2-3): agg[i] local aggregate id or -1. */

@@ -20,7 +20,7 @@ using SparseArrays
 
 export Context, ExchangePlan, DeviceVector, DeviceMatrix, HostCSR, VCycle, ExchangeTask, PamgError,
        own_values, ghost_values, consistent!, residual!, jacobi!, vcycle!, pcg!, set_sweeps!,
-       setup_hierarchy, gen_grid, gen_xstar, read_mtx, unique_id, comm_init!, runtime_versions, hip
+       setup_hierarchy, gen_grid, gen_xstar, read_mtx, rcm_order, unique_id, comm_init!, runtime_versions, hip
 
 """
     hip(ctxs, A::PSparseMatrix) / hip(ctxs, x::PVector)
@@ -372,6 +372,14 @@ function mtx_row_counts(path::AbstractString)
     counts = Vector{Int64}(undef, n[])
     check(ccall((:pamg_mtx_row_counts, libpamg), Cint, (Cstring, Ptr{Int64}, Ptr{Int64}), path, n, counts))
     counts
+end
+
+"Reverse Cuthill-McKee order (1-based): new row k is old row order[k] (the graph partitioner)."
+function rcm_order(A::HostCSR)
+    n = size(A)[1]
+    order = Vector{Int64}(undef, n)
+    check(ccall((:pamg_rcm_order, libpamg), Cint, (Ptr{Cvoid}, Ptr{Int64}), A.h, order))
+    order .+ 1
 end
 
 # ------------------------------------------------------------------ hierarchy / V-cycle

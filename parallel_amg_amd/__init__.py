@@ -7,7 +7,9 @@ exchange, and a host smoothed-aggregation setup.
 """
 from .backend import DistributedBackend, SequentialBackend  # noqa: F401
 from .checkpoint import load_hierarchy, save_hierarchy  # noqa: F401
-from .hierarchy import SAParams, build_hierarchy, generate_problem, load_problem, permute_problem  # noqa: F401
+from .hierarchy import (SAParams, build_hierarchy, generate_problem, load_problem, permute_problem,  # noqa: F401
+                        rcm_problem, split_problem)
 
 __all__ = ["SequentialBackend", "DistributedBackend", "SAParams", "build_hierarchy",
-           "generate_problem", "load_problem", "permute_problem", "save_hierarchy", "load_hierarchy"]
+           "generate_problem", "load_problem", "permute_problem", "rcm_problem", "split_problem", "save_hierarchy",
+           "load_hierarchy"]

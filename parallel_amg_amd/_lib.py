@@ -91,6 +91,7 @@ SIGNATURES = {
     "pamg_gen_xstar": [i64, i64, C.c_uint64, vp],
     "pamg_read_mtx": [C.c_char_p, i64, i64, pi64, pvp],
     "pamg_mtx_row_counts": [C.c_char_p, pi64, vp],
+    "pamg_rcm_order": [vp, vp],
     "pamg_setup_gershgorin": [vp, i64, pdbl],
     "pamg_setup_aggregate": [vp, i64, dbl, vp, pi64],
     "pamg_setup_tentative": [i64, vp, i64, i64, i64, pvp],

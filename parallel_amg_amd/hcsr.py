@@ -97,6 +97,14 @@ def mtx_row_counts(path: str) -> np.ndarray:
     return out
 
 
+def rcm_order(A: HCSR) -> np.ndarray:
+    """Reverse Cuthill-McKee order of a square host matrix (pamg_rcm_order): new row k is old
+    row order[k]."""
+    out = np.empty(A.nrows, np.int64)
+    call("pamg_rcm_order", A.handle, ptr(out))
+    return out
+
+
 def gen_xstar(i0: int, n: int, seed: int) -> np.ndarray:
     out = np.empty(n, np.float64)
     call("pamg_gen_xstar", i0, n, seed, ptr(out))

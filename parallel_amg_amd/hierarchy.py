@@ -184,17 +184,10 @@ def permutation(n: int, seed: int) -> np.ndarray:
     return np.random.default_rng(seed).permutation(n).astype(np.int64)
 
 
-def permute_problem(A: dict, xs: dict, seed: int):
-    """Symmetric permutation Q A Q^T of a one-part problem, x* permuted alike (bench
-    ``--permute``). A grid operator renumbered at random keeps its values and nonzero counts
-    but loses the banded, row-relative column pattern that the column dictionaries and the
-    banded tile order exploit, as an FE mesh numbering would (a Flan_1565 proxy).
-    Rows keep their columns sorted ascending (SPEC §S1)."""
-    if set(A) != {0}:
-        raise ValueError("permute_problem: one part only")
-    M = A[0]
+def reorder(M: HCSR, perm: np.ndarray) -> HCSR:
+    """Symmetric permutation Q M Q^T of a square host matrix: new row i is old row perm[i];
+    rows keep their columns sorted ascending (SPEC §S1)."""
     n = M.nrows
-    perm = permutation(n, seed)
     inv = np.empty(n, np.int64)
     inv[perm] = np.arange(n, dtype=np.int64)
     lens = np.diff(M.rowptr)[perm]
@@ -206,8 +199,43 @@ def permute_problem(A: dict, xs: dict, seed: int):
     # sort each row's columns: one global stable sort on (row, col)
     row = np.repeat(np.arange(n, dtype=np.int64), lens)
     order = np.lexsort((col, row))
-    P = HCSR.from_arrays(rp, col[order].astype(np.int32), val[order], M.ncols)
-    return {0: P}, {0: np.ascontiguousarray(xs[0][perm])}
+    return HCSR.from_arrays(rp, col[order].astype(np.int32), val[order], M.ncols)
+
+
+def permute_problem(A: dict, xs: dict, seed: int):
+    """Symmetric permutation Q A Q^T of a one-part problem, x* permuted alike (bench
+    ``--permute``). A grid operator renumbered at random keeps its values and nonzero counts
+    but loses the banded, row-relative column pattern that the column dictionaries and the
+    banded tile order exploit, as an FE mesh numbering would (a Flan_1565 proxy)."""
+    if set(A) != {0}:
+        raise ValueError("permute_problem: one part only")
+    perm = permutation(A[0].nrows, seed)
+    return {0: reorder(A[0], perm)}, {0: np.ascontiguousarray(xs[0][perm])}
+
+
+def rcm_problem(A: dict, xs: dict):
+    """Reverse Cuthill-McKee renumbering of a one-part problem (the graph partitioner,
+    pamg_rcm_order), x* permuted alike; split it afterwards with ``split_problem``."""
+    if set(A) != {0}:
+        raise ValueError("rcm_problem: one part only")
+    perm = H.rcm_order(A[0])
+    return {0: reorder(A[0], perm)}, {0: np.ascontiguousarray(xs[0][perm])}, perm
+
+
+def split_problem(backend, A: dict, xs: dict, partition: str = "nnz"):
+    """Cut a whole (one-part) problem into the backend's parts: contiguous row blocks, uniform
+    or nnz-balanced (SPEC §S7). Every rank holds the whole problem and keeps its own rows."""
+    M = A[0]
+    if partition == "nnz":
+        offs = balanced_offsets(np.diff(M.rowptr), backend.nparts)
+    else:
+        offs = np.array([(p * M.nrows) // backend.nparts for p in range(backend.nparts + 1)], np.int64)
+    parts = {}
+    for p in backend.parts:
+        a, b = int(offs[p]), int(offs[p + 1])
+        lo, hi = int(M.rowptr[a]), int(M.rowptr[b])
+        parts[p] = HCSR.from_arrays(M.rowptr[a:b + 1] - lo, M.col[lo:hi].copy(), M.val[lo:hi].copy(), M.ncols)
+    return parts, offs, {p: np.ascontiguousarray(xs[0][offs[p]:offs[p + 1]]) for p in backend.parts}
 
 
 def balanced_offsets(row_counts: np.ndarray, nparts: int) -> np.ndarray:
@@ -225,7 +253,16 @@ def load_problem(backend, path: str, partition: str = "uniform"):
     """Partitioned rows of a Matrix Market matrix (pamg_read_mtx; BASELINE.json configs[4],
     SuiteSparse Flan_1565) and the SPEC §S2 synthetic solution x* for b = A x*. Each part reads
     only its own rows; the partition is SPEC §S7's uniform one, or nnz-balanced
-    (``partition="nnz"``: equal nonzeros per part, for matrices with irregular rows)."""
+    (``partition="nnz"``: equal nonzeros per part, for matrices with irregular rows), or
+    ``partition="rcm"``: every rank reads the whole matrix, renumbers it with the graph
+    partitioner (reverse Cuthill-McKee, identical on every rank) and keeps its nnz-balanced
+    block of the renumbered rows; x* is drawn in the new numbering."""
+    if partition == "rcm":
+        M, N = H.read_mtx(path)
+        perm = H.rcm_order(M)
+        R = reorder(M, perm)
+        del M
+        return split_problem(backend, {0: R}, {0: H.gen_xstar(0, N, SEED)}, "nnz")
     head = H.read_mtx(path, 0, 0)
     N = head[1]
     if partition == "nnz" and backend.nparts > 1:

@@ -44,6 +44,11 @@ def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, poison
         be = pa.DistributedBackend()
         if kind.startswith("mtx:"):
             A, offs, xs = pa.load_problem(be, kind[4:])
+        elif kind.startswith("rcm:"):  # rcm:<kind>: shuffled, then the graph partitioner
+            whole, _o, wx = pa.generate_problem(pa.SequentialBackend(1), kind[4:], n)
+            whole, wx = pa.permute_problem(whole, wx, 11)
+            whole, wx, _perm = pa.rcm_problem(whole, wx)
+            A, offs, xs = pa.split_problem(be, whole, wx, "nnz")
         else:
             A, offs, xs = pa.generate_problem(be, kind, n)
         H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse, agglomerate=agglomerate))
@@ -122,6 +127,45 @@ def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, agglomerate, poi
         if res[r][5] is not None:
             gid, gv = res[r][5]
             assert len(gid) > 0 and np.array_equal(bits(gv), bits(x[gid]))
+
+
+@pytest.mark.parametrize("world,kind,n", [(3, "elastic3d", 6), (4, "poisson3d", 16)])
+def test_multipart_rcm_partition_bit_exact(world, kind, n, built):
+    """The graph partitioner through the HIP path: a randomly renumbered grid
+    operator, reverse Cuthill-McKee renumbering, nnz-balanced contiguous blocks, N ranks on one
+    GPU (host transport, NaN-poisoned ghosts); b, x and residual histories against the oracle's
+    setup of the same renumbered matrix with the same offsets."""
+    from oracle import oracle as O
+    ncycles, max_coarse = 4, 60
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, "rcm:" + kind, n, max_coarse, 0, ncycles, 1, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r = q.get(timeout=300)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+    assert all(res[r][1] == "ok" for r in range(world)), "\n".join(str(res[r][1]) for r in range(world))
+    import parallel_amg_amd as pa
+    whole, _o, wx = pa.generate_problem(pa.SequentialBackend(1), kind, n)
+    whole, wx = pa.permute_problem(whole, wx, 11)
+    whole, wx, _perm = pa.rcm_problem(whole, wx)
+    _parts, offs, _xp = pa.split_problem(pa.SequentialBackend(world), whole, wx, "nnz")
+    M = whole[0]
+    Ao = O.CSR(M.rowptr.copy(), M.col.astype(np.int64), M.val.copy(), M.ncols)
+    Ho = O.setup(Ao, offsets=offs, max_coarse=max_coarse, agglomerate=0)
+    bo = O.spmv(Ao, wx[0])
+    xo, ho = Ho.solve(bo, ncycles, res_hist=True)
+    bits = lambda a: np.asarray(a, np.float64).view(np.int64)
+    assert np.array_equal(bits(np.concatenate([res[r][2] for r in range(world)])), bits(bo))
+    assert np.array_equal(bits(np.concatenate([res[r][3] for r in range(world)])), bits(xo))
+    for r in range(world):
+        np.testing.assert_allclose(res[r][4], ho, rtol=1e-12)
 
 
 def test_multipart_with_an_empty_part(tmp_path, built):

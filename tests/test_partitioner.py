@@ -1,0 +1,95 @@
+"""Graph partitioner: reverse Cuthill-McKee renumbering (pamg_rcm_order) +
+contiguous nnz-balanced blocks (SPEC §S7). Checked against scipy's RCM (an independent
+implementation) on the bandwidth it reaches, for determinism and permutation validity, on a
+disconnected graph, and end to end: the RCM-renumbered, nnz-split problem sets up bit for bit
+like the oracle's setup of the same renumbered matrix with the same offsets."""
+import numpy as np
+import scipy.sparse as sp
+from scipy.sparse.csgraph import reverse_cuthill_mckee
+
+import parallel_amg_amd as pa
+from oracle import oracle as O
+from parallel_amg_amd import hcsr as HC
+from parallel_amg_amd.hcsr import HCSR
+
+
+def bits(a):
+    return np.asarray(a, np.float64).view(np.int64)
+
+
+def bandwidth(M):
+    rows = np.repeat(np.arange(M.shape[0]), np.diff(M.indptr))
+    return int(np.abs(M.indices - rows).max()) if M.nnz else 0
+
+
+def as_hcsr(M):
+    M = M.tocsr()
+    M.sort_indices()
+    return HCSR.from_arrays(M.indptr.astype(np.int64), M.indices.astype(np.int32), M.data.astype(np.float64),
+                            M.shape[1])
+
+
+def shuffled(kind, n, seed, built=True):
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, kind, n)
+    return pa.permute_problem(A, xs, seed)
+
+
+def test_rcm_restores_a_narrow_band(built):
+    A, xs = shuffled("poisson3d", 12, 5)
+    M = A[0].to_scipy()
+    order = HC.rcm_order(A[0])
+    assert np.array_equal(np.sort(order), np.arange(M.shape[0]))          # a permutation
+    assert np.array_equal(order, HC.rcm_order(A[0]))                       # deterministic
+    mine = bandwidth(M[order][:, order].tocsr())
+    ref = reverse_cuthill_mckee(M.tocsr(), symmetric_mode=True)
+    theirs = bandwidth(M[ref][:, ref].tocsr())
+    assert bandwidth(M) > 10 * mine          # the shuffle is undone...
+    assert mine <= 1.5 * theirs, (mine, theirs)  # ...about as well as scipy's RCM
+
+
+def test_rcm_disconnected_and_isolated(built):
+    a = sp.diags([-1.0, 2.0, -1.0], [-1, 0, 1], shape=(30, 30))
+    M = sp.block_diag([a, sp.identity(5), a.tocsr()[:20, :20]]).tocsr()   # 2 chains + 5 isolated nodes
+    perm = np.random.default_rng(2).permutation(M.shape[0])
+    M = M[perm][:, perm].tocsr()
+    order = HC.rcm_order(as_hcsr(M))
+    assert np.array_equal(np.sort(order), np.arange(M.shape[0]))
+    assert bandwidth(M[order][:, order].tocsr()) == 1   # every component becomes a contiguous chain
+
+
+def test_rcm_split_setup_matches_oracle(built):
+    A, xs = shuffled("elastic3d", 5, 3)
+    R, xr, perm = pa.rcm_problem(A, xs)
+    assert np.array_equal(xr[0], xs[0][perm])
+    be = pa.SequentialBackend(3)
+    parts, offs, xp = pa.split_problem(be, R, xr, "nnz")
+    per = [parts[p].nnz for p in range(3)]
+    assert max(per) - min(per) <= 2 * int(np.diff(R[0].rowptr).max())
+    assert np.array_equal(np.concatenate([xp[p] for p in range(3)]), xr[0])
+    H = pa.build_hierarchy(be, parts, offs, pa.SAParams(max_coarse=40))
+    M = R[0]
+    Ao = O.CSR(M.rowptr.copy(), M.col.astype(np.int64), M.val.copy(), M.ncols)
+    Ho = O.setup(Ao, offsets=offs, max_coarse=40)
+    assert H.nlevels == Ho.nlevels
+    for l in range(H.nlevels):
+        assert np.array_equal(H.offsets(l), Ho.offsets[l])
+        full = np.concatenate([X.val for X in H.part_rows(l)])
+        assert np.array_equal(bits(full), bits(Ho.A[l].val))
+
+
+def test_rcm_partition_of_a_matrix_market_file(tmp_path, built):
+    import scipy.io
+    A, xs = shuffled("poisson2d", 30, 9)
+    M = A[0].to_scipy().tocoo()
+    path = str(tmp_path / "shuffled.mtx")
+    scipy.io.mmwrite(path, M, symmetry="symmetric")
+    be = pa.SequentialBackend(2)
+    parts, offs, xp = pa.load_problem(be, path, partition="rcm")
+    order = HC.rcm_order(A[0])
+    full = A[0].to_scipy().tocsr()[order][:, order].tocsr()
+    full.sort_indices()
+    got = sp.vstack([parts[p].to_scipy(full.shape[1]) for p in range(2)]).tocsr()
+    assert np.array_equal(got.indptr, full.indptr) and np.array_equal(got.indices, full.indices)
+    assert np.array_equal(bits(got.data), bits(full.data))
+    assert np.array_equal(np.concatenate([xp[0], xp[1]]), HC.gen_xstar(0, full.shape[0], pa.hierarchy.SEED))
