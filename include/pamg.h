@@ -222,6 +222,8 @@ int pamg_mtx_row_counts(const char* path, int64_t* n_global, int64_t* counts);
  * §8(f)-3): renumber with it, then cut contiguous nnz-balanced row blocks (SPEC §S7).
  * Deterministic (pseudo-peripheral start, neighbours by degree then index). */
 int pamg_rcm_order(const pamg_hcsr* A, int64_t* order);
+/* Dense coarsest-level limit of pamg_setup_cholinv (rows); larger levels get PAMG_E_ARG. */
+#define PAMG_MAX_DENSE_COARSE 16384
 /* Gershgorin bound over own rows; A's rows are global rows row0.. (diagonal at col row0+i). */
 int pamg_setup_gershgorin(const pamg_hcsr* A, int64_t row0, double* rho);
 /* Decoupled standard aggregation (SPEC §S4.2-3): agg[i] local aggregate id or -1. */

@@ -19,6 +19,8 @@ using pamg::fail;
 
 namespace {
 
+constexpr int64_t kMaxDenseCoarse = PAMG_MAX_DENSE_COARSE;
+
 inline uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
@@ -511,6 +513,11 @@ int pamg_setup_hstack_rows(int k, const pamg_hcsr* const* pieces, pamg_hcsr** ou
 int pamg_setup_cholinv(const pamg_hcsr* A, double* ainv) {
     if (!valid(A) || !ainv || A->nc != A->nr) return fail(PAMG_E_ARG, "cholinv: bad args");
     const int64_t n = A->nr;
+    // the dense coarsest solve holds n^2 doubles twice (and the caller's inverse): refuse sizes
+    // no coarsest level should have (SPEC §S5: max_coarse <= 2048) instead of exhausting memory
+    if (n > kMaxDenseCoarse)
+        return fail(PAMG_E_ARG, "cholinv: coarsest level of %lld rows exceeds the dense-solve limit %lld "
+                    "(raise max_levels or lower max_coarse)", (long long)n, (long long)kMaxDenseCoarse);
     std::vector<double> Ad((size_t)(n * n), 0.0), L((size_t)(n * n), 0.0);
     for (int64_t i = 0; i < n; ++i)
         for (int64_t a = A->rp[i]; a < A->rp[i + 1]; ++a) Ad[i * n + A->col[a]] = A->val[a];

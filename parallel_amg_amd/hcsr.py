@@ -166,8 +166,15 @@ def hstack_rows(pieces) -> HCSR:
     return HCSR(h)
 
 
+MAX_DENSE_COARSE = 16384  # PAMG_MAX_DENSE_COARSE
+
+
 def cholinv(A: HCSR) -> np.ndarray:
     """Column-major inverse (SPEC §S5) as a flat array of n*n."""
+    if A.nrows > MAX_DENSE_COARSE:  # checked before allocating n*n doubles (pamg.h)
+        raise _lib.PamgError(-1, "pamg_setup_cholinv",
+                             f"coarsest level of {A.nrows} rows exceeds the dense-solve limit {MAX_DENSE_COARSE} "
+                             "(raise max_levels or lower max_coarse)")
     out = np.empty(A.nrows * A.nrows, np.float64)
     call("pamg_setup_cholinv", A.handle, ptr(out))
     return out

@@ -132,3 +132,21 @@ def test_hcsr_roundtrip_and_rows(built):
     assert r.tolist() == [0, 4, 7] and np.array_equal(c, np.concatenate([col[3:7], col[0:3]]))
     with pytest.raises(OverflowError):
         HC.HCSR.from_arrays(rp, np.full(8, 2**31 - 1, np.int64), val, 2**31)
+
+
+def test_dense_coarse_solve_refuses_oversized_levels(built):
+    """A coarsest level above PAMG_MAX_DENSE_COARSE rows is refused before any n^2 allocation
+    (a max_levels cap can leave 10^5+ rows there: 10^11 doubles)."""
+    import ctypes
+
+    import pytest
+    from parallel_amg_amd import hcsr as HC
+    from parallel_amg_amd._lib import PamgError, call
+    n = HC.MAX_DENSE_COARSE + 1
+    idx = np.arange(n, dtype=np.int64)
+    M = HC.HCSR.from_arrays(np.arange(n + 1, dtype=np.int64), idx.astype(np.int32), np.full(n, 2.0), n)
+    with pytest.raises(PamgError, match="dense-solve limit"):
+        HC.cholinv(M)
+    one = (ctypes.c_double * 1)()
+    with pytest.raises(PamgError, match="dense-solve limit"):  # the C entry point checks too
+        call("pamg_setup_cholinv", M.handle, one)
