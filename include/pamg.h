@@ -133,8 +133,9 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * out[3] column-dictionary index width (0, 4 or 8), out[4] column-dictionary offsets,
  * out[5] tile-major padded copy, out[6] its row-length slot per tile, out[7] the tile
  * budget (nonzeros per tile) the set was cut with, out[8] the number of short tiles (the
- * grid of the set's tile kernel), out[9] 1 when the dictionary is anchored (offsets from each
- * row's first column, kept in the tile-major slots) instead of row-relative. */
+ * grid of the set's tile kernel), out[9] bit 0: the dictionary is anchored (offsets from each
+ * row's first column) instead of row-relative; bit 1: every tile has its own table of out[4]
+ * entries (per-tile dictionaries) instead of one table for the set. */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[10]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
@@ -193,7 +194,7 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
 
 /* Process-wide knobs. Applied to later pamg_mat_upload calls: "tile_nnz" (1024 | 2048 | 4096,
  * nonzero budget of a 256-row tile), "tile_order" (0 natural | 1 banded XCD-blocked), "col24",
- * "long_tiles", "row_len8", "value_dict", "col_dict", "col_dict_anchor" (0 | 1 layout
+ * "long_tiles", "row_len8", "value_dict", "col_dict", "col_dict_anchor", "col_dict_tile" (0 | 1 layout
  * features), "tile_major" (0 | 1 where measured faster | 2 every eligible set). Applied at
  * every exchange:
  * "poison_ghosts" (0 | 1, debug: NaN-fill the ghost slots before each exchange). */

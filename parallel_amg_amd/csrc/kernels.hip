@@ -126,7 +126,8 @@ __device__ __forceinline__ double row_sum_lds(const double* __restrict__ lp, int
 // at kernel entry together with the row-pointer slice; all x gathers of a lane are then
 // issued back to back (branch-free: invalid lanes gather x[0] and discard it) before the
 // products go to LDS.
-template <int OP, int TNNZ, bool C24 = false, bool VD = false, bool RL8 = false, int CD = 0>
+template <int OP, int TNNZ, bool C24 = false, bool VD = false, bool RL8 = false, int CD = 0, bool PT = false,
+          bool ANC = false>
 __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     const int4* __restrict__ tiles, const int* __restrict__ rowptr,
     const int* __restrict__ col, const double* __restrict__ val, const double* __restrict__ x,
@@ -135,7 +136,11 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     const int* __restrict__ tbase = nullptr, const uint8_t* __restrict__ vidx = nullptr,
     const double* __restrict__ vtab = nullptr, const uint8_t* __restrict__ rlen = nullptr,
     const uint8_t* __restrict__ cidx = nullptr, const int* __restrict__ ctab = nullptr,
-    int ctab_n = 0) {
+    int ctab_n = 0, const uint16_t* __restrict__ anc16 = nullptr, const int* __restrict__ abase = nullptr) {
+    // PT: per-tile dictionary — this tile's table is ctab[bid * ctab_n ...]; ANC: columns are
+    // the row's anchor (abase[tile] + anc16[row]) + table[index] instead of row + table[index]
+    static_assert(!PT || CD != 0, "per-tile tables are column dictionaries");
+    static_assert(!ANC || PT, "anchored columns in the descriptor kernel come with per-tile tables");
     // C24: the column stream is 3 B/nonzero — per-tile base + 16-bit low part (8 B per lane)
     // + 8-bit high part (4 B per lane) instead of the 16-B int4 of 32-bit ids.
     // VD (opt-in): values are 4-bit indices (2 B per lane) into the tile's 16-value table,
@@ -156,6 +161,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     static_assert(CD == 0 || (RL8 && !C24 && !VD), "column dictionary: 8-bit rows, plain values");
     __shared__ int ltab[CD != 0 ? BS : 1];
     __shared__ __attribute__((aligned(4))) uint8_t lrow[CD ? TNNZ + 8 : 4];
+    __shared__ int lanc[ANC ? BS : 1];
 
     const int bid = blockIdx.x;
     const int tid = threadIdx.x;
@@ -173,7 +179,12 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
         rpa = rowptr[r0 + (tid < nr ? tid : nr)];
         rpb = rowptr[r0 + nr];
     }
-    if constexpr (CD != 0) tabv = ctab[tid];  // the table is allocated with 256 entries
+    if constexpr (CD != 0) {
+        if constexpr (PT) tabv = ctab[(size_t)bid * ctab_n + (tid < ctab_n ? tid : ctab_n - 1)];
+        else tabv = ctab[tid];  // the global table is allocated with 256 entries
+    }
+    int ancv = 0;
+    if constexpr (ANC) ancv = abase[bid] + (int)anc16[r0 + lr];
     int4 c4[G];
     double2 va[G], vb[G];
     uint16_t vn[G];  // VD: four 4-bit value indices per lane group
@@ -239,7 +250,8 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     };
     if constexpr (CD != 0) {
         ltab[tid] = tabv;
-        __syncthreads();  // lwt, ltab
+        if constexpr (ANC) lanc[tid] = ancv;
+        __syncthreads();  // lwt, ltab, lanc
         if (tid < nr) {
             const int e = rl_base() + rl_inc - za;
             for (int p = e - rl_len; p < e; ++p) lrow[p] = (uint8_t)tid;
@@ -253,7 +265,9 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int ix = CD == 4 ? (int)((cn[j] >> (4 * e)) & 15u) : (int)((cn[j] >> (8 * e)) & 255u);
-                cc[e] = r0 + (int)((rw >> (8 * e)) & 255u) + ltab[ix];
+                const int rid = (int)((rw >> (8 * e)) & 255u);
+                if constexpr (ANC) cc[e] = lanc[rid] + ltab[ix];
+                else cc[e] = r0 + rid + ltab[ix];
             }
             c4[j] = make_int4(cc[0], cc[1], cc[2], cc[3]);
         }
@@ -657,6 +671,31 @@ inline int grid_for(int64_t n, int cap = 8192) {
     return (int)(g < cap ? g : cap);
 }
 
+// descriptor kernel with column dictionaries: global tables, or per-tile (PT) ones, anchored or not
+template <int OP, int TNNZ, bool PT>
+void launch_tile2_cd(const pamg_mat& A, const TileSet& ts, const double* x, const double* b, double* y,
+                     double omega, hipStream_t s) {
+    const int n = ts.n_short;
+    if (PT && ts.anc) {
+        if (ts.cd == 4)
+            k_rows_tile2<OP, TNNZ, false, false, true, 4, true, true><<<n, kBlock, 0, s>>>(
+                ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, nullptr, nullptr,
+                A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n, A.d_anc16, ts.d_abase);
+        else
+            k_rows_tile2<OP, TNNZ, false, false, true, 8, true, true><<<n, kBlock, 0, s>>>(
+                ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, nullptr, nullptr,
+                A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n, A.d_anc16, ts.d_abase);
+    } else if (ts.cd == 4) {
+        k_rows_tile2<OP, TNNZ, false, false, true, 4, PT><<<n, kBlock, 0, s>>>(
+            ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, nullptr, nullptr,
+            A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n);
+    } else {
+        k_rows_tile2<OP, TNNZ, false, false, true, 8, PT><<<n, kBlock, 0, s>>>(
+            ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, nullptr, nullptr,
+            A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n);
+    }
+}
+
 template <int OP, int TNNZ>
 void launch_tile(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
                  double* y, double omega, hipStream_t s) {
@@ -683,14 +722,10 @@ void launch_tile(const pamg_mat& A, const TileSet& ts, const double* x, const do
                                                        ts.d_tm_chi, ts.d_base, ts.d_tm_rlen, ts.tm_rs, nullptr,
                                                        0, x, b, y, omega);
     } else if (ts.cd && A.d_cidx && ts.rl8 && A.d_rlen) {
-        if (ts.cd == 4)
-            k_rows_tile2<OP, TNNZ, false, false, true, 4><<<n, kBlock, 0, s>>>(
-                ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, nullptr,
-                nullptr, A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n);
+        if (ts.pt)
+            launch_tile2_cd<OP, TNNZ, true>(A, ts, x, b, y, omega, s);
         else
-            k_rows_tile2<OP, TNNZ, false, false, true, 8><<<n, kBlock, 0, s>>>(
-                ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, nullptr,
-                nullptr, A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n);
+            launch_tile2_cd<OP, TNNZ, false>(A, ts, x, b, y, omega, s);
     } else if (ts.c24 && A.d_clo && ts.vd && A.d_vidx) {
         k_rows_tile2<OP, TNNZ, true, true><<<n, kBlock, 0, s>>>(ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y,
                                                                omega, A.d_clo, A.d_chi, ts.d_base, A.d_vidx,

@@ -51,6 +51,10 @@ struct TileSet {
     // anchored dictionary (Options::col_dict_anchor; tile-major sets only): column = the row's
     // first column + d_ctab[i]; the row anchors sit in the tile-major slots (d_tm_anc)
     bool anc = false;
+    // per-tile dictionaries (Options::col_dict_tile; descriptor kernel only): d_ctab holds
+    // n_short tables of ctab_n entries; anchored ones take pamg_mat::d_anc16 + d_abase[tile]
+    bool pt = false;
+    int* d_abase = nullptr;
     // tile-major copies (Options::tile_major; kernels.hip k_rows_tm): tile t's values and
     // column stream at t * tile_nnz, its row lengths at t * tm_rs, zero-padded
     bool tm = false;
@@ -78,6 +82,7 @@ struct Options {
     int value_dict = 0;        // 1 (opt-in): 4-bit per-tile value dictionaries where they fit
     int col_dict = 1;          // 1: row-relative column dictionaries (4/8-bit) where they fit
     int tile_major = 1;        // tile-major padded copies (variant 4): 1 where measured faster, 2 all eligible
+    int col_dict_tile = 1;     // 1: per-tile column dictionaries where no global table fits (and they beat 24-bit)
     int col_dict_anchor = 1;   // 1: anchored column dictionaries (col - row's first column) where row-relative ones do not fit
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };
@@ -132,6 +137,7 @@ struct pamg_mat {
     uint8_t* d_vidx = nullptr;  // value dictionary indices, two per byte (TileSet::vd)
     uint8_t* d_rlen = nullptr;  // row lengths, when a tile set uses them (TileSet::rl8)
     uint8_t* d_cidx = nullptr;  // column dictionary indices (TileSet::cd; 4 or 8 bits each)
+    uint16_t* d_anc16 = nullptr;  // per-tile anchored dictionaries: row's first column - tile base
     double* d_val = nullptr;
     double* d_diag = nullptr;  // a_ii for square matrices (zero-guess Jacobi), else null
     const pamg_plan* plan = nullptr;

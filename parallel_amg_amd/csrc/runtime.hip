@@ -316,6 +316,114 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
     return PAMG_OK;
 }
 
+// Per-tile column dictionaries (Options::col_dict_tile) for tile sets no global table fits:
+// every tile carries its own table of <= 256 offsets (capacity ctab_n = the largest tile's
+// count rounded up to a power of two >= 16, so 4-bit indices where every tile has <= 16),
+// row-relative (col - row: the coarse operators, 33 offsets per tile on average for A1 at
+// 512^3 against ~10^4 in the whole matrix) or anchored (col - the row's middle column, stored
+// as a 16-bit delta from a per-tile base: the prolongators, a few per tile). The form
+// with fewer bytes is taken, and only if it streams less than the 24-bit columns; it runs in
+// the descriptor kernel (k_rows_tile2), not in tile-major slots.
+int build_tile_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci,
+                     const std::vector<int4>& tiles, pamg::TileSet* ts, std::vector<uint8_t>* idx,
+                     std::vector<int>* tab, std::vector<uint16_t>* anc16) {
+    const int64_t nt = (int64_t)tiles.size();
+    if (nt == 0) return PAMG_OK;
+    // anchor of a row: its middle column (for a prolongator row, its own aggregate's
+    // neighbourhood), so one tile's anchors stay within a 16-bit span
+    auto mid_col = [&](int r) { return rp[r + 1] > rp[r] ? ci[rp[r] + (rp[r + 1] - rp[r] - 1) / 2] : 0; };
+    int64_t nz = 0, rows = 0;
+    for (const int4& t : tiles) {
+        nz += t.w - t.z;
+        rows += t.y - t.x;
+    }
+    // per tile: distinct offsets in first-occurrence order (count only), both forms
+    std::vector<int> cnt_rel(nt), cnt_anc(nt), base(nt, 0);
+    std::vector<char> span_ok(nt, 1);
+    auto distinct = [&](const int4& t, bool anchored, int* out_tab, int cap) {
+        constexpr int kCells = 2048;
+        int key[kCells], slot[kCells];
+        std::fill(slot, slot + kCells, -1);
+        int n = 0;
+        for (int r = t.x; r < t.y; ++r) {
+            const int an = anchored ? mid_col(r) : r;
+            for (int64_t k = rp[r]; k < rp[r + 1]; ++k) {
+                const int o = ci[k] - an;
+                uint32_t h = ((uint32_t)o * 0x9E3779B1u) >> 21;
+                while (slot[h] >= 0 && key[h] != o) h = (h + 1) & (kCells - 1);
+                if (slot[h] < 0) {
+                    if (n == cap) return cap + 1;
+                    key[h] = o;
+                    slot[h] = n;
+                    if (out_tab) out_tab[n] = o;
+                    ++n;
+                }
+                if (idx && out_tab) (*idx)[k] = (uint8_t)slot[h];
+            }
+        }
+        return n;
+    };
+    par_for(nt, [&](int64_t a, int64_t b) {
+        for (int64_t t = a; t < b; ++t) {
+            const int4 d = tiles[t];
+            cnt_rel[t] = distinct(d, false, nullptr, 256);
+            cnt_anc[t] = distinct(d, true, nullptr, 256);
+            int mn = INT32_MAX, mx = INT32_MIN;
+            for (int r = d.x; r < d.y; ++r)
+                if (rp[r + 1] > rp[r]) {
+                    mn = std::min(mn, mid_col(r));
+                    mx = std::max(mx, mid_col(r));
+                }
+            base[t] = mn == INT32_MAX ? 0 : mn;
+            span_ok[t] = mn == INT32_MAX || (int64_t)mx - mn < 65536;
+        }
+    });
+    auto cap_of = [](int m) {
+        int c = 16;
+        while (c < m) c <<= 1;
+        return c;
+    };
+    const int mrel = *std::max_element(cnt_rel.begin(), cnt_rel.end());
+    const int manc = *std::max_element(cnt_anc.begin(), cnt_anc.end());
+    const bool anc_ok = manc <= 256 && std::all_of(span_ok.begin(), span_ok.end(), [](char c) { return c != 0; });
+    auto bytes = [&](int m, bool anchored) -> double {
+        const int c = cap_of(m);
+        return (c <= 16 ? 0.5 : 1.0) * (double)nz + 4.0 * c * nt + (anchored ? 2.0 * rows : 0.0);
+    };
+    const double b24 = 3.0 * (double)nz + 4.0 * nt;  // the 24-bit stream it would replace
+    bool use_anc = false;
+    double best = b24;
+    if (mrel <= 256 && bytes(mrel, false) < best) best = bytes(mrel, false);
+    if (anc_ok && bytes(manc, true) < best) {
+        best = bytes(manc, true);
+        use_anc = true;
+    }
+    if (std::getenv("PAMG_TRACE_UPLOAD"))
+        std::fprintf(stderr, "[pamg upload] per-tile dictionaries: %lld tiles, max offsets/tile row-relative %d, "
+                     "anchored %d (16-bit span %s) -> %s\n", (long long)nt, mrel, manc, anc_ok ? "ok" : "no",
+                     best >= b24 ? "24-bit kept" : use_anc ? "anchored" : "row-relative");
+    if (best >= b24) return PAMG_OK;
+    const int cap = cap_of(use_anc ? manc : mrel);
+    tab->assign((size_t)nt * cap, 0);
+    if (use_anc && anc16->empty()) anc16->assign((size_t)A->nrows + kVecPad, 0);
+    par_for(nt, [&](int64_t a, int64_t b) {
+        for (int64_t t = a; t < b; ++t) {
+            distinct(tiles[t], use_anc, tab->data() + (size_t)t * cap, cap);
+            if (use_anc)
+                for (int r = tiles[t].x; r < tiles[t].y; ++r)
+                    (*anc16)[r] = rp[r + 1] > rp[r] ? (uint16_t)(mid_col(r) - base[t]) : 0;
+        }
+    });
+    if (use_anc) {
+        CHECK(dalloc(&ts->d_abase, nt));
+        HIPC(hipMemcpy(ts->d_abase, base.data(), sizeof(int) * nt, hipMemcpyHostToDevice));
+    }
+    ts->pt = true;
+    ts->anc = use_anc;
+    ts->ctab_n = cap;
+    return PAMG_OK;
+}
+
 // Column dictionaries (Options::col_dict). A tile set whose short-tile nonzeros have at most
 // 256 distinct row-relative offsets col - row (the fine-grid stencils: 7 for the 7-point
 // Poisson, 5 in 2D, 99 for elastic3d) stores each column as an index into the set's offset
@@ -331,7 +439,8 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
     pamg::TileSet* sets[2] = {&A->interior, &A->boundary};
     const std::vector<int4>* tl[2] = {&t_in, &t_bd};
     std::vector<uint8_t> idx;  // 8-bit index per nonzero (packed to 4 bits below if they fit)
-    std::vector<int> tab[2];
+    std::vector<int> tab[2];   // global table, or (per-tile sets) nt x ctab_n tables
+    std::vector<uint16_t> anc16;  // per-tile anchored sets: each row's first column - tile base
     for (int q = 0; q < 2; ++q) {
         pamg::TileSet* ts = sets[q];
         if (!opt.col_dict || ts->vd || ts->n_short == 0 || ts->max_short_len > 255)
@@ -408,22 +517,41 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
             return true;
         };
         ts->anc = false;
-        if (!try_dict(false) && opt.col_dict_anchor && opt.tile_major) ts->anc = try_dict(true);
+        ts->pt = false;
+        if (try_dict(false)) continue;
+        if (opt.col_dict_anchor && opt.tile_major && try_dict(true)) {
+            ts->anc = true;
+            continue;
+        }
+        if (opt.col_dict_tile) CHECK(build_tile_dicts(A, rp, ci, tiles, ts, &idx, &tab[q], &anc16));
     }
     int width = 0;
-    for (int q = 0; q < 2; ++q)
-        if (!tab[q].empty()) width = std::max(width, tab[q].size() <= 16 ? 4 : 8);
+    for (int q = 0; q < 2; ++q) {
+        if (tab[q].empty()) continue;
+        const size_t entries = sets[q]->pt ? (size_t)sets[q]->ctab_n : tab[q].size();
+        width = std::max(width, entries <= 16 ? 4 : 8);
+    }
     if (width == 0) return PAMG_OK;
     for (int q = 0; q < 2; ++q) {
         if (tab[q].empty()) continue;
         pamg::TileSet* ts = sets[q];
-        std::vector<int> tab256(256, 0);  // any 8-bit index stays inside the allocation
-        std::copy(tab[q].begin(), tab[q].end(), tab256.begin());
-        CHECK(dalloc(&ts->d_ctab, (int64_t)tab256.size()));
-        HIPC(hipMemcpy(ts->d_ctab, tab256.data(), sizeof(int) * tab256.size(), hipMemcpyHostToDevice));
-        ts->ctab_n = (int)tab[q].size();
+        if (ts->pt) {  // nt x ctab_n per-tile tables (+ 256 so any index of the last tile stays inside)
+            tab[q].resize(tab[q].size() + 256, 0);
+            CHECK(dalloc(&ts->d_ctab, (int64_t)tab[q].size()));
+            CHECK(h2d(A->ctx, ts->d_ctab, tab[q].data(), sizeof(int) * tab[q].size()));
+        } else {
+            std::vector<int> tab256(256, 0);  // any 8-bit index stays inside the allocation
+            std::copy(tab[q].begin(), tab[q].end(), tab256.begin());
+            CHECK(dalloc(&ts->d_ctab, (int64_t)tab256.size()));
+            HIPC(hipMemcpy(ts->d_ctab, tab256.data(), sizeof(int) * tab256.size(), hipMemcpyHostToDevice));
+            ts->ctab_n = (int)tab[q].size();
+        }
         ts->cd = width;
         ts->rl8 = true;
+    }
+    if (!anc16.empty()) {
+        CHECK(dalloc(&A->d_anc16, (int64_t)anc16.size()));
+        CHECK(h2d(A->ctx, A->d_anc16, anc16.data(), sizeof(uint16_t) * anc16.size()));
     }
     if (width == 4) {
         std::vector<uint8_t> nib(((size_t)A->nnz + 1) / 2 + kVecPad, 0);
@@ -460,6 +588,7 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
     for (int q = 0; q < 2; ++q) {
         pamg::TileSet* ts = sets[q];
         ts->tm = false;
+        if (ts->pt) continue;  // per-tile dictionaries run in the descriptor kernel
         if (!opt.tile_major || ts->vd || ts->n_short == 0 || ts->max_short_len > 255 ||
             !(ts->cd || (ts->c24 && !lo.empty())) || (ts->cd && idx8.empty()) || !val) {
             if (ts->anc) return fail(PAMG_E_STATE, "upload: anchored column dictionary without tile-major slots");
@@ -560,7 +689,8 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_tm_chi);
     dfree(ts.d_tm_rlen);
     dfree(ts.d_tm_anc);
-    ts.anc = false;
+    dfree(ts.d_abase);
+    ts.anc = ts.pt = false;
     ts.tm = false;
     ts.tm_rs = 0;
     ts.c24 = ts.vd = ts.rl8 = false;
@@ -1340,7 +1470,8 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
                  (t->cd ? 4 * t->ctab_n : 0);
         } else {
             b += (t->rl8 ? 1 : 4) * t->rows_short;
-            b += t->cd ? (t->cd * nz + 7) / 8 + 4 * t->ctab_n : (t->c24 ? 3 : 4) * nz;
+            b += t->cd ? (t->cd * nz + 7) / 8 + 4 * t->ctab_n * (t->pt ? ns : 1) : (t->c24 ? 3 : 4) * nz;
+            if (t->pt && t->anc) b += 2 * t->rows_short + 4 * ns;  // 16-bit anchors + tile bases
             b += t->vd ? nz / 2 + 128 * ns : 8 * nz;
             b += (16 + (base ? 4 : 0)) * ns;
         }
@@ -1370,6 +1501,7 @@ int pamg_mat_destroy(pamg_mat* A) {
     dfree(A->d_chi);
     dfree(A->d_vidx);
     dfree(A->d_cidx);
+    dfree(A->d_anc16);
     dfree(A->d_val);
     dfree(A->d_diag);
     free_tiles(A->interior);
@@ -1404,7 +1536,7 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[6] = t.tm_rs;
     out[7] = t.tile_nnz;
     out[8] = t.n_short;
-    out[9] = t.anc;
+    out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0);
     return PAMG_OK;
 }
 
@@ -1816,6 +1948,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "col_dict" && (value == 0 || value == 1)) o.col_dict = (int)value;
     else if (k == "tile_major" && value >= 0 && value <= 2) o.tile_major = (int)value;
     else if (k == "col_dict_anchor" && (value == 0 || value == 1)) o.col_dict_anchor = (int)value;
+    else if (k == "col_dict_tile" && (value == 0 || value == 1)) o.col_dict_tile = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -1834,6 +1967,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "col_dict") *value = o.col_dict;
     else if (k == "tile_major") *value = o.tile_major;
     else if (k == "col_dict_anchor") *value = o.col_dict_anchor;
+    else if (k == "col_dict_tile") *value = o.col_dict_tile;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

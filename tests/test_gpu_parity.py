@@ -195,7 +195,7 @@ def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
     rows = np.repeat(np.arange(n), np.diff(M.rowptr))
     distinct = len(np.unique(M.col - rows))
     dist_anc = len(np.unique(M.col - np.repeat(M.col[np.minimum(M.rowptr[:-1], max(M.nnz - 1, 0))], np.diff(M.rowptr))))
-    keys = ("col_dict", "tile_nnz", "tile_major", "col_dict_anchor")
+    keys = ("col_dict", "tile_nnz", "tile_major", "col_dict_anchor", "col_dict_tile")
     old = []
     for k in keys:
         v = ctypes.c_int64()
@@ -203,6 +203,7 @@ def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
         old.append(v.value)
     try:
         call("pamg_set_option", b"col_dict_anchor", 1)
+        call("pamg_set_option", b"col_dict_tile", 0)  # set-wide tables only (per-tile: below)
         call("pamg_set_option", b"tile_nnz", tnnz)
         call("pamg_set_option", b"col_dict", 0)
         call("pamg_set_option", b"tile_major", 0)
@@ -433,8 +434,11 @@ def test_anchored_dictionary_bit_exact(ctx, nshape, maxlen, tnnz):
         call("pamg_set_option", b"tile_nnz", old.value)
     lay = layout_of(A)
     used = len(np.unique(M.col - np.repeat(M.col[M.rowptr[:-1]], np.diff(M.rowptr))))
-    assert lay["anchored"] == (used <= 256) and (lay["tm"] or used > 256)
-    assert lay["cd"] == (4 if used <= 16 else 8 if used <= 256 else 0), (lay, used)
+    if used <= 256:  # one set-wide anchored table in tile-major slots
+        assert lay["anchored"] and lay["tm"] and not lay["per_tile"]
+        assert lay["cd"] == (4 if used <= 16 else 8), (lay, used)
+    else:            # too many for one table: per-tile tables (if they pay) or 24-bit columns
+        assert lay["per_tile"] or lay["cd"] == 0, lay
     xh, bh = rng.standard_normal(nc), rng.standard_normal(nr)
     x, b = PVector(ctx, nc, 0, xh), PVector(ctx, nr, 0, bh)
     y = PVector(ctx, nr)
@@ -449,6 +453,114 @@ def test_anchored_dictionary_bit_exact(ctx, nshape, maxlen, tnnz):
     call("pamg_bench_rowop", ctx.handle, A.handle, 3, x.handle, None, yy.handle, 0.0, 1, ctypes.byref(ms))
     assert np.array_equal(bits(yy.own_values()), bits((bh + ref) + ref))
 
+
+
+def _layout_ops_match_oracle(ctx, M, rng):
+    """SpMV / residual / prolongate-add (and Jacobi on square M) of the uploaded M against
+    the oracle, bit for bit."""
+    import ctypes
+    from parallel_amg_amd._lib import call
+    A, _h = upload(ctx, M)
+    nr, nc = M.nrows, M.ncols
+    xh, bh = rng.standard_normal(nc), rng.standard_normal(nr)
+    x, b = PVector(ctx, nc, 0, xh), PVector(ctx, nr, 0, bh)
+    y = PVector(ctx, nr)
+    mul(y, A, x)
+    ref = O.spmv(M, xh)
+    assert np.array_equal(bits(y.own_values()), bits(ref))
+    r = PVector(ctx, nr)
+    residual(r, A, x, b)
+    assert np.array_equal(bits(r.own_values()), bits(O.residual(M, xh, bh)))
+    ms = ctypes.c_double()
+    yy = PVector(ctx, nr, 0, bh)
+    call("pamg_bench_rowop", ctx.handle, A.handle, 3, x.handle, None, yy.handle, 0.0, 1, ctypes.byref(ms))
+    assert np.array_equal(bits(yy.own_values()), bits((bh + ref) + ref))
+    if nr == nc:
+        t = PVector(ctx, nr)
+        jacobi(x, A, b, t, 0.7, 2)
+        rj = O.jacobi(M, O.jacobi(M, xh, bh, 0.7), bh, 0.7)
+        assert np.array_equal(bits(x.own_values()), bits(rj))
+    return A
+
+
+def drift_csr(rng, n, ncols, anchored, nset=12, every=200, step=37):
+    """Rows whose columns are (row | a slowly drifting anchor) + a subset of an offset set that
+    shifts by `step` every `every` rows: far more than 256 offsets in the matrix, a few dozen
+    per tile — the shape of the coarse operators (row-relative) and prolongators (anchored)."""
+    base = np.sort(rng.choice(np.arange(-300, 300), nset, replace=False))
+    rows, cols = [0], []
+    for i in range(n):
+        g = (i // every) % 30
+        m = int(rng.integers(1, nset + 1))
+        if anchored:  # 30 scaled copies of the set around a drifting anchor
+            c = np.unique(3 * i + int(rng.integers(0, 4)) + (g + 1) * rng.choice(base, m, replace=False))
+        else:         # 30 shifted copies of the set, relative to the row
+            c = np.unique(i + g * step - 15 * step + rng.choice(base, m, replace=False))
+        c = c[(c >= 0) & (c < ncols)]  # dropped, not clipped: no new offsets at the edges
+        if not anchored:
+            c = np.unique(np.concatenate([c, [i]]))  # square: keep the diagonal
+        cols.append(c)
+        rows.append(rows[-1] + len(c))
+    col = np.concatenate(cols).astype(np.int64)
+    val = rng.standard_normal(len(col))
+    if not anchored:  # diagonally dominant rows for Jacobi
+        rp = np.asarray(rows)
+        for i in range(n):
+            seg = slice(rp[i], rp[i + 1])
+            val[seg][col[seg] == i] = 4.0 + (rp[i + 1] - rp[i])
+    return O.CSR(np.asarray(rows, np.int64), col, val, ncols)
+
+
+@pytest.mark.parametrize("anchored,tnnz", [(False, 1024), (False, 4096), (True, 1024), (True, 2048)])
+def test_per_tile_dictionaries_bit_exact(ctx, anchored, tnnz):
+    """col_dict_tile: no table fits the whole matrix (> 256 offsets) but every tile's fits —
+    per-tile row-relative tables (coarse-operator shape) or per-tile anchored ones with 16-bit
+    anchors (prolongator shape) in the descriptor kernel; SpMV / residual / prolongate-add (and
+    Jacobi for the square case) give the oracle's bits."""
+    import ctypes
+    from parallel_amg_amd._lib import call, layout_of
+    rng = np.random.default_rng(tnnz + anchored)
+    n = 6000
+    M = drift_csr(rng, n, 3 * n if anchored else n, anchored, nset=6 if anchored else 12)
+    old = ctypes.c_int64()
+    call("pamg_get_option", b"tile_nnz", ctypes.byref(old))
+    try:
+        call("pamg_set_option", b"tile_nnz", tnnz)
+        D = _layout_ops_match_oracle(ctx, M, rng)
+    finally:
+        call("pamg_set_option", b"tile_nnz", old.value)
+    lay = layout_of(D)
+    assert lay["per_tile"] and lay["anchored"] == anchored and not lay["tm"], lay
+    assert lay["cd"] in (4, 8) and lay["cd_offsets"] in (16, 32, 64, 128, 256), lay
+
+
+def test_hierarchy_operators_any_dictionary_bit_exact(ctx):
+    """The level-1 operator and the level-0 prolongator of a real hierarchy, in whatever column
+    format the upload picks (per-tile tables at 512^3, 24-bit or set-wide tables at this size),
+    give the oracle's bits."""
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 48)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=100))
+    rng = np.random.default_rng(5)
+    for M in (H.levels[1][0].A, H.levels[0][0].P, H.levels[1][0].P):
+        Mo = O.CSR(M.rowptr.copy(), M.col.astype(np.int64), M.val.copy(), M.ncols)
+        _layout_ops_match_oracle(ctx, Mo, rng)
+
+
+@pytest.mark.parametrize("name,ndist,lengths", [("d300", 300, [30, 1, 7, 64]), ("d2000", 2000, [9, 3, 40]),
+                                                ("wide_ragged", 600, [1, 255, 2, 17])])
+def test_per_tile_dictionaries_random(ctx, name, ndist, lengths):
+    """Random offset patterns too wide for one table: per-tile tables where they stream less
+    than 24-bit columns (else 24-bit), bit-exact either way."""
+    from parallel_amg_amd._lib import layout_of
+    rng = np.random.default_rng(len(name))
+    n = 5000
+    offs = rng.choice(np.arange(-n // 2, n // 2), size=ndist + 1, replace=False)
+    offs = offs[offs != 0][:ndist]
+    M = offset_csr(rng, n, offs, lengths)
+    D = _layout_ops_match_oracle(ctx, M, rng)
+    lay = layout_of(D)
+    assert lay["per_tile"] or lay["cd"] == 0, lay
 
 def test_restriction_takes_anchored_dictionary(ctx):
     """The level-0 restriction of the 7-point Poisson hierarchy (5x5x5 neighbourhoods of the
