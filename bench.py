@@ -259,12 +259,16 @@ def main():
     # count (the uploaded layout) and the same kernels.hip source as this run.
     lay = _lib.layout_of(A0)
     cd, tm, tn = lay["cd"], lay["tm"], lay["tile_nnz"]
-    kname = (f"k_rows_tm<2, {tn}, {cd}>" if tm
-             else f"k_rows_tile2<2, {tn}, false, false, true, {cd}>" if cd
-             else f"k_rows_tile2<2, {tn}, true, true>" if lay["vd"]
-             else f"k_rows_tile2<2, {tn}, true, false, true>" if lay["rl8"]
-             else f"k_rows_tile2<2, {tn}, true>" if lay["c24"]
-             else f"k_rows_tile2<2, {tn}>")
+    # the instance name as rocprofv3 demangles it (every template argument, defaults included)
+    tf = lambda v: "true" if v else "false"  # noqa: E731
+    if tm:
+        kname = f"k_rows_tm<2, {tn}, {cd}, {tf(lay['anchored'])}>"
+    elif cd:
+        kname = f"k_rows_tile2<2, {tn}, false, false, true, {cd}, {tf(lay['per_tile'])}, {tf(lay['anchored'])}>"
+    else:
+        c24 = lay["c24"]
+        kname = (f"k_rows_tile2<2, {tn}, {tf(c24)}, {tf(lay['vd'])}, {tf(lay['rl8'] and c24 and not lay['vd'])}, "
+                 f"0, false, false>")
     workload_key = f"{args.matrix or args.kind}:{args.grid}:p{world}:perm{args.permute}" + (":rcm" if args.rcm else "")
     src = kernel_source_sha()
     traffic = pmc_lookup("traffic_jacobi.json", kname, lay["tiles"], workload_key, src)
