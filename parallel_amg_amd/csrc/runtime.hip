@@ -209,7 +209,7 @@ int build_value_dict(const std::vector<int4>& tiles, const double* val, pamg::Ti
     return PAMG_OK;
 }
 
-int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
+int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows, bool square,
                 pamg::TileSet* ts, int64_t band, const std::vector<int>& ci,
                 std::vector<uint16_t>* lo, std::vector<uint8_t>* hi, const double* val,
                 std::vector<uint8_t>* vidx, std::vector<int4>* tiles_out) {
@@ -220,8 +220,10 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows,
     // average) take 4096-nonzero tiles instead of the default 1024 — their time goes into the
     // in-order add chain of each row (SPEC §S3), and a tile of 4x the rows runs 4x the chains
     // side by side (512^3: A2 0.139 -> 0.110 ms, R1 0.458 -> 0.439 ms,
-    // profiles/r01_kbench_512_tnnz.jsonl); the 7- and 27-point levels keep 1024.
-    if (opt.long_tiles && tnnz == 1024 && !rows.empty()) {
+    // profiles/r01_kbench_512_tnnz.jsonl); the 7- and 27-point levels keep 1024. Square
+    // operators only: the long-row restriction R1 (188 nonzeros per row, tile-major) is 9 %
+    // faster with 1024 (profiles/r02_exp/kbench512_level12_tiles.jsonl), A2 13 % slower.
+    if (opt.long_tiles && square && tnnz == 1024 && !rows.empty()) {
         int64_t nz = 0;
         for (int r : rows) nz += rp[r + 1] - rp[r];
         if (nz >= 48 * (int64_t)rows.size()) tnnz = 4096;
@@ -1431,8 +1433,9 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     std::vector<uint8_t> hi, vidx;
     {
         std::vector<int4> t_in, t_bd;
-        CHECK(build_tiles(rp, inner, &A->interior, band, ci, &lo, &hi, val, &vidx, &t_in));
-        CHECK(build_tiles(rp, bnd, &A->boundary, band, ci, &lo, &hi, val, &vidx, &t_bd));
+        const bool square = n_own_cols == nrows;
+        CHECK(build_tiles(rp, inner, square, &A->interior, band, ci, &lo, &hi, val, &vidx, &t_in));
+        CHECK(build_tiles(rp, bnd, square, &A->boundary, band, ci, &lo, &hi, val, &vidx, &t_bd));
         tr.mark("tiles");
         std::vector<uint8_t> idx8;
         CHECK(build_col_dicts(A.get(), rp, ci, t_in, t_bd, &idx8));
