@@ -135,7 +135,8 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * budget (nonzeros per tile) the set was cut with, out[8] the number of short tiles (the
  * grid of the set's tile kernel), out[9] bit 0: the dictionary is anchored (offsets from each
  * row's first column) instead of row-relative; bit 1: every tile has its own table of out[4]
- * entries (per-tile dictionaries) instead of one table for the set. */
+ * entries (per-tile dictionaries) instead of one table for the set; bit 2: the tile kernel
+ * stages x in LDS (x_stage: the runs the set's offset clusters read, no x gathers). */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[10]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
@@ -194,8 +195,8 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
 
 /* Process-wide knobs. Applied to later pamg_mat_upload calls: "tile_nnz" (1024 | 2048 | 4096,
  * nonzero budget of a 256-row tile), "tile_order" (0 natural | 1 banded XCD-blocked), "col24",
- * "long_tiles", "row_len8", "value_dict", "col_dict", "col_dict_anchor", "col_dict_tile" (0 | 1 layout
- * features), "tile_major" (0 | 1 where measured faster | 2 every eligible set). Applied at
+ * "long_tiles", "row_len8", "value_dict", "col_dict", "col_dict_anchor", "col_dict_tile", "x_stage" (0 | 1
+ * layout features), "tile_major" (0 | 1 where measured faster | 2 every eligible set). Applied at
  * every exchange:
  * "poison_ghosts" (0 | 1, debug: NaN-fill the ghost slots before each exchange). */
 int pamg_set_option(const char* key, int64_t value);

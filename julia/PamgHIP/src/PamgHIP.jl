@@ -285,7 +285,8 @@ function layout(A::DeviceMatrix, set::Integer = 0)
     out = zeros(Cint, 10)
     check(ccall((:pamg_mat_layout, libpamg), Cint, (Ptr{Cvoid}, Cint, Ptr{Cint}), A.h, set, out))
     (c24 = out[1] != 0, vd = out[2] != 0, rl8 = out[3] != 0, cd = Int(out[4]), cd_offsets = Int(out[5]),
-     tm = out[6] != 0, tm_rs = Int(out[7]), tile_nnz = Int(out[8]), tiles = Int(out[9]), anchored = (out[10] & 1) != 0, per_tile = (out[10] & 2) != 0)
+     tm = out[6] != 0, tm_rs = Int(out[7]), tile_nnz = Int(out[8]), tiles = Int(out[9]), anchored = (out[10] & 1) != 0, per_tile = (out[10] & 2) != 0,
+     x_stage = (out[10] & 4) != 0)
 end
 Base.size(A::DeviceMatrix) = (A.nrows, A.ncols_local)
 

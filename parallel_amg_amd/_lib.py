@@ -172,7 +172,8 @@ def layout_of(M, part_set: int = 0) -> dict:
     call("pamg_mat_layout", M.handle, part_set, out)
     return {"c24": bool(out[0]), "vd": bool(out[1]), "rl8": bool(out[2]), "cd": int(out[3]),
             "cd_offsets": int(out[4]), "tm": bool(out[5]), "tm_rs": int(out[6]),
-            "tile_nnz": int(out[7]), "tiles": int(out[8]), "anchored": bool(out[9] & 1), "per_tile": bool(out[9] & 2)}
+            "tile_nnz": int(out[7]), "tiles": int(out[8]), "anchored": bool(out[9] & 1), "per_tile": bool(out[9] & 2),
+            "x_stage": bool(out[9] & 4)}
 
 
 def last_error() -> str:

@@ -366,26 +366,37 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
 // lengths; positions are tile-relative (no alignment head: a tile's slot starts at its first
 // nonzero). Summation order, epilogues and Jacobi's in-tile diagonal are k_rows_tile2's
 // (SPEC §S3).
-template <int OP, int TNNZ, int CD, bool ANC = false>
+// XS (x staging, TileSet::xs, row-relative dictionaries only): the tile's x values are the
+// runs [r0 + omin_c, r0 + nr - 1 + omin_c + wid_c] of the dictionary's offset clusters; each
+// lane loads one element of every run at entry, beside the other independent loads, into LDS
+// (segments of xst.stride doubles), and the products read x there at the LDS position the
+// table holds at kXsIoff + index. The x gathers — dependent on the column stream and the row
+// map, one round trip after them — disappear; Jacobi's diagonal is the entry of offset 0.
+template <int OP, int TNNZ, int CD, bool ANC = false, bool XS = false>
 __global__ __launch_bounds__(kBlock) void k_rows_tm(
     const int4* __restrict__ tiles, const double* __restrict__ tval,
     const uint8_t* __restrict__ tcidx, const uint16_t* __restrict__ tclo,
     const uint8_t* __restrict__ tchi, const int* __restrict__ tbase,
     const uint8_t* __restrict__ trlen, int rs, const int* __restrict__ ctab, int ctab_n,
     const double* __restrict__ x, const double* __restrict__ b, double* __restrict__ y,
-    double omega, const int* __restrict__ tanc = nullptr) {
+    double omega, const int* __restrict__ tanc = nullptr, const XStage xst = XStage{}) {
     // ANC (anchored dictionary): column = the row's first column (slot anchors, tanc) +
     // table[index] instead of row + table[index]
     static_assert(!ANC || CD != 0, "anchored columns are dictionary columns");
+    static_assert(!XS || (CD != 0 && !ANC), "x staging needs row-relative dictionary columns");
     constexpr int BS = kBlock;
     constexpr int G = TNNZ / (4 * BS);
     static_assert(G >= 1 && TNNZ % (4 * BS) == 0, "tile budget must be a multiple of 4 x block");
     __shared__ __attribute__((aligned(16))) double lprod[TNNZ + 8];
     __shared__ double ldiag[OP == OP_JACOBI ? BS : 1];
     __shared__ int lwt[BS / 64];
-    __shared__ int ltab[CD != 0 ? BS : 1];
+    // XS keeps only the table's LDS positions (kXsIoff + index): 16 / 128 entries, so the
+    // staged runs fit beside Jacobi's arrays at 8 blocks per CU
+    constexpr int NTAB = CD == 0 ? 1 : !XS ? BS : CD == 4 ? 16 : kXsIoff;
+    __shared__ int ltab[NTAB];
     __shared__ __attribute__((aligned(4))) uint8_t lrow[TNNZ + 8];
     __shared__ int lanc[ANC ? BS : 1];
+    __shared__ double lxs[XS ? kXsCap + 1 : 1];  // + 1: the dump slot of lanes past a run
 
     const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int4 d = tiles[t];
@@ -399,7 +410,8 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     // values are still in flight (previously the scan's wait on the row lengths also waited
     // for the whole value stream, and the gathers' wait on the columns for b / x).
     int tabv = 0, ancv = 0;
-    if constexpr (CD != 0) tabv = ctab[tid];  // the table is allocated with 256 entries
+    if constexpr (XS) tabv = ctab[kXsIoff + (tid < NTAB ? tid : NTAB - 1)];
+    else if constexpr (CD != 0) tabv = ctab[tid];  // the table is allocated with 256 entries
     const size_t rsl = (size_t)t * rs + (tid < rs ? tid : rs - 1);
     if constexpr (ANC) ancv = tanc[rsl];
     const int rlv = (int)trlen[rsl];
@@ -427,6 +439,18 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
         if constexpr (OP == OP_JACOBI) px = x[r];
         if constexpr (OP == OP_PROLONG) py = y[r];
     }
+    double xsv[XS ? kXsMaxClusters : 1];
+    if constexpr (XS) {
+#pragma unroll
+        for (int c = 0; c < kXsMaxClusters; ++c) {
+            xsv[c] = 0.0;
+            if (c < xst.ncl) {  // uniform
+                const int g = r0 + xst.omin[c] + tid;
+                const bool ok = tid < nr + xst.wid[c] && g >= 0 && g < xst.ncols;
+                xsv[c] = x[ok ? g : 0];
+            }
+        }
+    }
     asm volatile("" ::: "memory");  // keep the loads above ahead of the value stream
     // the whole value slot is loaded at entry (padding included: a load that waits for the
     // descriptor's nonzero count brings its round trip back — measured 2-15 % slower)
@@ -439,8 +463,14 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     int rl_len = tid < rs ? rlv : 0;
     // every lane stores its entry (unconditionally: a conditional store lets the compiler sink
     // the table load into the branch, behind the value stream)
-    if constexpr (CD != 0) ltab[tid] = tabv;
+    if constexpr (XS) ltab[tid < NTAB ? tid : NTAB - 1] = tabv;  // lanes past NTAB rewrite the last entry's value
+    else if constexpr (CD != 0) ltab[tid] = tabv;
     if constexpr (ANC) lanc[tid] = tid < rs ? ancv : 0;
+    if constexpr (XS) {
+#pragma unroll
+        for (int c = 0; c < kXsMaxClusters; ++c)
+            if (c < xst.ncl) lxs[tid < xst.stride ? c * xst.stride + tid : kXsCap] = xsv[c];
+    }
     const int rl_inc = wave_incl_scan(rl_len);
     if (lane == 63) lwt[tid >> 6] = rl_inc;
     // end of this lane's row (tile-relative): the wave's inclusive sum + the earlier waves'
@@ -471,6 +501,16 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
         const int q = 4 * (tid + j * BS);
         uint32_t rw = 0u;
         if constexpr (NEED_ROWS) rw = q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
+        if constexpr (XS) {  // x from the staged runs; cc holds the dictionary index
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int ix = CD == 4 ? (int)((cn[j] >> (4 * e)) & 15u) : (int)((cn[j] >> (8 * e)) & 255u);
+                const int rid = (int)((rw >> (8 * e)) & 255u);
+                cc[j][e] = ix;
+                xv[j][e] = lxs[ltab[ix] + rid];
+            }
+            continue;
+        }
         if constexpr (CD == 0) {
             const uint16_t l4[4] = {clo4[j].x, clo4[j].y, clo4[j].z, clo4[j].w};
 #pragma unroll
@@ -501,7 +541,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
             p[e] = ok ? vv[e] * xv[j][e] : 0.0;
             if constexpr (OP == OP_JACOBI) {
                 const int rl = (int)((rw >> (8 * e)) & 255u);
-                if (ok && cc[j][e] - r0 == rl) ldiag[rl] = vv[e];
+                if (ok && (XS ? cc[j][e] == xst.zix : cc[j][e] - r0 == rl)) ldiag[rl] = vv[e];
             }
         }
         *reinterpret_cast<double2*>(&lprod[q]) = make_double2(p[0], p[1]);
@@ -709,6 +749,14 @@ void launch_tile(const pamg_mat& A, const TileSet& ts, const double* x, const do
             k_rows_tm<OP, TNNZ, 8, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
                                                              nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n,
                                                              x, b, y, omega, ts.d_tm_anc);
+        else if (ts.xs && ts.cd == 4)
+            k_rows_tm<OP, TNNZ, 4, false, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr,
+                                                                   nullptr, nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab,
+                                                                   ts.ctab_n, x, b, y, omega, nullptr, ts.xst);
+        else if (ts.xs)
+            k_rows_tm<OP, TNNZ, 8, false, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr,
+                                                                   nullptr, nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab,
+                                                                   ts.ctab_n, x, b, y, omega, nullptr, ts.xst);
         else if (ts.cd == 4)
             k_rows_tm<OP, TNNZ, 4><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
                                                        nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n, x,

@@ -18,6 +18,21 @@ namespace pamg {
 constexpr int kBlock = 256;
 constexpr int kTileRows = 256;
 
+// x staging of row-relative dictionary tiles (TileSet::xs, k_rows_tm<..., XS>): the x values a
+// tile reads are the runs [r0 + omin_c, r0 + nr - 1 + omin_c + wid_c] of its offset clusters c
+// (offsets within kXsGap of each other share a run); they are loaded coalesced at kernel entry
+// into LDS segments of `stride` doubles and the products read them there — no dependent x
+// gathers. The dictionary table holds, at kXsIoff + index, each offset's LDS position
+// c * stride + offset - omin_c.
+constexpr int kXsMaxClusters = 12;
+constexpr int kXsCap = 1088;   // LDS doubles (8.5 KiB; 512^3 7-point: 5 runs x 210)
+constexpr int kXsIoff = 128;   // table entries [128, 256): the LDS positions of offsets [0, 128)
+constexpr int kXsGap = 48;
+struct XStage {
+    int ncl = 0, stride = 0, zix = -1, ncols = 0;
+    int omin[kXsMaxClusters] = {}, wid[kXsMaxClusters] = {};
+};
+
 enum RowOp : int {
     OP_SPMV = 0,     // y = A x
     OP_RESID = 1,    // y = b - A x
@@ -55,6 +70,9 @@ struct TileSet {
     // n_short tables of ctab_n entries; anchored ones take pamg_mat::d_anc16 + d_abase[tile]
     bool pt = false;
     int* d_abase = nullptr;
+    // x staging (Options::x_stage): see XStage
+    bool xs = false;
+    XStage xst;
     // tile-major copies (Options::tile_major; kernels.hip k_rows_tm): tile t's values and
     // column stream at t * tile_nnz, its row lengths at t * tm_rs, zero-padded
     bool tm = false;
@@ -83,6 +101,7 @@ struct Options {
     int col_dict = 1;          // 1: row-relative column dictionaries (4/8-bit) where they fit
     int tile_major = 1;        // tile-major padded copies (variant 4): 1 where measured faster, 2 all eligible
     int col_dict_tile = 1;     // 1: per-tile column dictionaries where no global table fits (and they beat 24-bit)
+    int x_stage = 1;           // 1: stage x runs in LDS for row-relative dictionary tile-major sets (no x gathers)
     int col_dict_anchor = 1;   // 1: anchored column dictionaries (col - row's first column) where row-relative ones do not fit
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
 };

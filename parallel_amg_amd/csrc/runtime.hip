@@ -574,6 +574,57 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
     return PAMG_OK;
 }
 
+// x staging (Options::x_stage; pamg::XStage) for a tile-major set with a set-wide row-relative
+// dictionary: cluster the sorted offsets (a new run where the gap exceeds kXsGap), and when
+// the runs of the widest tile fit (<= kXsMaxClusters runs, rows + run width <= 256 lanes,
+// all runs in kXsCap doubles) write each offset's LDS position into the table at kXsIoff.
+int build_x_stage(pamg_mat* A, pamg::TileSet* ts, int rs) {
+    using pamg::kXsCap;
+    using pamg::kXsGap;
+    using pamg::kXsIoff;
+    using pamg::kXsMaxClusters;
+    ts->xs = false;
+    if (!pamg::options().x_stage || !ts->cd || ts->anc || ts->pt || ts->ctab_n > kXsIoff || ts->ctab_n == 0)
+        return PAMG_OK;
+    std::vector<int> tab(256);
+    HIPC(hipMemcpy(tab.data(), ts->d_ctab, sizeof(int) * 256, hipMemcpyDeviceToHost));
+    std::vector<int> off(tab.begin(), tab.begin() + ts->ctab_n);
+    std::vector<int> srt(off);
+    std::sort(srt.begin(), srt.end());
+    std::vector<int> cmin, cmax;
+    for (int o : srt) {
+        if (cmin.empty() || (int64_t)o - cmax.back() > kXsGap) {
+            cmin.push_back(o);
+            cmax.push_back(o);
+        } else {
+            cmax.back() = o;
+        }
+    }
+    const int ncl = (int)cmin.size();
+    int wmax = 0;
+    for (int c = 0; c < ncl; ++c) wmax = std::max(wmax, cmax[c] - cmin[c]);
+    const int stride = rs + wmax;
+    if (ncl > kXsMaxClusters || stride > 256 || ncl * stride > kXsCap) return PAMG_OK;
+    pamg::XStage& x = ts->xst;
+    x = pamg::XStage{};
+    x.ncl = ncl;
+    x.stride = stride;
+    x.ncols = (int)A->ncols;
+    for (int c = 0; c < ncl; ++c) {
+        x.omin[c] = cmin[c];
+        x.wid[c] = cmax[c] - cmin[c];
+    }
+    for (int i = 0; i < ts->ctab_n; ++i) {
+        int c = 0;
+        while (off[i] > cmax[c]) ++c;
+        tab[kXsIoff + i] = c * stride + (off[i] - cmin[c]);
+        if (off[i] == 0) x.zix = i;
+    }
+    HIPC(hipMemcpy(ts->d_ctab, tab.data(), sizeof(int) * 256, hipMemcpyHostToDevice));
+    ts->xs = true;
+    return PAMG_OK;
+}
+
 // Tile-major copies (Options::tile_major, kernel variant 4 k_rows_tm): for a tile set with
 // one row per lane (<= 256 rows per tile, rows <= 255 nonzeros) and 24-bit or dictionary
 // columns, tile t's values, column stream and row lengths are copied to fixed, zero-padded
@@ -674,6 +725,7 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
         }
         ts->tm_rs = rs;
         ts->tm = true;
+        CHECK(build_x_stage(A, ts, rs));
     }
     return PAMG_OK;
 }
@@ -692,7 +744,7 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_tm_rlen);
     dfree(ts.d_tm_anc);
     dfree(ts.d_abase);
-    ts.anc = ts.pt = false;
+    ts.anc = ts.pt = ts.xs = false;
     ts.tm = false;
     ts.tm_rs = 0;
     ts.c24 = ts.vd = ts.rl8 = false;
@@ -1539,7 +1591,7 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[6] = t.tm_rs;
     out[7] = t.tile_nnz;
     out[8] = t.n_short;
-    out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0);
+    out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0);
     return PAMG_OK;
 }
 
@@ -1952,6 +2004,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "tile_major" && value >= 0 && value <= 2) o.tile_major = (int)value;
     else if (k == "col_dict_anchor" && (value == 0 || value == 1)) o.col_dict_anchor = (int)value;
     else if (k == "col_dict_tile" && (value == 0 || value == 1)) o.col_dict_tile = (int)value;
+    else if (k == "x_stage" && (value == 0 || value == 1)) o.x_stage = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -1971,6 +2024,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "tile_major") *value = o.tile_major;
     else if (k == "col_dict_anchor") *value = o.col_dict_anchor;
     else if (k == "col_dict_tile") *value = o.col_dict_tile;
+    else if (k == "x_stage") *value = o.x_stage;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

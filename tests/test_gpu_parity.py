@@ -562,6 +562,65 @@ def test_per_tile_dictionaries_random(ctx, name, ndist, lengths):
     lay = layout_of(D)
     assert lay["per_tile"] or lay["cd"] == 0, lay
 
+def _with_options(opts, fn):
+    import ctypes
+    from parallel_amg_amd._lib import call
+    old = {}
+    for k in opts:
+        v = ctypes.c_int64()
+        call("pamg_get_option", k.encode(), ctypes.byref(v))
+        old[k] = v.value
+    try:
+        for k, v in opts.items():
+            call("pamg_set_option", k.encode(), v)
+        return fn()
+    finally:
+        for k, v in old.items():
+            call("pamg_set_option", k.encode(), v)
+
+
+# x_stage cases (name -> matrix, x staged?): clustered row-relative offsets — the stencils
+# (7-point: 5 runs; 27-point and elastic: 9), ragged rows, offsets past both ends of the
+# vector; 13 runs (more than kXsMaxClusters) and a run too wide for the lanes fall back to
+# gathers
+def _xs_case(name):
+    rng = np.random.default_rng(11)
+    if name == "poisson3d_24":
+        return O.generate("poisson3d", 24, 24, 24), True
+    if name == "poisson2d_64":
+        return O.generate("poisson2d", 64, 64, 1), True
+    if name == "aniso3d_20":
+        return O.generate("aniso3d", 20, 20, 20), True
+    if name == "elastic3d_12":
+        return O.generate("elastic3d", 12, 12, 12), True
+    if name == "ragged":
+        offs = [-1500, -201, -200, -199, -1, 1, 199, 200, 201, 1500]
+        return offset_csr(rng, 4000, offs, [1, 11, 6, 9, 12, 9, 8]), True  # <= 171 rows per tile: 5 runs fit
+    if name == "clusters13":
+        offs = [k * 400 + d for k in range(-6, 7) for d in (-1, 0, 1) if k * 400 + d != 0]
+        return offset_csr(rng, 6000, offs, [20, 3, 39]), False
+    assert name == "wide_run"  # one run 0..220 wide: rows + 220 > 256 lanes
+    return offset_csr(rng, 3000, [-700, -1, 1, 60, 100, 140, 180, 220], [8, 2, 5]), False
+
+
+@pytest.mark.parametrize("name", ["poisson3d_24", "poisson2d_64", "aniso3d_20", "elastic3d_12", "ragged",
+                                  "clusters13", "wide_run"])
+@pytest.mark.parametrize("x_stage", [1, 0])
+def test_x_stage_bit_exact(ctx, name, x_stage):
+    """x_stage: row-relative dictionary tiles read x from LDS copies of the runs their offset
+    clusters cover (loaded coalesced at entry) instead of gathering it; SpMV / residual /
+    prolongate-add / Jacobi (diagonal = offset 0's entry) give the oracle's bits either way,
+    and the layout stages x exactly where the runs fit."""
+    from parallel_amg_amd._lib import layout_of
+    M, staged = _xs_case(name)
+    rng = np.random.default_rng(len(name))
+    D = _with_options({"x_stage": x_stage, "tile_major": 2},
+                      lambda: _layout_ops_match_oracle(ctx, M, rng))
+    lay = layout_of(D)
+    assert lay["tm"] and lay["cd"] in (4, 8) and not lay["anchored"], lay
+    assert lay["x_stage"] == (staged and x_stage == 1), lay
+
+
 def test_restriction_takes_anchored_dictionary(ctx):
     """The level-0 restriction of the 7-point Poisson hierarchy (5x5x5 neighbourhoods of the
     aggregate roots) is uploaded with an anchored 8-bit dictionary in tile-major slots."""
