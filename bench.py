@@ -262,7 +262,7 @@ def main():
     # the instance name as rocprofv3 demangles it (every template argument, defaults included)
     tf = lambda v: "true" if v else "false"  # noqa: E731
     if tm:
-        kname = f"k_rows_tm<2, {tn}, {cd}, {tf(lay['anchored'])}>"
+        kname = f"k_rows_tm<2, {tn}, {cd}, {tf(lay['anchored'])}, {tf(lay['x_stage'])}>"
     elif cd:
         kname = f"k_rows_tile2<2, {tn}, false, false, true, {cd}, {tf(lay['per_tile'])}, {tf(lay['anchored'])}>"
     else:
@@ -317,6 +317,7 @@ def main():
                 "kernel": kname + " (level-0 post-smoothing Jacobi"
                           + (", tile-major slots" if tm else "")
                           + (f", {cd}-bit column dictionary" if cd else "")
+                          + (", x staged in LDS" if lay.get("x_stage") else "")
                           + (", value dictionaries" if lay["vd"] else "")
                           + (", 24-bit column stream" if lay["c24"] and not cd else "")
                           + (", 8-bit row lengths)" if lay["rl8"] else ")"),
