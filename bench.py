@@ -262,7 +262,8 @@ def main():
     # the instance name as rocprofv3 demangles it (every template argument, defaults included)
     tf = lambda v: "true" if v else "false"  # noqa: E731
     if tm:
-        kname = f"k_rows_tm<2, {tn}, {cd}, {tf(lay['anchored'])}, {tf(lay['x_stage'])}>"
+        kname = (f"k_rows_tm<2, {tn}, {cd}, {tf(lay['anchored'])}, {tf(lay['x_stage'])}, "
+                 f"{tf(lay['per_tile'])}>")
     elif cd:
         kname = f"k_rows_tile2<2, {tn}, false, false, true, {cd}, {tf(lay['per_tile'])}, {tf(lay['anchored'])}>"
     else:

@@ -372,7 +372,10 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
 // (segments of xst.stride doubles), and the products read x there at the LDS position the
 // table holds at kXsIoff + index. The x gathers — dependent on the column stream and the row
 // map, one round trip after them — disappear; Jacobi's diagonal is the entry of offset 0.
-template <int OP, int TNNZ, int CD, bool ANC = false, bool XS = false>
+// PT (Options::tm_tile_dicts): per-tile row-relative dictionaries (TileSet::pt) in tile-major
+// slots — this tile's table is ctab[t * ctab_n ...], addressed from the block index like
+// every other pre-gather load.
+template <int OP, int TNNZ, int CD, bool ANC = false, bool XS = false, bool PT = false>
 __global__ __launch_bounds__(kBlock) void k_rows_tm(
     const int4* __restrict__ tiles, const double* __restrict__ tval,
     const uint8_t* __restrict__ tcidx, const uint16_t* __restrict__ tclo,
@@ -384,6 +387,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     // table[index] instead of row + table[index]
     static_assert(!ANC || CD != 0, "anchored columns are dictionary columns");
     static_assert(!XS || (CD != 0 && !ANC), "x staging needs row-relative dictionary columns");
+    static_assert(!PT || (CD != 0 && !ANC && !XS), "per-tile tables: row-relative, gathered");
     constexpr int BS = kBlock;
     constexpr int G = TNNZ / (4 * BS);
     static_assert(G >= 1 && TNNZ % (4 * BS) == 0, "tile budget must be a multiple of 4 x block");
@@ -411,6 +415,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     // for the whole value stream, and the gathers' wait on the columns for b / x).
     int tabv = 0, ancv = 0;
     if constexpr (XS) tabv = ctab[kXsIoff + (tid < NTAB ? tid : NTAB - 1)];
+    else if constexpr (PT) tabv = ctab[(size_t)t * ctab_n + (tid < ctab_n ? tid : ctab_n - 1)];
     else if constexpr (CD != 0) tabv = ctab[tid];  // the table is allocated with 256 entries
     const size_t rsl = (size_t)t * rs + (tid < rs ? tid : rs - 1);
     if constexpr (ANC) ancv = tanc[rsl];
@@ -749,6 +754,16 @@ void launch_tile(const pamg_mat& A, const TileSet& ts, const double* x, const do
             k_rows_tm<OP, TNNZ, 8, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
                                                              nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n,
                                                              x, b, y, omega, ts.d_tm_anc);
+        else if (ts.pt && ts.cd == 4)
+            k_rows_tm<OP, TNNZ, 4, false, false, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx,
+                                                                          nullptr, nullptr, nullptr, ts.d_tm_rlen,
+                                                                          ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y,
+                                                                          omega);
+        else if (ts.pt)
+            k_rows_tm<OP, TNNZ, 8, false, false, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx,
+                                                                          nullptr, nullptr, nullptr, ts.d_tm_rlen,
+                                                                          ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y,
+                                                                          omega);
         else if (ts.xs && ts.cd == 4)
             k_rows_tm<OP, TNNZ, 4, false, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr,
                                                                    nullptr, nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab,

@@ -66,7 +66,7 @@ struct TileSet {
     // anchored dictionary (Options::col_dict_anchor; tile-major sets only): column = the row's
     // first column + d_ctab[i]; the row anchors sit in the tile-major slots (d_tm_anc)
     bool anc = false;
-    // per-tile dictionaries (Options::col_dict_tile; descriptor kernel only): d_ctab holds
+    // per-tile dictionaries (Options::col_dict_tile; anchored: descriptor kernel, row-relative: tile-major slots): d_ctab holds
     // n_short tables of ctab_n entries; anchored ones take pamg_mat::d_anc16 + d_abase[tile]
     bool pt = false;
     int* d_abase = nullptr;
@@ -101,6 +101,7 @@ struct Options {
     int col_dict = 1;          // 1: row-relative column dictionaries (4/8-bit) where they fit
     int tile_major = 1;        // tile-major padded copies (variant 4): 1 where measured faster, 2 all eligible
     int col_dict_tile = 1;     // 1: per-tile column dictionaries where no global table fits (and they beat 24-bit)
+    int tm_tile_dicts = 1;     // 1: row-relative per-tile dictionary sets in tile-major slots (512^3 A1: -1..-3 %)
     int x_stage = 1;           // 1: stage x runs in LDS for row-relative dictionary tile-major sets (no x gathers)
     int col_dict_anchor = 1;   // 1: anchored column dictionaries (col - row's first column) where row-relative ones do not fit
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange

@@ -641,7 +641,9 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
     for (int q = 0; q < 2; ++q) {
         pamg::TileSet* ts = sets[q];
         ts->tm = false;
-        if (ts->pt) continue;  // per-tile dictionaries run in the descriptor kernel
+        // per-tile dictionaries run in the descriptor kernel, row-relative ones in tile-major
+        // slots with tm_tile_dicts
+        if (ts->pt && (ts->anc || !opt.tm_tile_dicts)) continue;
         if (!opt.tile_major || ts->vd || ts->n_short == 0 || ts->max_short_len > 255 ||
             !(ts->cd || (ts->c24 && !lo.empty())) || (ts->cd && idx8.empty()) || !val) {
             if (ts->anc) return fail(PAMG_E_STATE, "upload: anchored column dictionary without tile-major slots");
@@ -1522,7 +1524,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
             const int64_t tn = t->tile_nnz;
             const int64_t rowb = t->tm_rs;
             b += ns * (rowb * (t->anc ? 5 : 1) + 8 * tn + (t->cd ? t->cd * tn / 8 : 3 * tn) + 16 + (base ? 4 : 0)) +
-                 (t->cd ? 4 * t->ctab_n : 0);
+                 (t->cd ? 4 * t->ctab_n * (t->pt ? ns : 1) : 0);
         } else {
             b += (t->rl8 ? 1 : 4) * t->rows_short;
             b += t->cd ? (t->cd * nz + 7) / 8 + 4 * t->ctab_n * (t->pt ? ns : 1) : (t->c24 ? 3 : 4) * nz;
@@ -2005,6 +2007,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "col_dict_anchor" && (value == 0 || value == 1)) o.col_dict_anchor = (int)value;
     else if (k == "col_dict_tile" && (value == 0 || value == 1)) o.col_dict_tile = (int)value;
     else if (k == "x_stage" && (value == 0 || value == 1)) o.x_stage = (int)value;
+    else if (k == "tm_tile_dicts" && (value == 0 || value == 1)) o.tm_tile_dicts = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -2025,6 +2028,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "col_dict_anchor") *value = o.col_dict_anchor;
     else if (k == "col_dict_tile") *value = o.col_dict_tile;
     else if (k == "x_stage") *value = o.x_stage;
+    else if (k == "tm_tile_dicts") *value = o.tm_tile_dicts;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

@@ -511,12 +511,14 @@ def drift_csr(rng, n, ncols, anchored, nset=12, every=200, step=37):
     return O.CSR(np.asarray(rows, np.int64), col, val, ncols)
 
 
-@pytest.mark.parametrize("anchored,tnnz", [(False, 1024), (False, 4096), (True, 1024), (True, 2048)])
-def test_per_tile_dictionaries_bit_exact(ctx, anchored, tnnz):
+@pytest.mark.parametrize("anchored,tnnz,tm", [(False, 1024, 0), (False, 4096, 0), (True, 1024, 0), (True, 2048, 0),
+                                             (False, 1024, 1), (False, 4096, 1), (True, 1024, 1)])
+def test_per_tile_dictionaries_bit_exact(ctx, anchored, tnnz, tm):
     """col_dict_tile: no table fits the whole matrix (> 256 offsets) but every tile's fits —
     per-tile row-relative tables (coarse-operator shape) or per-tile anchored ones with 16-bit
     anchors (prolongator shape) in the descriptor kernel; SpMV / residual / prolongate-add (and
-    Jacobi for the square case) give the oracle's bits."""
+    Jacobi for the square case) give the oracle's bits; tm_tile_dicts moves the row-relative
+    ones into tile-major slots (the anchored ones stay in the descriptor kernel)."""
     import ctypes
     from parallel_amg_amd._lib import call, layout_of
     rng = np.random.default_rng(tnnz + anchored)
@@ -526,11 +528,11 @@ def test_per_tile_dictionaries_bit_exact(ctx, anchored, tnnz):
     call("pamg_get_option", b"tile_nnz", ctypes.byref(old))
     try:
         call("pamg_set_option", b"tile_nnz", tnnz)
-        D = _layout_ops_match_oracle(ctx, M, rng)
+        D = _with_options({"tm_tile_dicts": tm}, lambda: _layout_ops_match_oracle(ctx, M, rng))
     finally:
         call("pamg_set_option", b"tile_nnz", old.value)
     lay = layout_of(D)
-    assert lay["per_tile"] and lay["anchored"] == anchored and not lay["tm"], lay
+    assert lay["per_tile"] and lay["anchored"] == anchored and lay["tm"] == (tm == 1 and not anchored), lay
     assert lay["cd"] in (4, 8) and lay["cd_offsets"] in (16, 32, 64, 128, 256), lay
 
 

@@ -55,7 +55,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--configs", default="1024:1,1024:0",
                     help="tile_nnz:tile_order:col24:value_dict:long_tiles:row_len8:col_dict:tile_major:col_dict_anchor:"
-                         "col_dict_tile:x_stage,...")
+                         "col_dict_tile:x_stage:tm_tile_dicts,...")
     ap.add_argument("--ops", default="0,2")
     ap.add_argument("--mats", default=None, help="comma list of level matrices to run (e.g. R0,A1); default all")
     ap.add_argument("--ab", default=None,
@@ -77,10 +77,10 @@ def main():
     ops = [int(o) for o in args.ops.split(",")]
     for cfg in args.configs.split(","):
         given = [int(v) for v in cfg.split(":")]
-        vals = given + [1024, 1, 1, 0, 1, 1, 1, 1, 1, 1, 1][len(given):]  # defaults for missing fields
-        tnnz, order, c24, vd, lt, rl8, cd, tm, anc, ptd, xst = vals[:11]
+        vals = given + [1024, 1, 1, 0, 1, 1, 1, 1, 1, 1, 1, 1][len(given):]  # defaults for missing fields
+        tnnz, order, c24, vd, lt, rl8, cd, tm, anc, ptd, xst, tmpt = vals[:12]
         set_opts(tile_nnz=tnnz, tile_order=order, col24=c24, value_dict=vd, long_tiles=lt, row_len8=rl8,
-                 col_dict=cd, tile_major=tm, col_dict_anchor=anc, col_dict_tile=ptd, x_stage=xst)
+                 col_dict=cd, tile_major=tm, col_dict_anchor=anc, col_dict_tile=ptd, x_stage=xst, tm_tile_dicts=tmpt)
         for name, (M, plan) in mats.items():
             if args.mats and name not in args.mats.split(","):
                 continue
