@@ -701,6 +701,31 @@ __global__ __launch_bounds__(kBlock) void k_dot_partial(int64_t n, const double*
     if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 
+// PCG's x += alpha p; r -= alpha q; partials of r.r — one pass instead of two axpby and a
+// dot. Each element is computed exactly as k_axpby computes it (a * x + 1.0 * y), and the
+// partials walk the same grid-stride order as k_dot_partial on the same grid, so x, r and the
+// dot carry the unfused sequence's bits.
+__global__ __launch_bounds__(kBlock) void k_cg_update(int64_t n, double alpha, const double* __restrict__ p,
+                                                      const double* __restrict__ q, double* __restrict__ x,
+                                                      double* __restrict__ r, double* __restrict__ partials) {
+    __shared__ double lds[kBlock / 64];
+    const double na = -alpha;
+    double v = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * kBlock) {
+        const double u = alpha * p[i];
+        const double w = 1.0 * x[i];
+        x[i] = u + w;
+        const double u2 = na * q[i];
+        const double w2 = 1.0 * r[i];
+        const double rn = u2 + w2;
+        r[i] = rn;
+        v += rn * rn;
+    }
+    const double s = block_sum(v, lds);
+    if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
 __global__ __launch_bounds__(kBlock) void k_dot_final(int np, const double* __restrict__ partials,
                                                       double* __restrict__ out) {
     __shared__ double lds[kBlock / 64];
@@ -859,6 +884,12 @@ int dot_partials(int64_t n) { return grid_for(n, 1024); }
 void launch_dot(int64_t n, const double* x, const double* y, double* partials, int np,
                 double* out, hipStream_t s) {
     k_dot_partial<<<np, kBlock, 0, s>>>(n, x, y, partials);
+    k_dot_final<<<1, kBlock, 0, s>>>(np, partials, out);
+}
+
+void launch_cg_update(int64_t n, double alpha, const double* p, const double* q, double* x, double* r,
+                      double* partials, int np, double* out, hipStream_t s) {
+    k_cg_update<<<np, kBlock, 0, s>>>(n, alpha, p, q, x, r, partials);
     k_dot_final<<<1, kBlock, 0, s>>>(np, partials, out);
 }
 

@@ -182,5 +182,8 @@ void launch_axpby(int64_t n, double a, const double* x, double b, double* y, hip
 void launch_dot(int64_t n, const double* x, const double* y, double* partials, int nparts,
                 double* out, hipStream_t s);
 int dot_partials(int64_t n);
+// x += alpha p; r -= alpha q; out = r.r (bit-identical to two launch_axpby + launch_dot)
+void launch_cg_update(int64_t n, double alpha, const double* p, const double* q, double* x, double* r,
+                      double* partials, int np, double* out, hipStream_t s);
 
 }  // namespace pamg

@@ -826,12 +826,15 @@ int apply(pamg_ctx* ctx, const pamg_mat* A, int op, double* x, const double* b, 
     return PAMG_OK;
 }
 
-int reduce_scalar(pamg_ctx* ctx, int64_t n, const double* x, const double* y, double* out) {
+// The deterministic dot x.y over the own rows of every rank (fixed-grid partials, then the
+// cross-rank sum); `partial` enqueues the partials + final kernels (default: launch_dot).
+template <class F>
+int reduce_with(pamg_ctx* ctx, int64_t n, double* out, F partial) {
     hipStream_t s = ctx->s_comp;
     const int np = pamg::dot_partials(n);
     if (np + 1 > ctx->red_cap) return fail(PAMG_E_STATE, "reduction workspace too small");
     double* res = ctx->d_red + ctx->red_cap - 1;
-    pamg::launch_dot(n, x, y, ctx->d_red, np, res, s);
+    partial(np, ctx->d_red, res, s);
     if (ctx->comm && ctx->nranks > 1) NCCLC(ncclAllReduce(res, res, 1, ncclDouble, ncclSum, ctx->comm, s));
     HIPC(hipMemcpyAsync(ctx->h_red, res, sizeof(double), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
@@ -844,6 +847,12 @@ int reduce_scalar(pamg_ctx* ctx, int64_t n, const double* x, const double* y, do
         *out = sum;
     }
     return PAMG_OK;
+}
+
+int reduce_scalar(pamg_ctx* ctx, int64_t n, const double* x, const double* y, double* out) {
+    return reduce_with(ctx, n, out, [&](int np, double* parts, double* res, hipStream_t s) {
+        pamg::launch_dot(n, x, y, parts, np, res, s);
+    });
 }
 
 }  // namespace
@@ -1971,9 +1980,10 @@ int pamg_pcg(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, double
             double pq = 0.0;
             CHECK(reduce_scalar(ctx, n, p, q, &pq));
             const double alpha = rz / pq;
-            pamg::launch_axpby(n, alpha, p, 1.0, x->d, s);
-            pamg::launch_axpby(n, -alpha, q, 1.0, r, s);
-            CHECK(reduce_scalar(ctx, n, r, r, &rr));
+            // x += alpha p; r -= alpha q; rr = r.r in one pass (bits of the unfused sequence)
+            CHECK(reduce_with(ctx, n, &rr, [&](int np, double* parts, double* res, hipStream_t st) {
+                pamg::launch_cg_update(n, alpha, p, q, x->d, r, parts, np, res, st);
+            }));
             const double nr = std::sqrt(rr);
             if (res_hist) res_hist[k] = nr;
             if (nr <= rtol * nr0) break;

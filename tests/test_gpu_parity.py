@@ -313,6 +313,50 @@ def test_pcg_matches_oracle(ctx, kind, n, max_coarse):
     assert np.linalg.norm(xg - xs[0]) <= 1e-8 * np.linalg.norm(xs[0])
 
 
+def test_pcg_equals_primitive_sequence(ctx):
+    """pamg_pcg (fused x / r update + r.r in one kernel) gives the bits of the same CG written
+    with the separate C-ABI primitives (mul, dot, axpby, V-cycle from zero)."""
+    from parallel_amg_amd.partitioned import copy
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 20)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=100))
+    S = AMGSolver(ctx, H)
+    A0 = S.A[0]
+    b = PVector(ctx, A0.nrows)
+    mul(b, A0, PVector(ctx, A0.nrows, 0, xs[0]))
+    x1 = S.new_vector()
+    k1, h1 = S.pcg(x1, b, 1e-9, 40)
+
+    x = S.new_vector()
+    r, z, p, q = S.new_vector(), S.new_vector(), S.new_vector(), S.new_vector()
+    residual(r, A0, x, b)
+    nr0 = np.sqrt(dot(r, r))
+    hist = [nr0]
+    z.fill(0.0)
+    S.vcycle(z, r, 1)
+    copy(p, z)
+    rz = dot(r, z)
+    k = 0
+    while k < 40:
+        k += 1
+        mul(q, A0, p)
+        alpha = rz / dot(p, q)
+        axpby(alpha, p, 1.0, x)
+        axpby(-alpha, q, 1.0, r)
+        hist.append(np.sqrt(dot(r, r)))
+        if hist[-1] <= 1e-9 * nr0:
+            break
+        z.fill(0.0)
+        S.vcycle(z, r, 1)
+        rz_new = dot(r, z)
+        beta = rz_new / rz
+        rz = rz_new
+        axpby(1.0, z, beta, p)
+    assert k == k1
+    assert np.array_equal(bits(np.asarray(hist)), bits(h1))
+    assert np.array_equal(bits(x.own_values()), bits(x1.own_values()))
+
+
 def test_graph_equals_eager(ctx):
     be = pa.SequentialBackend(1)
     A, offs, xs = pa.generate_problem(be, "poisson3d", 20)
