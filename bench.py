@@ -334,6 +334,10 @@ def main():
                 "format_bytes_per_launch": int(post_fbytes),
                 "format_GBps": round(post_fbytes / (post_ms * 1e-3) / 1e9, 1),
                 "ms_per_launch": round(post_ms, 4),
+                # the practical streaming ceiling beside the 8 TB/s spec: plain coalesced kernels
+                # reading 11 streams per written one (the Jacobi's read:write mix) / reading only,
+                # measured on an MI355X with tools/stream_ceiling.hip
+                "stream_ceiling": STREAM_CEILING,
             },
             "cpu_baseline": cpu,
             "time_to_solution": pcg,
@@ -350,6 +354,10 @@ def kernel_source_sha() -> str:
     import hashlib
     with open(os.path.join(ROOT, "parallel_amg_amd", "csrc", "kernels.hip"), "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+STREAM_CEILING = {"mix11to1_GBps": 5104.0, "read_GBps": 6311.0,
+                  "source": "profiles/r02_exp/stream_ceiling.jsonl (tools/stream_ceiling.hip, 8 GiB, best grid)"}
 
 
 def pmc_lookup(fname, kname, tiles, workload_key, src):
