@@ -95,7 +95,8 @@ struct Options {
     int tile_nnz = 1024;       // 1024 / 2048 / 4096 (tiles always hold <= kTileRows rows)
     int tile_order = 1;        // 1: banded XCD-blocked tile order (see build_tiles)
     int col24 = 1;             // 1: 3-byte column stream where every tile's span fits 2^24
-    int long_tiles = 1;        // 1: 4096-nonzero tiles for operators averaging >= 48 nnz/row
+    int long_tiles = 1;        // 1: 4096-nonzero tiles for square operators with long rows (build_tiles)
+    int long_tiles_min = 24;   // nonzeros per row from which long_tiles applies to sets of >= 64 M nonzeros
     int row_len8 = 1;          // 1: 8-bit row lengths instead of 32-bit row pointers where they fit
     int value_dict = 0;        // 1 (opt-in): 4-bit per-tile value dictionaries where they fit
     int col_dict = 1;          // 1: row-relative column dictionaries (4/8-bit) where they fit

@@ -226,7 +226,12 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows, bo
     if (opt.long_tiles && square && tnnz == 1024 && !rows.empty()) {
         int64_t nz = 0;
         for (int r : rows) nz += rp[r + 1] - rp[r];
-        if (nz >= 48 * (int64_t)rows.size()) tnnz = 4096;
+        // >= 48 per row always; from long_tiles_min (24) per row when the set is large enough
+        // to fill the chip with 4096-nonzero tiles (>= 64 M nonzeros: 512^3 A1, 31 per row,
+        // residual -3 %, Jacobi -2 %; the 8 M-nonzero A1 of 128^3 is 9 % slower with them,
+        // profiles/r02_exp/bench_long_tiles_min_ab/)
+        const int64_t nr = (int64_t)rows.size();
+        if (nz >= 48 * nr || (nz >= (int64_t)opt.long_tiles_min * nr && nz >= (int64_t(64) << 20))) tnnz = 4096;
     }
     ts->tile_nnz = tnnz;
     std::vector<int4> tiles;
@@ -2017,6 +2022,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "col_dict_anchor" && (value == 0 || value == 1)) o.col_dict_anchor = (int)value;
     else if (k == "col_dict_tile" && (value == 0 || value == 1)) o.col_dict_tile = (int)value;
     else if (k == "x_stage" && (value == 0 || value == 1)) o.x_stage = (int)value;
+    else if (k == "long_tiles_min" && value >= 1 && value <= 255) o.long_tiles_min = (int)value;
     else if (k == "tm_tile_dicts" && (value == 0 || value == 1)) o.tm_tile_dicts = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
@@ -2038,6 +2044,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "col_dict_anchor") *value = o.col_dict_anchor;
     else if (k == "col_dict_tile") *value = o.col_dict_tile;
     else if (k == "x_stage") *value = o.x_stage;
+    else if (k == "long_tiles_min") *value = o.long_tiles_min;
     else if (k == "tm_tile_dicts") *value = o.tm_tile_dicts;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
