@@ -197,7 +197,8 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
  * nonzero budget of a 256-row tile), "tile_order" (0 natural | 1 banded XCD-blocked), "col24",
  * "long_tiles", "row_len8", "value_dict", "col_dict", "col_dict_anchor", "col_dict_tile", "x_stage", "tm_tile_dicts" (0 | 1
  * layout features), "long_tiles_min" (1..255 nonzeros per row from which sets of >= 64 M
- * nonzeros take long tiles), "tile_major" (0 | 1 where measured faster | 2 every eligible set). Applied at
+ * nonzeros take long tiles), "band_pct" / "band_pct_restrict" (percent scale of the banded
+ * order's band; the second for operators with fewer rows than columns), "tile_major" (0 | 1 where measured faster | 2 every eligible set). Applied at
  * every exchange:
  * "poison_ghosts" (0 | 1, debug: NaN-fill the ghost slots before each exchange). */
 int pamg_set_option(const char* key, int64_t value);

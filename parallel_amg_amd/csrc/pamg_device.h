@@ -103,6 +103,8 @@ struct Options {
     int tile_major = 1;        // tile-major padded copies (variant 4): 1 where measured faster, 2 all eligible
     int col_dict_tile = 1;     // 1: per-tile column dictionaries where no global table fits (and they beat 24-bit)
     int tm_tile_dicts = 1;     // 1: row-relative per-tile dictionary sets in tile-major slots (512^3 A1: -1..-3 %)
+    int band_pct = 100;        // scale of the measured band of the XCD-blocked tile order (percent)
+    int band_pct_restrict = 50;  // the same for operators with fewer rows than columns (restrictions)
     int x_stage = 1;           // 1: stage x runs in LDS for row-relative dictionary tile-major sets (no x gathers)
     int col_dict_anchor = 1;   // 1: anchored column dictionaries (col - row's first column) where row-relative ones do not fit
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange

@@ -1480,6 +1480,13 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
             auto q = max_gap.begin() + (ptrdiff_t)((m * 9) / 10);
             std::nth_element(max_gap.begin(), q, end);
             band = *q;
+            // restriction-shaped operators (fewer rows than columns: R0 reads the fine vector
+            // through 5x5x5 root neighbourhoods) walk half-layer bands: each XCD's window
+            // of fine lines between reuses halves (512^3 R0 -3 % in kbench,
+            // profiles/r02_exp/kbench512_band_pct_r0_p0.jsonl; in the bench R0 -1 %, R1 -2.5 %,
+            // the cycle within noise: bench_band_pct_restrict_ab/)
+            const int pct = nrows < n_own_cols ? pamg::options().band_pct_restrict : pamg::options().band_pct;
+            if (pct != 100) band = std::max<int64_t>(1, band * pct / 100);
         }
     }
     tr.mark("band");
@@ -2022,6 +2029,8 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "col_dict_anchor" && (value == 0 || value == 1)) o.col_dict_anchor = (int)value;
     else if (k == "col_dict_tile" && (value == 0 || value == 1)) o.col_dict_tile = (int)value;
     else if (k == "x_stage" && (value == 0 || value == 1)) o.x_stage = (int)value;
+    else if (k == "band_pct" && value >= 1 && value <= 10000) o.band_pct = (int)value;
+    else if (k == "band_pct_restrict" && value >= 1 && value <= 10000) o.band_pct_restrict = (int)value;
     else if (k == "long_tiles_min" && value >= 1 && value <= 255) o.long_tiles_min = (int)value;
     else if (k == "tm_tile_dicts" && (value == 0 || value == 1)) o.tm_tile_dicts = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
@@ -2044,6 +2053,8 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "col_dict_anchor") *value = o.col_dict_anchor;
     else if (k == "col_dict_tile") *value = o.col_dict_tile;
     else if (k == "x_stage") *value = o.x_stage;
+    else if (k == "band_pct") *value = o.band_pct;
+    else if (k == "band_pct_restrict") *value = o.band_pct_restrict;
     else if (k == "long_tiles_min") *value = o.long_tiles_min;
     else if (k == "tm_tile_dicts") *value = o.tm_tile_dicts;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);

@@ -60,7 +60,12 @@ def main():
     ap.add_argument("--mats", default=None, help="comma list of level matrices to run (e.g. R0,A1); default all")
     ap.add_argument("--ab", default=None,
                     help="launch-time option to A/B on the same upload (e.g. stream_nt): runs 0,1,0,1")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra pamg_set_option before the uploads (e.g. band_pct=50)")
     args = ap.parse_args()
+    for kv in args.set:
+        k, v = kv.split("=")
+        set_opts(**{k: int(v)})
     ctx = Context(0)
     be = pa.SequentialBackend(1)
     t = time.time()
@@ -95,7 +100,7 @@ def main():
                         set_opts(**{args.ab: abv})
                     ms, byt, fbyt = bench(ctx, D, op, args.reps)
                     # GBps: SURVEY §8(d) CSR bytes; format_GBps: the bytes the uploaded layout streams
-                    rec = {"cfg": cfg, "mat": name, "op": OPNAME[op], "rows": D.nrows, "nnz": D.nnz,
+                    rec = {"cfg": cfg + "".join(f"+{kv}" for kv in args.set), "mat": name, "op": OPNAME[op], "rows": D.nrows, "nnz": D.nnz,
                            "ms": round(ms, 4), "GBps": round(byt / ms / 1e6, 1),
                            "format_GBps": round(fbyt / ms / 1e6, 1), "layout": layout_of(D)}
                     if abv is not None:
