@@ -104,3 +104,33 @@ def test_load_order_binds_opt_rocm_runtime(built):
     assert set(prov) == {"hip", "rccl"}
     for k, path in prov.items():
         assert "/torch/" not in path and path.startswith("/opt/rocm"), (k, path)
+
+
+# every pamg_set_option key with its default and another legal value (include/pamg.h, the
+# INTEGRATION.md option table)
+OPTION_DEFAULTS = {"tile_nnz": (1024, 4096), "tile_order": (1, 0), "col24": (1, 0), "long_tiles": (1, 0),
+                   "long_tiles_min": (24, 48), "row_len8": (1, 0), "value_dict": (0, 1), "col_dict": (1, 0),
+                   "col_dict_anchor": (1, 0), "col_dict_tile": (1, 0), "x_stage": (1, 0), "tm_tile_dicts": (1, 0),
+                   "band_pct": (100, 50), "band_pct_restrict": (50, 100), "tile_major": (1, 2), "poison_ghosts": (0, 1)}
+
+
+def test_option_keys_defaults_and_docs(built):
+    """Each knob reads back its documented default, takes another legal value, rejects an
+    illegal one, and is listed in INTEGRATION.md's table and pamg.h's option comment."""
+    import os
+    from parallel_amg_amd._lib import PamgError, call
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    integ = open(os.path.join(root, "INTEGRATION.md")).read()
+    header = open(os.path.join(root, "include", "pamg.h")).read()
+    v = C.c_int64()
+    for k, (default, other) in OPTION_DEFAULTS.items():
+        call("pamg_get_option", k.encode(), C.byref(v))
+        assert v.value == default, k
+        call("pamg_set_option", k.encode(), other)
+        call("pamg_get_option", k.encode(), C.byref(v))
+        assert v.value == other, k
+        with pytest.raises(PamgError):
+            call("pamg_set_option", k.encode(), -7)
+        call("pamg_set_option", k.encode(), default)
+        assert f"`{k}`" in integ, k
+        assert f'"{k}"' in header, k
