@@ -130,3 +130,67 @@ def test_vcycle_deterministic_and_converging(ctx, h256):
     assert np.array_equal(bits(out[0][0]), bits(out[1][0]))
     assert np.array_equal(bits(out[0][0]), bits(out[2][0]))
     np.testing.assert_array_equal(out[0][1], out[2][1])
+
+
+def _stencil27(m, seed=3):
+    """27-point operator on an m^3 grid (random off-diagonal values, dominant diagonal) in CSR
+    with columns ascending: ~26 nonzeros per row, built vectorised."""
+    N = m ** 3
+    idx = np.arange(N, dtype=np.int64)
+    z, y, x = idx // (m * m), (idx // m) % m, idx % m
+    cols, valid = [], []
+    for dz in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                ok = (z + dz >= 0) & (z + dz < m) & (y + dy >= 0) & (y + dy < m) & (x + dx >= 0) & (x + dx < m)
+                cols.append(idx + dz * m * m + dy * m + dx)
+                valid.append(ok)
+    C = np.stack(cols, axis=1)
+    V = np.stack(valid, axis=1)
+    del cols, valid
+    rowptr = np.zeros(N + 1, np.int64)
+    np.cumsum(V.sum(axis=1), out=rowptr[1:])
+    col = C[V]
+    del C
+    rng = np.random.default_rng(seed)
+    val = rng.standard_normal(col.size)
+    rows = np.repeat(idx, np.diff(rowptr))
+    val[col == rows] = 40.0
+    return rowptr, col, val, N
+
+
+def test_long_row_operator_full_size(ctx):
+    """A square operator of >= 64 M nonzeros at ~26 per row (the 512^3 A1 regime): the upload
+    takes 4096-nonzero tiles (long_tiles_min) and SpMV / Jacobi give the oracle's bits, the
+    same bits as the 1024-nonzero tiles."""
+    import ctypes
+    from oracle import oracle as O
+    from parallel_amg_amd._lib import call, layout_of
+    from parallel_amg_amd.hcsr import HCSR
+    from parallel_amg_amd.partitioned import jacobi
+    rowptr, col, val, N = _stencil27(140)
+    assert col.size >= 64 << 20 and col.size >= 24 * N
+    M = HCSR.from_arrays(rowptr, col.astype(np.int32), val, N)
+    rng = np.random.default_rng(9)
+    xh, bh = rng.standard_normal(N), rng.standard_normal(N)
+    Mo = O.CSR(rowptr, col, val, N)
+    ref = O.spmv(Mo, xh)
+    refj = O.jacobi(Mo, xh, bh, 0.6)
+    outs = []
+    for ltm in (24, 48):
+        old = ctypes.c_int64()
+        call("pamg_get_option", b"long_tiles_min", ctypes.byref(old))
+        try:
+            call("pamg_set_option", b"long_tiles_min", ltm)
+            D = PSparseMatrix(ctx, M)
+        finally:
+            call("pamg_set_option", b"long_tiles_min", old.value)
+        assert layout_of(D)["tile_nnz"] == (4096 if ltm == 24 else 1024)
+        x, b, y, t = PVector(ctx, N, 0, xh), PVector(ctx, N, 0, bh), PVector(ctx, N), PVector(ctx, N)
+        mul(y, D, x)
+        assert np.array_equal(bits(y.own_values()), bits(ref))
+        jacobi(x, D, b, t, 0.6, 1)
+        assert np.array_equal(bits(x.own_values()), bits(refj))
+        outs.append(x.own_values())
+        del D
+    assert np.array_equal(bits(outs[0]), bits(outs[1]))
