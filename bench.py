@@ -75,6 +75,9 @@ def main():
     ap.add_argument("--permute", type=int, default=None, metavar="SEED",
                     help="apply a seeded random symmetric permutation to the problem before setup "
                          "(destroys the grid numbering, as an FE mesh ordering would; 1 part only)")
+    ap.add_argument("--reorder", choices=["auto", "off", "on"], default="auto",
+                    help="locality permutation of the level operators inside the device layout "
+                         "(AMGSolver reorder; one part; bits unchanged)")
     ap.add_argument("--pcg-rtol", type=float, default=1e-8,
                     help="time-to-solution leg: PCG with the V-cycle preconditioner to this "
                          "relative residual from x = 0 (0: skip)")
@@ -145,15 +148,19 @@ def main():
 
     # hipGraph replay on one part; multi-part cycles run eagerly (RCCL + host-side exchange)
     use_graph = (not args.no_graph) and (world == 1 or args.transport == "rccl")
-    S = AMGSolver(ctx, H, part=rank, graph=use_graph)
+    S = AMGSolver(ctx, H, part=rank, graph=use_graph, reorder=args.reorder if world == 1 else "off")
+    if S.reordered:
+        log(f"locality permutation on levels {S.reordered} (mean row span before/after: "
+            f"{[S.span[l] for l in S.reordered]})")
     nu1, nu2 = (int(v) for v in args.sweeps.split(","))
     S.set_sweeps(nu1, nu2)
     A0 = S.A[0]
-    xst = PVector(ctx, A0.n_own_cols, A0.n_ghost, xs[rank])
-    b = PVector(ctx, A0.nrows)
-    mul(b, A0, xst)
+    Af = S.fine_operator()  # the caller's numbering (b = A x* as the caller forms it)
+    xst = PVector(ctx, Af.n_own_cols, Af.n_ghost, xs[rank])
+    b = PVector(ctx, Af.nrows)
+    mul(b, Af, xst)
     x = S.new_vector()
-    del xst
+    del xst, Af
     t_upload = time.time() - t0 - t_setup
     log(f"upload {t_upload:.1f}s")
 
@@ -307,6 +314,8 @@ def main():
                 # levels >= this one are held whole on every rank (SPEC §S7 agglomeration)
                 "replicated_from_level": int(S.rep_level) if world > 1 else None,
                 "value_dict": bool(args.value_dict),
+                # levels uploaded with a locality permutation (AMGSolver reorder)
+                "reordered_levels": S.reordered,
                 "options": list(args.set),
             },
             "fine_spmv_GBps": round(spmv_gbps, 1),

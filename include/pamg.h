@@ -122,6 +122,16 @@ int pamg_exchange_end(pamg_ctx* ctx, pamg_plan* plan, pamg_vec* x);
 int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols_local, const int64_t* rowptr,
                     const void* col, int col_is_64, const double* val, int index_base,
                     const pamg_plan* col_plan, pamg_mat** out);
+/* The same upload with a locality permutation inside the device layout (replaces nothing in
+ * PartitionedArrays: it is how a solver keeps a scattered numbering — an FE mesh, a random
+ * renumbering — off the gather path). Device row i is caller row row_perm[i]; device own
+ * column k is caller own column col_perm[k] (ghost columns are never permuted). NULL = the
+ * identity. Each row keeps its entries in the caller's storage order, so every row sum
+ * (SPEC §S3) has the caller's bits. Vectors applied to the matrix are in device numbering. */
+int pamg_mat_upload_perm(pamg_ctx* ctx, int64_t nrows, int64_t ncols_local, const int64_t* rowptr,
+                         const void* col, int col_is_64, const double* val, int index_base,
+                         const pamg_plan* col_plan, const int64_t* row_perm,
+                         const int64_t* col_perm, pamg_mat** out);
 int pamg_mat_destroy(pamg_mat* A);
 int pamg_mat_info(const pamg_mat* A, int64_t* nrows, int64_t* ncols_local, int64_t* nnz);
 /* Bytes of matrix data one row operation streams in the layout chosen at upload: 8 B values +
@@ -170,6 +180,12 @@ int pamg_hier_set_graph(pamg_hier* H, int enable);
 /* V(nu1, nu2): Jacobi sweeps before / after the coarse correction (SPEC §S6; default 1, 1;
  * 1..64). The first pre-sweep on levels >= 1 is the zero-guess form. */
 int pamg_hier_set_sweeps(pamg_hier* H, int nu1, int nu2);
+/* Level-0 numbering of a hierarchy whose operators were uploaded with pamg_mat_upload_perm
+ * (one part only): device row i of level 0 is caller row perm[i]. pamg_vcycle(_async) and
+ * pamg_pcg then take x and b in the caller's numbering — gathered into the device numbering at
+ * entry, x scattered back at exit — and return the bits of the unpermuted hierarchy's cycle.
+ * perm = NULL (or n = 0) removes it. */
+int pamg_hier_set_perm(pamg_hier* H, int64_t n, const int64_t* perm);
 /* enabled: graph replay currently on; captured: a graph exists; failed: a capture failed. */
 int pamg_hier_graph_state(const pamg_hier* H, int* enabled, int* captured, int* failed);
 /* x <- V(x) ncycles times (SPEC §S6); res_hist (ncycles, may be NULL) gets ||b - A x||. */
@@ -226,6 +242,13 @@ int pamg_mtx_row_counts(const char* path, int64_t* n_global, int64_t* counts);
  * §8(f)-3): renumber with it, then cut contiguous nnz-balanced row blocks (SPEC §S7).
  * Deterministic (pseudo-peripheral start, neighbours by degree then index). */
 int pamg_rcm_order(const pamg_hcsr* A, int64_t* order);
+/* Locality order of a square level operator for pamg_mat_upload_perm: mode 0 identity,
+ * 2 reverse Cuthill-McKee, 1 (auto) RCM only where the numbering is scattered — the mean row
+ * span (largest - smallest column of a row) exceeds n/32 on a matrix of >= 4096 rows — and RCM
+ * cuts that mean span at least 4x; else the identity. *applied = 1 when order is not the
+ * identity; span_before / span_after (may be NULL) get the mean spans. */
+int pamg_locality_order(const pamg_hcsr* A, int mode, int64_t* order, int* applied,
+                        double* span_before, double* span_after);
 /* Dense coarsest-level limit of pamg_setup_cholinv (rows); larger levels get PAMG_E_ARG. */
 #define PAMG_MAX_DENSE_COARSE 16384
 /* Gershgorin bound over own rows; A's rows are global rows row0.. (diagonal at col row0+i). */

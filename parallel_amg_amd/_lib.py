@@ -63,6 +63,7 @@ SIGNATURES = {
     "pamg_exchange_begin": [vp, vp, vp],
     "pamg_exchange_end": [vp, vp, vp],
     "pamg_mat_upload": [vp, i64, i64, vp, vp, i32, vp, i32, vp, pvp],
+    "pamg_mat_upload_perm": [vp, i64, i64, vp, vp, i32, vp, i32, vp, vp, vp, pvp],
     "pamg_mat_destroy": [vp],
     "pamg_mat_info": [vp, pi64, pi64, pi64],
     "pamg_mat_stream_bytes": [vp, pi64],
@@ -74,6 +75,7 @@ SIGNATURES = {
     "pamg_hier_destroy": [vp],
     "pamg_hier_set_graph": [vp, i32],
     "pamg_hier_set_sweeps": [vp, i32, i32],
+    "pamg_hier_set_perm": [vp, i64, vp],
     "pamg_hier_graph_state": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "pamg_vcycle": [vp, vp, vp, vp, i32, vp],
     "pamg_vcycle_async": [vp, vp, vp, vp, i32],
@@ -92,6 +94,7 @@ SIGNATURES = {
     "pamg_read_mtx": [C.c_char_p, i64, i64, pi64, pvp],
     "pamg_mtx_row_counts": [C.c_char_p, pi64, vp],
     "pamg_rcm_order": [vp, vp],
+    "pamg_locality_order": [vp, i32, vp, C.POINTER(C.c_int), pdbl, pdbl],
     "pamg_setup_gershgorin": [vp, i64, pdbl],
     "pamg_setup_aggregate": [vp, i64, dbl, vp, pi64],
     "pamg_setup_tentative": [i64, vp, i64, i64, i64, pvp],

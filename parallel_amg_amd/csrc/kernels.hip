@@ -661,6 +661,18 @@ __global__ void k_pack(int64_t n, const int* __restrict__ idx, const double* __r
         out[i] = x[idx[i]];
 }
 
+// Level-0 locality permutation at the V-cycle boundary (pamg_hier_set_perm): gather
+// dst[i] = src[perm[i]] (caller -> device numbering) or scatter dst[perm[i]] = src[i].
+template <bool SCATTER>
+__global__ void k_permute(int64_t n, const int* __restrict__ perm, const double* __restrict__ src,
+                          double* __restrict__ dst) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if constexpr (SCATTER) dst[perm[i]] = src[i];
+        else dst[i] = src[perm[i]];
+    }
+}
+
 __global__ void k_fill(int64_t n, double v, double* __restrict__ y) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -869,6 +881,12 @@ void launch_dense_gemv(int64_t n_rows, int64_t n_cols, int64_t row0, const doubl
 
 void launch_pack(int64_t n, const int* idx, const double* x, double* out, hipStream_t s) {
     if (n > 0) k_pack<<<grid_for(n), kBlock, 0, s>>>(n, idx, x, out);
+}
+
+void launch_permute(int64_t n, const int* perm, const double* src, double* dst, bool scatter, hipStream_t s) {
+    if (n <= 0) return;
+    if (scatter) k_permute<true><<<grid_for(n), kBlock, 0, s>>>(n, perm, src, dst);
+    else k_permute<false><<<grid_for(n), kBlock, 0, s>>>(n, perm, src, dst);
 }
 
 void launch_fill(int64_t n, double v, double* y, hipStream_t s) {

@@ -302,3 +302,53 @@ extern "C" int pamg_rcm_order(const pamg_hcsr* A, int64_t* order) {
     }
     return PAMG_OK;
 }
+
+// Mean over the rows with entries of (largest - smallest column), the columns read through a
+// permutation inv (device column of caller column j = inv[j]; NULL: identity) and the rows
+// taken in any order (the span of a row does not depend on where the row goes).
+static double mean_row_span(const pamg_hcsr& A, const int64_t* inv) {
+    double sum = 0.0;
+    int64_t rows = 0;
+    for (int64_t i = 0; i < A.nr; ++i) {
+        if (A.rp[i + 1] == A.rp[i]) continue;
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+            const int64_t c = inv ? inv[A.col[k]] : A.col[k];
+            lo = std::min(lo, c);
+            hi = std::max(hi, c);
+        }
+        sum += (double)(hi - lo);
+        ++rows;
+    }
+    return rows ? sum / (double)rows : 0.0;
+}
+
+// Locality order of one square level operator for the device layout (pamg_mat_upload_perm /
+// pamg_hier_set_perm): a scattered numbering (an FE mesh or a random renumbering, and the
+// coarse levels aggregated from it) makes every x gather of the row kernels a cache miss.
+extern "C" int pamg_locality_order(const pamg_hcsr* A, int mode, int64_t* order, int* applied,
+                                   double* span_before, double* span_after) {
+    if (!A || !order || mode < 0 || mode > 2) return fail(PAMG_E_ARG, "locality_order: bad args");
+    if (A->nr != A->nc) return fail(PAMG_E_ARG, "locality_order: matrix is %lld x %lld, not square",
+                                    (long long)A->nr, (long long)A->nc);
+    const int64_t n = A->nr;
+    for (int64_t i = 0; i < n; ++i) order[i] = i;
+    const double before = mean_row_span(*A, nullptr);
+    if (span_before) *span_before = before;
+    if (span_after) *span_after = before;
+    if (applied) *applied = 0;
+    // auto: only a numbering whose rows span more than n/32 columns on average is a candidate
+    // (grid numberings span ~2 n^(2/3): 0.8 % of n for 512^3, 2.5 % for elastic3d 80^3)
+    if (mode == 0 || (mode == 1 && (n < 4096 || before <= (double)n / 32.0))) return PAMG_OK;
+    std::vector<int64_t> rcm(n), inv(n);
+    const int rc = pamg_rcm_order(A, rcm.data());
+    if (rc != PAMG_OK) return rc;
+    for (int64_t k = 0; k < n; ++k) inv[rcm[k]] = k;
+    const double after = mean_row_span(*A, inv.data());
+    // auto: taken when it cuts the mean span at least 4x
+    if (mode == 1 && after * 4.0 > before) return PAMG_OK;
+    std::copy(rcm.begin(), rcm.end(), order);
+    if (span_after) *span_after = after;
+    if (applied) *applied = 1;
+    return PAMG_OK;
+}

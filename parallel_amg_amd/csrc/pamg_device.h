@@ -180,6 +180,8 @@ void launch_dense_gemv(int64_t n_rows, int64_t n_cols, int64_t row0, const doubl
                        const double* b, double* y, hipStream_t s);
 void launch_pack(int64_t n, const int* idx, const double* x, double* out, hipStream_t s);
 void launch_fill(int64_t n, double v, double* y, hipStream_t s);
+// dst[i] = src[perm[i]] (gather), or dst[perm[i]] = src[i] (scatter)
+void launch_permute(int64_t n, const int* perm, const double* src, double* dst, bool scatter, hipStream_t s);
 void launch_axpby(int64_t n, double a, const double* x, double b, double* y, hipStream_t s);
 // Deterministic two-pass dot: writes the local sum to *out (device).
 void launch_dot(int64_t n, const double* x, const double* y, double* partials, int nparts,

@@ -892,6 +892,10 @@ struct pamg_hier {
     bool graph_failed = false;
     // PCG workspace (level-0 layout, allocated on first use)
     double *pcg_r = nullptr, *pcg_z = nullptr, *pcg_p = nullptr, *pcg_q = nullptr;
+    // level-0 locality permutation (pamg_hier_set_perm): device row i = caller row perm[i];
+    // the caller's x and b are gathered into px / pb at entry and x is scattered back at exit
+    int* d_perm = nullptr;
+    double *px = nullptr, *pb = nullptr;
     // profiling
     int nu1 = 1, nu2 = 1;  // V(nu1, nu2) Jacobi sweeps (SPEC §S6)
     bool prof = false;
@@ -1568,6 +1572,70 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     return PAMG_OK;
 }
 
+// Locality permutation inside the device layout: device row i = caller row row_perm[i], own
+// column c of the caller = device column inv(col_perm)[c] (ghost columns stay). Each row keeps
+// its entries in the caller's storage order, so every row sum (SPEC §S3) keeps its bits; only
+// the rows' places and the x entries they gather move.
+static int check_perm(const int64_t* p, int64_t n, const char* what) {
+    std::vector<char> seen(n, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        if (p[i] < 0 || p[i] >= n || seen[p[i]])
+            return fail(PAMG_E_ARG, "mat_upload_perm: %s is not a permutation of 0..%lld", what, (long long)(n - 1));
+        seen[p[i]] = 1;
+    }
+    return PAMG_OK;
+}
+
+int pamg_mat_upload_perm(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* rowptr,
+                         const void* col, int col_is_64, const double* val, int index_base,
+                         const pamg_plan* plan, const int64_t* row_perm, const int64_t* col_perm,
+                         pamg_mat** out) {
+    if (!ctx || !out || nrows < 0 || ncols < 0 || !rowptr || (index_base != 0 && index_base != 1))
+        return fail(PAMG_E_ARG, "mat_upload_perm: bad args");
+    const int64_t nnz = rowptr[nrows] - index_base;
+    if (nnz < 0 || rowptr[0] != index_base || (nnz > 0 && (!col || !val)))
+        return fail(PAMG_E_ARG, "mat_upload_perm: bad arrays");
+    if (nnz >= INT32_MAX - 16 || nrows >= INT32_MAX || ncols >= INT32_MAX)
+        return fail(PAMG_E_OVERFLOW, "mat_upload_perm: nnz/rows/cols exceed the int32 device layout");
+    const int64_t n_own_cols = plan ? plan->n_own : ncols;
+    if (n_own_cols > ncols) return fail(PAMG_E_ARG, "mat_upload_perm: plan has more own columns than the matrix");
+    if (row_perm) CHECK(check_perm(row_perm, nrows, "row_perm"));
+    std::vector<int> cinv;
+    if (col_perm) {
+        CHECK(check_perm(col_perm, n_own_cols, "col_perm"));
+        cinv.resize(n_own_cols);
+        for (int64_t k = 0; k < n_own_cols; ++k) cinv[col_perm[k]] = (int)k;
+    }
+    std::vector<int64_t> rp(nrows + 1, 0);
+    for (int64_t i = 0; i < nrows; ++i) {
+        const int64_t r = row_perm ? row_perm[i] : i;
+        const int64_t len = rowptr[r + 1] - rowptr[r];
+        if (len < 0) return fail(PAMG_E_ARG, "mat_upload_perm: rowptr not monotone at %lld", (long long)r);
+        rp[i + 1] = rp[i] + len;
+    }
+    std::vector<int> ci(nnz);
+    std::vector<double> va(nnz);
+    std::atomic<bool> bad{false};
+    par_for(nrows, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            const int64_t r = row_perm ? row_perm[i] : i;
+            const int64_t s = rowptr[r] - index_base;
+            for (int64_t k = 0; k < rp[i + 1] - rp[i]; ++k) {
+                const int64_t c = (col_is_64 ? static_cast<const int64_t*>(col)[s + k]
+                                             : (int64_t) static_cast<const int32_t*>(col)[s + k]) - index_base;
+                if (c < 0 || c >= ncols) {
+                    bad = true;
+                    return;
+                }
+                ci[rp[i] + k] = (c < n_own_cols && col_perm) ? cinv[c] : (int)c;
+                va[rp[i] + k] = val[s + k];
+            }
+        }
+    });
+    if (bad) return fail(PAMG_E_ARG, "mat_upload_perm: column out of range");
+    return pamg_mat_upload(ctx, nrows, ncols, rp.data(), ci.data(), 0, va.data(), 0, plan, out);
+}
+
 int pamg_mat_destroy(pamg_mat* A) {
     if (!A) return PAMG_OK;
     (void)hipSetDevice(A->ctx->device);
@@ -1809,6 +1877,9 @@ int pamg_hier_destroy(pamg_hier* H) {
     dfree(H->pcg_z);
     dfree(H->pcg_p);
     dfree(H->pcg_q);
+    dfree(H->d_perm);
+    dfree(H->px);
+    dfree(H->pb);
     for (auto e : H->ev) (void)hipEventDestroy(e);
     delete H;
     return PAMG_OK;
@@ -1833,6 +1904,35 @@ int pamg_hier_set_sweeps(pamg_hier* H, int nu1, int nu2) {
     }
     H->nu1 = nu1;
     H->nu2 = nu2;
+    return PAMG_OK;
+}
+
+int pamg_hier_set_perm(pamg_hier* H, int64_t n, const int64_t* perm) {
+    if (!H) return fail(PAMG_E_ARG, "hier_set_perm: NULL");
+    pamg_ctx* ctx = H->ctx;
+    CHECK(set_device(ctx));
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    dfree(H->d_perm);
+    dfree(H->px);
+    dfree(H->pb);
+    if (!perm || n == 0) return PAMG_OK;
+    if (ctx->nranks > 1) return fail(PAMG_E_STATE, "hier_set_perm: one part only (permute a partition's rows before setup)");
+    const pamg_mat* A0 = H->A[0];
+    if (n != H->nown[0] || n != A0->ncols)
+        return fail(PAMG_E_ARG, "hier_set_perm: %lld entries for a %lld-row level 0", (long long)n, (long long)H->nown[0]);
+    std::vector<int> p(n);
+    std::vector<char> seen(n, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        if (perm[i] < 0 || perm[i] >= n || seen[perm[i]]) return fail(PAMG_E_ARG, "hier_set_perm: not a permutation");
+        seen[perm[i]] = 1;
+        p[i] = (int)perm[i];
+    }
+    CHECK(dalloc(&H->d_perm, n));
+    CHECK(dalloc(&H->px, n + kVecPad));
+    CHECK(dalloc(&H->pb, n + kVecPad));
+    HIPC(hipMemcpy(H->d_perm, p.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+    HIPC(hipMemset(H->px, 0, sizeof(double) * (n + kVecPad)));
+    HIPC(hipMemset(H->pb, 0, sizeof(double) * (n + kVecPad)));
     return PAMG_OK;
 }
 
@@ -1910,13 +2010,38 @@ static int vcycle_raw(pamg_hier* H, double* x, const double* b, int ncycles, boo
     return PAMG_OK;
 }
 
+// The caller's level-0 vectors in the device numbering: with a level-0 permutation, b is
+// gathered into pb and (unless the guess is zero) x into px; without one they are used as is.
+struct DeviceSpace {
+    pamg_hier* H;
+    double* x;
+    const double* b;
+    DeviceSpace(pamg_hier* h, pamg_vec* xv, const pamg_vec* bv, bool gather_x) : H(h), x(xv->d), b(bv->d) {
+        if (!H->d_perm) return;
+        const int64_t n = H->nown[0];
+        hipStream_t s = H->ctx->s_comp;
+        pamg::launch_permute(n, H->d_perm, bv->d, H->pb, false, s);
+        if (gather_x) pamg::launch_permute(n, H->d_perm, xv->d, H->px, false, s);
+        x = H->px;
+        b = H->pb;
+    }
+    // x back to the caller's numbering
+    void finish(pamg_vec* xv) {
+        if (H->d_perm) pamg::launch_permute(H->nown[0], H->d_perm, H->px, xv->d, true, H->ctx->s_comp);
+    }
+};
+
 static int vcycle_common(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles) {
     if (!ctx || !H || !x || !b || ncycles < 0 || H->ctx != ctx) return fail(PAMG_E_ARG, "vcycle: bad args");
     const pamg_mat* A0 = H->A[0];
     CHECK(check_vec_for(A0, x, "vcycle"));
     if (b->n_own != A0->nrows) return fail(PAMG_E_ARG, "vcycle: b size mismatch");
     CHECK(set_device(ctx));
-    return vcycle_raw(H, x->d, b->d, ncycles, false);
+    DeviceSpace d(H, x, b, true);
+    CHECK(vcycle_raw(H, d.x, d.b, ncycles, false));
+    d.finish(x);
+    HIPC(hipGetLastError());
+    return PAMG_OK;
 }
 
 int pamg_vcycle_async(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles) {
@@ -1930,9 +2055,14 @@ int pamg_vcycle(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int
         HIPC(hipStreamSynchronize(ctx->s_comp));
         return PAMG_OK;
     }
-    if (!H || H->L < 1 || (!H->t[0] && H->L > 1)) return fail(PAMG_E_ARG, "vcycle: bad hierarchy");
+    if (!ctx || !H || !x || !b || ncycles < 0 || H->ctx != ctx) return fail(PAMG_E_ARG, "vcycle: bad args");
+    if (H->L < 1 || (!H->t[0] && H->L > 1)) return fail(PAMG_E_ARG, "vcycle: bad hierarchy");
+    CHECK(check_vec_for(H->A[0], x, "vcycle"));
+    if (b->n_own != H->A[0]->nrows) return fail(PAMG_E_ARG, "vcycle: b size mismatch");
+    CHECK(set_device(ctx));
+    DeviceSpace d(H, x, b, true);
     for (int k = 0; k < ncycles; ++k) {
-        CHECK(vcycle_common(ctx, H, x, b, 1));
+        CHECK(vcycle_raw(H, d.x, d.b, 1, false));
         // r = b - A x into the level-0 residual buffer (1-level hierarchies use a temporary)
         double* r = H->L > 1 ? H->r[0] : nullptr;
         double* tmp = nullptr;
@@ -1940,13 +2070,14 @@ int pamg_vcycle(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int
             CHECK(dalloc(&tmp, H->nown[0] + kVecPad));
             r = tmp;
         }
-        int rc = apply(ctx, H->A[0], pamg::OP_RESID, x->d, b->d, r, 0.0);
+        int rc = apply(ctx, H->A[0], pamg::OP_RESID, d.x, d.b, r, 0.0);
         double s = 0.0;
         if (rc == PAMG_OK) rc = reduce_scalar(ctx, H->nown[0], r, r, &s);
         dfree(tmp);
         CHECK(rc);
         res_hist[k] = std::sqrt(s);
     }
+    d.finish(x);
     HIPC(hipStreamSynchronize(ctx->s_comp));
     return PAMG_OK;
 }
@@ -1975,7 +2106,10 @@ int pamg_pcg(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, double
     }
     hipStream_t s = ctx->s_comp;
     double *r = H->pcg_r, *z = H->pcg_z, *p = H->pcg_p, *q = H->pcg_q;
-    CHECK(apply(ctx, A, pamg::OP_RESID, x->d, b->d, r, 0.0));
+    // with a level-0 permutation the whole iteration runs in the device numbering
+    DeviceSpace d(H, x, b, true);
+    double* xd = d.x;
+    CHECK(apply(ctx, A, pamg::OP_RESID, xd, d.b, r, 0.0));
     double rr = 0.0;
     CHECK(reduce_scalar(ctx, n, r, r, &rr));
     const double nr0 = std::sqrt(rr);
@@ -1994,7 +2128,7 @@ int pamg_pcg(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, double
             const double alpha = rz / pq;
             // x += alpha p; r -= alpha q; rr = r.r in one pass (bits of the unfused sequence)
             CHECK(reduce_with(ctx, n, &rr, [&](int np, double* parts, double* res, hipStream_t st) {
-                pamg::launch_cg_update(n, alpha, p, q, x->d, r, parts, np, res, st);
+                pamg::launch_cg_update(n, alpha, p, q, xd, r, parts, np, res, st);
             }));
             const double nr = std::sqrt(rr);
             if (res_hist) res_hist[k] = nr;
@@ -2007,6 +2141,7 @@ int pamg_pcg(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, double
             pamg::launch_axpby(n, 1.0, z, beta, p, s);
         }
     }
+    d.finish(x);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(s));
     if (iters) *iters = k;

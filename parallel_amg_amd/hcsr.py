@@ -105,6 +105,18 @@ def rcm_order(A: HCSR) -> np.ndarray:
     return out
 
 
+def locality_order(A: HCSR, mode: int = 1):
+    """Locality order of a square level operator for the device layout (pamg_locality_order):
+    mode 0 identity, 1 auto (reverse Cuthill-McKee only where the numbering is scattered and
+    RCM cuts the mean row span 4x), 2 always RCM. Returns (order or None for the identity,
+    mean row span before, after)."""
+    out = np.empty(A.nrows, np.int64)
+    applied, before, after = C.c_int(), C.c_double(), C.c_double()
+    call("pamg_locality_order", A.handle, int(mode), ptr(out), C.byref(applied), C.byref(before),
+         C.byref(after))
+    return (out if applied.value else None), before.value, after.value
+
+
 def gen_xstar(i0: int, n: int, seed: int) -> np.ndarray:
     out = np.empty(n, np.float64)
     call("pamg_gen_xstar", i0, n, seed, ptr(out))

@@ -227,7 +227,10 @@ class PSparseMatrix:
     """Device CSR of one part: own rows, columns local to ``plan`` (own, then ghosts)."""
 
     def __init__(self, ctx: Context, M: HCSR, plan: HostPlan | None = None,
-                 dplan: DevicePlan | None = None):
+                 dplan: DevicePlan | None = None, row_perm=None, col_perm=None):
+        """``row_perm`` / ``col_perm`` (pamg_mat_upload_perm): device row i is row
+        ``row_perm[i]`` of M, device own column k is own column ``col_perm[k]`` (None: the
+        identity); rows keep their storage order, so row sums keep their bits."""
         self.ctx = ctx
         if plan is not None and dplan is None and plan.nbrs:
             dplan = DevicePlan(ctx, plan)
@@ -239,8 +242,16 @@ class PSparseMatrix:
             col, ncols = M.col, M.ncols
         col = np.ascontiguousarray(col, np.int32)
         h = C.c_void_p()
-        call("pamg_mat_upload", ctx.handle, M.nrows, ncols, ptr(M.rowptr), ptr(col), 0,
-             ptr(M.val), 0, dplan.handle if dplan is not None else None, C.byref(h))
+        if row_perm is None and col_perm is None:
+            call("pamg_mat_upload", ctx.handle, M.nrows, ncols, ptr(M.rowptr), ptr(col), 0,
+                 ptr(M.val), 0, dplan.handle if dplan is not None else None, C.byref(h))
+        else:
+            rperm = None if row_perm is None else np.ascontiguousarray(row_perm, np.int64)
+            cperm = None if col_perm is None else np.ascontiguousarray(col_perm, np.int64)
+            call("pamg_mat_upload_perm", ctx.handle, M.nrows, ncols, ptr(M.rowptr), ptr(col), 0,
+                 ptr(M.val), 0, dplan.handle if dplan is not None else None,
+                 ptr(rperm) if rperm is not None else None, ptr(cperm) if cperm is not None else None,
+                 C.byref(h))
         self._h = h
         self.nrows, self.ncols, self.nnz = M.nrows, ncols, M.nnz
         self.n_own_cols = plan.n_own if plan is not None else ncols

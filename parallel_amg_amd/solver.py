@@ -17,20 +17,49 @@ from .partitioned import Context, PSparseMatrix, PVector, _release
 OPS = ("jacobi_pre", "residual", "restrict", "prolong", "jacobi_post", "coarse")
 
 
+REORDER = {"off": 0, "auto": 1, "on": 2}
+
+
 class AMGSolver:
-    def __init__(self, ctx: Context, H: HostHierarchy, part: int = 0, graph: bool | None = None):
+    def __init__(self, ctx: Context, H: HostHierarchy, part: int = 0, graph: bool | None = None,
+                 reorder: str = "auto"):
+        """``reorder`` (one part only): a locality permutation of every level but the coarsest
+        inside the device layout (pamg_locality_order / pamg_mat_upload_perm): "auto" takes
+        reverse Cuthill-McKee on the levels whose numbering is scattered (FE meshes, random
+        renumberings and the levels aggregated from them), "on" on every level, "off" never.
+        A_l, P_l and R_l are uploaded through the fine and coarse permutations with each row
+        in its storage order, and the V-cycle gathers / scatters the caller's level-0 vectors
+        (pamg_hier_set_perm), so every result keeps the unpermuted hierarchy's bits."""
         self.ctx, self.part, self.L = ctx, part, H.nlevels
         self.A, self.P, self.R, self.omega = [], [], [], []
+        self._H = H
         # levels >= rep are whole on every part (agglomerated tail / coarsest level): the
         # prolongation into rep - 1 reads that whole vector, so its columns stay global
         rep = H.rep_level if H.nparts > 1 else H.nlevels - 1
+        mode = REORDER[reorder]
+        if H.nparts > 1 and mode == 2:
+            raise ValueError("reorder='on' needs a one-part hierarchy (renumber a partitioned "
+                             "matrix before setup: partition='rcm')")
+        # per level: device row i = host row perm[l][i] (None: identity); the coarsest level
+        # keeps its numbering (its dense inverse sums in column order)
+        self.perm = [None] * H.nlevels
+        self.span = [None] * H.nlevels
+        if H.nparts == 1 and mode:
+            from .hcsr import locality_order
+            for l in range(H.nlevels - 1):
+                order, before, after = locality_order(H.levels[l][part].A, mode)
+                self.perm[l] = order
+                self.span[l] = (round(before, 1), round(after, 1))
         for l in range(H.nlevels):
             lp = H.levels[l][part]
-            self.A.append(PSparseMatrix(ctx, lp.A, lp.planA))
+            pl = self.perm[l]
+            pn = self.perm[l + 1] if l + 1 < H.nlevels else None
+            self.A.append(PSparseMatrix(ctx, lp.A, lp.planA, row_perm=pl, col_perm=pl))
             self.omega.append(lp.omega)
             if l < H.nlevels - 1:
-                self.P.append(PSparseMatrix(ctx, lp.P, None if l + 1 >= rep else lp.planP))
-                self.R.append(PSparseMatrix(ctx, lp.R, lp.planR))
+                self.P.append(PSparseMatrix(ctx, lp.P, None if l + 1 >= rep else lp.planP,
+                                            row_perm=pl, col_perm=pn))
+                self.R.append(PSparseMatrix(ctx, lp.R, lp.planR, row_perm=pn, col_perm=pl))
         self.level_rows = [int(H.levels[l][part].A.nrows) for l in range(H.nlevels)]
         self.n_coarse = H.n_coarse
         L = self.L
@@ -45,8 +74,25 @@ class AMGSolver:
         call("pamg_hier_create", ctx.handle, L, arrA, arrP, arrR, ptr(om), H.n_coarse,
              ptr(self._ainv), int(rep), ptr(roffs) if roffs is not None else None, C.byref(h))
         self._h = h
+        if self.perm[0] is not None:
+            p0 = np.ascontiguousarray(self.perm[0], np.int64)
+            call("pamg_hier_set_perm", h, len(p0), ptr(p0))
         if graph is not None:
             self.set_graph(graph)
+
+    @property
+    def reordered(self) -> list:
+        """Levels whose device layout carries a locality permutation."""
+        return [l for l, p in enumerate(self.perm) if p is not None]
+
+    def fine_operator(self) -> PSparseMatrix:
+        """The level-0 operator in the caller's numbering (for b = A x and residuals of the
+        caller's vectors): the hierarchy's own A_0 when level 0 is not permuted, else a fresh
+        unpermuted upload."""
+        if self.perm[0] is None:
+            return self.A[0]
+        lp = self._H.levels[0][self.part]
+        return PSparseMatrix(self.ctx, lp.A, lp.planA)
 
     @property
     def handle(self):

@@ -729,3 +729,86 @@ def test_vcycle_permuted_bit_exact(ctx, kind, n, seed):
     hist = S.vcycle(x, b, 5, res_hist=True)
     assert np.array_equal(bits(x.own_values()), bits(xo))
     np.testing.assert_allclose(hist, ho, rtol=1e-12)
+
+
+# ---------------------------------------------------------------- locality permutation (reorder)
+def test_upload_perm_rows_and_columns_bit_exact(ctx):
+    """pamg_mat_upload_perm: device row i = row perm[i], device column k = column perm[k], each
+    row in its storage order — SpMV / residual / Jacobi of the permuted vectors are the
+    unpermuted results, moved."""
+    rng = np.random.default_rng(7)
+    M = random_csr(rng, [7, 0, 3, 27, 1, 9] * 400, 2400, square=True)
+    n = M.nrows
+    h = HCSR.from_arrays(M.rowptr, M.col.astype(np.int32), M.val, M.ncols)
+    perm = rng.permutation(n).astype(np.int64)
+    A = PSparseMatrix(ctx, h, row_perm=perm, col_perm=perm)
+    xh = rng.standard_normal(n)
+    bh = rng.standard_normal(n)
+    x, b, y = PVector(ctx, n, 0, xh[perm]), PVector(ctx, n, 0, bh[perm]), PVector(ctx, n)
+    mul(y, A, x)
+    assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)[perm]))
+    residual(y, A, x, b)
+    assert np.array_equal(bits(y.own_values()), bits(O.residual(M, xh, bh)[perm]))
+    t = PVector(ctx, n)
+    jacobi(x, A, b, t, 0.61, 2)
+    xj = O.jacobi(M, O.jacobi(M, xh, bh, 0.61), bh, 0.61)
+    assert np.array_equal(bits(x.own_values()), bits(xj[perm]))
+
+
+@pytest.mark.parametrize("kind,n,seed", [("poisson3d", 20, 1), ("elastic3d", 14, 2), ("aniso3d", 18, 3),
+                                         ("poisson2d", 96, 4)])
+@pytest.mark.parametrize("reorder", ["auto", "on"])
+def test_reorder_vcycle_bit_exact_caller_numbering(ctx, kind, n, seed, reorder):
+    """a randomly renumbered problem (the Flan_1565 proxy) set up in the
+    caller's numbering; the device layout carries a per-level locality permutation (reverse
+    Cuthill-McKee of each A_l, P_l / R_l through the fine and coarse permutations, rows in
+    storage order). The V-cycle takes and returns the caller's vectors and is bit-exact with the
+    oracle run on the caller's (unpermuted) numbering; PCG matches the oracle's iterations."""
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, kind, n)
+    A, xs = pa.permute_problem(A, xs, seed)
+    M = A[0]
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=100), device=ctx)
+    S = AMGSolver(ctx, H, reorder=reorder)
+    assert 0 in S.reordered, (S.reordered, S.span)   # the shuffled fine level is always permuted
+    if reorder == "on":
+        assert S.reordered == list(range(H.nlevels - 1))
+    b = PVector(ctx, M.nrows)
+    mul(b, S.fine_operator(), PVector(ctx, M.nrows, 0, xs[0]))
+    Ao = O.CSR(M.rowptr.copy(), M.col.astype(np.int64), M.val.copy(), M.ncols)
+    bo = O.spmv(Ao, xs[0])
+    assert np.array_equal(bits(b.own_values()), bits(bo))
+    Ho = O.setup(Ao, max_coarse=100)
+    assert Ho.nlevels == H.nlevels
+    xo, ho = Ho.solve(bo, 5, res_hist=True)
+    x = S.new_vector()
+    hist = S.vcycle(x, b, 5, res_hist=True)
+    assert np.array_equal(bits(x.own_values()), bits(xo))
+    np.testing.assert_allclose(hist, ho, rtol=1e-12)
+    # stationary cycles without history (graph replay) continue from the same caller vector
+    x2 = S.new_vector()
+    S.vcycle(x2, b, 3)
+    S.vcycle(x2, b, 2)
+    assert np.array_equal(bits(x2.own_values()), bits(xo))
+    xpo, ko, hpo = Ho.pcg(bo, 1e-10, 80)
+    xp = S.new_vector()
+    k, hp = S.pcg(xp, b, 1e-10, 80)
+    assert k == ko
+    np.testing.assert_allclose(hp, hpo, rtol=1e-6)
+    assert np.linalg.norm(xp.own_values() - xpo) <= 1e-8 * np.linalg.norm(xpo)
+
+
+def test_reorder_graph_equals_eager(ctx):
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 18)
+    A, xs = pa.permute_problem(A, xs, 5)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=100))
+    S = AMGSolver(ctx, H, reorder="on")
+    b = PVector(ctx, A[0].nrows, 0, xs[0])
+    out = []
+    for g in (True, False):
+        S.set_graph(g)
+        x = S.new_vector()
+        S.vcycle(x, b, 4)
+        out.append(x.own_values())
+    assert np.array_equal(bits(out[0]), bits(out[1]))

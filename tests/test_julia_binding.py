@@ -149,3 +149,71 @@ def test_the_binding_covers_the_header():
                                     ("const char* key", "Cstring", True)])
 def test_type_rules(c, j, ok):
     assert compatible(c, j) == ok
+
+
+# PartitionedArrays' / LinearAlgebra's generic-function surface an AMG solver calls unqualified
+# (the PartitionedArrays tables): PamgHIP must not export a generic of its own
+# under any of these names, or `using PartitionedArrays, PamgHIP` makes the solver's calls
+# ambiguous.
+PA_SURFACE = {"consistent!", "assemble!", "own_values", "ghost_values", "local_values", "partition",
+              "exchange", "exchange!", "mul!", "dot", "norm", "axpy!", "axpby!", "ldiv!", "fill!",
+              "copy!", "copyto!", "similar", "PVector", "PSparseMatrix", "PRange", "own_to_local",
+              "ghost_to_local", "local_to_global", "global_to_local", "uniform_partition",
+              "variable_partition", "gather", "scatter", "reduction", "wait", "fetch"}
+
+
+def _strip_comments(src):
+    src = re.sub(r'"""(.*?)"""', '""', src, flags=re.S)
+    return re.sub(r"#[^\n]*", "", src)
+
+
+def test_pamghip_exports_no_partitionedarrays_name():
+    src = _strip_comments(open(JL[0]).read())
+    m = re.search(r"\bexport\b(.*?)\n(?!\s)", src, flags=re.S)
+    exported = {w.strip() for w in m.group(1).replace("\n", " ").split(",") if w.strip()}
+    assert "DeviceVector" in exported and "download_own" in exported
+    clash = exported & PA_SURFACE
+    assert not clash, f"PamgHIP exports PartitionedArrays/LinearAlgebra names: {sorted(clash)}"
+    # and defines no unqualified generic of those names either (exported or not)
+    defs = set(re.findall(r"^function\s+([A-Za-z_][\w!]*)\s*\(", src, flags=re.M))
+    defs |= set(re.findall(r"^([A-Za-z_][\w!]*)\s*\([^\n]*\)\s*=", src, flags=re.M))
+    assert not (defs & PA_SURFACE), sorted(defs & PA_SURFACE)
+
+
+def test_device_vector_is_not_an_abstract_vector():
+    """A DeviceVector lives on the GPU: the AbstractVector fallbacks (getindex per element)
+    would download it once per element."""
+    src = _strip_comments(open(JL[0]).read())
+    assert re.search(r"mutable struct DeviceVector\s*\n", src)
+    assert "DeviceVector <:" not in src
+    assert not re.search(r"Base\.getindex\(\s*v::DeviceVector", src)
+
+
+def test_extension_methods_extend_the_owning_generics():
+    """Every method the extension defines on its distributed types is a method of the owning
+    package's generic (PartitionedArrays., LinearAlgebra., Base., PamgHIP.), never a new
+    function of the same name; consistent! returns a waitable Task; no invented
+    PartitionedArrays names."""
+    src = _strip_comments(open(JL[1]).read())
+    types = ("HIPPVector", "HIPPSparseMatrix", "HIPPVCycle")
+    heads = re.findall(r"^function\s+([\w\.!]+)\s*\(([^\n]*)\)", src, flags=re.M)
+    heads += re.findall(r"^([\w\.!]+)\s*\(([^\n=]*)\)\s*=", src, flags=re.M)
+    checked = 0
+    for name, args in heads:
+        if not any(f"::{t}" in args for t in types) or name in types:
+            continue
+        checked += 1
+        assert re.match(r"^(PartitionedArrays|LinearAlgebra|Base|PamgHIP)\.", name), \
+            f"extension method {name}({args}) is not a qualified extension"
+    assert checked >= 12, checked
+    for needed in ("PartitionedArrays.consistent!", "PartitionedArrays.own_values", "PartitionedArrays.partition",
+                   "LinearAlgebra.mul!", "LinearAlgebra.dot", "LinearAlgebra.norm", "LinearAlgebra.axpy!",
+                   "LinearAlgebra.ldiv!"):
+        assert re.search(rf"^(function\s+)?{re.escape(needed)}\(", src, flags=re.M), needed
+    body = src[src.index("function PartitionedArrays.consistent!"):]
+    body = body[:body.index("\nend")]
+    assert "@async" in body
+    assert "PartitionedArrays.Future" not in src
+    # the distributed setup driver exists and uses the split-format blocks of v0.5 local matrices
+    assert re.search(r"^function HIPPVCycle\(ctxs, A::PSparseMatrix", src, flags=re.M)
+    assert "own_own_values(A)" in src and "own_ghost_values(A)" in src

@@ -93,3 +93,21 @@ def test_rcm_partition_of_a_matrix_market_file(tmp_path, built):
     assert np.array_equal(got.indptr, full.indptr) and np.array_equal(got.indices, full.indices)
     assert np.array_equal(bits(got.data), bits(full.data))
     assert np.array_equal(np.concatenate([xp[0], xp[1]]), HC.gen_xstar(0, full.shape[0], pa.hierarchy.SEED))
+
+
+def test_locality_order_auto_criterion(built):
+    """pamg_locality_order (the AMGSolver reorder): grid numberings are kept, a random
+    renumbering gets reverse Cuthill-McKee (the same order as pamg_rcm_order) and its mean row
+    span falls more than 4x; mode 0 is the identity, mode 2 always RCM; deterministic."""
+    be = pa.SequentialBackend(1)
+    for kind, n in (("poisson3d", 24), ("elastic3d", 14), ("poisson2d", 100)):
+        A, offs, xs = pa.generate_problem(be, kind, n)
+        order, before, after = HC.locality_order(A[0], 1)
+        assert order is None and before == after
+        P, _ = pa.permute_problem(A, xs, 3)
+        order, before, after = HC.locality_order(P[0], 1)
+        assert order is not None and after * 4 <= before, (kind, before, after)
+        assert np.array_equal(order, HC.rcm_order(P[0]))
+        assert np.array_equal(order, HC.locality_order(P[0], 1)[0])
+        assert HC.locality_order(P[0], 0)[0] is None
+        assert np.array_equal(HC.locality_order(A[0], 2)[0], HC.rcm_order(A[0]))

@@ -51,6 +51,9 @@ def bench(ctx, M, op, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--kind", default="poisson3d", choices=["poisson2d", "poisson3d", "aniso3d", "elastic3d"])
+    ap.add_argument("--permute", type=int, default=None, metavar="SEED",
+                    help="seeded random symmetric renumbering before setup (the irregular path)")
     ap.add_argument("--levels", type=int, default=1)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--configs", default="1024:1,1024:0",
@@ -69,7 +72,9 @@ def main():
     ctx = Context(0)
     be = pa.SequentialBackend(1)
     t = time.time()
-    A, offs, xs = pa.generate_problem(be, "poisson3d", args.n)
+    A, offs, xs = pa.generate_problem(be, args.kind, args.n)
+    if args.permute is not None:
+        A, xs = pa.permute_problem(A, xs, args.permute)
     mats = {"A0": (A[0], None)}
     if args.levels > 1:
         H = pa.build_hierarchy(be, A, offs, device=ctx)
