@@ -249,11 +249,18 @@ def main():
     spmv_gbps = spmv_bytes / (spmv_ms * 1e-3) / 1e9
     hist = S.vcycle(x, b, 1, res_hist=True)
 
+    # per-(level, op) ms: this rank's, and the max over ranks (the critical path of a step)
+    pmax = prof
+    if world > 1:
+        pmax = np.max(np.stack(be.allgather_array(prof.ravel())), axis=0).reshape(prof.shape)
     levels = [{"rows": int(H.levels[l][rank].A.nrows), "nnz": int(H.levels[l][rank].A.nnz),
-               "ms": {op: round(float(prof[l, k]), 4) for k, op in enumerate(OPS) if prof[l, k] > 0}}
+               "ms": {op: round(float(prof[l, k]), 4) for k, op in enumerate(OPS) if prof[l, k] > 0},
+               **({"ms_max_over_ranks": {op: round(float(pmax[l, k]), 4) for k, op in enumerate(OPS)
+                                         if pmax[l, k] > 0}} if world > 1 else {})}
               for l in range(S.L)]
+    exch = exchange_times(ctx, S, be, nu1, nu2) if world > 1 else None
     if rank == 0:
-        log(json.dumps({"levels": levels}))
+        log(json.dumps({"levels": levels, "exchange": exch}))
 
     # ---- CPU baseline: the oracle V-cycle on this same hierarchy (rank 0, N=1) --------
     cpu = None
@@ -268,7 +275,9 @@ def main():
     cd, tm, tn = lay["cd"], lay["tm"], lay["tile_nnz"]
     # the instance name as rocprofv3 demangles it (every template argument, defaults included)
     tf = lambda v: "true" if v else "false"  # noqa: E731
-    if tm:
+    if lay.get("sym"):
+        kname = f"k_rows_sym<2, {lay['cd_offsets']}>"
+    elif tm:
         kname = (f"k_rows_tm<2, {tn}, {cd}, {tf(lay['anchored'])}, {tf(lay['x_stage'])}, "
                  f"{tf(lay['per_tile'])}>")
     elif cd:
@@ -324,13 +333,15 @@ def main():
             "fine_spmv_traffic_GBps": spmv_traffic_gbps,
             "samples_ms_per_step": [round(t / args.steps * 1e3, 4) for t in times],
             "roofline": {
-                "kernel": kname + " (level-0 post-smoothing Jacobi"
+                "kernel": kname + (" (level-0 post-smoothing Jacobi, symmetric diagonal-class layout: "
+                                   "diagonal + upper values per row, lower values from their mirrors)"
+                                   if lay.get("sym") else " (level-0 post-smoothing Jacobi"
                           + (", tile-major slots" if tm else "")
                           + (f", {cd}-bit column dictionary" if cd else "")
                           + (", x staged in LDS" if lay.get("x_stage") else "")
                           + (", value dictionaries" if lay["vd"] else "")
                           + (", 24-bit column stream" if lay["c24"] and not cd else "")
-                          + (", 8-bit row lengths)" if lay["rl8"] else ")"),
+                          + (", 8-bit row lengths)" if lay["rl8"] else ")")),
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "frac_basis": "algorithmic bytes (SURVEY 8(d) plain CSR, 12 B/nnz) / launch time / peak",
@@ -349,6 +360,10 @@ def main():
                 "stream_ceiling": STREAM_CEILING,
             },
             "cpu_baseline": cpu,
+            # per level: rows / nonzeros of rank 0's part and ms per V-cycle per op (HIP events,
+            # eager launches; N > 1: + the max over ranks); exchange: ghost-exchange times
+            "levels": levels,
+            "exchange": exch,
             "time_to_solution": pcg,
             "setup_s": round(t_setup, 1),
             "setup_products": args.setup,
@@ -357,6 +372,45 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def exchange_times(ctx, S, be, nu1, nu2, reps=20) -> dict:
+    """N > 1: time of one ghost exchange (consistent!, synchronous, this rank's view) of every
+    level's A / R / P column plan, and the exchanges one V(nu1, nu2) cycle makes — A_l: nu1 (level
+    0) or nu1 - 1 (zero-guess first sweep on l >= 1) + 1 residual + nu2 post sweeps; R_l and P_l:
+    one each — as ms per cycle (an upper bound: each timed call syncs the stream; inside the
+    graph-replayed cycle the A exchanges overlap the interior rows). Max over ranks."""
+    from parallel_amg_amd.partitioned import PVector, consistent
+    out, total = [], 0.0
+    for l in range(S.L):
+        rec = {}
+        mats = [("A", S.A[l])] + ([("R", S.R[l]), ("P", S.P[l])] if l < S.L - 1 else [])
+        for name, M in mats:
+            if M.plan is None:
+                continue
+            v = PVector(ctx, M.plan.n_own, M.plan.n_ghost)
+            consistent(v, M.plan)
+            t = time.perf_counter()
+            for _ in range(reps):
+                consistent(v, M.plan)
+            rec[name] = (time.perf_counter() - t) / reps * 1e3
+        out.append(rec)
+    # max over ranks per (level, plan)
+    keys = [(l, k) for l in range(S.L) for k in ("A", "R", "P")]
+    mine = [out[l].get(k, 0.0) for l, k in keys]
+    allv = np.max(np.stack(be.allgather_array(np.asarray(mine, np.float64))), axis=0)
+    per = []
+    for l in range(S.L):
+        d = {k: round(float(allv[3 * l + j]), 4) for j, k in enumerate(("A", "R", "P")) if allv[3 * l + j] > 0}
+        na = (nu1 if l == 0 else nu1 - 1) + 1 + nu2 if l < S.L - 1 else 0
+        cyc = na * d.get("A", 0.0) + d.get("R", 0.0) + d.get("P", 0.0)
+        total += cyc
+        per.append({"ms_per_exchange": d, "exchanges_per_cycle": {"A": na, "R": 1 if "R" in d else 0,
+                                                                   "P": 1 if "P" in d else 0},
+                    "ms_per_cycle": round(cyc, 4)})
+    return {"per_level": per, "ms_per_cycle_upper_bound": round(total, 4),
+            "note": "synchronous consistent! per plan, max over ranks; the replicated tail's all-gather is "
+                    "inside levels[rep-1].restrict"}
 
 
 def kernel_source_sha() -> str:
@@ -394,9 +448,33 @@ def ctypes_bench_spmv(ctx, A0, x, S, reps=20) -> float:
     return ms.value
 
 
+def host_cpu_info() -> dict:
+    """Cores this process may run on (affinity set), the machine's count, OMP_NUM_THREADS, the
+    cgroup CPU quota (cpu.max, in cores) and the CPU model."""
+    info = {"affinity": len(os.sched_getaffinity(0)), "nproc": os.cpu_count(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cgroup_quota_cores": None, "cpu_model": "?"}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            info["cgroup_quota_cores"] = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/proc/cpuinfo") as f:
+            info["cpu_model"] = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    return info
+
+
 def cpu_baseline(H, xstar, ncycles, log, sweeps=(1, 1)):
-    """Time the CPU oracle's V-cycle (oracle/pamg_oracle.c, OpenMP) on the same hierarchy."""
+    """Time the CPU oracle's V-cycle (oracle/pamg_oracle.c, OpenMP) on the same hierarchy, on
+    every core of this process's affinity set (all host cores), plus the CPU
+    fine-level SpMV rate on the same algorithmic bytes as the GPU's fine_spmv_GBps."""
     from oracle import oracle as O
+    info = host_cpu_info()
+    cores = info["affinity"]
+    O.lib().orc_set_threads(cores)
     lv = [H.levels[l][0] for l in range(H.nlevels)]
     Ho = O.hierarchy_from_levels([p.A for p in lv], [p.P for p in lv[:-1]], [p.R for p in lv[:-1]],
                                  [p.omega for p in lv], H.ainv)
@@ -407,19 +485,27 @@ def cpu_baseline(H, xstar, ncycles, log, sweeps=(1, 1)):
     t = time.perf_counter()
     O.lib().orc_solve(Ho._h, x, rhs, ncycles, None)
     dt = time.perf_counter() - t
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    model = "?"
-    try:
-        with open("/proc/cpuinfo") as f:
-            model = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
-    except (OSError, StopIteration):
-        pass
-    log(f"cpu baseline: {ncycles} V-cycle(s) in {dt:.2f}s on {cores} threads ({model})")
-    return {"value": round(ncycles / dt, 5), "unit": "V-cycles/s", "cores": cores, "kind": "port",
-            "nproc": os.cpu_count(), "cpu_model": model,
+    # fine SpMV: the oracle's y = A0 x (int64 indices), reps timed; GB/s on SURVEY 8(d) bytes
+    Ao = O.CSR(A0.rowptr, A0.col.astype(np.int64), A0.val, A0.ncols)
+    y = np.empty(A0.nrows)
+    O.lib().orc_spmv(Ao.nrows, Ao.rowptr, Ao.col, Ao.val, rhs, y)  # warm
+    reps = 3
+    t = time.perf_counter()
+    for _ in range(reps):
+        O.lib().orc_spmv(Ao.nrows, Ao.rowptr, Ao.col, Ao.val, rhs, y)
+    ts = (time.perf_counter() - t) / reps
+    spmv_bytes = 12 * A0.nnz + 4 * (A0.nrows + 1) + 8 * A0.ncols + 8 * A0.nrows
+    threads = int(O.lib().orc_get_threads())
+    log(f"cpu baseline: {ncycles} V-cycle(s) in {dt:.2f}s, fine SpMV {ts * 1e3:.1f} ms on {threads} threads "
+        f"(affinity {cores}, nproc {info['nproc']}, quota {info['cgroup_quota_cores']}; {info['cpu_model']})")
+    return {"value": round(ncycles / dt, 5), "unit": "V-cycles/s", "cores": threads, "kind": "port",
+            "fine_spmv_GBps": round(spmv_bytes / ts / 1e9, 2), "fine_spmv_ms": round(ts * 1e3, 2),
+            "affinity_cores": cores, "nproc": info["nproc"], "omp_num_threads_env": info["omp_num_threads"],
+            "cgroup_quota_cores": info["cgroup_quota_cores"], "cpu_model": info["cpu_model"],
             "sample": f"{ncycles} full V-cycle(s) of the same {A0.nrows}-row hierarchy by the C "
-                      f"oracle (oracle/pamg_oracle.c, OpenMP, int64 indices); reference "
-                      f"(Julia/PartitionedArrays) not runnable: no code in /root/reference"}
+                      f"oracle (oracle/pamg_oracle.c, OpenMP on the {cores}-core affinity set, int64 "
+                      f"indices) + {reps} fine SpMVs; reference (Julia/PartitionedArrays) not runnable: "
+                      f"no code in /root/reference"}
 
 
 if __name__ == "__main__":

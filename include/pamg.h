@@ -146,7 +146,10 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * grid of the set's tile kernel), out[9] bit 0: the dictionary is anchored (offsets from each
  * row's first column) instead of row-relative; bit 1: every tile has its own table of out[4]
  * entries (per-tile dictionaries) instead of one table for the set; bit 2: the tile kernel
- * stages x in LDS (x_stage: the runs the set's offset clusters read, no x gathers). */
+ * stages x in LDS (x_stage: the runs the set's offset clusters read, no x gathers); bit 3: the
+ * set runs in the symmetric diagonal-class layout (sym_dia: diagonal + upper values per row,
+ * lower values read from their mirrors; then out[4] = the upper offset classes and out[8] =
+ * the kernel's grid). */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[10]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
@@ -212,7 +215,8 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
 /* Process-wide knobs. Applied to later pamg_mat_upload calls: "tile_nnz" (1024 | 2048 | 4096,
  * nonzero budget of a 256-row tile), "tile_order" (0 natural | 1 banded XCD-blocked), "col24",
  * "long_tiles", "row_len8", "value_dict", "col_dict", "col_dict_anchor", "col_dict_tile", "x_stage", "tm_tile_dicts" (0 | 1
- * layout features), "long_tiles_min" (1..255 nonzeros per row from which sets of >= 64 M
+ * layout features; "sym_dia": symmetric diagonal-class layout of a square operator's interior
+ * rows where they qualify), "long_tiles_min" (1..255 nonzeros per row from which sets of >= 64 M
  * nonzeros take long tiles), "band_pct" / "band_pct_restrict" (percent scale of the banded
  * order's band; the second for operators with fewer rows than columns), "tile_major" (0 | 1 where measured faster | 2 every eligible set). Applied at
  * every exchange:
@@ -234,6 +238,11 @@ int pamg_gen_xstar(int64_t i0, int64_t n, uint64_t seed, double* out);
  * pattern, general / symmetric), 1-based on disk, returned 0-based with ascending columns;
  * duplicates are summed in file order (BASELINE.json configs[4], SuiteSparse Flan_1565). */
 int pamg_read_mtx(const char* path, int64_t r0, int64_t r1, int64_t* n_global, pamg_hcsr** out);
+/* The file rows rows[0..nsel) (0-based, distinct) in that order — output row k is file row
+ * rows[k]; columns keep the file numbering, ascending. A part's own rows under a renumbering
+ * (e.g. its block of a reverse Cuthill-McKee order), without the whole matrix in memory. */
+int pamg_read_mtx_rows(const char* path, int64_t nsel, const int64_t* rows, int64_t* n_global,
+                       pamg_hcsr** out);
 /* Entries per row of a Matrix Market file (symmetric mirrored): weights for the nnz-balanced
  * row partition (SPEC §S7). counts may be NULL to query *n_global only. */
 int pamg_mtx_row_counts(const char* path, int64_t* n_global, int64_t* counts);

@@ -419,6 +419,14 @@ function read_mtx(path::AbstractString; r0::Integer = 0, r1::Integer = -1)
                 path, r0, r1, n, h))
     (HostCSR(h[]), Int(n[]))
 end
+"File rows `rows` (1-based, in that order) of a Matrix Market file, columns in the file numbering."
+function read_mtx_rows(path::AbstractString, rows::AbstractVector{<:Integer})
+    r = Int64.(rows) .- 1
+    n, h = Ref{Int64}(0), Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:pamg_read_mtx_rows, libpamg), Cint, (Cstring, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Ptr{Cvoid}}),
+                path, length(r), r, n, h))
+    (HostCSR(h[]), Int(n[]))
+end
 function mtx_row_counts(path::AbstractString)
     n = Ref{Int64}(0)
     check(ccall((:pamg_mtx_row_counts, libpamg), Cint, (Cstring, Ptr{Int64}, Ptr{Int64}), path, n, C_NULL))

@@ -45,6 +45,8 @@ def lib():
         L.orc_setup.restype = vp
         L.orc_setup.argtypes = [i64, _i64p, _i64p, _f64p, C.c_int, _i64p, dbl, C.c_int, i64, i64]
         L.orc_free.argtypes = [vp]
+        L.orc_set_threads.argtypes = [C.c_int]
+        L.orc_get_threads.restype = C.c_int
         L.orc_set_sweeps.argtypes = [vp, C.c_int, C.c_int]
         L.orc_status.argtypes = [vp]
         L.orc_nlev.argtypes = [vp]

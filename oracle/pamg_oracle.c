@@ -18,6 +18,7 @@
  * (-O2 -ffp-contract=off).
  */
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -440,6 +441,10 @@ void orc_offs_get(const ohier* h, int l, i64* offs) {
 void orc_ainv_get(const ohier* h, double* out) {
     const i64 n = h->A[h->nlev - 1].nr; memcpy(out, h->ainv, sizeof(double) * (size_t)(n * n));
 }
+
+/* OpenMP threads of the row-independent loops (bench cpu_baseline: the host's affinity set) */
+void orc_set_threads(int n) { if (n > 0) omp_set_num_threads(n); }
+int orc_get_threads(void) { return omp_get_max_threads(); }
 
 /* ------------------------------------------------------------------ V-cycle §S6 */
 

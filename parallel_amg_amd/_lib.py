@@ -93,6 +93,7 @@ SIGNATURES = {
     "pamg_gen_xstar": [i64, i64, C.c_uint64, vp],
     "pamg_read_mtx": [C.c_char_p, i64, i64, pi64, pvp],
     "pamg_mtx_row_counts": [C.c_char_p, pi64, vp],
+    "pamg_read_mtx_rows": [C.c_char_p, i64, vp, pi64, pvp],
     "pamg_rcm_order": [vp, vp],
     "pamg_locality_order": [vp, i32, vp, C.POINTER(C.c_int), pdbl, pdbl],
     "pamg_setup_gershgorin": [vp, i64, pdbl],
@@ -176,7 +177,7 @@ def layout_of(M, part_set: int = 0) -> dict:
     return {"c24": bool(out[0]), "vd": bool(out[1]), "rl8": bool(out[2]), "cd": int(out[3]),
             "cd_offsets": int(out[4]), "tm": bool(out[5]), "tm_rs": int(out[6]),
             "tile_nnz": int(out[7]), "tiles": int(out[8]), "anchored": bool(out[9] & 1), "per_tile": bool(out[9] & 2),
-            "x_stage": bool(out[9] & 4)}
+            "x_stage": bool(out[9] & 4), "sym": bool(out[9] & 8)}
 
 
 def last_error() -> str:

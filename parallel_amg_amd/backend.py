@@ -118,6 +118,16 @@ class DistributedBackend:
         self.dist.all_gather(out, self._tensor(pad), group=self.group)
         return [o.numpy()[:s].copy() for o, s in zip(out, sizes)]
 
+    def allgather_array(self, a: np.ndarray) -> list:
+        """Every rank's float64 array (any lengths), in rank order."""
+        bufs = self.allgather_bytes(np.ascontiguousarray(a, np.float64).view(np.uint8))
+        return [b.view(np.float64) for b in bufs]
+
+    def broadcast_array(self, a, dtype, root: int = 0) -> np.ndarray:
+        """Rank root's array (of dtype) on every rank; the others pass None."""
+        buf = np.ascontiguousarray(a, dtype).view(np.uint8) if self.rank == root else np.zeros(0, np.uint8)
+        return self.allgather_bytes(buf)[root].view(dtype)
+
     def exchange(self, sends: dict) -> dict:
         import torch
         me = self.rank

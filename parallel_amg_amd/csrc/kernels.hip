@@ -510,7 +510,9 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int ix = CD == 4 ? (int)((cn[j] >> (4 * e)) & 15u) : (int)((cn[j] >> (8 * e)) & 255u);
-                const int rid = (int)((rw >> (8 * e)) & 255u);
+                // past the tile's last nonzero the row byte is stale LDS: read slot 0 instead (the
+                // product is discarded), so every LDS read stays inside lxs
+                const int rid = q + e < cnt ? (int)((rw >> (8 * e)) & 255u) : 0;
                 cc[j][e] = ix;
                 xv[j][e] = lxs[ltab[ix] + rid];
             }
@@ -572,6 +574,69 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     }
     if (tid < nr) y[r0 + tid] = out;
 }
+// k_rows_sym: the symmetric diagonal-class layout (pamg::SymDia). One row per lane; every
+// operand is a coalesced stream over consecutive rows — the diagonal, the NU upper-value
+// arrays U_c[i], their mirrors U_c[i - o_c] (the lower values: the same lines a block o_c rows
+// earlier read, so L2 / Infinity-Cache hits, not HBM traffic), x[i +- o_c], b, y — with no
+// column stream, no row map and no LDS. Products are summed in ascending offset order from
+// +0.0, present entries only (mask), which is each row's storage order (checked at upload):
+// SPEC §S3 bits. Blocks walk the rows XCD-banded: block b runs on XCD b % 8 (dispatch deals
+// blocks round-robin), and XCD k takes the k-th eighth of every band of `band` rows (a grid
+// plane), so the mirror and x lines of planes z-1, z, z+1 stay in that XCD's L2.
+template <int OP, int NU>
+__global__ __launch_bounds__(kBlock) void k_rows_sym(
+    int nrows, int ncols, const uint16_t* __restrict__ mask, const double* __restrict__ dg,
+    const double* __restrict__ up, int64_t ld, const SymDia sd, const double* __restrict__ x,
+    const double* __restrict__ b, double* __restrict__ y, double omega) {
+    const int bid = blockIdx.x, tid = threadIdx.x;
+    const int xcd = bid & 7, j = bid >> 3;
+    const int plane = j / sd.eighth, blk = xcd * sd.eighth + j % sd.eighth;
+    const int64_t lo = (int64_t)plane * sd.band;
+    const int64_t i64 = lo + (int64_t)blk * kBlock + tid;
+    const int64_t hi = lo + sd.band < nrows ? lo + sd.band : nrows;
+    const bool in = blk < sd.band_blocks && i64 < hi;
+    const int i = in ? (int)i64 : 0;
+    const uint32_t m = mask[i];
+    // operands in ascending offset order: lower classes (mirrors), diagonal, upper classes
+    double v[2 * NU + 1], xv[2 * NU + 1];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+        const int o = sd.off[NU - 1 - c];
+        const int jl = i - o >= 0 ? i - o : 0;
+        v[c] = up[(size_t)(NU - 1 - c) * ld + jl];
+        xv[c] = x[jl];
+    }
+    v[NU] = dg[i];
+    xv[NU] = x[i];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+        const int ju = i + sd.off[c] < ncols ? i + sd.off[c] : i;
+        v[NU + 1 + c] = up[(size_t)c * ld + i];
+        xv[NU + 1 + c] = x[ju];
+    }
+    double pb = 0.0;
+    if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[i];
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 2 * NU + 1; ++k) {
+        const double p = v[k] * xv[k];
+        const double t = s + p;
+        s = ((m >> k) & 1u) ? t : s;
+    }
+    double out;
+    if constexpr (OP == OP_SPMV) {
+        out = s;
+    } else if constexpr (OP == OP_RESID) {
+        out = pb - s;
+    } else {
+        const double u = pb - s;
+        const double w = omega * u;
+        const double q = w / v[NU];
+        out = xv[NU] + q;
+    }
+    if (in && (m & 0x8000u)) y[i] = out;
+}
+
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_rows_long(
     const int* __restrict__ rows, const int* __restrict__ rowptr, const int* __restrict__ col,
@@ -842,9 +907,37 @@ void launch_tile(const pamg_mat& A, const TileSet& ts, const double* x, const do
     }
 }
 
+template <int OP, int NU>
+void launch_sym_nu(const pamg_mat& A, const double* x, const double* b, double* y, double omega, hipStream_t s) {
+    const SymDia& sd = A.sym;
+    const int grid = sd.nbands * 8 * sd.eighth;
+    // bound of the upper x index: the own rows (interior rows never read a ghost; rows outside
+    // the set are not stored, and must not read the ghost slots an exchange may be writing)
+    k_rows_sym<OP, NU><<<grid, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld,
+                                             sd, x, b, y, omega);
+}
+
+template <int OP>
+void launch_sym(const pamg_mat& A, const double* x, const double* b, double* y, double omega, hipStream_t s) {
+    if constexpr (OP == OP_PROLONG) {
+        return;  // square operators only (the upload never builds the layout for P)
+    } else {
+        switch (A.sym.nu) {
+            case 1: launch_sym_nu<OP, 1>(A, x, b, y, omega, s); break;
+            case 2: launch_sym_nu<OP, 2>(A, x, b, y, omega, s); break;
+            case 3: launch_sym_nu<OP, 3>(A, x, b, y, omega, s); break;
+            case 4: launch_sym_nu<OP, 4>(A, x, b, y, omega, s); break;
+            case 5: launch_sym_nu<OP, 5>(A, x, b, y, omega, s); break;
+            case 6: launch_sym_nu<OP, 6>(A, x, b, y, omega, s); break;
+            default: launch_sym_nu<OP, 7>(A, x, b, y, omega, s); break;
+        }
+    }
+}
+
 template <int OP>
 void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
                     double* y, double omega, hipStream_t s) {
+    if (ts.sym) launch_sym<OP>(A, x, b, y, omega, s);
     if (ts.n_short > 0) {
         if (ts.tile_nnz == 1024) launch_tile<OP, 1024>(A, ts, x, b, y, omega, s);
         else if (ts.tile_nnz == 4096) launch_tile<OP, 4096>(A, ts, x, b, y, omega, s);

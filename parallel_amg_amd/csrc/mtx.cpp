@@ -94,9 +94,11 @@ extern "C" int pamg_mtx_row_counts(const char* path, int64_t* n_global, int64_t*
     return PAMG_OK;
 }
 
-extern "C" int pamg_read_mtx(const char* path, int64_t r0, int64_t r1, int64_t* n_global,
-                             pamg_hcsr** out) {
-    if (!path || !out) return fail(PAMG_E_ARG, "read_mtx: bad args");
+// Rows [r0, r1) of the file (sel == NULL), or the rows sel[0..nsel) in that order (output row
+// k = file row sel[k]); columns keep the file's numbering.
+static int read_rows(const char* path, int64_t r0, int64_t r1, const int64_t* sel, int64_t nsel,
+                     int64_t* n_global, pamg_hcsr** out) {
+    if (!path || !out || (sel == nullptr && nsel != 0) || nsel < 0) return fail(PAMG_E_ARG, "read_mtx: bad args");
     Mapped m;
     m.fd = open(path, O_RDONLY);
     if (m.fd < 0) return fail(PAMG_E_ARG, "read_mtx: cannot open %s", path);
@@ -126,8 +128,25 @@ extern "C" int pamg_read_mtx(const char* path, int64_t r0, int64_t r1, int64_t* 
     const long long nz = std::strtoll(q, &q, 10);
     if (nr <= 0 || nc != nr || nz < 0) return fail(PAMG_E_ARG, "read_mtx: need a square matrix (got %lld x %lld)", nr, nc);
     if (nr >= INT32_MAX) return fail(PAMG_E_OVERFLOW, "read_mtx: n >= 2^31");
-    if (r1 < 0) r1 = nr;
-    if (r0 < 0 || r1 > nr || r0 > r1) return fail(PAMG_E_ARG, "read_mtx: bad row range");
+    // pos[file row] = output row, or -1 (selection); a range needs no table
+    std::vector<int64_t> pos;
+    if (sel) {
+        pos.assign(nr, -1);
+        for (int64_t k = 0; k < nsel; ++k) {
+            if (sel[k] < 0 || sel[k] >= nr || pos[sel[k]] >= 0)
+                return fail(PAMG_E_ARG, "read_mtx_rows: row %lld out of range or repeated", (long long)sel[k]);
+            pos[sel[k]] = k;
+        }
+        r0 = 0;
+        r1 = nsel;
+    } else {
+        if (r1 < 0) r1 = nr;
+        if (r0 < 0 || r1 > nr || r0 > r1) return fail(PAMG_E_ARG, "read_mtx: bad row range");
+    }
+    auto out_row = [&](long long i) -> long long {
+        if (sel) return pos[i];
+        return (i >= r0 && i < r1) ? i : -1;
+    };
     s = next_line(q, e);
 
     std::vector<Entry> ent;
@@ -139,8 +158,12 @@ extern "C" int pamg_read_mtx(const char* path, int64_t r0, int64_t r1, int64_t* 
         const long long j = std::strtoll(q, &q, 10) - 1;
         const double v = pattern ? 1.0 : std::strtod(q, &q);
         if (i < 0 || i >= nr || j < 0 || j >= nc) return fail(PAMG_E_ARG, "read_mtx: entry %lld out of range", k + 1);
-        if (i >= r0 && i < r1) ent.push_back({i, j, v, seq++});
-        if (symmetric && i != j && j >= r0 && j < r1) ent.push_back({j, i, v, seq++});
+        const long long oi = out_row(i);
+        if (oi >= 0) ent.push_back({sel ? oi + r0 : i, j, v, seq++});
+        if (symmetric && i != j) {
+            const long long oj = out_row(j);
+            if (oj >= 0) ent.push_back({sel ? oj + r0 : j, i, v, seq++});
+        }
         s = next_line(q, e);
     }
     std::sort(ent.begin(), ent.end(), [](const Entry& a, const Entry& b) {
@@ -163,6 +186,20 @@ extern "C" int pamg_read_mtx(const char* path, int64_t r0, int64_t r1, int64_t* 
     if (n_global) *n_global = nr;
     *out = M.release();
     return PAMG_OK;
+}
+
+extern "C" int pamg_read_mtx(const char* path, int64_t r0, int64_t r1, int64_t* n_global,
+                             pamg_hcsr** out) {
+    return read_rows(path, r0, r1, nullptr, 0, n_global, out);
+}
+
+// The rows rows[0..nsel) of the file, in that order (a part's rows under a renumbering, e.g. a
+// reverse Cuthill-McKee block: each rank stores only its own rows).
+extern "C" int pamg_read_mtx_rows(const char* path, int64_t nsel, const int64_t* rows, int64_t* n_global,
+                                  pamg_hcsr** out) {
+    if (!rows && nsel > 0) return fail(PAMG_E_ARG, "read_mtx_rows: rows is NULL");
+    static const int64_t none = 0;
+    return read_rows(path, 0, 0, rows ? rows : &none, nsel, n_global, out);
 }
 
 // ------------------------------------------------------------------ graph partitioner (RCM)

@@ -83,6 +83,9 @@ struct TileSet {
     uint8_t* d_tm_chi = nullptr;   //   high 8 bits
     uint8_t* d_tm_rlen = nullptr;
     int* d_tm_anc = nullptr;       // anchored dictionary: each row's first column (tm_rs per tile)
+    // symmetric diagonal-class layout (Options::sym_dia; interior set of a square operator,
+    // pamg_mat::sym): the set's rows run in k_rows_sym instead of tiles
+    bool sym = false;
     int max_short_len = 0;    // longest row in a short tile
     int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
@@ -108,6 +111,25 @@ struct Options {
     int x_stage = 1;           // 1: stage x runs in LDS for row-relative dictionary tile-major sets (no x gathers)
     int col_dict_anchor = 1;   // 1: anchored column dictionaries (col - row's first column) where row-relative ones do not fit
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
+    int sym_dia = 1;           // 1: symmetric diagonal-class layout for stencil-shaped symmetric operators
+};
+
+// Symmetric diagonal-class layout (k_rows_sym): a square operator whose interior rows use at
+// most 2*kSymMaxU+1 row-relative offsets {-o_NU..-o_1, 0, o_1..o_NU} (a symmetric set), each
+// row in ascending offset order, with bitwise-symmetric values a_ij == a_ji. Per own row i:
+// the diagonal D[i], the upper values U_c[i] = a(i, i+o_c) (0 where absent), and a 16-bit
+// mask (bit k: the k-th offset in ascending order is present; bit 15: the row belongs to the
+// set). A lower value a(i, i-o_c) is read from its mirror U_c[i-o_c], so the matrix streams
+// NU+1 values per row instead of 2*NU+1, with no column stream at all.
+constexpr int kSymMaxU = 7;
+struct SymDia {
+    int nu = 0;                     // upper offset classes
+    int off[kSymMaxU] = {};         // ascending positive offsets
+    int64_t ld = 0;                 // leading dimension of the U arrays
+    int band = 0, band_blocks = 0, eighth = 0, nbands = 0;  // XCD-banded block order
+    uint16_t* d_mask = nullptr;     // nrows (+ pad)
+    double* d_diag = nullptr;       // nrows (+ pad)
+    double* d_upper = nullptr;      // nu * ld
 };
 Options& options();
 
@@ -126,6 +148,10 @@ struct pamg_ctx {
     double* d_red = nullptr;  // reduction workspace (partials + result)
     int red_cap = 0;
     double* h_red = nullptr;  // pinned host scalar
+    // upload staging (runtime.hip h2d): two pinned 64 MiB buffers and their DMA-done events,
+    // created on first use on this context's device and owned by the context
+    char* stage[2] = {nullptr, nullptr};
+    hipEvent_t stage_done[2] = {nullptr, nullptr};
 };
 
 struct pamg_plan {
@@ -164,6 +190,7 @@ struct pamg_mat {
     double* d_val = nullptr;
     double* d_diag = nullptr;  // a_ii for square matrices (zero-guess Jacobi), else null
     const pamg_plan* plan = nullptr;
+    pamg::SymDia sym;        // the interior set's symmetric diagonal-class layout (TileSet::sym)
     pamg::TileSet interior;  // rows with own columns only (overlap with the exchange)
     pamg::TileSet boundary;  // rows with >= 1 ghost column
     int64_t stream_bytes = 0;  // matrix bytes one apply reads (values, columns, row pointers, tiles)

@@ -111,10 +111,9 @@ int h2d(pamg_ctx* ctx, void* dst, const void* src, size_t bytes) {
         HIPC(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
         return PAMG_OK;
     }
-    static std::mutex mu;
-    static char* stage[2] = {nullptr, nullptr};
-    static hipEvent_t done[2] = {nullptr, nullptr};
-    std::lock_guard<std::mutex> lock(mu);
+    // per context (one host thread per context, pamg.h): the events belong to ctx's device
+    char** stage = ctx->stage;
+    hipEvent_t* done = ctx->stage_done;
     for (int k = 0; k < 2; ++k) {
         if (!stage[k]) HIPC(hipHostMalloc(reinterpret_cast<void**>(&stage[k]), kChunk, hipHostMallocPortable));
         if (!done[k]) HIPC(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
@@ -151,6 +150,15 @@ struct UploadTrace {
         t = now;
     }
 };
+
+// Compute units of the current device (256 on MI355X), for occupancy-keyed layout rules
+int device_cus() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        return 256;
+    return cus;
+}
 
 // Greedy tiling of the rows listed in `rows` (ascending) into runs of consecutive rows with
 // <= kTileRows rows and <= tile_nnz nonzeros; rows above the budget become "long" rows.
@@ -227,11 +235,14 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows, bo
         int64_t nz = 0;
         for (int r : rows) nz += rp[r + 1] - rp[r];
         // >= 48 per row always; from long_tiles_min (24) per row when the set is large enough
-        // to fill the chip with 4096-nonzero tiles (>= 64 M nonzeros: 512^3 A1, 31 per row,
-        // residual -3 %, Jacobi -2 %; the 8 M-nonzero A1 of 128^3 is 9 % slower with them,
-        // profiles/r02_exp/bench_long_tiles_min_ab/)
+        // to keep the chip full with 4096-nonzero tiles: >= 32 of them per CU (512^3 A1, 31 per
+        // row, ~500 tiles per CU on one GPU and ~60 on each of 8: residual -3 %, Jacobi -2 %;
+        // the 6 M-nonzero A1 of 128^3, 6 per CU, is 9 % slower with them,
+        // profiles/r02_exp/bench_long_tiles_min_ab/). Keyed on the CU count, not on a fixed
+        // nonzero count, so a part of an 8-GPU run takes the layout one GPU takes.
         const int64_t nr = (int64_t)rows.size();
-        if (nz >= 48 * nr || (nz >= (int64_t)opt.long_tiles_min * nr && nz >= (int64_t(64) << 20))) tnnz = 4096;
+        if (nz >= 48 * nr || (nz >= (int64_t)opt.long_tiles_min * nr && nz >= int64_t(32) * 4096 * device_cus()))
+            tnnz = 4096;
     }
     ts->tile_nnz = tnnz;
     std::vector<int4> tiles;
@@ -737,6 +748,116 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
     return PAMG_OK;
 }
 
+// Symmetric diagonal-class layout of the interior rows (pamg::SymDia, k_rows_sym), when they
+// qualify: <= 2*kSymMaxU+1 distinct row-relative offsets forming a symmetric set with 0, every
+// interior row's entries in strictly ascending offset order (so the kernel's ascending sum is
+// the storage-order sum of SPEC §S3), and every lower entry bit-identical to its mirror
+// a(i-o, i) in row i-o. Otherwise nothing is built and the rows keep their tiles.
+int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci, const double* val,
+                  const std::vector<int>& inner, int64_t band) {
+    using pamg::kSymMaxU;
+    const int64_t n = A->nrows;
+    constexpr int kMaxOff = 2 * kSymMaxU + 1;
+    // distinct offsets of the interior rows (per thread, merged)
+    std::mutex mu;
+    std::vector<int> offs;
+    std::atomic<bool> too_many{false};
+    par_for((int64_t)inner.size(), [&](int64_t a, int64_t b) {
+        std::vector<int> loc;
+        for (int64_t q = a; q < b && !too_many; ++q) {
+            const int i = inner[q];
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                const int o = ci[k] - i;
+                if (std::find(loc.begin(), loc.end(), o) == loc.end()) {
+                    loc.push_back(o);
+                    if ((int)loc.size() > kMaxOff) {
+                        too_many = true;
+                        return;
+                    }
+                }
+            }
+        }
+        std::lock_guard<std::mutex> g(mu);
+        for (int o : loc)
+            if (std::find(offs.begin(), offs.end(), o) == offs.end()) offs.push_back(o);
+    });
+    if (too_many || (int)offs.size() > kMaxOff) return PAMG_OK;
+    std::sort(offs.begin(), offs.end());
+    const int no = (int)offs.size();
+    if (no % 2 == 0 || offs[no / 2] != 0) return PAMG_OK;
+    for (int k = 0; k < no; ++k)
+        if (offs[k] != -offs[no - 1 - k]) return PAMG_OK;
+    const int nu = no / 2;
+    pamg::SymDia sd;
+    sd.nu = nu;
+    for (int c = 0; c < nu; ++c) sd.off[c] = offs[nu + 1 + c];
+    sd.ld = (n + 63) / 64 * 64 + 64;
+    std::vector<uint16_t> mask(n + kVecPad, 0);
+    std::vector<double> dg(n + kVecPad, 0.0), up((size_t)nu * sd.ld, 0.0);
+    std::vector<char> in_set(n, 0);
+    for (int i : inner) in_set[i] = 1;
+    auto cls = [&](int o) { return (int)(std::lower_bound(offs.begin(), offs.end(), o) - offs.begin()); };
+    std::atomic<bool> bad{false};
+    par_for(n, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b && !bad; ++i) {
+            // every own row: diagonal and upper values (the mirrors interior rows read)
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                const int o = ci[k] - (int)i;
+                if (ci[k] >= n) continue;  // ghost column (boundary rows)
+                if (o == 0) dg[i] = val[k];
+                else if (o > 0) {
+                    const int c = cls(o);
+                    if (c < no && offs[c] == o) up[(size_t)(c - nu - 1) * sd.ld + i] = val[k];
+                }
+            }
+            if (!in_set[i]) continue;
+            uint32_t m = 0x8000u;
+            int last = -1;
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                const int o = ci[k] - (int)i;
+                const int c = cls(o);
+                if (c <= last) {  // not strictly ascending
+                    bad = true;
+                    break;
+                }
+                last = c;
+                m |= 1u << c;
+                if (o < 0) {  // the mirror a(i+o, i) must exist with the same bits
+                    const int64_t j = i + o;
+                    bool found = false;
+                    for (int64_t kk = rp[j]; kk < rp[j + 1]; ++kk)
+                        if (ci[kk] == (int)i) {
+                            found = std::memcmp(&val[kk], &val[k], sizeof(double)) == 0;
+                            break;
+                        }
+                    if (!found) {
+                        bad = true;
+                        break;
+                    }
+                }
+            }
+            mask[i] = (uint16_t)m;
+        }
+    });
+    if (bad) return PAMG_OK;
+    // XCD-banded block order (natural order: one band)
+    int64_t bd = (pamg::options().tile_order == 1 && band >= 8 * pamg::kBlock) ? band : n;
+    sd.band = (int)bd;
+    sd.band_blocks = (int)((bd + pamg::kBlock - 1) / pamg::kBlock);
+    sd.eighth = (sd.band_blocks + 7) / 8;
+    sd.nbands = (int)((n + bd - 1) / bd);
+    CHECK(dalloc(&sd.d_mask, n + kVecPad));
+    CHECK(dalloc(&sd.d_diag, n + kVecPad));
+    CHECK(dalloc(&sd.d_upper, (int64_t)nu * sd.ld));
+    CHECK(h2d(A->ctx, sd.d_mask, mask.data(), sizeof(uint16_t) * mask.size()));
+    CHECK(h2d(A->ctx, sd.d_diag, dg.data(), sizeof(double) * dg.size()));
+    CHECK(h2d(A->ctx, sd.d_upper, up.data(), sizeof(double) * up.size()));
+    A->sym = sd;
+    A->interior.sym = true;
+    A->interior.rows_short = (int64_t)inner.size();
+    return PAMG_OK;
+}
+
 void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_short);
     dfree(ts.d_long);
@@ -1076,6 +1197,10 @@ int pamg_ctx_destroy(pamg_ctx* ctx) {
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     dfree(ctx->d_red);
     if (ctx->h_red) (void)hipHostFree(ctx->h_red);
+    for (int k = 0; k < 2; ++k) {
+        if (ctx->stage[k]) (void)hipHostFree(ctx->stage[k]);
+        if (ctx->stage_done[k]) (void)hipEventDestroy(ctx->stage_done[k]);
+    }
     (void)hipEventDestroy(ctx->ev_fork);
     (void)hipEventDestroy(ctx->ev_join);
     (void)hipStreamDestroy(ctx->s_comp);
@@ -1494,6 +1619,10 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         }
     }
     tr.mark("band");
+    if (pamg::options().sym_dia && n_own_cols == nrows && has_all_diag && !inner.empty())
+        CHECK(build_sym_dia(A.get(), rp, ci, val, inner, band));
+    if (A->interior.sym) inner.clear();  // the interior rows run in k_rows_sym, not in tiles
+    tr.mark("sym dia");
     std::vector<int> rp32(nrows + 1);
     for (int64_t i = 0; i <= nrows; ++i) rp32[i] = (int)rp[i];
     CHECK(dalloc(&A->d_rowptr, nrows + 1));
@@ -1541,7 +1670,11 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     // column base with 24-bit columns); a tile-major set streams whole padded slots
     // (tile_nnz values and column entries, tm_rs row lengths per tile). + the closing pointer.
     A->stream_bytes = 4;
+    // symmetric diagonal-class layout: 16-bit mask, diagonal and nu upper values per row (the
+    // mirrored lower values are the same lines, re-read from cache)
+    if (A->interior.sym) A->stream_bytes += nrows * (2 + 8 + 8 * (int64_t)A->sym.nu);
     for (const pamg::TileSet* t : {&A->interior, &A->boundary}) {
+        if (t->sym) continue;  // counted above
         const int64_t ns = t->n_short, nz = t->nnz_short;
         int64_t b = 8 * (int64_t)t->n_long + 12 * t->nnz_long;
         const bool base = t->c24 && !t->cd;
@@ -1650,6 +1783,9 @@ int pamg_mat_destroy(pamg_mat* A) {
     dfree(A->d_anc16);
     dfree(A->d_val);
     dfree(A->d_diag);
+    dfree(A->sym.d_mask);
+    dfree(A->sym.d_diag);
+    dfree(A->sym.d_upper);
     free_tiles(A->interior);
     free_tiles(A->boundary);
     delete A;
@@ -1682,7 +1818,11 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[6] = t.tm_rs;
     out[7] = t.tile_nnz;
     out[8] = t.n_short;
-    out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0);
+    out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0);
+    if (t.sym) {  // the symmetric diagonal-class layout: upper classes, k_rows_sym's grid
+        out[4] = A->sym.nu;
+        out[8] = A->sym.nbands * 8 * A->sym.eighth;
+    }
     return PAMG_OK;
 }
 
@@ -2168,6 +2308,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "band_pct_restrict" && value >= 1 && value <= 10000) o.band_pct_restrict = (int)value;
     else if (k == "long_tiles_min" && value >= 1 && value <= 255) o.long_tiles_min = (int)value;
     else if (k == "tm_tile_dicts" && (value == 0 || value == 1)) o.tm_tile_dicts = (int)value;
+    else if (k == "sym_dia" && (value == 0 || value == 1)) o.sym_dia = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -2192,6 +2333,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "band_pct_restrict") *value = o.band_pct_restrict;
     else if (k == "long_tiles_min") *value = o.long_tiles_min;
     else if (k == "tm_tile_dicts") *value = o.tm_tile_dicts;
+    else if (k == "sym_dia") *value = o.sym_dia;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

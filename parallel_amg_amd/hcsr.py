@@ -89,6 +89,16 @@ def read_mtx(path: str, r0: int = 0, r1: int = -1):
     return HCSR(h), n.value
 
 
+def read_mtx_rows(path: str, rows: np.ndarray):
+    """File rows ``rows`` (in that order) of a Matrix Market file -> (HCSR in the file's column
+    numbering, n_global)."""
+    rows = np.ascontiguousarray(rows, np.int64)
+    h = C.c_void_p()
+    n = C.c_int64()
+    call("pamg_read_mtx_rows", str(path).encode(), len(rows), ptr(rows), C.byref(n), C.byref(h))
+    return HCSR(h), n.value
+
+
 def mtx_row_counts(path: str) -> np.ndarray:
     n = C.c_int64()
     call("pamg_mtx_row_counts", str(path).encode(), C.byref(n), None)

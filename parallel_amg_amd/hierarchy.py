@@ -254,15 +254,37 @@ def load_problem(backend, path: str, partition: str = "uniform"):
     SuiteSparse Flan_1565) and the SPEC §S2 synthetic solution x* for b = A x*. Each part reads
     only its own rows; the partition is SPEC §S7's uniform one, or nnz-balanced
     (``partition="nnz"``: equal nonzeros per part, for matrices with irregular rows), or
-    ``partition="rcm"``: every rank reads the whole matrix, renumbers it with the graph
-    partitioner (reverse Cuthill-McKee, identical on every rank) and keeps its nnz-balanced
-    block of the renumbered rows; x* is drawn in the new numbering."""
+    ``partition="rcm"``: the graph partitioner — rank 0 reads the whole matrix and computes the
+    reverse Cuthill-McKee order and the nnz-balanced blocks of the renumbered rows, broadcasts
+    them, and every rank reads only its own block's rows (pamg_read_mtx_rows) and renumbers
+    their columns; x* is drawn in the new numbering (so it differs from other partitions')."""
     if partition == "rcm":
-        M, N = H.read_mtx(path)
-        perm = H.rcm_order(M)
-        R = reorder(M, perm)
-        del M
-        return split_problem(backend, {0: R}, {0: H.gen_xstar(0, N, SEED)}, "nnz")
+        if not backend.distributed:  # every part in this process: one read, one renumbering
+            M, N = H.read_mtx(path)
+            perm = H.rcm_order(M)
+            R = reorder(M, perm)
+            del M
+            return split_problem(backend, {0: R}, {0: H.gen_xstar(0, N, SEED)}, "nnz")
+        me = backend.rank
+        perm = offs = None
+        if me == 0:
+            M, N = H.read_mtx(path)
+            perm = H.rcm_order(M)
+            offs = balanced_offsets(np.diff(M.rowptr)[perm], backend.nparts)
+            del M
+        perm = backend.broadcast_array(perm, np.int64)
+        offs = backend.broadcast_array(offs, np.int64)
+        N = len(perm)
+        inv = np.empty(N, np.int64)
+        inv[perm] = np.arange(N, dtype=np.int64)
+        Mp, _ = H.read_mtx_rows(path, perm[offs[me]:offs[me + 1]])
+        # columns into the new numbering, each row sorted ascending (as reorder() leaves them)
+        lens = np.diff(Mp.rowptr)
+        row = np.repeat(np.arange(Mp.nrows, dtype=np.int64), lens)
+        col = inv[Mp.col]
+        order = np.lexsort((col, row))
+        A = {me: HCSR.from_arrays(Mp.rowptr.copy(), col[order].astype(np.int32), Mp.val[order], N)}
+        return A, offs, {me: H.gen_xstar(int(offs[me]), int(offs[me + 1] - offs[me]), SEED)}
     head = H.read_mtx(path, 0, 0)
     N = head[1]
     if partition == "nnz" and backend.nparts > 1:

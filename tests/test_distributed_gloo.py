@@ -97,3 +97,56 @@ def test_distributed_setup_matches_oracle(world, kind, n, max_coarse, agglomerat
         p.join(timeout=60)
     for r in range(world):
         assert res.get(r) == "ok", res.get(r)
+
+
+def _rcm_worker(rank, world, port, path, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), OMP_NUM_THREADS="1")
+    import torch.distributed as dist
+
+    import parallel_amg_amd as pa
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        be = pa.DistributedBackend()
+        A, offs, xs = pa.load_problem(be, path, partition="rcm")
+        # the in-process path (whole matrix, renumbered once, split) gives the same parts
+        As, offs_s, xs_s = pa.load_problem(pa.SequentialBackend(world), path, partition="rcm")
+        assert np.array_equal(offs, offs_s)
+        a, s = A[rank], As[rank]
+        assert np.array_equal(a.rowptr, s.rowptr) and np.array_equal(a.col, s.col)
+        assert np.array_equal(a.val.view(np.int64), s.val.view(np.int64))
+        assert np.array_equal(xs[rank], xs_s[rank])
+        q.put((rank, "ok"))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_rcm_partition_reads_only_own_rows(tmp_path, built):
+    """partition="rcm" over gloo: rank 0 computes the reverse Cuthill-McKee order
+    and the nnz-balanced blocks, broadcasts them, and every rank reads only its block's rows
+    (pamg_read_mtx_rows) — the same parts as renumbering the whole matrix in one process."""
+    import scipy.io
+    import scipy.sparse as sp
+    rng = np.random.default_rng(4)
+    n = 900
+    G = sp.random(n, n, density=0.006, random_state=5, format="csr")
+    M = (G + G.T + sp.identity(n) * 10.0).tocoo()
+    path = str(tmp_path / "r.mtx")
+    scipy.io.mmwrite(path, M, symmetry="symmetric")
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rcm_worker, args=(r, world, port, path, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert res.get(r) == "ok", res.get(r)

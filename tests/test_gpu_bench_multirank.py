@@ -40,3 +40,11 @@ def test_bench_two_ranks_host_transport():
     assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1.5
     assert d["cpu_baseline"] is None  # rank 0 at N = 1 only
     assert d["final_residual"] > 0
+    # N > 1 diagnostics: per-level ms with the max over ranks, and the
+    # ghost-exchange times per level / per cycle
+    lv = d["levels"]
+    assert len(lv) == d["config"]["levels"] and lv[0]["ms"]["residual"] > 0
+    assert all(lv[l]["ms_max_over_ranks"][op] >= lv[l]["ms"][op] for l in range(len(lv)) for op in lv[l]["ms"])
+    ex = d["exchange"]
+    assert ex["per_level"][0]["exchanges_per_cycle"]["A"] == 3 and ex["per_level"][0]["ms_per_exchange"]["A"] > 0
+    assert ex["ms_per_cycle_upper_bound"] >= ex["per_level"][0]["ms_per_cycle"] > 0

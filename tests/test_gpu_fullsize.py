@@ -49,8 +49,9 @@ def test_fine_512_rowsums(ctx):
 
 def test_fine_512_layouts_agree(ctx):
     """The metric's level-0 Jacobi gives the same bits in every upload layout at full size:
-    tile-major slots + 4-bit column dictionary (default), variant 1 with the dictionary,
-    24-bit columns + 8-bit row lengths, and plain 32-bit CSR tiles."""
+    the symmetric diagonal-class layout (default), tile-major slots + 4-bit column dictionary
+    (+ x staging), variant 1 with the dictionary, 24-bit columns + 8-bit row lengths, and plain
+    32-bit CSR tiles."""
     import ctypes
     from parallel_amg_amd._lib import call, layout_of
     from parallel_amg_amd.partitioned import jacobi
@@ -62,9 +63,9 @@ def test_fine_512_layouts_agree(ctx):
     xh = rng.standard_normal(N)
     bh = rng.standard_normal(N)
     b = PVector(ctx, N, 0, bh)
-    layouts = [{}, {"tile_major": 0}, {"tile_major": 0, "col_dict": 0},
-               {"tile_major": 0, "col_dict": 0, "col24": 0, "row_len8": 0}]
-    keys = ("tile_major", "col_dict", "col24", "row_len8")
+    layouts = [{}, {"sym_dia": 0}, {"sym_dia": 0, "tile_major": 0}, {"sym_dia": 0, "tile_major": 0, "col_dict": 0},
+               {"sym_dia": 0, "tile_major": 0, "col_dict": 0, "col24": 0, "row_len8": 0}]
+    keys = ("sym_dia", "tile_major", "col_dict", "col24", "row_len8")
     old = []
     for k in keys:
         v = ctypes.c_int64()
@@ -88,8 +89,9 @@ def test_fine_512_layouts_agree(ctx):
     finally:
         for k, v in zip(keys, old):
             call("pamg_set_option", k.encode(), v)
-    assert seen[0]["tm"] and seen[0]["cd"] == 4 and not seen[1]["tm"] and seen[1]["cd"] == 4
-    assert seen[2]["cd"] == 0 and seen[2]["c24"] and not seen[3]["c24"]
+    assert seen[0]["sym"] and seen[0]["cd_offsets"] == 3
+    assert seen[1]["tm"] and seen[1]["cd"] == 4 and seen[1]["x_stage"] and not seen[2]["tm"] and seen[2]["cd"] == 4
+    assert seen[3]["cd"] == 0 and seen[3]["c24"] and not seen[4]["c24"]
 
 
 @pytest.fixture(scope="module")

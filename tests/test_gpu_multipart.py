@@ -94,6 +94,12 @@ def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, poison
     (3, "aniso3d", 16, 30, 600, 1),        # agglomerated from level 2 on
     (2, "poisson2d", 20, 1000, 0, 0),      # one level: the distributed coarsest solve
     (4, "poisson3d", 24, 60, 0, 1),        # four parts, interior parts with two neighbours
+    # eight parts (BASELINE.json configs[2]'s part count) at a size the oracle sets up in
+    # seconds: decoupled on every level and agglomerated (SPEC §S7)
+    (8, "poisson3d", 64, 1000, 0, 1),
+    (8, "poisson3d", 64, 1000, 32768, 0),
+    (8, "aniso3d", 64, 1000, 0, 1),
+    (8, "aniso3d", 64, 1000, 32768, 1),
 ])
 def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, agglomerate, poison, built):
     from oracle import oracle as O
@@ -107,7 +113,7 @@ def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, agglomerate, poi
         p.start()
     res = {}
     for _ in procs:
-        r = q.get(timeout=300)
+        r = q.get(timeout=600)
         res[r[0]] = r
     for p in procs:
         p.join(timeout=60)

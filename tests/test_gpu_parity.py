@@ -60,28 +60,31 @@ LENGTHS = {
 # (tile_nnz, tile_order, col24, value_dict, long_tiles, row_len8, col_dict, tile_major): every
 # layout the upload can produce and the kernel that runs it (kernels.hip launch_tile):
 TILE_CONFIGS = [
-    (1024, 1, 0, 0, 1, 0, 0, 0),  # k_rows_tile2, 32-bit columns + row pointers
-    (2048, 1, 0, 0, 1, 0, 0, 0),
-    (4096, 0, 0, 0, 0, 0, 0, 0),  #   natural tile order, 4096-nonzero tiles everywhere
-    (1024, 1, 1, 0, 1, 0, 0, 0),  # k_rows_tile2 <C24>
-    (1024, 1, 1, 0, 1, 1, 0, 0),  # k_rows_tile2 <C24, RL8>
-    (1024, 1, 1, 1, 1, 0, 0, 0),  # k_rows_tile2 <C24, VD> (opt-in value dictionaries)
-    (2048, 1, 1, 1, 1, 1, 0, 0),
-    (1024, 1, 1, 0, 1, 1, 1, 0),  # k_rows_tile2 <RL8, CD 4/8>
-    (1024, 1, 0, 0, 1, 0, 1, 0),  #   column dictionaries without the 24-bit stream
-    (1024, 1, 1, 0, 1, 1, 1, 1),  # default: k_rows_tm on dictionary / slot-filling sets
-    (1024, 0, 1, 0, 0, 1, 1, 1),  #   natural order, no long tiles
-    (2048, 1, 1, 0, 1, 1, 1, 1),
-    (4096, 1, 1, 0, 1, 1, 1, 1),
-    (1024, 1, 1, 0, 1, 1, 1, 2),  # k_rows_tm on every eligible set (24-bit tile-major too)
-    (1024, 1, 1, 0, 1, 0, 0, 2),  #   24-bit tile-major only
-    (4096, 1, 1, 0, 1, 1, 1, 2),
+    (1024, 1, 0, 0, 1, 0, 0, 0, 0),  # k_rows_tile2, 32-bit columns + row pointers
+    (2048, 1, 0, 0, 1, 0, 0, 0, 0),
+    (4096, 0, 0, 0, 0, 0, 0, 0, 0),  #   natural tile order, 4096-nonzero tiles everywhere
+    (1024, 1, 1, 0, 1, 0, 0, 0, 0),  # k_rows_tile2 <C24>
+    (1024, 1, 1, 0, 1, 1, 0, 0, 0),  # k_rows_tile2 <C24, RL8>
+    (1024, 1, 1, 1, 1, 0, 0, 0, 0),  # k_rows_tile2 <C24, VD> (opt-in value dictionaries)
+    (2048, 1, 1, 1, 1, 1, 0, 0, 0),
+    (1024, 1, 1, 0, 1, 1, 1, 0, 0),  # k_rows_tile2 <RL8, CD 4/8>
+    (1024, 1, 0, 0, 1, 0, 1, 0, 0),  #   column dictionaries without the 24-bit stream
+    (1024, 1, 1, 0, 1, 1, 1, 1, 1),  # default: k_rows_sym on symmetric stencils, k_rows_tm on
+    #   dictionary / slot-filling sets
+    (1024, 1, 1, 0, 1, 1, 1, 1, 0),  # the same without the symmetric layout
+    (1024, 0, 1, 0, 0, 1, 1, 1, 0),  #   natural order, no long tiles
+    (2048, 1, 1, 0, 1, 1, 1, 1, 0),
+    (4096, 1, 1, 0, 1, 1, 1, 1, 0),
+    (1024, 1, 1, 0, 1, 1, 1, 2, 0),  # k_rows_tm on every eligible set (24-bit tile-major too)
+    (1024, 1, 1, 0, 1, 0, 0, 2, 0),  #   24-bit tile-major only
+    (4096, 1, 1, 0, 1, 1, 1, 2, 0),
 ]
-OPT_KEYS = ("tile_nnz", "tile_order", "col24", "value_dict", "long_tiles", "row_len8", "col_dict", "tile_major")
+OPT_KEYS = ("tile_nnz", "tile_order", "col24", "value_dict", "long_tiles", "row_len8", "col_dict", "tile_major",
+            "sym_dia")
 
 
 @pytest.fixture(params=TILE_CONFIGS,
-                ids=lambda c: "t{}_ord{}_c24{}_vd{}_lt{}_rl{}_cd{}_tm{}".format(*c))
+                ids=lambda c: "t{}_ord{}_c24{}_vd{}_lt{}_rl{}_cd{}_tm{}_sym{}".format(*c))
 def tile_cfg(request, built):
     import ctypes
     from parallel_amg_amd._lib import call
@@ -423,6 +426,20 @@ def test_stream_bytes_layout(ctx):
             for k in opts:
                 call("pamg_set_option", k.encode(), 0 if k == "value_dict" else 1)
 
+    from parallel_amg_amd._lib import layout_of
+    # the symmetric diagonal-class layout: 2-B mask + diagonal + 3 upper values per row
+    A, _h = upload(ctx, M)
+    assert layout_of(A)["sym"] and A.stream_bytes == n * (2 + 8 + 24) + 4
+    call("pamg_set_option", b"sym_dia", 0)
+    try:
+        _stream_bytes_tiles(ctx, M, stream_bytes)
+    finally:
+        call("pamg_set_option", b"sym_dia", 1)
+
+
+def _stream_bytes_tiles(ctx, M, stream_bytes):
+    from parallel_amg_amd._lib import layout_of
+    n, nnz = M.nrows, len(M.col)
     got0 = stream_bytes(col24=0, row_len8=0, col_dict=0, tile_major=0)
     nt, rem = divmod(got0 - 12 * nnz - 4 * (n + 1), 16)
     assert rem == 0 and nt > 0
@@ -435,7 +452,6 @@ def test_stream_bytes_layout(ctx):
     assert stream_bytes(tile_major=0) == 8 * nnz + (nnz + 1) // 2 + 4 * 7 + n + 4 + 16 * nt
     # tile-major (default): whole padded slots of 1024 values + 512 B of indices + the
     # row-length slot per tile
-    from parallel_amg_amd._lib import layout_of
     A, _h = upload(ctx, M)
     lay = layout_of(A)
     assert lay["tm"] and lay["cd"] == 4 and 0 < lay["tm_rs"] <= 256 and lay["tm_rs"] % 4 == 0
@@ -660,7 +676,7 @@ def test_x_stage_bit_exact(ctx, name, x_stage):
     from parallel_amg_amd._lib import layout_of
     M, staged = _xs_case(name)
     rng = np.random.default_rng(len(name))
-    D = _with_options({"x_stage": x_stage, "tile_major": 2},
+    D = _with_options({"x_stage": x_stage, "tile_major": 2, "sym_dia": 0},
                       lambda: _layout_ops_match_oracle(ctx, M, rng))
     lay = layout_of(D)
     assert lay["tm"] and lay["cd"] in (4, 8) and not lay["anchored"], lay
@@ -812,3 +828,110 @@ def test_reorder_graph_equals_eager(ctx):
         S.vcycle(x, b, 4)
         out.append(x.own_values())
     assert np.array_equal(bits(out[0]), bits(out[1]))
+
+
+# ---------------------------------------------------------------- symmetric diagonal-class layout
+def _with_option(key, value):
+    import contextlib
+    import ctypes
+    from parallel_amg_amd._lib import call
+
+    @contextlib.contextmanager
+    def cm():
+        v = ctypes.c_int64()
+        call("pamg_get_option", key.encode(), ctypes.byref(v))
+        call("pamg_set_option", key.encode(), value)
+        try:
+            yield
+        finally:
+            call("pamg_set_option", key.encode(), v.value)
+    return cm()
+
+
+def _sym_grid(kind, n, seed=None):
+    """The SPEC grid operator, or (seed) the same pattern with random symmetric values."""
+    M = O.generate(kind, *O.grid_shape(kind, n))
+    if seed is None:
+        return M
+    import scipy.sparse as sp
+    S = sp.csr_matrix((M.val, M.col, M.rowptr), shape=(M.nrows, M.ncols))
+    R = S.copy()
+    R.data = np.random.default_rng(seed).standard_normal(R.nnz)
+    T = (R + R.T).tocsr()                       # bitwise symmetric: a + b == b + a
+    T.setdiag(np.abs(T).sum(axis=1).A1 + 1.0)
+    T.sort_indices()
+    return O.CSR(T.indptr.astype(np.int64), T.indices.astype(np.int64), T.data.copy(), M.ncols)
+
+
+@pytest.mark.parametrize("kind,n,seed", [("poisson3d", 24, None), ("poisson2d", 80, None), ("aniso3d", 20, None),
+                                         ("poisson3d", 7, None), ("poisson3d", 19, 5), ("poisson2d", 33, 6),
+                                         ("poisson3d", 40, None)])
+@pytest.mark.parametrize("order", [0, 1])
+def test_sym_dia_bit_exact(ctx, kind, n, seed, order):
+    """k_rows_sym (diagonal + upper values per row, lower values read from their mirrors, no
+    column stream): SpMV, residual and Jacobi bit-exact with the oracle, natural and XCD-banded
+    block orders."""
+    from parallel_amg_amd._lib import layout_of
+    M = _sym_grid(kind, n, seed)
+    with _with_option("tile_order", order):
+        A, _h = upload(ctx, M)
+    lay = layout_of(A)
+    assert lay["sym"] and lay["cd_offsets"] == (2 if kind == "poisson2d" else 3), lay
+    rng = np.random.default_rng(n)
+    xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
+    x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
+    mul(y, A, x)
+    assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
+    residual(y, A, x, b)
+    assert np.array_equal(bits(y.own_values()), bits(O.residual(M, xh, bh)))
+    t = PVector(ctx, M.nrows)
+    jacobi(x, A, b, t, 0.57, 2)
+    assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.57), bh, 0.57)))
+
+
+@pytest.mark.parametrize("breaker", ["asym_value", "signed_zero", "unsorted_row"])
+def test_sym_dia_declines_what_it_cannot_reproduce(ctx, breaker):
+    """A mirror that differs in one bit (or +0.0 against -0.0), or a row whose storage order is
+    not the ascending offset order, keeps the rows in tiles — still bit-exact."""
+    from parallel_amg_amd._lib import layout_of
+    M = _sym_grid("poisson3d", 12)
+    val, col = M.val.copy(), M.col.copy()
+    i = 700
+    a, e = int(M.rowptr[i]), int(M.rowptr[i + 1])
+    if breaker == "asym_value":
+        val[a] = np.nextafter(val[a], 0.0)             # a(i, i-n^2) one ulp off its mirror
+    elif breaker == "signed_zero":
+        val[a] = 0.0
+        j = int(col[a])
+        for k in range(M.rowptr[j], M.rowptr[j + 1]):
+            if col[k] == i:
+                val[k] = -0.0
+    else:
+        col[a:e] = col[a:e][::-1].copy()               # same entries, descending storage order
+        val[a:e] = val[a:e][::-1].copy()
+    M2 = O.CSR(M.rowptr.copy(), col, val, M.ncols)
+    A, _h = upload(ctx, M2)
+    assert not layout_of(A)["sym"]
+    xh = np.random.default_rng(1).standard_normal(M.nrows)
+    x, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows)
+    mul(y, A, x)
+    assert np.array_equal(bits(y.own_values()), bits(O.spmv(M2, xh)))
+
+
+def test_sym_dia_vcycle_same_bits_either_layout(ctx):
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 28)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=200))
+    out = []
+    for on in (1, 0):
+        with _with_option("sym_dia", on):
+            S = AMGSolver(ctx, H)
+        from parallel_amg_amd._lib import layout_of
+        assert layout_of(S.A[0])["sym"] == bool(on)
+        b = PVector(ctx, S.A[0].nrows, 0, xs[0])
+        x = S.new_vector()
+        h = S.vcycle(x, b, 4, res_hist=True)
+        out.append((x.own_values(), h))
+        del S
+    assert np.array_equal(bits(out[0][0]), bits(out[1][0]))
+    assert np.array_equal(bits(out[0][1]), bits(out[1][1]))
