@@ -276,7 +276,7 @@ def main():
     # the instance name as rocprofv3 demangles it (every template argument, defaults included)
     tf = lambda v: "true" if v else "false"  # noqa: E731
     if lay.get("sym"):
-        kname = f"k_rows_sym<2, {lay['cd_offsets']}>"
+        kname = f"k_rows_sym{'2' if lay['sym_rows'] == 2 else ''}<2, {lay['cd_offsets']}>"
     elif tm:
         kname = (f"k_rows_tm<2, {tn}, {cd}, {tf(lay['anchored'])}, {tf(lay['x_stage'])}, "
                  f"{tf(lay['per_tile'])}>")
@@ -473,7 +473,12 @@ def cpu_baseline(H, xstar, ncycles, log, sweeps=(1, 1)):
     fine-level SpMV rate on the same algorithmic bytes as the GPU's fine_spmv_GBps."""
     from oracle import oracle as O
     info = host_cpu_info()
+    # every core this process may use: the affinity set, capped by the cgroup CPU quota (a
+    # 256-CPU affinity under a 16-core quota runs 256 threads time-sliced on 16 cores: measured
+    # 4.5x slower than 16 threads, profiles/r03_sym/bench.log)
     cores = info["affinity"]
+    if info["cgroup_quota_cores"]:
+        cores = max(1, min(cores, int(info["cgroup_quota_cores"])))
     O.lib().orc_set_threads(cores)
     lv = [H.levels[l][0] for l in range(H.nlevels)]
     Ho = O.hierarchy_from_levels([p.A for p in lv], [p.P for p in lv[:-1]], [p.R for p in lv[:-1]],
@@ -503,7 +508,8 @@ def cpu_baseline(H, xstar, ncycles, log, sweeps=(1, 1)):
             "affinity_cores": cores, "nproc": info["nproc"], "omp_num_threads_env": info["omp_num_threads"],
             "cgroup_quota_cores": info["cgroup_quota_cores"], "cpu_model": info["cpu_model"],
             "sample": f"{ncycles} full V-cycle(s) of the same {A0.nrows}-row hierarchy by the C "
-                      f"oracle (oracle/pamg_oracle.c, OpenMP on the {cores}-core affinity set, int64 "
+                      f"oracle (oracle/pamg_oracle.c, OpenMP on {cores} threads = the affinity set capped "
+                      f"by the cgroup CPU quota, int64 "
                       f"indices) + {reps} fine SpMVs; reference (Julia/PartitionedArrays) not runnable: "
                       f"no code in /root/reference"}
 

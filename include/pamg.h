@@ -149,7 +149,9 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * stages x in LDS (x_stage: the runs the set's offset clusters read, no x gathers); bit 3: the
  * set runs in the symmetric diagonal-class layout (sym_dia: diagonal + upper values per row,
  * lower values read from their mirrors; then out[4] = the upper offset classes and out[8] =
- * the kernel's grid). */
+ * the kernel's grid); bit 4: that kernel takes two rows per lane (sym_rows 2); bit 5: the
+ * level-0 pre-smoothing sweep and residual of a V-cycle run fused in one pipelined pass
+ * (jr_fuse) on this matrix. */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[10]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
@@ -216,7 +218,8 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
  * nonzero budget of a 256-row tile), "tile_order" (0 natural | 1 banded XCD-blocked), "col24",
  * "long_tiles", "row_len8", "value_dict", "col_dict", "col_dict_anchor", "col_dict_tile", "x_stage", "tm_tile_dicts" (0 | 1
  * layout features; "sym_dia": symmetric diagonal-class layout of a square operator's interior
- * rows where they qualify), "long_tiles_min" (1..255 nonzeros per row from which sets of >= 64 M
+ * rows where they qualify; "sym_rows" 1 | 2: rows per lane of its kernel; "jr_fuse": the fused
+ * level-0 Jacobi -> residual pass of the V-cycle, read at graph capture), "long_tiles_min" (1..255 nonzeros per row from which sets of >= 64 M
  * nonzeros take long tiles), "band_pct" / "band_pct_restrict" (percent scale of the banded
  * order's band; the second for operators with fewer rows than columns), "tile_major" (0 | 1 where measured faster | 2 every eligible set). Applied at
  * every exchange:

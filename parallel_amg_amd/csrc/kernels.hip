@@ -583,9 +583,32 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
 // SPEC §S3 bits. Blocks walk the rows XCD-banded: block b runs on XCD b % 8 (dispatch deals
 // blocks round-robin), and XCD k takes the k-th eighth of every band of `band` rows (a grid
 // plane), so the mirror and x lines of planes z-1, z, z+1 stay in that XCD's L2.
+// The row mask is one byte per row where 2 NU + 1 <= 7 entries fit beside the in-set flag (bit 7;
+// the 7-point stencils), else 16 bits (flag bit 15).
+template <int NU>
+struct SymMask {
+    static constexpr bool kByte = 2 * NU + 1 <= 7;
+    static constexpr uint32_t kIn = kByte ? 0x80u : 0x8000u;
+    __device__ static uint32_t one(const uint8_t* m, int64_t i) {
+        if constexpr (kByte) return m[i];
+        else return reinterpret_cast<const uint16_t*>(m)[i];
+    }
+    __device__ static void two(const uint8_t* m, int64_t i, uint32_t (&out)[2]) {  // i even
+        if constexpr (kByte) {
+            const uint32_t w = *reinterpret_cast<const uint16_t*>(m + i);
+            out[0] = w & 0xffu;
+            out[1] = w >> 8;
+        } else {
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(m + 2 * i);
+            out[0] = w & 0xffffu;
+            out[1] = w >> 16;
+        }
+    }
+};
+
 template <int OP, int NU>
 __global__ __launch_bounds__(kBlock) void k_rows_sym(
-    int nrows, int ncols, const uint16_t* __restrict__ mask, const double* __restrict__ dg,
+    int nrows, int ncols, const uint8_t* __restrict__ mask, const double* __restrict__ dg,
     const double* __restrict__ up, int64_t ld, const SymDia sd, const double* __restrict__ x,
     const double* __restrict__ b, double* __restrict__ y, double omega) {
     const int bid = blockIdx.x, tid = threadIdx.x;
@@ -596,7 +619,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_sym(
     const int64_t hi = lo + sd.band < nrows ? lo + sd.band : nrows;
     const bool in = blk < sd.band_blocks && i64 < hi;
     const int i = in ? (int)i64 : 0;
-    const uint32_t m = mask[i];
+    const uint32_t m = SymMask<NU>::one(mask, i);
     // operands in ascending offset order: lower classes (mirrors), diagonal, upper classes
     double v[2 * NU + 1], xv[2 * NU + 1];
 #pragma unroll
@@ -634,7 +657,322 @@ __global__ __launch_bounds__(kBlock) void k_rows_sym(
         const double q = w / v[NU];
         out = xv[NU] + q;
     }
-    if (in && (m & 0x8000u)) y[i] = out;
+    if (in && (m & SymMask<NU>::kIn)) y[i] = out;
+}
+
+// Two consecutive rows per lane (Options::sym_rows = 2): the own-row streams (mask, diagonal,
+// upper values, b, x[i]) become 16-byte loads; a mirror or x run at an odd offset is not
+// 16-byte aligned and is read as two 8-byte loads (the offsets are uniform, so is the branch).
+__device__ __forceinline__ double2 ld_pair(const double* __restrict__ p, int64_t j, int64_t n, bool even) {
+    if (even && j >= 0 && j + 1 < n) return *reinterpret_cast<const double2*>(p + j);
+    return make_double2(p[j >= 0 && j < n ? j : 0], p[j + 1 >= 0 && j + 1 < n ? j + 1 : 0]);
+}
+
+template <int OP, int NU>
+__global__ __launch_bounds__(kBlock) void k_rows_sym2(
+    int nrows, int ncols, const uint8_t* __restrict__ mask, const double* __restrict__ dg,
+    const double* __restrict__ up, int64_t ld, const SymDia sd, const double* __restrict__ x,
+    const double* __restrict__ b, double* __restrict__ y, double omega) {
+    constexpr int RB = 2 * kBlock;  // rows per block
+    const int bid = blockIdx.x, tid = threadIdx.x;
+    const int xcd = bid & 7, j = bid >> 3;
+    const int plane = j / sd.eighth, blk = xcd * sd.eighth + j % sd.eighth;
+    const int64_t lo = (int64_t)plane * sd.band;
+    const int64_t i0 = lo + (int64_t)blk * RB + 2 * tid;
+    const int64_t hi = lo + sd.band < nrows ? lo + sd.band : nrows;
+    const bool blk_ok = blk < sd.band_blocks;
+    const bool in0 = blk_ok && i0 < hi, in1 = blk_ok && i0 + 1 < hi;
+    const int64_t n = nrows;
+    const int64_t ib = in0 ? i0 : 0;  // even
+    uint32_t m[2];
+    SymMask<NU>::two(mask, ib, m);
+    double v[2][2 * NU + 1], xv[2][2 * NU + 1];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+        const int o = sd.off[NU - 1 - c];
+        const double2 a = ld_pair(up + (size_t)(NU - 1 - c) * ld, ib - o, n, (o & 1) == 0);
+        const double2 xx = ld_pair(x, ib - o, ncols, (o & 1) == 0);
+        v[0][c] = a.x;
+        v[1][c] = a.y;
+        xv[0][c] = xx.x;
+        xv[1][c] = xx.y;
+    }
+    {
+        const double2 d = *reinterpret_cast<const double2*>(dg + ib);
+        const double2 xx = ld_pair(x, ib, ncols, true);
+        v[0][NU] = d.x;
+        v[1][NU] = d.y;
+        xv[0][NU] = xx.x;
+        xv[1][NU] = xx.y;
+    }
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+        const int o = sd.off[c];
+        const double2 a = *reinterpret_cast<const double2*>(up + (size_t)c * ld + ib);
+        const double2 xx = ld_pair(x, ib + o, ncols, (o & 1) == 0);
+        v[0][NU + 1 + c] = a.x;
+        v[1][NU + 1 + c] = a.y;
+        xv[0][NU + 1 + c] = xx.x;
+        xv[1][NU + 1 + c] = xx.y;
+    }
+    double2 pb = make_double2(0.0, 0.0);
+    if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = ld_pair(b, ib, n, true);
+    const double pbv[2] = {pb.x, pb.y};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 2 * NU + 1; ++k) {
+            const double p = v[r][k] * xv[r][k];
+            const double t = s + p;
+            s = ((m[r] >> k) & 1u) ? t : s;
+        }
+        double out;
+        if constexpr (OP == OP_SPMV) {
+            out = s;
+        } else if constexpr (OP == OP_RESID) {
+            out = pbv[r] - s;
+        } else {
+            const double u = pbv[r] - s;
+            const double w = omega * u;
+            const double q = w / v[r][NU];
+            out = xv[r][NU] + q;
+        }
+        if ((r == 0 ? in0 : in1) && (m[r] & SymMask<NU>::kIn)) y[ib + r] = out;
+    }
+}
+
+// ------------------------------------------------------------------ fused Jacobi -> residual
+// k_sym_jr: the level-0 pre-smoothing sweep t = x + w D^-1 (b - A x) and the residual
+// r = b - A t in ONE pass over the symmetric diagonal-class layout (Options::jr_fuse). The
+// residual of a row needs t at its neighbours, so the two are pipelined over row units of
+// kJrRows rows: a persistent grid (one 1024-thread workgroup per CU) draws items from 8 queues
+// (queue = blockIdx % 8: the blocks of one XCD under round-robin dispatch, so an item's D / U /
+// mask / b are still in that XCD's L2 when the residual of the same rows re-reads them L items
+// later; placement changes only speed). Queue k owns the k-th eighth of every band (a grid plane,
+// the layout's XCD-banded order) and interleaves: T(z, p) computes t of unit p of band z and
+// publishes it; R(z-1, u) computes r of unit u of band z-1 once the t units it reads — u-1, u,
+// u+1 of band z-1 (neighbouring queues' at eighth ends) and u of bands z-2, z — are published.
+// Hand-off (MI355X_MICROARCH.md visibility, Valid forms row 1): t is stored write-through (sc1,
+// 16-B buffer stores), every storing wave drains (s_waitcnt vmcnt(0)), a workgroup barrier,
+// then ONE lane stores the unit's flag with an agent-scope relaxed store; the consumer polls the
+// flags with agent-scope relaxed loads (sc1), a barrier, then reads t ONLY through sc1 16-B
+// buffer loads. T items never wait and R items wait only for T items issued earlier in some
+// queue (own queue: same or earlier band; neighbour queues: the same band), all workgroups are
+// co-resident (grid = CUs x 1), so the pipeline drains; every spin is bounded anyway (timeout ->
+// the error word, checked by the host). Bits: T and R evaluate exactly k_rows_sym2's Jacobi and
+// residual expressions (SPEC §S3).
+constexpr int kJrThreads = 1024;
+constexpr int kJrRows = 2 * kJrThreads;
+constexpr unsigned kJrSpinLimit = 1u << 22;
+
+__device__ __forceinline__ bool jr_decode(const JrSched& js, int t, int& kind, int& z, int& p) {
+    const int e = js.e, L = js.lag;
+    if (t >= 2 * e * js.nb) return false;
+    if (t < e) {
+        kind = 0;
+        z = 0;
+        p = t;
+        return true;
+    }
+    const int t2 = t - e, blk = 1 + t2 / (2 * e), q = t2 % (2 * e);
+    if (blk == js.nb) {
+        kind = 1;
+        z = js.nb - 1;
+        p = q;
+        return true;
+    }
+    if (q < L) {
+        kind = 0;
+        z = blk;
+        p = q;
+        return true;
+    }
+    const int w = q - L;
+    if (w < 2 * (e - L)) {
+        kind = (w & 1) ? 0 : 1;
+        z = (w & 1) ? blk : blk - 1;
+        p = (w & 1) ? L + w / 2 : w / 2;
+        return true;
+    }
+    kind = 1;
+    z = blk - 1;
+    p = e - L + (w - 2 * (e - L));
+    return true;
+}
+
+// t[j], t[j+1] for an even j through ONE sc1 16-B buffer load (out of range: zeros)
+__device__ __forceinline__ double2 jr_tpair(__amdgpu_buffer_rsrc_t rt, int64_t j) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rt, (int)(j * 8), 0, 16 /* sc1 */);
+    double2 d;
+    __builtin_memcpy(&d, &v, 16);
+    return d;
+}
+// t[j], t[j+1] for any j >= -1 (the pair(s) holding them)
+__device__ __forceinline__ double2 jr_tany(__amdgpu_buffer_rsrc_t rt, int64_t j) {
+    if ((j & 1) == 0) return jr_tpair(rt, j);
+    const double2 a = jr_tpair(rt, j - 1), c = jr_tpair(rt, j + 1);
+    return make_double2(a.y, c.x);
+}
+
+template <int NU>
+__global__ __launch_bounds__(kJrThreads) void k_sym_jr(
+    int nrows, const uint8_t* __restrict__ mask, const double* __restrict__ dg, const double* __restrict__ up,
+    int64_t ld, const SymDia sd, const JrSched js, const double* __restrict__ x, const double* __restrict__ b,
+    double* t, double* __restrict__ r, double omega, unsigned* sync, unsigned* err) {
+    __shared__ int s_item[3];
+    __shared__ int s_abort;
+    const int tid = threadIdx.x;
+    const int k = blockIdx.x & 7;
+    unsigned* head = sync + 16 * k;  // one 64-B line per queue head
+    unsigned* flags = sync + 128;
+    const int64_t n = nrows;
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc((void*)t, 0, (int)(8 * n), 0x00020000);
+    int next = 0;
+    if (tid == 0) next = (int)atomicAdd(head, 1u);
+    for (;;) {
+        if (tid == 0) {
+            int kind, z, p;
+            if (!jr_decode(js, next, kind, z, p)) {
+                s_item[0] = -1;
+            } else {
+                s_item[0] = kind;
+                s_item[1] = z;
+                s_item[2] = p;
+                next = (int)atomicAdd(head, 1u);  // the following ticket, in flight during this item
+            }
+            s_abort = 0;
+        }
+        __syncthreads();
+        const int kind = s_item[0], z = s_item[1], p = s_item[2];
+        if (kind < 0) break;
+        const int64_t g = (int64_t)z * js.ub + (int64_t)k * js.e + p;  // global unit
+        const int64_t i0 = g * kJrRows + 2 * tid;                      // even; rows i0, i0 + 1
+        uint32_t m[2];
+        SymMask<NU>::two(mask, i0, m);
+        double dv[2], uo[NU][2], pb[2];
+        {
+            const double2 d2 = *reinterpret_cast<const double2*>(dg + i0);
+            dv[0] = d2.x;
+            dv[1] = d2.y;
+            const double2 b2 = *reinterpret_cast<const double2*>(b + i0);
+            pb[0] = b2.x;
+            pb[1] = b2.y;
+        }
+#pragma unroll
+        for (int c = 0; c < NU; ++c) {
+            const double2 a = *reinterpret_cast<const double2*>(up + (size_t)c * ld + i0);
+            uo[c][0] = a.x;
+            uo[c][1] = a.y;
+        }
+        double lo[NU][2];  // mirrors U_c[i - o_c]
+#pragma unroll
+        for (int c = 0; c < NU; ++c) {
+            const int o = sd.off[c];
+            const double2 a = ld_pair(up + (size_t)c * ld, i0 - o, n, (o & 1) == 0);
+            lo[c][0] = a.x;
+            lo[c][1] = a.y;
+        }
+        // operands in ascending offset order, for rows i0 and i0 + 1
+        double v[2][2 * NU + 1], xv[2][2 * NU + 1];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+            for (int c = 0; c < NU; ++c) {
+                v[q][c] = lo[NU - 1 - c][q];
+                v[q][NU + 1 + c] = uo[c][q];
+            }
+            v[q][NU] = dv[q];
+        }
+        if (kind == 0) {
+            // ---- T: t = x + w D^-1 (b - A x), published write-through
+#pragma unroll
+            for (int c = 0; c < NU; ++c) {
+                const int o = sd.off[NU - 1 - c];
+                const double2 xl = ld_pair(x, i0 - o, n, (o & 1) == 0);
+                const double2 xu = ld_pair(x, i0 + sd.off[c], n, (sd.off[c] & 1) == 0);
+                xv[0][c] = xl.x;
+                xv[1][c] = xl.y;
+                xv[0][NU + 1 + c] = xu.x;
+                xv[1][NU + 1 + c] = xu.y;
+            }
+            const double2 xc = *reinterpret_cast<const double2*>(x + i0);
+            xv[0][NU] = xc.x;
+            xv[1][NU] = xc.y;
+            double out[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                double s = 0.0;
+#pragma unroll
+                for (int kk = 0; kk < 2 * NU + 1; ++kk) {
+                    const double pr = v[q][kk] * xv[q][kk];
+                    const double tt = s + pr;
+                    s = ((m[q] >> kk) & 1u) ? tt : s;
+                }
+                const double u = pb[q] - s;
+                const double w = omega * u;
+                const double qq = w / v[q][NU];
+                out[q] = xv[q][NU] + qq;
+            }
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 pk;
+            __builtin_memcpy(&pk, out, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(pk, rt, (int)(i0 * 8), 0, 16 /* sc1 */);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(flags + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            // ---- R: r = b - A t, after the t units it reads are published
+            if (tid == 0) {
+                const int64_t nu_tot = (int64_t)js.nb * js.ub;
+                const int64_t need[5] = {g - js.ub, g - 1, g, g + 1, g + js.ub};
+                for (int q = 0; q < 5; ++q) {
+                    if (need[q] < 0 || need[q] >= nu_tot) continue;
+                    unsigned spins = 0;
+                    while (__hip_atomic_load(flags + need[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > kJrSpinLimit) {
+                            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            s_abort = 1;
+                            break;
+                        }
+                    }
+                    if (s_abort) break;
+                }
+            }
+            __syncthreads();
+            if (!s_abort) {
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    const int o = sd.off[NU - 1 - c];
+                    const double2 tl = jr_tany(rt, i0 - o);
+                    const double2 tu = jr_tany(rt, i0 + sd.off[c]);
+                    xv[0][c] = tl.x;
+                    xv[1][c] = tl.y;
+                    xv[0][NU + 1 + c] = tu.x;
+                    xv[1][NU + 1 + c] = tu.y;
+                }
+                const double2 tc = jr_tpair(rt, i0);
+                xv[0][NU] = tc.x;
+                xv[1][NU] = tc.y;
+                double out[2];
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    double s = 0.0;
+#pragma unroll
+                    for (int kk = 0; kk < 2 * NU + 1; ++kk) {
+                        const double pr = v[q][kk] * xv[q][kk];
+                        const double tt = s + pr;
+                        s = ((m[q] >> kk) & 1u) ? tt : s;
+                    }
+                    out[q] = pb[q] - s;
+                }
+                *reinterpret_cast<double2*>(r + i0) = make_double2(out[0], out[1]);
+            }
+        }
+        __syncthreads();  // s_item / s_abort are rewritten by the next item
+    }
 }
 
 template <int OP>
@@ -911,6 +1249,11 @@ template <int OP, int NU>
 void launch_sym_nu(const pamg_mat& A, const double* x, const double* b, double* y, double omega, hipStream_t s) {
     const SymDia& sd = A.sym;
     const int grid = sd.nbands * 8 * sd.eighth;
+    if (sd.rpl == 2) {
+        k_rows_sym2<OP, NU><<<grid, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper,
+                                                  sd.ld, sd, x, b, y, omega);
+        return;
+    }
     // bound of the upper x index: the own rows (interior rows never read a ghost; rows outside
     // the set are not stored, and must not read the ghost slots an exchange may be writing)
     k_rows_sym<OP, NU><<<grid, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld,
@@ -948,6 +1291,20 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
                                                      b, y, omega);
 }
 }  // namespace
+
+void launch_sym_jr(const pamg_mat& A, const double* x, const double* b, double* t, double* r, double omega,
+                   unsigned* sync, size_t sync_bytes, unsigned* err, int grid, hipStream_t s) {
+    const SymDia& sd = A.sym;
+    (void)hipMemsetAsync(sync, 0, sync_bytes, s);
+    switch (sd.nu) {
+        case 1: k_sym_jr<1><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, sd.jr,
+                                                        x, b, t, r, omega, sync, err); break;
+        case 2: k_sym_jr<2><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, sd.jr,
+                                                        x, b, t, r, omega, sync, err); break;
+        default: k_sym_jr<3><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, sd.jr,
+                                                          x, b, t, r, omega, sync, err); break;
+    }
+}
 
 void launch_rows(const pamg_mat& A, const TileSet& ts, int op, const double* x, const double* b,
                  const double* /*xold*/, double* y, double omega, hipStream_t s) {

@@ -112,6 +112,8 @@ struct Options {
     int col_dict_anchor = 1;   // 1: anchored column dictionaries (col - row's first column) where row-relative ones do not fit
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
     int sym_dia = 1;           // 1: symmetric diagonal-class layout for stencil-shaped symmetric operators
+    int sym_rows = 2;          // rows per lane of its kernel (1 | 2)
+    int jr_fuse = 1;           // 1: fused level-0 pre-smoothing Jacobi + residual where the layout allows
 };
 
 // Symmetric diagonal-class layout (k_rows_sym): a square operator whose interior rows use at
@@ -120,14 +122,30 @@ struct Options {
 // the diagonal D[i], the upper values U_c[i] = a(i, i+o_c) (0 where absent), and a 16-bit
 // mask (bit k: the k-th offset in ascending order is present; bit 15: the row belongs to the
 // set). A lower value a(i, i-o_c) is read from its mirror U_c[i-o_c], so the matrix streams
-// NU+1 values per row instead of 2*NU+1, with no column stream at all.
+// NU+1 values per row instead of 2*NU+1, with no column stream at all. (Where 2*NU+1 <= 7 the
+// mask is one byte, the set flag in bit 7.)
 constexpr int kSymMaxU = 7;
+// Schedule of the fused Jacobi -> residual kernel (kernels.hip k_sym_jr): units of 2048 rows,
+// ub per band, e per queue (XCD eighth) per band, nb bands, R items lag T items by `lag` units.
+struct JrSched {
+    int ub = 0, e = 0, nb = 0, lag = 0;
+};
 struct SymDia {
     int nu = 0;                     // upper offset classes
     int off[kSymMaxU] = {};         // ascending positive offsets
     int64_t ld = 0;                 // leading dimension of the U arrays
     int band = 0, band_blocks = 0, eighth = 0, nbands = 0;  // XCD-banded block order
-    uint16_t* d_mask = nullptr;     // nrows (+ pad)
+    int rpl = 1;                    // rows per lane (k_rows_sym / k_rows_sym2)
+    // fused Jacobi -> residual (Options::jr_fuse; one part, every row in the set, 2 nu + 1 <= 7,
+    // bands of a multiple of 8 x 2048 rows, every offset < 2048 or = the band)
+    bool jr_ok = false;
+    JrSched jr;
+    unsigned* d_jr_sync = nullptr;  // queue heads (8 lines) + one flag per unit; zeroed per launch
+    size_t jr_sync_bytes = 0;
+    unsigned* d_jr_err = nullptr;   // set by a timed-out spin; checked by the host
+    int jr_grid = 0;
+    uint8_t* d_mask = nullptr;      // nrows (+ pad) masks of 1 byte (2 nu + 1 <= 7) or 2 bytes
+    int mask_bytes = 2;
     double* d_diag = nullptr;       // nrows (+ pad)
     double* d_upper = nullptr;      // nu * ld
 };
@@ -207,6 +225,9 @@ void launch_dense_gemv(int64_t n_rows, int64_t n_cols, int64_t row0, const doubl
                        const double* b, double* y, hipStream_t s);
 void launch_pack(int64_t n, const int* idx, const double* x, double* out, hipStream_t s);
 void launch_fill(int64_t n, double v, double* y, hipStream_t s);
+// t = Jacobi(x), r = b - A t in one launch (k_sym_jr; A.sym.jr_ok)
+void launch_sym_jr(const pamg_mat& A, const double* x, const double* b, double* t, double* r, double omega,
+                   unsigned* sync, size_t sync_bytes, unsigned* err, int grid, hipStream_t s);
 // dst[i] = src[perm[i]] (gather), or dst[perm[i]] = src[i] (scatter)
 void launch_permute(int64_t n, const int* perm, const double* src, double* dst, bool scatter, hipStream_t s);
 void launch_axpby(int64_t n, double a, const double* x, double b, double* y, hipStream_t s);

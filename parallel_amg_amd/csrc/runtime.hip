@@ -792,6 +792,8 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
     sd.nu = nu;
     for (int c = 0; c < nu; ++c) sd.off[c] = offs[nu + 1 + c];
     sd.ld = (n + 63) / 64 * 64 + 64;
+    const int mb = 2 * nu + 1 <= 7 ? 1 : 2;  // mask bytes per row (kernels.hip SymMask)
+    const uint32_t in_flag = mb == 1 ? 0x80u : 0x8000u;
     std::vector<uint16_t> mask(n + kVecPad, 0);
     std::vector<double> dg(n + kVecPad, 0.0), up((size_t)nu * sd.ld, 0.0);
     std::vector<char> in_set(n, 0);
@@ -811,7 +813,7 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
                 }
             }
             if (!in_set[i]) continue;
-            uint32_t m = 0x8000u;
+            uint32_t m = in_flag;
             int last = -1;
             for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
                 const int o = ci[k] - (int)i;
@@ -843,15 +845,45 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
     // XCD-banded block order (natural order: one band)
     int64_t bd = (pamg::options().tile_order == 1 && band >= 8 * pamg::kBlock) ? band : n;
     sd.band = (int)bd;
-    sd.band_blocks = (int)((bd + pamg::kBlock - 1) / pamg::kBlock);
+    sd.rpl = pamg::options().sym_rows;
+    const int64_t rows_per_block = (int64_t)pamg::kBlock * sd.rpl;
+    sd.band_blocks = (int)((bd + rows_per_block - 1) / rows_per_block);
     sd.eighth = (sd.band_blocks + 7) / 8;
     sd.nbands = (int)((n + bd - 1) / bd);
-    CHECK(dalloc(&sd.d_mask, n + kVecPad));
+    sd.mask_bytes = mb;
+    CHECK(dalloc(&sd.d_mask, (n + kVecPad) * mb));
     CHECK(dalloc(&sd.d_diag, n + kVecPad));
     CHECK(dalloc(&sd.d_upper, (int64_t)nu * sd.ld));
-    CHECK(h2d(A->ctx, sd.d_mask, mask.data(), sizeof(uint16_t) * mask.size()));
+    if (mb == 1) {
+        std::vector<uint8_t> m8(mask.begin(), mask.end());
+        CHECK(h2d(A->ctx, sd.d_mask, m8.data(), m8.size()));
+    } else {
+        CHECK(h2d(A->ctx, sd.d_mask, mask.data(), sizeof(uint16_t) * mask.size()));
+    }
     CHECK(h2d(A->ctx, sd.d_diag, dg.data(), sizeof(double) * dg.size()));
     CHECK(h2d(A->ctx, sd.d_upper, up.data(), sizeof(double) * up.size()));
+    // fused Jacobi -> residual schedule (kernels.hip k_sym_jr): one part with every row in the
+    // set, byte masks, bands of whole 8 x 2048-row eighths, every offset inside a unit's
+    // neighbours or exactly one band, byte offsets within int32 (buffer descriptors)
+    {
+        constexpr int64_t kUnit = 2048;
+        bool ok = A->ncols == n && (int64_t)inner.size() == n && mb == 1 && bd % (8 * kUnit) == 0 &&
+                  n % bd == 0 && 8 * (n + 64) < INT32_MAX;
+        for (int c = 0; c < nu && ok; ++c) ok = sd.off[c] < kUnit || sd.off[c] == bd;
+        if (ok) {
+            sd.jr.ub = (int)(bd / kUnit);
+            sd.jr.e = sd.jr.ub / 8;
+            sd.jr.nb = (int)(n / bd);
+            sd.jr.lag = std::min(4, sd.jr.e);
+            const int64_t words = 128 + (int64_t)sd.jr.nb * sd.jr.ub;
+            sd.jr_sync_bytes = (size_t)((words * 4 + 15) / 16 * 16);
+            CHECK(dalloc(reinterpret_cast<char**>(&sd.d_jr_sync), (int64_t)sd.jr_sync_bytes));
+            CHECK(dalloc(&sd.d_jr_err, 4));
+            HIPC(hipMemset(sd.d_jr_err, 0, 16));
+            sd.jr_grid = std::max(8, device_cus() / 8 * 8);
+            sd.jr_ok = true;
+        }
+    }
     A->sym = sd;
     A->interior.sym = true;
     A->interior.rows_short = (int64_t)inner.size();
@@ -1112,7 +1144,16 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false)
     for (int l = 0; l < L - 1; ++l) {
         const pamg_mat* A = H->A[l];
         double *c = H->t[l], *o = H->r[l];
-        {
+        // level 0, V(1, nu2) from a given guess: the pre-smoothing sweep and the residual in one
+        // pipelined pass (k_sym_jr; both timed as jacobi_pre)
+        const bool fuse = l == 0 && !zero0 && H->nu1 == 1 && pamg::options().jr_fuse && A->interior.sym &&
+                          A->sym.jr_ok && !(A->plan && !A->plan->nbr.empty());
+        if (fuse) {
+            ProfScope p(H, l, 0, s);
+            pamg::launch_sym_jr(*A, H->x[0], H->b[0], c, o, H->omega[0], A->sym.d_jr_sync, A->sym.jr_sync_bytes,
+                                A->sym.d_jr_err, A->sym.jr_grid, s);
+            HIPC(hipGetLastError());
+        } else {
             ProfScope p(H, l, 0, s);
             if (l == 0 && !zero0)
                 CHECK(apply(ctx, A, pamg::OP_JACOBI, H->x[0], H->b[0], c, H->omega[0]));
@@ -1125,7 +1166,7 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false)
         }
         cur[l] = c;
         spare[l] = o;
-        {
+        if (!fuse) {
             ProfScope p(H, l, 1, s);
             CHECK(apply(ctx, A, pamg::OP_RESID, c, H->b[l], o, 0.0));
         }
@@ -1670,9 +1711,9 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     // column base with 24-bit columns); a tile-major set streams whole padded slots
     // (tile_nnz values and column entries, tm_rs row lengths per tile). + the closing pointer.
     A->stream_bytes = 4;
-    // symmetric diagonal-class layout: 16-bit mask, diagonal and nu upper values per row (the
+    // symmetric diagonal-class layout: 8/16-bit mask, diagonal and nu upper values per row (the
     // mirrored lower values are the same lines, re-read from cache)
-    if (A->interior.sym) A->stream_bytes += nrows * (2 + 8 + 8 * (int64_t)A->sym.nu);
+    if (A->interior.sym) A->stream_bytes += nrows * (A->sym.mask_bytes + 8 + 8 * (int64_t)A->sym.nu);
     for (const pamg::TileSet* t : {&A->interior, &A->boundary}) {
         if (t->sym) continue;  // counted above
         const int64_t ns = t->n_short, nz = t->nnz_short;
@@ -1786,6 +1827,8 @@ int pamg_mat_destroy(pamg_mat* A) {
     dfree(A->sym.d_mask);
     dfree(A->sym.d_diag);
     dfree(A->sym.d_upper);
+    if (A->sym.d_jr_sync) (void)hipFree(A->sym.d_jr_sync);
+    dfree(A->sym.d_jr_err);
     free_tiles(A->interior);
     free_tiles(A->boundary);
     delete A;
@@ -1818,7 +1861,8 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[6] = t.tm_rs;
     out[7] = t.tile_nnz;
     out[8] = t.n_short;
-    out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0);
+    out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
+             (t.sym && A->sym.jr_ok ? 32 : 0);
     if (t.sym) {  // the symmetric diagonal-class layout: upper classes, k_rows_sym's grid
         out[4] = A->sym.nu;
         out[8] = A->sym.nbands * 8 * A->sym.eighth;
@@ -2171,6 +2215,18 @@ struct DeviceSpace {
     }
 };
 
+// A timed-out spin of the fused Jacobi -> residual kernel (never expected: its queues drain by
+// construction) leaves the error word set; the synchronous entry points report it.
+static int check_jr_err(pamg_hier* H) {
+    const pamg_mat* A0 = H->A[0];
+    if (!A0->sym.d_jr_err) return PAMG_OK;
+    unsigned e = 0;
+    HIPC(hipMemcpy(&e, A0->sym.d_jr_err, sizeof(unsigned), hipMemcpyDeviceToHost));
+    if (e) return fail(PAMG_E_STATE, "vcycle: the fused Jacobi-residual kernel timed out waiting for a unit "
+                                     "(set option jr_fuse=0)");
+    return PAMG_OK;
+}
+
 static int vcycle_common(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles) {
     if (!ctx || !H || !x || !b || ncycles < 0 || H->ctx != ctx) return fail(PAMG_E_ARG, "vcycle: bad args");
     const pamg_mat* A0 = H->A[0];
@@ -2193,7 +2249,7 @@ int pamg_vcycle(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int
     if (!res_hist) {
         CHECK(vcycle_common(ctx, H, x, b, ncycles));
         HIPC(hipStreamSynchronize(ctx->s_comp));
-        return PAMG_OK;
+        return check_jr_err(H);
     }
     if (!ctx || !H || !x || !b || ncycles < 0 || H->ctx != ctx) return fail(PAMG_E_ARG, "vcycle: bad args");
     if (H->L < 1 || (!H->t[0] && H->L > 1)) return fail(PAMG_E_ARG, "vcycle: bad hierarchy");
@@ -2219,7 +2275,7 @@ int pamg_vcycle(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int
     }
     d.finish(x);
     HIPC(hipStreamSynchronize(ctx->s_comp));
-    return PAMG_OK;
+    return check_jr_err(H);
 }
 
 // Preconditioned CG with one V-cycle from a zero guess as M^-1 (SPEC §S8). The V(1,1) cycle
@@ -2309,6 +2365,8 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "long_tiles_min" && value >= 1 && value <= 255) o.long_tiles_min = (int)value;
     else if (k == "tm_tile_dicts" && (value == 0 || value == 1)) o.tm_tile_dicts = (int)value;
     else if (k == "sym_dia" && (value == 0 || value == 1)) o.sym_dia = (int)value;
+    else if (k == "sym_rows" && (value == 1 || value == 2)) o.sym_rows = (int)value;
+    else if (k == "jr_fuse" && (value == 0 || value == 1)) o.jr_fuse = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -2334,6 +2392,8 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "long_tiles_min") *value = o.long_tiles_min;
     else if (k == "tm_tile_dicts") *value = o.tm_tile_dicts;
     else if (k == "sym_dia") *value = o.sym_dia;
+    else if (k == "sym_rows") *value = o.sym_rows;
+    else if (k == "jr_fuse") *value = o.jr_fuse;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

@@ -427,9 +427,9 @@ def test_stream_bytes_layout(ctx):
                 call("pamg_set_option", k.encode(), 0 if k == "value_dict" else 1)
 
     from parallel_amg_amd._lib import layout_of
-    # the symmetric diagonal-class layout: 2-B mask + diagonal + 3 upper values per row
+    # the symmetric diagonal-class layout: 1-B mask + diagonal + 3 upper values per row
     A, _h = upload(ctx, M)
-    assert layout_of(A)["sym"] and A.stream_bytes == n * (2 + 8 + 24) + 4
+    assert layout_of(A)["sym"] and A.stream_bytes == n * (1 + 8 + 24) + 4
     call("pamg_set_option", b"sym_dia", 0)
     try:
         _stream_bytes_tiles(ctx, M, stream_bytes)
@@ -849,8 +849,17 @@ def _with_option(key, value):
 
 
 def _sym_grid(kind, n, seed=None):
-    """The SPEC grid operator, or (seed) the same pattern with random symmetric values."""
-    M = O.generate(kind, *O.grid_shape(kind, n))
+    """The SPEC grid operator, or (seed) the same pattern with random symmetric values;
+    "p9": the 2D 9-point pattern (9 offsets: 16-bit row masks)."""
+    if kind == "p9":
+        import scipy.sparse as sp
+        t = sp.diags([1.0, 1.0, 1.0], [-1, 0, 1], shape=(n, n))
+        P = sp.kron(t, t).tocsr()
+        P.sort_indices()
+        M = O.CSR(P.indptr.astype(np.int64), P.indices.astype(np.int64), P.data.copy(), n * n)
+        seed = 9 if seed is None else seed
+    else:
+        M = O.generate(kind, *O.grid_shape(kind, n))
     if seed is None:
         return M
     import scipy.sparse as sp
@@ -865,18 +874,19 @@ def _sym_grid(kind, n, seed=None):
 
 @pytest.mark.parametrize("kind,n,seed", [("poisson3d", 24, None), ("poisson2d", 80, None), ("aniso3d", 20, None),
                                          ("poisson3d", 7, None), ("poisson3d", 19, 5), ("poisson2d", 33, 6),
-                                         ("poisson3d", 40, None)])
+                                         ("poisson3d", 40, None), ("p9", 45, None)])
 @pytest.mark.parametrize("order", [0, 1])
-def test_sym_dia_bit_exact(ctx, kind, n, seed, order):
-    """k_rows_sym (diagonal + upper values per row, lower values read from their mirrors, no
-    column stream): SpMV, residual and Jacobi bit-exact with the oracle, natural and XCD-banded
-    block orders."""
+@pytest.mark.parametrize("rows", [1, 2])
+def test_sym_dia_bit_exact(ctx, kind, n, seed, order, rows):
+    """k_rows_sym / k_rows_sym2 (diagonal + upper values per row, lower values read from their
+    mirrors, no column stream; one or two rows per lane): SpMV, residual and Jacobi bit-exact
+    with the oracle, natural and XCD-banded block orders, odd and even row counts."""
     from parallel_amg_amd._lib import layout_of
     M = _sym_grid(kind, n, seed)
-    with _with_option("tile_order", order):
+    with _with_option("tile_order", order), _with_option("sym_rows", rows):
         A, _h = upload(ctx, M)
     lay = layout_of(A)
-    assert lay["sym"] and lay["cd_offsets"] == (2 if kind == "poisson2d" else 3), lay
+    assert lay["sym"] and lay["cd_offsets"] == {"poisson2d": 2, "p9": 4}.get(kind, 3), lay
     rng = np.random.default_rng(n)
     xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
     x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
@@ -935,3 +945,35 @@ def test_sym_dia_vcycle_same_bits_either_layout(ctx):
         del S
     assert np.array_equal(bits(out[0][0]), bits(out[1][0]))
     assert np.array_equal(bits(out[0][1]), bits(out[1][1]))
+
+
+@pytest.mark.parametrize("kind,n", [("poisson3d", 128), ("aniso3d", 128)])
+def test_fused_jacobi_residual_bit_exact(ctx, kind, n):
+    """jr_fuse: the level-0 pre-smoothing sweep and residual pipelined in one persistent
+    kernel (t handed between workgroups write-through) give the unfused cycle's bits — x and
+    the residual history — and the oracle's."""
+    from parallel_amg_amd._lib import layout_of
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, kind, n)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=ctx)
+    S = AMGSolver(ctx, H)
+    assert layout_of(S.A[0])["jr_fused"]
+    b = PVector(ctx, S.A[0].nrows)
+    mul(b, S.A[0], PVector(ctx, S.A[0].nrows, 0, xs[0]))
+    out = []
+    for fuse in (1, 0):
+        with _with_option("jr_fuse", fuse):
+            S.set_graph(False)   # re-capture with the option (read at capture)
+            S.set_graph(True)
+            x = S.new_vector()
+            h = S.vcycle(x, b, 3, res_hist=True)
+            x2 = S.new_vector()
+            S.vcycle(x2, b, 3)    # graph replay
+            out.append((x.own_values(), h, x2.own_values()))
+    assert np.array_equal(bits(out[0][0]), bits(out[1][0]))
+    assert np.array_equal(bits(out[0][1]), bits(out[1][1]))
+    assert np.array_equal(bits(out[0][2]), bits(out[0][0]))
+    Ao = O.generate(kind, n, n, n)
+    Ho = O.setup(Ao, max_coarse=1000)
+    xo, ho = Ho.solve(O.spmv(Ao, O.xstar(Ao.nrows)), 3, res_hist=True)
+    assert np.array_equal(bits(out[0][0]), bits(xo))

@@ -24,6 +24,9 @@ timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o write --ou
     -- python3 -u $KB > "$OUT/pmc_write.jsonl" 2> "$OUT/pmc_write.err"
 echo "write pass done"
 mkdir -p "$OUT/pmc"
-python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --kernel "k_rows_tm<2" > "$OUT/pmc/traffic_jacobi.json"
-python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --kernel "k_rows_tm<0" > "$OUT/pmc/traffic_spmv.json"
+# the level-0 kernel of the default layout: the symmetric diagonal-class kernel (r03; the
+# tile-major one before)
+K=${PMCKERNEL:-k_rows_sym2}
+python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --kernel "$K<2" > "$OUT/pmc/traffic_jacobi.json"
+python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --kernel "$K<0" > "$OUT/pmc/traffic_spmv.json"
 echo "traffic records in $OUT/pmc (copy to profiles/pmc/ to let bench.py report them)"
