@@ -248,6 +248,7 @@ def main():
     spmv_bytes = S.csr_bytes(A0, 0)
     spmv_gbps = spmv_bytes / (spmv_ms * 1e-3) / 1e9
     hist = S.vcycle(x, b, 1, res_hist=True)
+    fused = fused_times(ctx, S, A0, x, b) if world == 1 and _lib.layout_of(A0).get("jr_fused") else None
 
     # per-(level, op) ms: this rank's, and the max over ranks (the critical path of a step)
     pmax = prof
@@ -327,6 +328,8 @@ def main():
                 "reordered_levels": S.reordered,
                 "options": list(args.set),
             },
+            # level-0 fused passes (Options::jr_fuse) beside the separate sweeps they replace
+            "fused_level0": fused,
             "fine_spmv_GBps": round(spmv_gbps, 1),
             "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
             # HBM bytes actually moved (PMC record of this kernel/layout/source) per second
@@ -421,6 +424,47 @@ def kernel_source_sha() -> str:
 
 STREAM_CEILING = {"mix11to1_GBps": 5104.0, "read_GBps": 6311.0,
                   "source": "profiles/r02_exp/stream_ceiling.jsonl (tools/stream_ceiling.hip, 8 GiB, best grid)"}
+
+
+def fused_times(ctx, S, A0, x, b, reps=10):
+    """ms of the level-0 fused passes: k_sym_jr (Jacobi -> residual, through pamg_jacobi_residual,
+    synchronous calls) and the pipeline's k_sym_chain (post -> pre -> residual, HIP events), with
+    the separate sweeps they replace measured the same way."""
+    from parallel_amg_amd.partitioned import jacobi_residual, residual
+    from parallel_amg_amd import _lib
+    t, r, xx = S.new_vector(), S.new_vector(), S.new_vector()
+
+    def per_call(fn):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    out = {"jacobi_residual_fused_ms": round(per_call(lambda: jacobi_residual(t, r, A0, x, b, 0.66)), 4)}
+    with option("jr_fuse", 0):
+        out["jacobi_then_residual_ms"] = round(per_call(lambda: (jacobi_residual(t, r, A0, x, b, 0.66))), 4)
+    out["residual_ms"] = round(per_call(lambda: residual(r, A0, t, b)), 4)
+    ch = S.bench_chain(xx, b, reps)
+    out["chain3_ms"] = round(ch, 4) if ch is not None else None
+    return out
+
+
+def option(name, value):
+    import contextlib
+
+    from parallel_amg_amd import _lib
+
+    @contextlib.contextmanager
+    def cm():
+        old = ctypes.c_int64()
+        _lib.call("pamg_get_option", name.encode(), ctypes.byref(old))
+        _lib.call("pamg_set_option", name.encode(), int(value))
+        try:
+            yield
+        finally:
+            _lib.call("pamg_set_option", name.encode(), old.value)
+    return cm()
 
 
 def pmc_lookup(fname, kname, tiles, workload_key, src):

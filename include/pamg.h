@@ -162,6 +162,12 @@ int pamg_residual(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec*
 /* nsweeps weighted-Jacobi sweeps on x (tmp is the ping-pong buffer; result in x). */
 int pamg_jacobi(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec* b,
                 pamg_vec* tmp, double omega, int nsweeps);
+/* One weighted-Jacobi sweep and the residual of its result: t = x + omega D^-1 (b - A x),
+ * r = b - A t (the level-0 pre-smoothing + residual of a V-cycle). On one part in the symmetric
+ * layout with jr_fuse on, both run in one pipelined pass (*fused = 1); otherwise two sweeps.
+ * The bits are the same either way. fused may be NULL. */
+int pamg_jacobi_residual(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec* b,
+                         pamg_vec* t, pamg_vec* r, double omega, int* fused);
 
 /* ------------------------------------------------------------------ hierarchy / V-cycle */
 /* Levels 0..nlevels-1; P[l], R[l] for l < nlevels-1 (NULL entries otherwise). The coarsest
@@ -213,6 +219,12 @@ int pamg_hier_profile_read(pamg_hier* H, double* ms_per_level_op /* nlevels*6 */
  * launch in ms measured with HIP events on the launch stream. */
 int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, const pamg_vec* b,
                      pamg_vec* y, double omega, int reps, double* avg_ms);
+
+/* Micro-benchmark hook of the cross-cycle pipeline: `reps` launches of its level-0 chain kernel
+ * (post-smoothing -> next pre-smoothing -> residual, k_sym_chain) on the hierarchy's own level-0
+ * buffers and the given x / b (x is overwritten); average ms per launch (HIP events).
+ * PAMG_E_STATE when the hierarchy does not qualify (one part, V(1,1), symmetric level 0). */
+int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps, double* avg_ms);
 
 /* Process-wide knobs. Applied to later pamg_mat_upload calls: "tile_nnz" (1024 | 2048 | 4096,
  * nonzero budget of a 256-row tile), "tile_order" (0 natural | 1 banded XCD-blocked), "col24",

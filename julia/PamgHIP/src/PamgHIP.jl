@@ -23,7 +23,7 @@ using SparseArrays
 # by the package extension with methods of PartitionedArrays' own generic functions, so a solver
 # that does `using PartitionedArrays, PamgHIP` calls them unqualified and unambiguously.
 export Context, ExchangePlan, DeviceVector, DeviceMatrix, HostCSR, VCycle, ExchangeTask, PamgError,
-       download_own, download_ghosts, exchange_begin, residual!, jacobi!, vcycle!, pcg!, set_sweeps!,
+       download_own, download_ghosts, exchange_begin, residual!, jacobi!, jacobi_residual!, vcycle!, pcg!, set_sweeps!,
        set_perm!, setup_hierarchy, gen_grid, gen_xstar, read_mtx, rcm_order, locality_order, unique_id,
        comm_init!, runtime_versions, hip
 
@@ -334,6 +334,14 @@ jacobi!(x::DeviceVector, A::DeviceMatrix, b::DeviceVector, tmp::DeviceVector, om
     (check(ccall((:pamg_jacobi, libpamg), Cint,
                  (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cdouble, Cint),
                  A.ctx.h, A.h, x.h, b.h, tmp.h, omega, nsweeps)); x)
+"t = x + ω D⁻¹ (b - A x), r = b - A t (one fused pass where the matrix qualifies); returns whether it fused."
+function jacobi_residual!(t::DeviceVector, r::DeviceVector, A::DeviceMatrix, x::DeviceVector, b::DeviceVector, omega::Real)
+    f = Ref{Cint}(0)
+    check(ccall((:pamg_jacobi_residual, libpamg), Cint,
+                (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cdouble, Ptr{Cint}),
+                A.ctx.h, A.h, x.h, b.h, t.h, r.h, omega, f))
+    f[] != 0
+end
 
 # ------------------------------------------------------------------ host CSR + setup (SPEC §S4)
 mutable struct HostCSR
@@ -704,6 +712,14 @@ function bench_rowop(A::DeviceMatrix, op::Integer, x::DeviceVector, b::Union{Not
     check(ccall((:pamg_bench_rowop, libpamg), Cint,
                 (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cdouble, Cint, Ptr{Cdouble}),
                 A.ctx.h, A.h, op, x.h, b === nothing ? C_NULL : b.h, y.h, omega, reps, ms))
+    ms[]
+end
+
+"Average ms of `reps` launches of the cross-cycle pipeline's level-0 chain kernel (x is overwritten)."
+function bench_chain(x::DeviceVector, M::VCycle, b::DeviceVector; reps::Integer = 10)
+    ms = Ref{Cdouble}(0.0)
+    check(ccall((:pamg_hier_bench_chain, libpamg), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ptr{Cdouble}),
+                M.h, x.h, b.h, reps, ms))
     ms[]
 end
 

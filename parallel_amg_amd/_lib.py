@@ -71,6 +71,7 @@ SIGNATURES = {
     "pamg_spmv": [vp, vp, vp, vp],
     "pamg_residual": [vp, vp, vp, vp, vp, pdbl],
     "pamg_jacobi": [vp, vp, vp, vp, vp, dbl, i32],
+    "pamg_jacobi_residual": [vp, vp, vp, vp, vp, vp, dbl, pi32],
     "pamg_hier_create": [vp, i32, vp, vp, vp, vp, i64, vp, i32, vp, pvp],
     "pamg_hier_destroy": [vp],
     "pamg_hier_set_graph": [vp, i32],
@@ -83,6 +84,7 @@ SIGNATURES = {
     "pamg_hier_profile": [vp, i32],
     "pamg_hier_profile_read": [vp, vp],
     "pamg_bench_rowop": [vp, vp, i32, vp, vp, vp, dbl, i32, pdbl],
+    "pamg_hier_bench_chain": [vp, vp, vp, i32, pdbl],
     "pamg_set_option": [C.c_char_p, i64],
     "pamg_get_option": [C.c_char_p, pi64],
     "pamg_hcsr_create": [i64, i64, i64, pvp],

@@ -809,11 +809,44 @@ __device__ __forceinline__ double2 jr_tpair(__amdgpu_buffer_rsrc_t rt, int64_t j
     __builtin_memcpy(&d, &v, 16);
     return d;
 }
-// t[j], t[j+1] for any j >= -1 (the pair(s) holding them)
+// t[j], t[j+1] for any j (zeros outside [0, n)). An odd j is one 8-B-aligned 16-B load (the
+// compiler merges the two pair loads into exactly that, so it is written out); j = -1 would put
+// the load's start out of range — the descriptor then returns zeros for all 16 bytes, t[0]
+// included — so that lane reads the pair at 0 and shifts it.
 __device__ __forceinline__ double2 jr_tany(__amdgpu_buffer_rsrc_t rt, int64_t j) {
     if ((j & 1) == 0) return jr_tpair(rt, j);
-    const double2 a = jr_tpair(rt, j - 1), c = jr_tpair(rt, j + 1);
-    return make_double2(a.y, c.x);
+    const bool m1 = j == -1;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rt, (int)((m1 ? 0 : j) * 8), 0, 16 /* sc1 */);
+    double2 d;
+    __builtin_memcpy(&d, &v, 16);
+    return m1 ? make_double2(0.0, d.x) : d;
+}
+
+// Wave 0 of the workgroup waits until every flag in need[0..4] (entries outside [0, nflags)
+// skipped) is set: lanes 0-4 poll one flag each with agent-scope relaxed loads (sc1), together,
+// so a wait costs one round trip, not five. Bounded: a timeout (or another workgroup's) sets
+// *err and returns false.
+__device__ __forceinline__ bool jr_wait5(const unsigned* flags, const int64_t (&need)[5], int64_t nflags,
+                                         unsigned* err) {
+    const int lane = threadIdx.x & 63;
+    int64_t f = -1;
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        if (lane == k) f = need[k];
+    bool ready = f < 0 || f >= nflags;
+    unsigned spins = 0;
+    for (;;) {
+        if (!ready) ready = __hip_atomic_load(flags + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        if (__all(ready)) return true;
+        __builtin_amdgcn_s_sleep(1);
+        if ((++spins & 63u) == 0u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+            return false;
+        if (spins > kJrSpinLimit) {
+            if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+    }
 }
 
 template <int NU>
@@ -924,22 +957,10 @@ __global__ __launch_bounds__(kJrThreads) void k_sym_jr(
             if (tid == 0) __hip_atomic_store(flags + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             // ---- R: r = b - A t, after the t units it reads are published
-            if (tid == 0) {
-                const int64_t nu_tot = (int64_t)js.nb * js.ub;
+            if (tid < 64) {
                 const int64_t need[5] = {g - js.ub, g - 1, g, g + 1, g + js.ub};
-                for (int q = 0; q < 5; ++q) {
-                    if (need[q] < 0 || need[q] >= nu_tot) continue;
-                    unsigned spins = 0;
-                    while (__hip_atomic_load(flags + need[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-                        __builtin_amdgcn_s_sleep(1);
-                        if (++spins > kJrSpinLimit) {
-                            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            s_abort = 1;
-                            break;
-                        }
-                    }
-                    if (s_abort) break;
-                }
+                const bool ok = jr_wait5(flags, need, (int64_t)js.nb * js.ub, err);
+                if (tid == 0 && !ok) s_abort = 1;
             }
             __syncthreads();
             if (!s_abort) {
@@ -970,6 +991,158 @@ __global__ __launch_bounds__(kJrThreads) void k_sym_jr(
                 }
                 *reinterpret_cast<double2*>(r + i0) = make_double2(out[0], out[1]);
             }
+        }
+        __syncthreads();  // s_item / s_abort are rewritten by the next item
+    }
+}
+
+// k_sym_chain: S (2 or 3) dependent sweeps over the symmetric layout in ONE pipelined pass — the
+// generalisation of k_sym_jr with an explicit per-queue item list (ChainArgs::items: stage << 28
+// | global unit, built on the host, runtime.hip build_chain): stage 0 reads in0 with plain loads
+// and every later stage reads its predecessor's output through sc1 16-B buffer loads after
+// polling the predecessor's flags of the units it reads (g, g +- 1, g +- one band); outputs
+// consumed inside the launch are published write-through (sc1 stores, drained, barrier, one
+// agent flag store), the last stage's output with plain stores. Stages are weighted-Jacobi
+// sweeps, the last one optionally the residual. Every wait is on an item placed earlier in the
+// merged item timeline of some queue, so the pipeline drains; spins are bounded. No buffer is
+// both read with plain loads and rewritten inside one launch (the caller rotates buffers), so
+// no XCD's L2 can hold a stale copy of a handed-off line. (ChainArgs: pamg_device.h)
+
+template <int NU>
+__global__ __launch_bounds__(kJrThreads) void k_sym_chain(int nrows, const uint8_t* __restrict__ mask,
+                                                         const double* __restrict__ dg,
+                                                         const double* __restrict__ up, int64_t ld,
+                                                         const SymDia sd, const ChainArgs ca) {
+    __shared__ int s_item;
+    __shared__ int s_abort;
+    const int tid = threadIdx.x;
+    const int q = blockIdx.x & 7;
+    unsigned* head = ca.sync + 16 * q;
+    unsigned* flags = ca.sync + 128;
+    const int* items = ca.items + (size_t)q * ca.per_queue;
+    const int64_t n = nrows;
+    __amdgpu_buffer_rsrc_t rin[3], rout[3];
+#pragma unroll
+    for (int st = 0; st < 3; ++st) {
+        rout[st] = __builtin_amdgcn_make_buffer_rsrc((void*)ca.out[st], 0, (int)(8 * n), 0x00020000);
+        rin[st] = st == 0 ? __builtin_amdgcn_make_buffer_rsrc((void*)ca.in0, 0, (int)(8 * n), 0x00020000) : rout[st - 1];
+    }
+    int next_item = -1;
+    if (tid == 0) {
+        const int t0 = (int)atomicAdd(head, 1u);
+        next_item = t0 < ca.per_queue ? items[t0] : -1;
+    }
+    for (;;) {
+        if (tid == 0) {
+            s_item = next_item;
+            s_abort = 0;
+            if (next_item >= 0) {  // the following item, in flight during this one
+                const int t1 = (int)atomicAdd(head, 1u);
+                next_item = t1 < ca.per_queue ? items[t1] : -1;
+            }
+        }
+        __syncthreads();
+        const int it = s_item;
+        if (it < 0) break;
+        const int st = it >> 28;
+        const int64_t g = it & 0x0FFFFFFF;
+        const int64_t i0 = g * kJrRows + 2 * tid;
+        const bool resid = ca.last_resid && st == ca.nstages - 1;
+        const bool publish = st < ca.nstages - 1;
+        uint32_t m[2];
+        SymMask<NU>::two(mask, i0, m);
+        double v[2][2 * NU + 1], xv[2][2 * NU + 1], pb[2];
+        {
+            const double2 d2 = *reinterpret_cast<const double2*>(dg + i0);
+            const double2 b2 = *reinterpret_cast<const double2*>(ca.b + i0);
+            v[0][NU] = d2.x;
+            v[1][NU] = d2.y;
+            pb[0] = b2.x;
+            pb[1] = b2.y;
+        }
+#pragma unroll
+        for (int c = 0; c < NU; ++c) {
+            const double2 a = *reinterpret_cast<const double2*>(up + (size_t)c * ld + i0);
+            v[0][NU + 1 + c] = a.x;
+            v[1][NU + 1 + c] = a.y;
+            const int o = sd.off[c];
+            const double2 lo = ld_pair(up + (size_t)c * ld, i0 - o, n, (o & 1) == 0);
+            v[0][NU - 1 - c] = lo.x;
+            v[1][NU - 1 - c] = lo.y;
+        }
+        if (st > 0) {  // the predecessor's units this item reads
+            if (tid < 64) {
+                const int64_t need[5] = {g - ca.ub, g - 1, g, g + 1, g + ca.ub};
+                const bool ok = jr_wait5(flags + (size_t)(st - 1) * ca.nunits, need, ca.nunits, ca.err);
+                if (tid == 0 && !ok) s_abort = 1;
+            }
+            __syncthreads();
+        }
+        if (!s_abort) {
+            if (st == 0) {
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    const int o = sd.off[c];
+                    const double2 xl = ld_pair(ca.in0, i0 - o, n, (o & 1) == 0);
+                    const double2 xu = ld_pair(ca.in0, i0 + o, n, (o & 1) == 0);
+                    xv[0][NU - 1 - c] = xl.x;
+                    xv[1][NU - 1 - c] = xl.y;
+                    xv[0][NU + 1 + c] = xu.x;
+                    xv[1][NU + 1 + c] = xu.y;
+                }
+                const double2 xc = *reinterpret_cast<const double2*>(ca.in0 + i0);
+                xv[0][NU] = xc.x;
+                xv[1][NU] = xc.y;
+            } else {
+                const __amdgpu_buffer_rsrc_t ri = st == 1 ? rin[1] : rin[2];
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    const int o = sd.off[c];
+                    const double2 tl = jr_tany(ri, i0 - o);
+                    const double2 tu = jr_tany(ri, i0 + o);
+                    xv[0][NU - 1 - c] = tl.x;
+                    xv[1][NU - 1 - c] = tl.y;
+                    xv[0][NU + 1 + c] = tu.x;
+                    xv[1][NU + 1 + c] = tu.y;
+                }
+                const double2 tc = jr_tpair(ri, i0);
+                xv[0][NU] = tc.x;
+                xv[1][NU] = tc.y;
+            }
+            double out[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                double sum = 0.0;
+#pragma unroll
+                for (int kk = 0; kk < 2 * NU + 1; ++kk) {
+                    const double pr = v[r][kk] * xv[r][kk];
+                    const double tt = sum + pr;
+                    sum = ((m[r] >> kk) & 1u) ? tt : sum;
+                }
+                if (resid) {
+                    out[r] = pb[r] - sum;
+                } else {
+                    const double u = pb[r] - sum;
+                    const double w = ca.omega * u;
+                    const double qq = w / v[r][NU];
+                    out[r] = xv[r][NU] + qq;
+                }
+            }
+            if (publish) {
+                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                u32x4 pk;
+                __builtin_memcpy(&pk, out, 16);
+                const __amdgpu_buffer_rsrc_t ro = st == 0 ? rout[0] : rout[1];
+                __builtin_amdgcn_raw_buffer_store_b128(pk, ro, (int)(i0 * 8), 0, 16 /* sc1 */);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+            } else {
+                *reinterpret_cast<double2*>(ca.out[st] + i0) = make_double2(out[0], out[1]);
+            }
+        }
+        if (publish) {
+            __syncthreads();
+            if (tid == 0 && !s_abort)
+                __hip_atomic_store(flags + (size_t)st * ca.nunits + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();  // s_item / s_abort are rewritten by the next item
     }
@@ -1303,6 +1476,16 @@ void launch_sym_jr(const pamg_mat& A, const double* x, const double* b, double* 
                                                         x, b, t, r, omega, sync, err); break;
         default: k_sym_jr<3><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, sd.jr,
                                                           x, b, t, r, omega, sync, err); break;
+    }
+}
+
+void launch_sym_chain(const pamg_mat& A, const ChainArgs& ca, size_t sync_bytes, int grid, hipStream_t s) {
+    const SymDia& sd = A.sym;
+    (void)hipMemsetAsync(ca.sync, 0, sync_bytes, s);
+    switch (sd.nu) {
+        case 1: k_sym_chain<1><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, ca); break;
+        case 2: k_sym_chain<2><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, ca); break;
+        default: k_sym_chain<3><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, ca); break;
     }
 }
 

@@ -113,7 +113,8 @@ struct Options {
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
     int sym_dia = 1;           // 1: symmetric diagonal-class layout for stencil-shaped symmetric operators
     int sym_rows = 2;          // rows per lane of its kernel (1 | 2)
-    int jr_fuse = 1;           // 1: fused level-0 pre-smoothing Jacobi + residual where the layout allows
+    int jr_fuse = 0;           // 1: fused level-0 Jacobi -> residual / cross-cycle pipeline where the layout allows
+                               //    (opt-in: measured slower than the separate sweeps so far)
 };
 
 // Symmetric diagonal-class layout (k_rows_sym): a square operator whose interior rows use at
@@ -144,6 +145,11 @@ struct SymDia {
     size_t jr_sync_bytes = 0;
     unsigned* d_jr_err = nullptr;   // set by a timed-out spin; checked by the host
     int jr_grid = 0;
+    // k_sym_chain item lists (stage << 28 | unit), 8 queues each: 2 stages (Jacobi -> residual)
+    // and 3 stages (Jacobi -> Jacobi -> residual: one cycle's post-smoothing + the next cycle's
+    // pre-smoothing and residual)
+    int* d_chain_items[4] = {nullptr, nullptr, nullptr, nullptr};
+    int chain_per_queue[4] = {0, 0, 0, 0};
     uint8_t* d_mask = nullptr;      // nrows (+ pad) masks of 1 byte (2 nu + 1 <= 7) or 2 bytes
     int mask_bytes = 2;
     double* d_diag = nullptr;       // nrows (+ pad)
@@ -225,6 +231,22 @@ void launch_dense_gemv(int64_t n_rows, int64_t n_cols, int64_t row0, const doubl
                        const double* b, double* y, hipStream_t s);
 void launch_pack(int64_t n, const int* idx, const double* x, double* out, hipStream_t s);
 void launch_fill(int64_t n, double v, double* y, hipStream_t s);
+// k_sym_chain arguments (kernels.hip)
+struct ChainArgs {
+    const int* items = nullptr;  // 8 queues x per_queue items
+    int per_queue = 0;
+    int ub = 0;                  // units per band
+    int nunits = 0;
+    int nstages = 0;
+    bool last_resid = false;
+    const double* in0 = nullptr;
+    double* out[3] = {nullptr, nullptr, nullptr};
+    const double* b = nullptr;
+    double omega = 0.0;
+    unsigned* sync = nullptr;    // 8 queue heads (one 64-B line each), then (nstages-1) x nunits flags
+    unsigned* err = nullptr;
+};
+void launch_sym_chain(const pamg_mat& A, const ChainArgs& ca, size_t sync_bytes, int grid, hipStream_t s);
 // t = Jacobi(x), r = b - A t in one launch (k_sym_jr; A.sym.jr_ok)
 void launch_sym_jr(const pamg_mat& A, const double* x, const double* b, double* t, double* r, double omega,
                    unsigned* sync, size_t sync_bytes, unsigned* err, int grid, hipStream_t s);

@@ -865,17 +865,44 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
     // fused Jacobi -> residual schedule (kernels.hip k_sym_jr): one part with every row in the
     // set, byte masks, bands of whole 8 x 2048-row eighths, every offset inside a unit's
     // neighbours or exactly one band, byte offsets within int32 (buffer descriptors)
+    // The schedule's band is the largest offset M (one grid plane): a unit's rows then read
+    // units g - ub, g -+ 1 and g + ub only, when every other offset stays inside one unit.
     {
         constexpr int64_t kUnit = 2048;
-        bool ok = A->ncols == n && (int64_t)inner.size() == n && mb == 1 && bd % (8 * kUnit) == 0 &&
-                  n % bd == 0 && 8 * (n + 64) < INT32_MAX;
-        for (int c = 0; c < nu && ok; ++c) ok = sd.off[c] < kUnit || sd.off[c] == bd;
+        const int64_t M = sd.off[nu - 1];
+        bool ok = A->ncols == n && (int64_t)inner.size() == n && mb == 1 && M % (8 * kUnit) == 0 &&
+                  n % M == 0 && 8 * (n + 64) < INT32_MAX;
+        for (int c = 0; c + 1 < nu && ok; ++c) ok = sd.off[c] < kUnit;
         if (ok) {
-            sd.jr.ub = (int)(bd / kUnit);
+            sd.jr.ub = (int)(M / kUnit);
             sd.jr.e = sd.jr.ub / 8;
-            sd.jr.nb = (int)(n / bd);
+            sd.jr.nb = (int)(n / M);
             sd.jr.lag = std::min(4, sd.jr.e);
-            const int64_t words = 128 + (int64_t)sd.jr.nb * sd.jr.ub;
+            // chain item lists: stage s runs D = e + lag items (one band + lag units) behind
+            // stage s-1 in the queue's timeline, so every unit a stage reads from its
+            // predecessor (same band +- 1 unit, +- one band) sits at an earlier slot
+            {
+                const int e = sd.jr.e, per = sd.jr.nb * e, D = e + sd.jr.lag;
+                for (int S = 2; S <= 3; ++S) {
+                    std::vector<int> items;
+                    items.reserve((size_t)8 * S * per);
+                    for (int q = 0; q < 8; ++q) {
+                        const size_t q0 = items.size();
+                        for (int tau = 0; tau < per + (S - 1) * D; ++tau)
+                            for (int st = 0; st < S; ++st) {
+                                const int P = tau - st * D;
+                                if (P < 0 || P >= per) continue;
+                                const int64_t g = (int64_t)(P / e) * sd.jr.ub + (int64_t)q * e + P % e;
+                                items.push_back((st << 28) | (int)g);
+                            }
+                        if (items.size() - q0 != (size_t)S * per) return fail(PAMG_E_STATE, "chain items");
+                    }
+                    sd.chain_per_queue[S] = S * per;
+                    CHECK(dalloc(&sd.d_chain_items[S], (int64_t)items.size()));
+                    HIPC(hipMemcpy(sd.d_chain_items[S], items.data(), sizeof(int) * items.size(), hipMemcpyHostToDevice));
+                }
+            }
+            const int64_t words = 128 + 2 * (int64_t)sd.jr.nb * sd.jr.ub;  // flags of up to 2 publishing stages
             sd.jr_sync_bytes = (size_t)((words * 4 + 15) / 16 * 16);
             CHECK(dalloc(reinterpret_cast<char**>(&sd.d_jr_sync), (int64_t)sd.jr_sync_bytes));
             CHECK(dalloc(&sd.d_jr_err, 4));
@@ -1039,6 +1066,14 @@ struct pamg_hier {
     // graph replay
     bool use_graph = true;
     hipGraphExec_t gexec = nullptr;
+    // cross-cycle pipeline (Options::jr_fuse, stationary cycles): head (first cycle without its
+    // level-0 post-smoothing), two steady segments (the previous cycle's post-smoothing fused
+    // with this cycle's pre-smoothing and residual, then the rest of the cycle; the level-0
+    // iterate alternates between t[0] and u0), two tails (the last post-smoothing)
+    hipGraphExec_t g_head = nullptr, g_steady[2] = {nullptr, nullptr}, g_tail[2] = {nullptr, nullptr};
+    const double* gp_x = nullptr;
+    const double* gp_b = nullptr;
+    double* u0 = nullptr;
     const double* g_x = nullptr;
     const double* g_b = nullptr;
     bool g_zero0 = false;
@@ -1127,7 +1162,18 @@ struct ProfScope {
 // One V-cycle (SPEC §S6), enqueued on the compute stream; result in x. zero0: the level-0
 // initial guess is zero (preconditioner use), so the level-0 pre-smoothing takes the
 // zero-guess form too (bit-identical to the full sweep from x = 0, SPEC §S3).
-int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false) {
+// Level-0 segments of the cross-cycle pipeline (vcycle_raw): l0_given — the level-0 pre-smoothed
+// iterate and residual are already in t0 / r0 (a k_sym_chain launch made them); l0_post —
+// whether this call ends with the level-0 post-smoothing (else the prolongated t0 is left for
+// the next chain launch). Defaults: one whole cycle.
+struct L0Seg {
+    bool given = false;
+    double* t0 = nullptr;
+    double* r0 = nullptr;
+    bool post = true;
+};
+
+int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false, L0Seg seg = L0Seg{}) {
     pamg_ctx* ctx = H->ctx;
     hipStream_t s = ctx->s_comp;
     const int L = H->L;
@@ -1144,6 +1190,13 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false)
     for (int l = 0; l < L - 1; ++l) {
         const pamg_mat* A = H->A[l];
         double *c = H->t[l], *o = H->r[l];
+        if (l == 0 && seg.given) {  // made by the chain launch before this call
+            cur[0] = seg.t0;
+            spare[0] = seg.r0;
+            ProfScope p(H, 0, 2, s);
+            CHECK(apply(ctx, H->R[0], pamg::OP_SPMV, seg.r0, nullptr, H->b[1], 0.0));
+            continue;
+        }
         // level 0, V(1, nu2) from a given guess: the pre-smoothing sweep and the residual in one
         // pipelined pass (k_sym_jr; both timed as jacobi_pre)
         const bool fuse = l == 0 && !zero0 && H->nu1 == 1 && pamg::options().jr_fuse && A->interior.sym &&
@@ -1189,6 +1242,7 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false)
             ProfScope p(H, l, 3, s);
             CHECK(apply(ctx, H->P[l], pamg::OP_PROLONG, H->x[l + 1], nullptr, cur[l], 0.0));
         }
+        if (l == 0 && !seg.post) break;
         {
             ProfScope p(H, l, 4, s);
             double* in = cur[l];
@@ -1828,6 +1882,7 @@ int pamg_mat_destroy(pamg_mat* A) {
     dfree(A->sym.d_diag);
     dfree(A->sym.d_upper);
     if (A->sym.d_jr_sync) (void)hipFree(A->sym.d_jr_sync);
+    for (int k = 0; k < 4; ++k) dfree(A->sym.d_chain_items[k]);
     dfree(A->sym.d_jr_err);
     free_tiles(A->interior);
     free_tiles(A->boundary);
@@ -1924,6 +1979,34 @@ int pamg_jacobi(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec* b
     if (cur != x->d)
         HIPC(hipMemcpyAsync(x->d, cur, sizeof(double) * x->n_own, hipMemcpyDeviceToDevice, ctx->s_comp));
     HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
+int pamg_jacobi_residual(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec* b, pamg_vec* t,
+                         pamg_vec* r, double omega, int* fused) {
+    if (!ctx || !A || !x || !b || !t || !r) return fail(PAMG_E_ARG, "jacobi_residual: NULL");
+    CHECK(check_vec_for(A, x, "jacobi_residual"));
+    CHECK(check_vec_for(A, t, "jacobi_residual"));
+    if (!A->d_diag) return fail(PAMG_E_SETUP, "jacobi_residual: matrix is not square or lacks a nonzero diagonal");
+    if (b->n_own != A->nrows || r->n_own != A->nrows || t == x || r == x || r == t || b == t || b == r)
+        return fail(PAMG_E_ARG, "jacobi_residual: size mismatch or aliasing");
+    CHECK(set_device(ctx));
+    const bool fuse = pamg::options().jr_fuse && A->interior.sym && A->sym.jr_ok && !(A->plan && !A->plan->nbr.empty());
+    if (fuse) {
+        pamg::launch_sym_jr(*A, x->d, b->d, t->d, r->d, omega, A->sym.d_jr_sync, A->sym.jr_sync_bytes,
+                            A->sym.d_jr_err, A->sym.jr_grid, ctx->s_comp);
+        HIPC(hipGetLastError());
+    } else {
+        CHECK(apply(ctx, A, pamg::OP_JACOBI, x->d, b->d, t->d, omega));
+        CHECK(apply(ctx, A, pamg::OP_RESID, t->d, b->d, r->d, 0.0));
+    }
+    if (fused) *fused = fuse ? 1 : 0;
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    if (fuse) {
+        unsigned e = 0;
+        HIPC(hipMemcpy(&e, A->sym.d_jr_err, sizeof(unsigned), hipMemcpyDeviceToHost));
+        if (e) return fail(PAMG_E_STATE, "jacobi_residual: the fused kernel timed out waiting for a unit");
+    }
     return PAMG_OK;
 }
 
@@ -2035,10 +2118,23 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
     return PAMG_OK;
 }
 
-static void drop_graph(pamg_hier* H) {
+static void drop_cycle_graph(pamg_hier* H) {
     if (H->gexec) (void)hipGraphExecDestroy(H->gexec);
     H->gexec = nullptr;
     H->g_x = H->g_b = nullptr;
+}
+
+static void drop_pipe_graphs(pamg_hier* H) {
+    for (hipGraphExec_t* g : {&H->g_head, &H->g_steady[0], &H->g_steady[1], &H->g_tail[0], &H->g_tail[1]}) {
+        if (*g) (void)hipGraphExecDestroy(*g);
+        *g = nullptr;
+    }
+    H->gp_x = H->gp_b = nullptr;
+}
+
+static void drop_graph(pamg_hier* H) {
+    drop_cycle_graph(H);
+    drop_pipe_graphs(H);
 }
 
 int pamg_hier_destroy(pamg_hier* H) {
@@ -2061,6 +2157,7 @@ int pamg_hier_destroy(pamg_hier* H) {
     dfree(H->pcg_z);
     dfree(H->pcg_p);
     dfree(H->pcg_q);
+    dfree(H->u0);
     dfree(H->d_perm);
     dfree(H->px);
     dfree(H->pb);
@@ -2123,7 +2220,7 @@ int pamg_hier_set_perm(pamg_hier* H, int64_t n, const int64_t* perm) {
 int pamg_hier_graph_state(const pamg_hier* H, int* enabled, int* captured, int* failed) {
     if (!H) return fail(PAMG_E_ARG, "hier_graph_state: NULL");
     if (enabled) *enabled = H->use_graph ? 1 : 0;
-    if (captured) *captured = H->gexec ? 1 : 0;
+    if (captured) *captured = (H->gexec || H->g_head) ? 1 : 0;
     if (failed) *failed = H->graph_failed ? 1 : 0;
     return PAMG_OK;
 }
@@ -2153,15 +2250,123 @@ int pamg_hier_profile_read(pamg_hier* H, double* out) {
 
 // ncycles V-cycles on raw device vectors (graph replay when enabled; the captured graph is
 // keyed on the vector addresses and the zero-guess flag).
+// The k_sym_chain launch of a steady segment: the previous cycle's level-0 post-smoothing
+// (t_prev -> x), this cycle's pre-smoothing (x -> t_next) and residual (t_next -> r[0]).
+static void launch_chain3(pamg_hier* H, double* x, const double* b, const double* t_prev, double* t_next) {
+    const pamg_mat* A = H->A[0];
+    const pamg::SymDia& sd = A->sym;
+    pamg::ChainArgs ca;
+    ca.items = sd.d_chain_items[3];
+    ca.per_queue = sd.chain_per_queue[3];
+    ca.ub = sd.jr.ub;
+    ca.nunits = sd.jr.nb * sd.jr.ub;
+    ca.nstages = 3;
+    ca.last_resid = true;
+    ca.in0 = t_prev;
+    ca.out[0] = x;
+    ca.out[1] = t_next;
+    ca.out[2] = H->r[0];
+    ca.b = b;
+    ca.omega = H->omega[0];
+    ca.sync = sd.d_jr_sync;
+    ca.err = sd.d_jr_err;
+    pamg::launch_sym_chain(*A, ca, sd.jr_sync_bytes, sd.jr_grid, H->ctx->s_comp);
+}
+
+// Segments of the cross-cycle pipeline. seg 0: head (first cycle, no level-0 post-smoothing,
+// iterate in t[0]); 1 / 2: steady, the iterate moving t[0] -> u0 / u0 -> t[0]; 3 / 4: tail (the
+// last post-smoothing from t[0] / u0).
+static int pipe_enqueue(pamg_hier* H, double* x, const double* b, int seg) {
+    L0Seg sg;
+    sg.post = false;
+    if (seg == 0) return vcycle_enqueue(H, x, b, false, sg);
+    double* t0 = H->t[0];
+    double* u0 = H->u0;
+    if (seg == 1 || seg == 2) {
+        double* prev = seg == 1 ? t0 : u0;
+        double* next = seg == 1 ? u0 : t0;
+        {
+            ProfScope p(H, 0, 0, H->ctx->s_comp);
+            launch_chain3(H, x, b, prev, next);
+        }
+        sg.given = true;
+        sg.t0 = next;
+        sg.r0 = H->r[0];
+        return vcycle_enqueue(H, x, b, false, sg);
+    }
+    ProfScope p(H, 0, 4, H->ctx->s_comp);
+    return apply(H->ctx, H->A[0], pamg::OP_JACOBI, seg == 3 ? t0 : u0, b, x, H->omega[0]);
+}
+
+// Eligible for the cross-cycle pipeline: one part, V(1, 1), level 0 in the symmetric layout with
+// chain schedules, fusion on, a stationary run of >= 2 cycles from a given guess.
+static bool pipe_ok(const pamg_hier* H, int ncycles, bool zero0) {
+    if (zero0 || ncycles < 2 || H->L < 2 || H->prof || !pamg::options().jr_fuse || H->nu1 != 1 || H->nu2 != 1)
+        return false;
+    const pamg_mat* A = H->A[0];
+    return H->ctx->nranks == 1 && A->interior.sym && A->sym.jr_ok && A->sym.d_chain_items[3] &&
+           !(A->plan && !A->plan->nbr.empty());
+}
+
+static int vcycle_pipe(pamg_hier* H, double* x, const double* b, int ncycles) {
+    pamg_ctx* ctx = H->ctx;
+    if (!H->u0) {
+        const int64_t n = H->nown[0] + (H->A[0]->plan ? H->A[0]->plan->n_ghost : 0) + kVecPad;
+        CHECK(dalloc(&H->u0, n));
+        HIPC(hipMemset(H->u0, 0, sizeof(double) * n));
+    }
+    const int K = ncycles;
+    auto seg_of = [K](int k) { return k == 0 ? 0 : k < K ? (k % 2 == 1 ? 1 : 2) : ((K - 1) % 2 == 1 ? 4 : 3); };
+    if (H->use_graph && (!H->g_head || H->gp_x != x || H->gp_b != b)) {
+        drop_pipe_graphs(H);
+        bool ok = true;
+        hipGraphExec_t* slot[5] = {&H->g_head, &H->g_steady[0], &H->g_steady[1], &H->g_tail[0], &H->g_tail[1]};
+        for (int sgi = 0; sgi < 5 && ok; ++sgi) {
+            hipGraph_t g = nullptr;
+            if (hipStreamBeginCapture(ctx->s_comp, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+                ok = false;
+                break;
+            }
+            const int rc = pipe_enqueue(H, x, b, sgi);
+            const hipError_t e2 = hipStreamEndCapture(ctx->s_comp, &g);
+            ok = rc == PAMG_OK && e2 == hipSuccess && g && hipGraphInstantiate(slot[sgi], g, nullptr, nullptr, 0) == hipSuccess;
+            if (g) (void)hipGraphDestroy(g);
+        }
+        if (ok) {
+            H->gp_x = x;
+            H->gp_b = b;
+        } else {
+            (void)hipGetLastError();
+            drop_pipe_graphs(H);
+            H->use_graph = false;
+            H->graph_failed = true;
+            fprintf(stderr, "[pamg] pipelined V-cycle graph capture failed (%s); using eager launches\n",
+                    pamg::last_error().c_str());
+        }
+    }
+    for (int k = 0; k <= K; ++k) {
+        const int sg = seg_of(k);
+        if (H->use_graph && H->g_head) {
+            hipGraphExec_t ge = sg == 0 ? H->g_head : sg <= 2 ? H->g_steady[sg - 1] : H->g_tail[sg - 3];
+            HIPC(hipGraphLaunch(ge, ctx->s_comp));
+        } else {
+            CHECK(pipe_enqueue(H, x, b, sg));
+        }
+    }
+    return PAMG_OK;
+}
+
 static int vcycle_raw(pamg_hier* H, double* x, const double* b, int ncycles, bool zero0) {
     pamg_ctx* ctx = H->ctx;
     if (zero0 && ncycles != 1) return fail(PAMG_E_ARG, "vcycle: zero initial guess applies to one cycle");
+    // stationary runs of >= 2 cycles: the cross-cycle pipeline (same operations, same bits)
+    if (pipe_ok(H, ncycles, zero0)) return vcycle_pipe(H, x, b, ncycles);
     if (H->use_graph && !H->prof && (!H->gexec || H->g_x != x || H->g_b != b || H->g_zero0 != zero0)) {
         // Capture one cycle (RCCL exchanges included on several parts: RCCL records its
         // send/recv/all-gather as graph nodes). If capture fails, fall back to eager launches
         // for this hierarchy: both paths issue the same RCCL sequence, so ranks that did
         // capture and ranks that did not still match.
-        drop_graph(H);
+        drop_cycle_graph(H);
         hipGraph_t g = nullptr;
         int rc = PAMG_OK;
         hipError_t e1 = hipStreamBeginCapture(ctx->s_comp, hipStreamCaptureModeThreadLocal);
@@ -2396,6 +2601,34 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "jr_fuse") *value = o.jr_fuse;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
+}
+
+int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps, double* avg_ms) {
+    if (!H || !x || !b || reps < 1 || !avg_ms) return fail(PAMG_E_ARG, "hier_bench_chain: bad args");
+    if (!pipe_ok(H, 2, false)) return fail(PAMG_E_STATE, "hier_bench_chain: the hierarchy does not run the cross-cycle pipeline");
+    pamg_ctx* ctx = H->ctx;
+    CHECK(check_vec_for(H->A[0], x, "hier_bench_chain"));
+    CHECK(set_device(ctx));
+    if (!H->u0) {
+        const int64_t n = H->nown[0] + kVecPad;
+        CHECK(dalloc(&H->u0, n));
+        HIPC(hipMemset(H->u0, 0, sizeof(double) * n));
+    }
+    hipEvent_t e0, e1;
+    HIPC(hipEventCreate(&e0));
+    HIPC(hipEventCreate(&e1));
+    hipStream_t s = ctx->s_comp;
+    launch_chain3(H, x->d, b->d, H->t[0], H->u0);
+    HIPC(hipEventRecord(e0, s));
+    for (int k = 0; k < reps; ++k) launch_chain3(H, x->d, b->d, (k & 1) ? H->u0 : H->t[0], (k & 1) ? H->t[0] : H->u0);
+    HIPC(hipEventRecord(e1, s));
+    HIPC(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, e0, e1));
+    *avg_ms = ms / reps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return check_jr_err(H);
 }
 
 int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, const pamg_vec* b,

@@ -292,6 +292,14 @@ def jacobi(x: PVector, A: PSparseMatrix, b: PVector, tmp: PVector, omega: float,
     return x
 
 
+def jacobi_residual(t: PVector, r: PVector, A: PSparseMatrix, x: PVector, b: PVector, omega: float) -> bool:
+    """t = x + omega D^-1 (b - A x); r = b - A t. Returns whether the fused pass ran."""
+    f = C.c_int(0)
+    call("pamg_jacobi_residual", A.ctx.handle, A.handle, x.handle, b.handle, t.handle, r.handle, float(omega),
+         C.byref(f))
+    return bool(f.value)
+
+
 def consistent(x: PVector, plan: DevicePlan) -> PVector:
     """``consistent!(x) |> wait``: owners' values into x's ghost slots."""
     call("pamg_exchange", x.ctx.handle, plan.handle, x.handle)

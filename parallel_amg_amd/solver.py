@@ -133,6 +133,17 @@ class AMGSolver:
     def vcycle_async(self, x: PVector, b: PVector, ncycles: int = 1):
         call("pamg_vcycle_async", self.ctx.handle, self._h, x.handle, b.handle, ncycles)
 
+    def bench_chain(self, x: PVector, b: PVector, reps: int = 10):
+        """ms per launch of the cross-cycle pipeline's level-0 chain kernel (None when the
+        hierarchy does not run the pipeline); x is overwritten."""
+        from ._lib import PamgError
+        ms = C.c_double()
+        try:
+            call("pamg_hier_bench_chain", self._h, x.handle, b.handle, int(reps), C.byref(ms))
+        except PamgError:
+            return None
+        return ms.value
+
     def profile(self, x: PVector, b: PVector, ncycles: int) -> np.ndarray:
         """Eager V-cycles with HIP events around every op; returns ms per (level, op) summed
         over the cycles (shape L x 6, columns = OPS)."""

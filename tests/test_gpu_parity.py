@@ -947,6 +947,42 @@ def test_sym_dia_vcycle_same_bits_either_layout(ctx):
     assert np.array_equal(bits(out[0][1]), bits(out[1][1]))
 
 
+@pytest.mark.parametrize("kind,n", [("poisson3d", 128), ("aniso3d", 128), ("poisson3d", 256)])
+def test_jacobi_residual_op_bit_exact(ctx, kind, n):
+    """pamg_jacobi_residual: the fused pass (k_sym_jr) against the two separate sweeps on
+    random x, b — t and r bit for bit, repeated (a hand-off hazard shows as scattered units)."""
+    from parallel_amg_amd.partitioned import jacobi_residual
+    Ao = O.generate(kind, n, n, n)
+    Ad, _h = upload(ctx, Ao)
+    rng = np.random.default_rng(7)
+    N = n ** 3
+    x = PVector(ctx, N, 0, rng.standard_normal(N))
+    b = PVector(ctx, N, 0, rng.standard_normal(N))
+    out = {}
+    for fuse in (0, 1):
+        with _with_option("jr_fuse", fuse):
+            for rep in range(3 if fuse else 1):
+                t = PVector(ctx, N)
+                r = PVector(ctx, N)
+                f = jacobi_residual(t, r, Ad, x, b, 0.66)
+                assert f == bool(fuse)
+                out[(fuse, rep)] = (t.own_values(), r.own_values())
+    t0, r0 = out[(0, 0)]
+    for rep in range(3):
+        t1, r1 = out[(1, rep)]
+        bt = np.flatnonzero(bits(t1) != bits(t0))
+        br = np.flatnonzero(bits(r1) != bits(r0))
+        if br.size:  # the row sums of SPEC §S3 at the first differing rows (diagnostic)
+            bh = b.own_values()
+            for i in br[:2]:
+                s = 0.0
+                for k in range(Ao.rowptr[i], Ao.rowptr[i + 1]):
+                    s = s + Ao.val[k] * t0[Ao.col[k]]
+                print("row", i, "fused", r1[i].hex(), "unfused", r0[i].hex(), "spec", (bh[i] - s).hex(),
+                      "cols", Ao.col[Ao.rowptr[i]:Ao.rowptr[i + 1]])
+        assert bt.size == 0 and br.size == 0, (rep, bt.size, br.size, bt[:8], br[:8], r1[br[:4]], r0[br[:4]])
+
+
 @pytest.mark.parametrize("kind,n", [("poisson3d", 128), ("aniso3d", 128)])
 def test_fused_jacobi_residual_bit_exact(ctx, kind, n):
     """jr_fuse: the level-0 pre-smoothing sweep and residual pipelined in one persistent
@@ -977,3 +1013,44 @@ def test_fused_jacobi_residual_bit_exact(ctx, kind, n):
     Ho = O.setup(Ao, max_coarse=1000)
     xo, ho = Ho.solve(O.spmv(Ao, O.xstar(Ao.nrows)), 3, res_hist=True)
     assert np.array_equal(bits(out[0][0]), bits(xo))
+
+
+@pytest.mark.parametrize("kind", ["poisson3d", "aniso3d"])
+def test_pipelined_cycles_bit_exact(ctx, kind):
+    """Stationary runs of K >= 2 cycles take the cross-cycle pipeline (one k_sym_chain launch per
+    cycle boundary: the level-0 post-smoothing of cycle k, the pre-smoothing and residual of
+    cycle k + 1; the iterate alternating between two level-0 buffers): x after K cycles has the
+    bits of K separate unfused cycles and of the oracle, with graph replay and eagerly."""
+    be = pa.SequentialBackend(1)
+    n = 128
+    A, offs, xs = pa.generate_problem(be, kind, n)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=ctx)
+    S = AMGSolver(ctx, H)
+    b = PVector(ctx, S.A[0].nrows)
+    mul(b, S.A[0], PVector(ctx, S.A[0].nrows, 0, xs[0]))
+    ref = {}
+    with _with_option("jr_fuse", 0):
+        S.set_graph(False)
+        for K in (2, 3, 4, 5):
+            x = S.new_vector()
+            for _ in range(K):
+                S.vcycle(x, b, 1)
+            ref[K] = x.own_values()
+    for graph in (True, False):
+        with _with_option("jr_fuse", 1):
+            S.set_graph(False)
+            S.set_graph(graph)
+            for K in (2, 3, 4, 5):
+                x = S.new_vector()
+                S.vcycle(x, b, K)
+                assert np.array_equal(bits(x.own_values()), bits(ref[K])), (graph, K)
+            # a continued run: 3 + 2 cycles == 5
+            x = S.new_vector()
+            S.vcycle(x, b, 3)
+            S.vcycle(x, b, 2)
+            assert np.array_equal(bits(x.own_values()), bits(ref[5]))
+            assert S.graph_state()["captured"] == graph
+    Ao = O.generate(kind, n, n, n)
+    Ho = O.setup(Ao, max_coarse=1000)
+    xo, _ho = Ho.solve(O.spmv(Ao, O.xstar(Ao.nrows)), 4, res_hist=True)
+    assert np.array_equal(bits(ref[4]), bits(xo))

@@ -6,8 +6,11 @@ export TMPDIR=/tmp
 TAG=${1:-r03_jr}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_parity.py -k "fused_jacobi" > "$OUT/tests_fused.log" 2>&1
-echo "fused tests ok"
+rc=0
+timeout -k 10 400 python -u -m pytest -v --timeout 240 --timeout-method thread tests/test_gpu_parity.py -k "jacobi_residual_op or fused_jacobi or pipelined_cycles" > "$OUT/tests_fused.log" 2>&1 || rc=$?
+echo "fused tests rc=$rc"
+# a failed parity test still leaves the speed of the path worth measuring; a crash / hang does not
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python3 -u bench.py --cpu-baseline off --pcg-rtol 0 --set jr_fuse=1 > "$OUT/bench_jr1.json" 2> "$OUT/bench_jr1.log"
 echo "bench jr1 ok"
 timeout -k 10 300 python3 -u bench.py --cpu-baseline off --pcg-rtol 0 --set jr_fuse=0 > "$OUT/bench_jr0.json" 2> "$OUT/bench_jr0.log"
