@@ -788,6 +788,7 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
     for (int k = 0; k < no; ++k)
         if (offs[k] != -offs[no - 1 - k]) return PAMG_OK;
     const int nu = no / 2;
+    if (nu < 1) return PAMG_OK;  // diagonal-only rows: the tile path (no class to mirror)
     pamg::SymDia sd;
     sd.nu = nu;
     for (int c = 0; c < nu; ++c) sd.off[c] = offs[nu + 1 + c];

@@ -24,6 +24,31 @@ def _free_port():
     return p
 
 
+def _collect(procs, q, timeout):
+    """Each rank's result; fails fast (instead of waiting out the timeout) when a rank died
+    without reporting — the others would block in a collective for ever."""
+    import queue
+    import time
+    res, t0 = {}, time.time()
+    while len(res) < len(procs):
+        try:
+            r = q.get(timeout=5)
+            res[r[0]] = r
+            continue
+        except queue.Empty:
+            pass
+        dead = [i for i, p in enumerate(procs) if p.exitcode not in (None, 0) and i not in res]
+        if dead or time.time() - t0 > timeout:
+            for p in procs:
+                if p.is_alive():
+                    p.kill()
+            raise AssertionError(f"ranks {dead} died (exit codes {[procs[i].exitcode for i in dead]})" if dead
+                                 else f"no result within {timeout} s")
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
 def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, poison, q):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -111,12 +136,7 @@ def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, agglomerate, poi
              for r in range(world)]
     for p in procs:
         p.start()
-    res = {}
-    for _ in procs:
-        r = q.get(timeout=600)
-        res[r[0]] = r
-    for p in procs:
-        p.join(timeout=60)
+    res = _collect(procs, q, 600)
     for r in range(world):
         assert res[r][1] == "ok", res[r][1]
     Ao = O.generate(kind, *O.grid_shape(kind, n))
@@ -150,12 +170,7 @@ def test_multipart_rcm_partition_bit_exact(world, kind, n, built):
              for r in range(world)]
     for p in procs:
         p.start()
-    res = {}
-    for _ in procs:
-        r = q.get(timeout=300)
-        res[r[0]] = r
-    for p in procs:
-        p.join(timeout=60)
+    res = _collect(procs, q, 300)
     assert all(res[r][1] == "ok" for r in range(world)), "\n".join(str(res[r][1]) for r in range(world))
     import parallel_amg_amd as pa
     whole, _o, wx = pa.generate_problem(pa.SequentialBackend(1), kind, n)
@@ -198,12 +213,7 @@ def test_multipart_with_an_empty_part(tmp_path, built):
              for r in range(world)]
     for p in procs:
         p.start()
-    res = {}
-    for _ in procs:
-        r = q.get(timeout=300)
-        res[r[0]] = r
-    for p in procs:
-        p.join(timeout=60)
+    res = _collect(procs, q, 300)
     assert all(res[r][1] == "ok" for r in range(world)), "\n".join(str(res[r][1]) for r in range(world))
     Ao = O.CSR(A.indptr.astype(np.int64), A.indices.astype(np.int64), A.data.copy(), 400)
     Ho = O.setup(Ao, nparts=2, max_coarse=10, agglomerate=0)

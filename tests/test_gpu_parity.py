@@ -899,12 +899,16 @@ def test_sym_dia_bit_exact(ctx, kind, n, seed, order, rows):
     assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.57), bh, 0.57)))
 
 
-@pytest.mark.parametrize("breaker", ["asym_value", "signed_zero", "unsorted_row"])
+@pytest.mark.parametrize("breaker", ["asym_value", "signed_zero", "unsorted_row", "diagonal_only"])
 def test_sym_dia_declines_what_it_cannot_reproduce(ctx, breaker):
-    """A mirror that differs in one bit (or +0.0 against -0.0), or a row whose storage order is
-    not the ascending offset order, keeps the rows in tiles — still bit-exact."""
+    """A mirror that differs in one bit (or +0.0 against -0.0), a row whose storage order is
+    not the ascending offset order, or an operator with no off-diagonal class at all (a part of
+    isolated rows) keeps the rows in tiles — still bit-exact."""
     from parallel_amg_amd._lib import layout_of
     M = _sym_grid("poisson3d", 12)
+    if breaker == "diagonal_only":
+        n = M.nrows
+        M = O.CSR(np.arange(n + 1, dtype=np.int64), np.arange(n, dtype=np.int64), 3.0 + np.arange(n) % 7, n)
     val, col = M.val.copy(), M.col.copy()
     i = 700
     a, e = int(M.rowptr[i]), int(M.rowptr[i + 1])
@@ -916,7 +920,7 @@ def test_sym_dia_declines_what_it_cannot_reproduce(ctx, breaker):
         for k in range(M.rowptr[j], M.rowptr[j + 1]):
             if col[k] == i:
                 val[k] = -0.0
-    else:
+    elif breaker == "unsorted_row":
         col[a:e] = col[a:e][::-1].copy()               # same entries, descending storage order
         val[a:e] = val[a:e][::-1].copy()
     M2 = O.CSR(M.rowptr.copy(), col, val, M.ncols)
