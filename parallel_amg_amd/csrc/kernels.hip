@@ -742,409 +742,228 @@ __global__ __launch_bounds__(kBlock) void k_rows_sym2(
     }
 }
 
-// ------------------------------------------------------------------ fused Jacobi -> residual
-// k_sym_jr: the level-0 pre-smoothing sweep t = x + w D^-1 (b - A x) and the residual
-// r = b - A t in ONE pass over the symmetric diagonal-class layout (Options::jr_fuse). The
-// residual of a row needs t at its neighbours, so the two are pipelined over row units of
-// kJrRows rows: a persistent grid (one 1024-thread workgroup per CU) draws items from 8 queues
-// (queue = blockIdx % 8: the blocks of one XCD under round-robin dispatch, so an item's D / U /
-// mask / b are still in that XCD's L2 when the residual of the same rows re-reads them L items
-// later; placement changes only speed). Queue k owns the k-th eighth of every band (a grid plane,
-// the layout's XCD-banded order) and interleaves: T(z, p) computes t of unit p of band z and
-// publishes it; R(z-1, u) computes r of unit u of band z-1 once the t units it reads — u-1, u,
-// u+1 of band z-1 (neighbouring queues' at eighth ends) and u of bands z-2, z — are published.
-// Hand-off (MI355X_MICROARCH.md visibility, Valid forms row 1): t is stored write-through (sc1,
-// 16-B buffer stores), every storing wave drains (s_waitcnt vmcnt(0)), a workgroup barrier,
-// then ONE lane stores the unit's flag with an agent-scope relaxed store; the consumer polls the
-// flags with agent-scope relaxed loads (sc1), a barrier, then reads t ONLY through sc1 16-B
-// buffer loads. T items never wait and R items wait only for T items issued earlier in some
-// queue (own queue: same or earlier band; neighbour queues: the same band), all workgroups are
-// co-resident (grid = CUs x 1), so the pipeline drains; every spin is bounded anyway (timeout ->
-// the error word, checked by the host). Bits: T and R evaluate exactly k_rows_sym2's Jacobi and
-// residual expressions (SPEC §S3).
-constexpr int kJrThreads = 1024;
-constexpr int kJrRows = 2 * kJrThreads;
-constexpr unsigned kJrSpinLimit = 1u << 22;
+// ------------------------------------------------------------------ temporally blocked sweeps
+// k_sym_tb<S>: S dependent sweeps (Jacobi, [Jacobi,] then Jacobi or the residual) over a 7-point
+// grid stencil held in the symmetric layout, in ONE pass over the matrix (Options::jr_fuse):
+// the V-cycle's level-0 pre-smoothing + residual (S = 2) and, across a cycle boundary, the
+// post-smoothing of one cycle + the pre-smoothing and residual of the next (S = 3).
+// 2.5-D temporal blocking: a workgroup owns a kTbX x kTbY column of the grid over a range of
+// planes and streams it along z. At step k it computes stage 0 on plane k over the tile plus a
+// halo of S-1 lines (and 2 points in x), stage 1 on plane k-1 (halo S-2), ..., each stage reading
+// its predecessor's planes k-s-1 .. k-s+1 from a 3-plane LDS ring; the halo is recomputed by
+// every workgroup that needs it, so nothing passes between workgroups inside the launch (no
+// flags, no cross-XCD visibility question). A thread keeps its row pair's operator values and b
+// for the last three planes in registers (the ring c0/c1/c2, rotated by a 3-way unrolled z loop),
+// so the matrix streams from HBM once for all S sweeps. Every value is computed by exactly
+// k_rows_sym2's expression for its row (ascending class order from +0.0, present entries only,
+// SPEC §S3), so halo copies are bit-identical and the outputs equal S separate sweeps.
+// Preconditions (runtime.hip build_sym_dia, SymDia::tb_ok): classes {1, nx, nx*ny}, n =
+// nx*ny*nz, nx % kTbX == 0, ny % kTbY == 0, every row in the set, and no row has an entry across
+// a grid line or plane (so points outside the grid contribute nothing and are held as zeros).
+constexpr int kTbPX = (kTbX + 4) / 2;  // row pairs per line: x0-2 .. x0+kTbX+1
+constexpr int kTbLW = kTbX + 8;        // LDS line: column x - x0 + 4 (even for even x; pads 0-1, kTbX+6-7)
 
-__device__ __forceinline__ bool jr_decode(const JrSched& js, int t, int& kind, int& z, int& p) {
-    const int e = js.e, L = js.lag;
-    if (t >= 2 * e * js.nb) return false;
-    if (t < e) {
-        kind = 0;
-        z = 0;
-        p = t;
-        return true;
+template <int S>
+struct TbShape {
+    static constexpr int H = S - 1;              // stage-0 halo in y and z
+    static constexpr int RY = kTbY + 2 * H;      // grid lines of stage 0
+    static constexpr int NT = kTbPX * RY;        // threads with a row pair
+    static constexpr int threads = (NT + 63) / 64 * 64;
+};
+
+struct TbCoef {        // one row pair on one plane: the 7 values in ascending class order, b, masks
+    double v[2][7];
+    double b[2];
+    uint32_t m[2];
+};
+
+__device__ __forceinline__ int tb_mod3(int k) { return ((k % 3) + 3) % 3; }
+
+__device__ __forceinline__ void tb_load(TbCoef& c, const uint8_t* __restrict__ mask, const double* __restrict__ dg,
+                                        const double* __restrict__ up, int64_t ld, const SymDia& sd,
+                                        const double* __restrict__ b, int64_t i, int64_t n) {
+    SymMask<3>::two(mask, i, c.m);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {  // lower classes -off[2], -off[1], -off[0] from the mirrors
+        const int o = sd.off[2 - q];
+        const double2 a = ld_pair(up + (size_t)(2 - q) * ld, i - o, n, (o & 1) == 0);
+        c.v[0][q] = a.x;
+        c.v[1][q] = a.y;
     }
-    const int t2 = t - e, blk = 1 + t2 / (2 * e), q = t2 % (2 * e);
-    if (blk == js.nb) {
-        kind = 1;
-        z = js.nb - 1;
-        p = q;
-        return true;
+    const double2 d = *reinterpret_cast<const double2*>(dg + i);
+    c.v[0][3] = d.x;
+    c.v[1][3] = d.y;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const double2 a = *reinterpret_cast<const double2*>(up + (size_t)q * ld + i);
+        c.v[0][4 + q] = a.x;
+        c.v[1][4 + q] = a.y;
     }
-    if (q < L) {
-        kind = 0;
-        z = blk;
-        p = q;
-        return true;
-    }
-    const int w = q - L;
-    if (w < 2 * (e - L)) {
-        kind = (w & 1) ? 0 : 1;
-        z = (w & 1) ? blk : blk - 1;
-        p = (w & 1) ? L + w / 2 : w / 2;
-        return true;
-    }
-    kind = 1;
-    z = blk - 1;
-    p = e - L + (w - 2 * (e - L));
-    return true;
+    const double2 bb = *reinterpret_cast<const double2*>(b + i);
+    c.b[0] = bb.x;
+    c.b[1] = bb.y;
 }
 
-// t[j], t[j+1] for an even j through ONE sc1 16-B buffer load (out of range: zeros)
-__device__ __forceinline__ double2 jr_tpair(__amdgpu_buffer_rsrc_t rt, int64_t j) {
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rt, (int)(j * 8), 0, 16 /* sc1 */);
-    double2 d;
-    __builtin_memcpy(&d, &v, 16);
-    return d;
-}
-// t[j], t[j+1] for any j (zeros outside [0, n)). An odd j is one 8-B-aligned 16-B load (the
-// compiler merges the two pair loads into exactly that, so it is written out); j = -1 would put
-// the load's start out of range — the descriptor then returns zeros for all 16 bytes, t[0]
-// included — so that lane reads the pair at 0 and shifts it.
-__device__ __forceinline__ double2 jr_tany(__amdgpu_buffer_rsrc_t rt, int64_t j) {
-    if ((j & 1) == 0) return jr_tpair(rt, j);
-    const bool m1 = j == -1;
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rt, (int)((m1 ? 0 : j) * 8), 0, 16 /* sc1 */);
-    double2 d;
-    __builtin_memcpy(&d, &v, 16);
-    return m1 ? make_double2(0.0, d.x) : d;
-}
-
-// Wave 0 of the workgroup waits until every flag in need[0..4] (entries outside [0, nflags)
-// skipped) is set: lanes 0-4 poll one flag each with agent-scope relaxed loads (sc1), together,
-// so a wait costs one round trip, not five. Bounded: a timeout (or another workgroup's) sets
-// *err and returns false.
-__device__ __forceinline__ bool jr_wait5(const unsigned* flags, const int64_t (&need)[5], int64_t nflags,
-                                         unsigned* err) {
-    const int lane = threadIdx.x & 63;
-    int64_t f = -1;
+// the row pair's outputs from its operator values and the 7 neighbour values of each row
+__device__ __forceinline__ void tb_rows(const TbCoef& c, const double (&xv)[2][7], bool resid, double omega,
+                                        double (&out)[2]) {
 #pragma unroll
-    for (int k = 0; k < 5; ++k)
-        if (lane == k) f = need[k];
-    bool ready = f < 0 || f >= nflags;
-    unsigned spins = 0;
-    for (;;) {
-        if (!ready) ready = __hip_atomic_load(flags + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-        if (__all(ready)) return true;
-        __builtin_amdgcn_s_sleep(1);
-        if ((++spins & 63u) == 0u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
-            return false;
-        if (spins > kJrSpinLimit) {
-            if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return false;
+    for (int r = 0; r < 2; ++r) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const double p = c.v[r][k] * xv[r][k];
+            const double t = s + p;
+            s = ((c.m[r] >> k) & 1u) ? t : s;
         }
-    }
-}
-
-template <int NU>
-__global__ __launch_bounds__(kJrThreads) void k_sym_jr(
-    int nrows, const uint8_t* __restrict__ mask, const double* __restrict__ dg, const double* __restrict__ up,
-    int64_t ld, const SymDia sd, const JrSched js, const double* __restrict__ x, const double* __restrict__ b,
-    double* t, double* __restrict__ r, double omega, unsigned* sync, unsigned* err) {
-    __shared__ int s_item[3];
-    __shared__ int s_abort;
-    const int tid = threadIdx.x;
-    const int k = blockIdx.x & 7;
-    unsigned* head = sync + 16 * k;  // one 64-B line per queue head
-    unsigned* flags = sync + 128;
-    const int64_t n = nrows;
-    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc((void*)t, 0, (int)(8 * n), 0x00020000);
-    int next = 0;
-    if (tid == 0) next = (int)atomicAdd(head, 1u);
-    for (;;) {
-        if (tid == 0) {
-            int kind, z, p;
-            if (!jr_decode(js, next, kind, z, p)) {
-                s_item[0] = -1;
-            } else {
-                s_item[0] = kind;
-                s_item[1] = z;
-                s_item[2] = p;
-                next = (int)atomicAdd(head, 1u);  // the following ticket, in flight during this item
-            }
-            s_abort = 0;
-        }
-        __syncthreads();
-        const int kind = s_item[0], z = s_item[1], p = s_item[2];
-        if (kind < 0) break;
-        const int64_t g = (int64_t)z * js.ub + (int64_t)k * js.e + p;  // global unit
-        const int64_t i0 = g * kJrRows + 2 * tid;                      // even; rows i0, i0 + 1
-        uint32_t m[2];
-        SymMask<NU>::two(mask, i0, m);
-        double dv[2], uo[NU][2], pb[2];
-        {
-            const double2 d2 = *reinterpret_cast<const double2*>(dg + i0);
-            dv[0] = d2.x;
-            dv[1] = d2.y;
-            const double2 b2 = *reinterpret_cast<const double2*>(b + i0);
-            pb[0] = b2.x;
-            pb[1] = b2.y;
-        }
-#pragma unroll
-        for (int c = 0; c < NU; ++c) {
-            const double2 a = *reinterpret_cast<const double2*>(up + (size_t)c * ld + i0);
-            uo[c][0] = a.x;
-            uo[c][1] = a.y;
-        }
-        double lo[NU][2];  // mirrors U_c[i - o_c]
-#pragma unroll
-        for (int c = 0; c < NU; ++c) {
-            const int o = sd.off[c];
-            const double2 a = ld_pair(up + (size_t)c * ld, i0 - o, n, (o & 1) == 0);
-            lo[c][0] = a.x;
-            lo[c][1] = a.y;
-        }
-        // operands in ascending offset order, for rows i0 and i0 + 1
-        double v[2][2 * NU + 1], xv[2][2 * NU + 1];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-#pragma unroll
-            for (int c = 0; c < NU; ++c) {
-                v[q][c] = lo[NU - 1 - c][q];
-                v[q][NU + 1 + c] = uo[c][q];
-            }
-            v[q][NU] = dv[q];
-        }
-        if (kind == 0) {
-            // ---- T: t = x + w D^-1 (b - A x), published write-through
-#pragma unroll
-            for (int c = 0; c < NU; ++c) {
-                const int o = sd.off[NU - 1 - c];
-                const double2 xl = ld_pair(x, i0 - o, n, (o & 1) == 0);
-                const double2 xu = ld_pair(x, i0 + sd.off[c], n, (sd.off[c] & 1) == 0);
-                xv[0][c] = xl.x;
-                xv[1][c] = xl.y;
-                xv[0][NU + 1 + c] = xu.x;
-                xv[1][NU + 1 + c] = xu.y;
-            }
-            const double2 xc = *reinterpret_cast<const double2*>(x + i0);
-            xv[0][NU] = xc.x;
-            xv[1][NU] = xc.y;
-            double out[2];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                double s = 0.0;
-#pragma unroll
-                for (int kk = 0; kk < 2 * NU + 1; ++kk) {
-                    const double pr = v[q][kk] * xv[q][kk];
-                    const double tt = s + pr;
-                    s = ((m[q] >> kk) & 1u) ? tt : s;
-                }
-                const double u = pb[q] - s;
-                const double w = omega * u;
-                const double qq = w / v[q][NU];
-                out[q] = xv[q][NU] + qq;
-            }
-            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 pk;
-            __builtin_memcpy(&pk, out, 16);
-            __builtin_amdgcn_raw_buffer_store_b128(pk, rt, (int)(i0 * 8), 0, 16 /* sc1 */);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store(flags + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (resid) {
+            out[r] = c.b[r] - s;
         } else {
-            // ---- R: r = b - A t, after the t units it reads are published
-            if (tid < 64) {
-                const int64_t need[5] = {g - js.ub, g - 1, g, g + 1, g + js.ub};
-                const bool ok = jr_wait5(flags, need, (int64_t)js.nb * js.ub, err);
-                if (tid == 0 && !ok) s_abort = 1;
-            }
-            __syncthreads();
-            if (!s_abort) {
-#pragma unroll
-                for (int c = 0; c < NU; ++c) {
-                    const int o = sd.off[NU - 1 - c];
-                    const double2 tl = jr_tany(rt, i0 - o);
-                    const double2 tu = jr_tany(rt, i0 + sd.off[c]);
-                    xv[0][c] = tl.x;
-                    xv[1][c] = tl.y;
-                    xv[0][NU + 1 + c] = tu.x;
-                    xv[1][NU + 1 + c] = tu.y;
-                }
-                const double2 tc = jr_tpair(rt, i0);
-                xv[0][NU] = tc.x;
-                xv[1][NU] = tc.y;
-                double out[2];
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    double s = 0.0;
-#pragma unroll
-                    for (int kk = 0; kk < 2 * NU + 1; ++kk) {
-                        const double pr = v[q][kk] * xv[q][kk];
-                        const double tt = s + pr;
-                        s = ((m[q] >> kk) & 1u) ? tt : s;
-                    }
-                    out[q] = pb[q] - s;
-                }
-                *reinterpret_cast<double2*>(r + i0) = make_double2(out[0], out[1]);
-            }
+            const double u = c.b[r] - s;
+            const double w = omega * u;
+            const double q = w / c.v[r][3];
+            out[r] = xv[r][3] + q;
         }
-        __syncthreads();  // s_item / s_abort are rewritten by the next item
     }
 }
 
-// k_sym_chain: S (2 or 3) dependent sweeps over the symmetric layout in ONE pipelined pass — the
-// generalisation of k_sym_jr with an explicit per-queue item list (ChainArgs::items: stage << 28
-// | global unit, built on the host, runtime.hip build_chain): stage 0 reads in0 with plain loads
-// and every later stage reads its predecessor's output through sc1 16-B buffer loads after
-// polling the predecessor's flags of the units it reads (g, g +- 1, g +- one band); outputs
-// consumed inside the launch are published write-through (sc1 stores, drained, barrier, one
-// agent flag store), the last stage's output with plain stores. Stages are weighted-Jacobi
-// sweeps, the last one optionally the residual. Every wait is on an item placed earlier in the
-// merged item timeline of some queue, so the pipeline drains; spins are bounded. No buffer is
-// both read with plain loads and rewritten inside one launch (the caller rotates buffers), so
-// no XCD's L2 can hold a stale copy of a handed-off line. (ChainArgs: pamg_device.h)
+template <int S>
+struct TbCtx {
+    int nx, ny, nz, zs, ze, kend;
+    int64_t M, n;
+    int ry, col;
+    int64_t ixy;          // y * nx + x of the pair's first row
+    bool pos_ok, own_xy;
+};
 
-template <int NU>
-__global__ __launch_bounds__(kJrThreads) void k_sym_chain(int nrows, const uint8_t* __restrict__ mask,
-                                                         const double* __restrict__ dg,
-                                                         const double* __restrict__ up, int64_t ld,
-                                                         const SymDia sd, const ChainArgs ca) {
-    __shared__ int s_item;
-    __shared__ int s_abort;
+// the 7 neighbour values of a row pair from an LDS plane ring (planes p-1, p, p+1 in slots
+// sm, s0, sp; lines ry-1, ry, ry+1)
+template <int RY>
+__device__ __forceinline__ void tb_gather_lds(const double (*ring)[RY][kTbLW], int sm, int s0, int sp, int ry, int col,
+                                              double (&xv)[2][7]) {
+    const double2 own = *reinterpret_cast<const double2*>(&ring[s0][ry][col]);
+    const double2 lft = *reinterpret_cast<const double2*>(&ring[s0][ry][col - 2]);
+    const double2 rgt = *reinterpret_cast<const double2*>(&ring[s0][ry][col + 2]);
+    const double2 dn = *reinterpret_cast<const double2*>(&ring[s0][ry - 1][col]);
+    const double2 upl = *reinterpret_cast<const double2*>(&ring[s0][ry + 1][col]);
+    const double2 zl = *reinterpret_cast<const double2*>(&ring[sm][ry][col]);
+    const double2 zh = *reinterpret_cast<const double2*>(&ring[sp][ry][col]);
+    xv[0][0] = zl.x;  xv[1][0] = zl.y;
+    xv[0][1] = dn.x;  xv[1][1] = dn.y;
+    xv[0][2] = lft.y; xv[1][2] = own.x;
+    xv[0][3] = own.x; xv[1][3] = own.y;
+    xv[0][4] = own.y; xv[1][4] = rgt.x;
+    xv[0][5] = upl.x; xv[1][5] = upl.y;
+    xv[0][6] = zh.x;  xv[1][6] = zh.y;
+}
+
+template <int S>
+__device__ __forceinline__ void tb_step(int k, TbCoef& cA, TbCoef& cB, TbCoef& cC, const TbCtx<S>& t,
+                                        const uint8_t* __restrict__ mask, const double* __restrict__ dg,
+                                        const double* __restrict__ up, int64_t ld, const SymDia& sd,
+                                        const TbArgs& ta, double (*l0)[TbShape<S>::RY][kTbLW],
+                                        double (*l1)[TbShape<S>::RY][kTbLW]) {
+    using Sh = TbShape<S>;
+    if (k >= t.kend) return;  // uniform: the whole workgroup
+    // ---- stage 0 on plane k: a Jacobi sweep from in0 (global: never written in this launch)
+    {
+        double o[2] = {0.0, 0.0};
+        if (t.pos_ok && k >= 0 && k < t.nz) {
+            const int64_t i = (int64_t)k * t.M + t.ixy;
+            tb_load(cA, mask, dg, up, ld, sd, ta.b, i, t.n);
+            double xv[2][7];
+            const double* x = ta.in0;
+            const double2 zl = ld_pair(x, i - t.M, t.n, true);
+            const double2 dn = ld_pair(x, i - t.nx, t.n, true);
+            const double2 lf = ld_pair(x, i - 1, t.n, false);
+            const double2 ow = *reinterpret_cast<const double2*>(x + i);
+            const double2 rg = ld_pair(x, i + 1, t.n, false);
+            const double2 upl = ld_pair(x, i + t.nx, t.n, true);
+            const double2 zh = ld_pair(x, i + t.M, t.n, true);
+            xv[0][0] = zl.x;  xv[1][0] = zl.y;
+            xv[0][1] = dn.x;  xv[1][1] = dn.y;
+            xv[0][2] = lf.x;  xv[1][2] = lf.y;
+            xv[0][3] = ow.x;  xv[1][3] = ow.y;
+            xv[0][4] = rg.x;  xv[1][4] = rg.y;
+            xv[0][5] = upl.x; xv[1][5] = upl.y;
+            xv[0][6] = zh.x;  xv[1][6] = zh.y;
+            tb_rows(cA, xv, S == 1 && ta.last_resid, ta.omega, o);
+            if (t.own_xy && k >= t.zs && k < t.ze) *reinterpret_cast<double2*>(ta.out[0] + i) = make_double2(o[0], o[1]);
+        }
+        if (t.ry >= 0) *reinterpret_cast<double2*>(&l0[tb_mod3(k)][t.ry][t.col]) = make_double2(o[0], o[1]);
+    }
+    __syncthreads();
+    // ---- stage 1 on plane k-1 from stage 0's ring
+    {
+        const int p = k - 1;
+        constexpr bool last = S == 2;
+        constexpr int hz = Sh::H - 1;  // planes / lines of halo stage 1 still needs
+        double o[2] = {0.0, 0.0};
+        const bool act = t.pos_ok && t.ry >= 1 && t.ry < Sh::RY - 1 && p >= 0 && p < t.nz && p >= t.zs - hz &&
+                         p < t.ze + hz && (!last || t.own_xy);
+        if (act) {
+            double xv[2][7];
+            tb_gather_lds<Sh::RY>(l0, tb_mod3(p - 1), tb_mod3(p), tb_mod3(p + 1), t.ry, t.col, xv);
+            tb_rows(cB, xv, last && ta.last_resid, ta.omega, o);
+            if (t.own_xy && p >= t.zs && p < t.ze)
+                *reinterpret_cast<double2*>(ta.out[1] + (int64_t)p * t.M + t.ixy) = make_double2(o[0], o[1]);
+        }
+        if constexpr (S == 3) {
+            if (t.ry >= 0) *reinterpret_cast<double2*>(&l1[tb_mod3(p)][t.ry][t.col]) = make_double2(o[0], o[1]);
+        }
+    }
+    __syncthreads();  // S = 3: stage 2 reads l1; S = 2: the next step's stage 0 rewrites l0
+    // ---- stage 2 on plane k-2 from stage 1's ring (S = 3)
+    if constexpr (S == 3) {
+        const int p = k - 2;
+        if (t.own_xy && t.ry >= 2 && t.ry < Sh::RY - 2 && p >= t.zs && p < t.ze) {
+            double xv[2][7], o[2];
+            tb_gather_lds<Sh::RY>(l1, tb_mod3(p - 1), tb_mod3(p), tb_mod3(p + 1), t.ry, t.col, xv);
+            tb_rows(cC, xv, ta.last_resid, ta.omega, o);
+            *reinterpret_cast<double2*>(ta.out[2] + (int64_t)p * t.M + t.ixy) = make_double2(o[0], o[1]);
+        }
+    }
+}
+
+template <int S>
+__global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tb(int nrows, const uint8_t* __restrict__ mask,
+                                                                 const double* __restrict__ dg,
+                                                                 const double* __restrict__ up, int64_t ld,
+                                                                 const SymDia sd, const TbArgs ta) {
+    using Sh = TbShape<S>;
+    __shared__ __attribute__((aligned(16))) double l0[3][Sh::RY][kTbLW];
+    __shared__ __attribute__((aligned(16))) double l1[S == 3 ? 3 : 1][Sh::RY][kTbLW];
+    const TbGeom& g = sd.tb;
+    // tile: consecutive tiles (shared halos) on one XCD (block b runs on XCD b % 8; speed only)
+    const int ntiles = g.tiles_x * g.tiles_y * g.zchunks;
+    const int per = (ntiles + 7) / 8;
+    const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (lin >= ntiles) return;  // the whole workgroup, before any barrier
+    const int tx = lin % g.tiles_x, ty = (lin / g.tiles_x) % g.tiles_y, zc = lin / (g.tiles_x * g.tiles_y);
+    const int x0 = tx * kTbX, y0 = ty * kTbY;
+    TbCtx<S> t;
+    t.nx = g.nx;
+    t.ny = g.ny;
+    t.nz = g.nz;
+    t.zs = zc * g.zlen;
+    t.ze = min(t.zs + g.zlen, g.nz);
+    t.kend = t.ze + Sh::H;
+    t.M = (int64_t)g.nx * g.ny;
+    t.n = nrows;
     const int tid = threadIdx.x;
-    const int q = blockIdx.x & 7;
-    unsigned* head = ca.sync + 16 * q;
-    unsigned* flags = ca.sync + 128;
-    const int* items = ca.items + (size_t)q * ca.per_queue;
-    const int64_t n = nrows;
-    __amdgpu_buffer_rsrc_t rin[3], rout[3];
-#pragma unroll
-    for (int st = 0; st < 3; ++st) {
-        rout[st] = __builtin_amdgcn_make_buffer_rsrc((void*)ca.out[st], 0, (int)(8 * n), 0x00020000);
-        rin[st] = st == 0 ? __builtin_amdgcn_make_buffer_rsrc((void*)ca.in0, 0, (int)(8 * n), 0x00020000) : rout[st - 1];
-    }
-    int next_item = -1;
-    if (tid == 0) {
-        const int t0 = (int)atomicAdd(head, 1u);
-        next_item = t0 < ca.per_queue ? items[t0] : -1;
-    }
-    for (;;) {
-        if (tid == 0) {
-            s_item = next_item;
-            s_abort = 0;
-            if (next_item >= 0) {  // the following item, in flight during this one
-                const int t1 = (int)atomicAdd(head, 1u);
-                next_item = t1 < ca.per_queue ? items[t1] : -1;
-            }
-        }
-        __syncthreads();
-        const int it = s_item;
-        if (it < 0) break;
-        const int st = it >> 28;
-        const int64_t g = it & 0x0FFFFFFF;
-        const int64_t i0 = g * kJrRows + 2 * tid;
-        const bool resid = ca.last_resid && st == ca.nstages - 1;
-        const bool publish = st < ca.nstages - 1;
-        uint32_t m[2];
-        SymMask<NU>::two(mask, i0, m);
-        double v[2][2 * NU + 1], xv[2][2 * NU + 1], pb[2];
-        {
-            const double2 d2 = *reinterpret_cast<const double2*>(dg + i0);
-            const double2 b2 = *reinterpret_cast<const double2*>(ca.b + i0);
-            v[0][NU] = d2.x;
-            v[1][NU] = d2.y;
-            pb[0] = b2.x;
-            pb[1] = b2.y;
-        }
-#pragma unroll
-        for (int c = 0; c < NU; ++c) {
-            const double2 a = *reinterpret_cast<const double2*>(up + (size_t)c * ld + i0);
-            v[0][NU + 1 + c] = a.x;
-            v[1][NU + 1 + c] = a.y;
-            const int o = sd.off[c];
-            const double2 lo = ld_pair(up + (size_t)c * ld, i0 - o, n, (o & 1) == 0);
-            v[0][NU - 1 - c] = lo.x;
-            v[1][NU - 1 - c] = lo.y;
-        }
-        if (st > 0) {  // the predecessor's units this item reads
-            if (tid < 64) {
-                const int64_t need[5] = {g - ca.ub, g - 1, g, g + 1, g + ca.ub};
-                const bool ok = jr_wait5(flags + (size_t)(st - 1) * ca.nunits, need, ca.nunits, ca.err);
-                if (tid == 0 && !ok) s_abort = 1;
-            }
-            __syncthreads();
-        }
-        if (!s_abort) {
-            if (st == 0) {
-#pragma unroll
-                for (int c = 0; c < NU; ++c) {
-                    const int o = sd.off[c];
-                    const double2 xl = ld_pair(ca.in0, i0 - o, n, (o & 1) == 0);
-                    const double2 xu = ld_pair(ca.in0, i0 + o, n, (o & 1) == 0);
-                    xv[0][NU - 1 - c] = xl.x;
-                    xv[1][NU - 1 - c] = xl.y;
-                    xv[0][NU + 1 + c] = xu.x;
-                    xv[1][NU + 1 + c] = xu.y;
-                }
-                const double2 xc = *reinterpret_cast<const double2*>(ca.in0 + i0);
-                xv[0][NU] = xc.x;
-                xv[1][NU] = xc.y;
-            } else {
-                const __amdgpu_buffer_rsrc_t ri = st == 1 ? rin[1] : rin[2];
-#pragma unroll
-                for (int c = 0; c < NU; ++c) {
-                    const int o = sd.off[c];
-                    const double2 tl = jr_tany(ri, i0 - o);
-                    const double2 tu = jr_tany(ri, i0 + o);
-                    xv[0][NU - 1 - c] = tl.x;
-                    xv[1][NU - 1 - c] = tl.y;
-                    xv[0][NU + 1 + c] = tu.x;
-                    xv[1][NU + 1 + c] = tu.y;
-                }
-                const double2 tc = jr_tpair(ri, i0);
-                xv[0][NU] = tc.x;
-                xv[1][NU] = tc.y;
-            }
-            double out[2];
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                double sum = 0.0;
-#pragma unroll
-                for (int kk = 0; kk < 2 * NU + 1; ++kk) {
-                    const double pr = v[r][kk] * xv[r][kk];
-                    const double tt = sum + pr;
-                    sum = ((m[r] >> kk) & 1u) ? tt : sum;
-                }
-                if (resid) {
-                    out[r] = pb[r] - sum;
-                } else {
-                    const double u = pb[r] - sum;
-                    const double w = ca.omega * u;
-                    const double qq = w / v[r][NU];
-                    out[r] = xv[r][NU] + qq;
-                }
-            }
-            if (publish) {
-                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-                u32x4 pk;
-                __builtin_memcpy(&pk, out, 16);
-                const __amdgpu_buffer_rsrc_t ro = st == 0 ? rout[0] : rout[1];
-                __builtin_amdgcn_raw_buffer_store_b128(pk, ro, (int)(i0 * 8), 0, 16 /* sc1 */);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-            } else {
-                *reinterpret_cast<double2*>(ca.out[st] + i0) = make_double2(out[0], out[1]);
-            }
-        }
-        if (publish) {
-            __syncthreads();
-            if (tid == 0 && !s_abort)
-                __hip_atomic_store(flags + (size_t)st * ca.nunits + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();  // s_item / s_abort are rewritten by the next item
+    const bool has = tid < Sh::NT;
+    const int px = has ? tid % kTbPX : 0;
+    t.ry = has ? tid / kTbPX : -1;
+    const int x = x0 - 2 + 2 * px, y = y0 - Sh::H + (has ? t.ry : 0);
+    t.col = 2 * px + 2;
+    t.ixy = (int64_t)y * g.nx + x;
+    t.pos_ok = has && x >= 0 && x < g.nx && y >= 0 && y < g.ny;
+    t.own_xy = t.pos_ok && px >= 1 && px <= kTbX / 2 && y >= y0 && y < y0 + kTbY;
+    TbCoef c0, c1, c2;  // planes k, k-1, k-2 at step k (rotated by the unrolled loop)
+    for (int k = t.zs - Sh::H; k < t.kend; k += 3) {
+        tb_step<S>(k, c0, c2, c1, t, mask, dg, up, ld, sd, ta, l0, l1);
+        tb_step<S>(k + 1, c1, c0, c2, t, mask, dg, up, ld, sd, ta, l0, l1);
+        tb_step<S>(k + 2, c2, c1, c0, t, mask, dg, up, ld, sd, ta, l0, l1);
     }
 }
 
@@ -1465,28 +1284,14 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
 }
 }  // namespace
 
-void launch_sym_jr(const pamg_mat& A, const double* x, const double* b, double* t, double* r, double omega,
-                   unsigned* sync, size_t sync_bytes, unsigned* err, int grid, hipStream_t s) {
+void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s) {
     const SymDia& sd = A.sym;
-    (void)hipMemsetAsync(sync, 0, sync_bytes, s);
-    switch (sd.nu) {
-        case 1: k_sym_jr<1><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, sd.jr,
-                                                        x, b, t, r, omega, sync, err); break;
-        case 2: k_sym_jr<2><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, sd.jr,
-                                                        x, b, t, r, omega, sync, err); break;
-        default: k_sym_jr<3><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, sd.jr,
-                                                          x, b, t, r, omega, sync, err); break;
-    }
-}
-
-void launch_sym_chain(const pamg_mat& A, const ChainArgs& ca, size_t sync_bytes, int grid, hipStream_t s) {
-    const SymDia& sd = A.sym;
-    (void)hipMemsetAsync(ca.sync, 0, sync_bytes, s);
-    switch (sd.nu) {
-        case 1: k_sym_chain<1><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, ca); break;
-        case 2: k_sym_chain<2><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, ca); break;
-        default: k_sym_chain<3><<<grid, kJrThreads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, ca); break;
-    }
+    const int ntiles = sd.tb.tiles_x * sd.tb.tiles_y * sd.tb.zchunks;
+    const int grid = (ntiles + 7) / 8 * 8;
+    if (ta.nstages == 2)
+        k_sym_tb<2><<<grid, TbShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, ta);
+    else
+        k_sym_tb<3><<<grid, TbShape<3>::threads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, ta);
 }
 
 void launch_rows(const pamg_mat& A, const TileSet& ts, int op, const double* x, const double* b,

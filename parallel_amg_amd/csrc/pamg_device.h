@@ -113,8 +113,8 @@ struct Options {
     int poison_ghosts = 0;     // 1 (debug): NaN-fill ghost slots before each exchange
     int sym_dia = 1;           // 1: symmetric diagonal-class layout for stencil-shaped symmetric operators
     int sym_rows = 2;          // rows per lane of its kernel (1 | 2)
-    int jr_fuse = 0;           // 1: fused level-0 Jacobi -> residual / cross-cycle pipeline where the layout allows
-                               //    (opt-in: measured slower than the separate sweeps so far)
+    int jr_fuse = 1;           // 1: temporally blocked level-0 Jacobi -> residual / cross-cycle pipeline where the
+                               //    operator is a grid stencil (k_sym_tb)
 };
 
 // Symmetric diagonal-class layout (k_rows_sym): a square operator whose interior rows use at
@@ -126,10 +126,15 @@ struct Options {
 // NU+1 values per row instead of 2*NU+1, with no column stream at all. (Where 2*NU+1 <= 7 the
 // mask is one byte, the set flag in bit 7.)
 constexpr int kSymMaxU = 7;
-// Schedule of the fused Jacobi -> residual kernel (kernels.hip k_sym_jr): units of 2048 rows,
-// ub per band, e per queue (XCD eighth) per band, nb bands, R items lag T items by `lag` units.
-struct JrSched {
-    int ub = 0, e = 0, nb = 0, lag = 0;
+// Temporal blocking of S dependent row sweeps (kernels.hip k_sym_tb): the operator is a 7-point
+// grid stencil in natural order — classes {1, nx, nx*ny}, n = nx*ny*nz, and no row reaching
+// across a grid line or plane (checked at upload) — so a workgroup owns a kTbX x kTbY column of
+// the grid over a range of planes and streams it along z, computing the earlier sweeps on a
+// halo it recomputes itself. No data passes between workgroups inside a launch.
+struct TbGeom {
+    int nx = 0, ny = 0, nz = 0;
+    int tiles_x = 0, tiles_y = 0;   // kTbX x kTbY tiles of a plane
+    int zchunks = 1, zlen = 0;      // planes per workgroup (the last chunk may be shorter)
 };
 struct SymDia {
     int nu = 0;                     // upper offset classes
@@ -137,19 +142,9 @@ struct SymDia {
     int64_t ld = 0;                 // leading dimension of the U arrays
     int band = 0, band_blocks = 0, eighth = 0, nbands = 0;  // XCD-banded block order
     int rpl = 1;                    // rows per lane (k_rows_sym / k_rows_sym2)
-    // fused Jacobi -> residual (Options::jr_fuse; one part, every row in the set, 2 nu + 1 <= 7,
-    // bands of a multiple of 8 x 2048 rows, every offset < 2048 or = the band)
-    bool jr_ok = false;
-    JrSched jr;
-    unsigned* d_jr_sync = nullptr;  // queue heads (8 lines) + one flag per unit; zeroed per launch
-    size_t jr_sync_bytes = 0;
-    unsigned* d_jr_err = nullptr;   // set by a timed-out spin; checked by the host
-    int jr_grid = 0;
-    // k_sym_chain item lists (stage << 28 | unit), 8 queues each: 2 stages (Jacobi -> residual)
-    // and 3 stages (Jacobi -> Jacobi -> residual: one cycle's post-smoothing + the next cycle's
-    // pre-smoothing and residual)
-    int* d_chain_items[4] = {nullptr, nullptr, nullptr, nullptr};
-    int chain_per_queue[4] = {0, 0, 0, 0};
+    // temporally blocked sweeps (Options::jr_fuse; one part, every row in the set, nu = 3)
+    bool tb_ok = false;
+    TbGeom tb;
     uint8_t* d_mask = nullptr;      // nrows (+ pad) masks of 1 byte (2 nu + 1 <= 7) or 2 bytes
     int mask_bytes = 2;
     double* d_diag = nullptr;       // nrows (+ pad)
@@ -231,25 +226,19 @@ void launch_dense_gemv(int64_t n_rows, int64_t n_cols, int64_t row0, const doubl
                        const double* b, double* y, hipStream_t s);
 void launch_pack(int64_t n, const int* idx, const double* x, double* out, hipStream_t s);
 void launch_fill(int64_t n, double v, double* y, hipStream_t s);
-// k_sym_chain arguments (kernels.hip)
-struct ChainArgs {
-    const int* items = nullptr;  // 8 queues x per_queue items
-    int per_queue = 0;
-    int ub = 0;                  // units per band
-    int nunits = 0;
+// S (2 | 3) dependent sweeps in one temporally blocked launch (k_sym_tb; A.sym.tb_ok): stage 0
+// is a weighted-Jacobi sweep from in0 into out[0]; stage s > 0 reads stage s-1's result, a
+// Jacobi sweep into out[s], the last one the residual b - A t when last_resid.
+struct TbArgs {
     int nstages = 0;
     bool last_resid = false;
     const double* in0 = nullptr;
     double* out[3] = {nullptr, nullptr, nullptr};
     const double* b = nullptr;
     double omega = 0.0;
-    unsigned* sync = nullptr;    // 8 queue heads (one 64-B line each), then (nstages-1) x nunits flags
-    unsigned* err = nullptr;
 };
-void launch_sym_chain(const pamg_mat& A, const ChainArgs& ca, size_t sync_bytes, int grid, hipStream_t s);
-// t = Jacobi(x), r = b - A t in one launch (k_sym_jr; A.sym.jr_ok)
-void launch_sym_jr(const pamg_mat& A, const double* x, const double* b, double* t, double* r, double omega,
-                   unsigned* sync, size_t sync_bytes, unsigned* err, int grid, hipStream_t s);
+constexpr int kTbX = 64, kTbY = 16;  // output tile of a workgroup (grid points in x, y)
+void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s);
 // dst[i] = src[perm[i]] (gather), or dst[perm[i]] = src[i] (scatter)
 void launch_permute(int64_t n, const int* perm, const double* src, double* dst, bool scatter, hipStream_t s);
 void launch_axpby(int64_t n, double a, const double* x, double b, double* y, hipStream_t s);

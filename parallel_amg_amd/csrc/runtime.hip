@@ -863,53 +863,41 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
     }
     CHECK(h2d(A->ctx, sd.d_diag, dg.data(), sizeof(double) * dg.size()));
     CHECK(h2d(A->ctx, sd.d_upper, up.data(), sizeof(double) * up.size()));
-    // fused Jacobi -> residual schedule (kernels.hip k_sym_jr): one part with every row in the
-    // set, byte masks, bands of whole 8 x 2048-row eighths, every offset inside a unit's
-    // neighbours or exactly one band, byte offsets within int32 (buffer descriptors)
-    // The schedule's band is the largest offset M (one grid plane): a unit's rows then read
-    // units g - ub, g -+ 1 and g + ub only, when every other offset stays inside one unit.
-    {
-        constexpr int64_t kUnit = 2048;
-        const int64_t M = sd.off[nu - 1];
-        bool ok = A->ncols == n && (int64_t)inner.size() == n && mb == 1 && M % (8 * kUnit) == 0 &&
-                  n % M == 0 && 8 * (n + 64) < INT32_MAX;
-        for (int c = 0; c + 1 < nu && ok; ++c) ok = sd.off[c] < kUnit;
-        if (ok) {
-            sd.jr.ub = (int)(M / kUnit);
-            sd.jr.e = sd.jr.ub / 8;
-            sd.jr.nb = (int)(n / M);
-            sd.jr.lag = std::min(4, sd.jr.e);
-            // chain item lists: stage s runs D = e + lag items (one band + lag units) behind
-            // stage s-1 in the queue's timeline, so every unit a stage reads from its
-            // predecessor (same band +- 1 unit, +- one band) sits at an earlier slot
-            {
-                const int e = sd.jr.e, per = sd.jr.nb * e, D = e + sd.jr.lag;
-                for (int S = 2; S <= 3; ++S) {
-                    std::vector<int> items;
-                    items.reserve((size_t)8 * S * per);
-                    for (int q = 0; q < 8; ++q) {
-                        const size_t q0 = items.size();
-                        for (int tau = 0; tau < per + (S - 1) * D; ++tau)
-                            for (int st = 0; st < S; ++st) {
-                                const int P = tau - st * D;
-                                if (P < 0 || P >= per) continue;
-                                const int64_t g = (int64_t)(P / e) * sd.jr.ub + (int64_t)q * e + P % e;
-                                items.push_back((st << 28) | (int)g);
-                            }
-                        if (items.size() - q0 != (size_t)S * per) return fail(PAMG_E_STATE, "chain items");
-                    }
-                    sd.chain_per_queue[S] = S * per;
-                    CHECK(dalloc(&sd.d_chain_items[S], (int64_t)items.size()));
-                    HIPC(hipMemcpy(sd.d_chain_items[S], items.data(), sizeof(int) * items.size(), hipMemcpyHostToDevice));
+    // temporally blocked sweeps (kernels.hip k_sym_tb): one part with every row in the set, a
+    // 7-point grid stencil in natural order (classes 1, nx, nx*ny; n = nx*ny*nz) whose rows
+    // never reach across a grid line (the -1 / +1 / -nx / +nx classes absent at x = 0 / nx-1 /
+    // y = 0 / ny-1), tiles of kTbX x kTbY
+    if (nu == 3 && mb == 1 && A->ncols == n && (int64_t)inner.size() == n && sd.off[0] == 1 &&
+        sd.off[2] % sd.off[1] == 0 && n % sd.off[2] == 0) {
+        const int nx = sd.off[1], ny = sd.off[2] / sd.off[1];
+        const int nz = (int)(n / sd.off[2]);
+        bool ok = nx % pamg::kTbX == 0 && ny % pamg::kTbY == 0;
+        std::atomic<bool> cross{false};
+        if (ok)
+            par_for(n, [&](int64_t a0, int64_t b0) {
+                for (int64_t i = a0; i < b0 && !cross; ++i) {
+                    const int x = (int)(i % nx), y = (int)((i / nx) % ny);
+                    const uint32_t m = mask[i];  // ascending classes -M, -nx, -1, 0, 1, nx, M
+                    if (((m & 4u) && x == 0) || ((m & 16u) && x == nx - 1) || ((m & 2u) && y == 0) ||
+                        ((m & 32u) && y == ny - 1))
+                        cross = true;
                 }
-            }
-            const int64_t words = 128 + 2 * (int64_t)sd.jr.nb * sd.jr.ub;  // flags of up to 2 publishing stages
-            sd.jr_sync_bytes = (size_t)((words * 4 + 15) / 16 * 16);
-            CHECK(dalloc(reinterpret_cast<char**>(&sd.d_jr_sync), (int64_t)sd.jr_sync_bytes));
-            CHECK(dalloc(&sd.d_jr_err, 4));
-            HIPC(hipMemset(sd.d_jr_err, 0, 16));
-            sd.jr_grid = std::max(8, device_cus() / 8 * 8);
-            sd.jr_ok = true;
+            });
+        if (ok && !cross) {
+            pamg::TbGeom& g = sd.tb;
+            g.nx = nx;
+            g.ny = ny;
+            g.nz = nz;
+            g.tiles_x = nx / pamg::kTbX;
+            g.tiles_y = ny / pamg::kTbY;
+            // about one workgroup per CU (one fits: registers), planes split when a plane has
+            // fewer tiles than the chip has CUs
+            const int tiles = g.tiles_x * g.tiles_y;
+            const int want = std::max(1, (device_cus() + tiles - 1) / tiles);
+            g.zchunks = std::max(1, std::min(want, nz / 4 > 0 ? nz / 4 : 1));
+            g.zlen = (nz + g.zchunks - 1) / g.zchunks;
+            g.zchunks = (nz + g.zlen - 1) / g.zlen;
+            sd.tb_ok = true;
         }
     }
     A->sym = sd;
@@ -1199,13 +1187,20 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false,
             continue;
         }
         // level 0, V(1, nu2) from a given guess: the pre-smoothing sweep and the residual in one
-        // pipelined pass (k_sym_jr; both timed as jacobi_pre)
+        // temporally blocked pass (k_sym_tb, S = 2; both timed as jacobi_pre)
         const bool fuse = l == 0 && !zero0 && H->nu1 == 1 && pamg::options().jr_fuse && A->interior.sym &&
-                          A->sym.jr_ok && !(A->plan && !A->plan->nbr.empty());
+                          A->sym.tb_ok && !(A->plan && !A->plan->nbr.empty());
         if (fuse) {
             ProfScope p(H, l, 0, s);
-            pamg::launch_sym_jr(*A, H->x[0], H->b[0], c, o, H->omega[0], A->sym.d_jr_sync, A->sym.jr_sync_bytes,
-                                A->sym.d_jr_err, A->sym.jr_grid, s);
+            pamg::TbArgs ta;
+            ta.nstages = 2;
+            ta.last_resid = true;
+            ta.in0 = H->x[0];
+            ta.out[0] = c;
+            ta.out[1] = o;
+            ta.b = H->b[0];
+            ta.omega = H->omega[0];
+            pamg::launch_sym_tb(*A, ta, s);
             HIPC(hipGetLastError());
         } else {
             ProfScope p(H, l, 0, s);
@@ -1882,9 +1877,6 @@ int pamg_mat_destroy(pamg_mat* A) {
     dfree(A->sym.d_mask);
     dfree(A->sym.d_diag);
     dfree(A->sym.d_upper);
-    if (A->sym.d_jr_sync) (void)hipFree(A->sym.d_jr_sync);
-    for (int k = 0; k < 4; ++k) dfree(A->sym.d_chain_items[k]);
-    dfree(A->sym.d_jr_err);
     free_tiles(A->interior);
     free_tiles(A->boundary);
     delete A;
@@ -1918,7 +1910,7 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[7] = t.tile_nnz;
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
-             (t.sym && A->sym.jr_ok ? 32 : 0);
+             (t.sym && A->sym.tb_ok ? 32 : 0);
     if (t.sym) {  // the symmetric diagonal-class layout: upper classes, k_rows_sym's grid
         out[4] = A->sym.nu;
         out[8] = A->sym.nbands * 8 * A->sym.eighth;
@@ -1992,10 +1984,17 @@ int pamg_jacobi_residual(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pa
     if (b->n_own != A->nrows || r->n_own != A->nrows || t == x || r == x || r == t || b == t || b == r)
         return fail(PAMG_E_ARG, "jacobi_residual: size mismatch or aliasing");
     CHECK(set_device(ctx));
-    const bool fuse = pamg::options().jr_fuse && A->interior.sym && A->sym.jr_ok && !(A->plan && !A->plan->nbr.empty());
+    const bool fuse = pamg::options().jr_fuse && A->interior.sym && A->sym.tb_ok && !(A->plan && !A->plan->nbr.empty());
     if (fuse) {
-        pamg::launch_sym_jr(*A, x->d, b->d, t->d, r->d, omega, A->sym.d_jr_sync, A->sym.jr_sync_bytes,
-                            A->sym.d_jr_err, A->sym.jr_grid, ctx->s_comp);
+        pamg::TbArgs ta;
+        ta.nstages = 2;
+        ta.last_resid = true;
+        ta.in0 = x->d;
+        ta.out[0] = t->d;
+        ta.out[1] = r->d;
+        ta.b = b->d;
+        ta.omega = omega;
+        pamg::launch_sym_tb(*A, ta, ctx->s_comp);
         HIPC(hipGetLastError());
     } else {
         CHECK(apply(ctx, A, pamg::OP_JACOBI, x->d, b->d, t->d, omega));
@@ -2003,11 +2002,6 @@ int pamg_jacobi_residual(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pa
     }
     if (fused) *fused = fuse ? 1 : 0;
     HIPC(hipStreamSynchronize(ctx->s_comp));
-    if (fuse) {
-        unsigned e = 0;
-        HIPC(hipMemcpy(&e, A->sym.d_jr_err, sizeof(unsigned), hipMemcpyDeviceToHost));
-        if (e) return fail(PAMG_E_STATE, "jacobi_residual: the fused kernel timed out waiting for a unit");
-    }
     return PAMG_OK;
 }
 
@@ -2255,23 +2249,16 @@ int pamg_hier_profile_read(pamg_hier* H, double* out) {
 // (t_prev -> x), this cycle's pre-smoothing (x -> t_next) and residual (t_next -> r[0]).
 static void launch_chain3(pamg_hier* H, double* x, const double* b, const double* t_prev, double* t_next) {
     const pamg_mat* A = H->A[0];
-    const pamg::SymDia& sd = A->sym;
-    pamg::ChainArgs ca;
-    ca.items = sd.d_chain_items[3];
-    ca.per_queue = sd.chain_per_queue[3];
-    ca.ub = sd.jr.ub;
-    ca.nunits = sd.jr.nb * sd.jr.ub;
-    ca.nstages = 3;
-    ca.last_resid = true;
-    ca.in0 = t_prev;
-    ca.out[0] = x;
-    ca.out[1] = t_next;
-    ca.out[2] = H->r[0];
-    ca.b = b;
-    ca.omega = H->omega[0];
-    ca.sync = sd.d_jr_sync;
-    ca.err = sd.d_jr_err;
-    pamg::launch_sym_chain(*A, ca, sd.jr_sync_bytes, sd.jr_grid, H->ctx->s_comp);
+    pamg::TbArgs ta;
+    ta.nstages = 3;
+    ta.last_resid = true;
+    ta.in0 = t_prev;
+    ta.out[0] = x;
+    ta.out[1] = t_next;
+    ta.out[2] = H->r[0];
+    ta.b = b;
+    ta.omega = H->omega[0];
+    pamg::launch_sym_tb(*A, ta, H->ctx->s_comp);
 }
 
 // Segments of the cross-cycle pipeline. seg 0: head (first cycle, no level-0 post-smoothing,
@@ -2305,8 +2292,7 @@ static bool pipe_ok(const pamg_hier* H, int ncycles, bool zero0) {
     if (zero0 || ncycles < 2 || H->L < 2 || H->prof || !pamg::options().jr_fuse || H->nu1 != 1 || H->nu2 != 1)
         return false;
     const pamg_mat* A = H->A[0];
-    return H->ctx->nranks == 1 && A->interior.sym && A->sym.jr_ok && A->sym.d_chain_items[3] &&
-           !(A->plan && !A->plan->nbr.empty());
+    return H->ctx->nranks == 1 && A->interior.sym && A->sym.tb_ok && !(A->plan && !A->plan->nbr.empty());
 }
 
 static int vcycle_pipe(pamg_hier* H, double* x, const double* b, int ncycles) {
@@ -2421,18 +2407,6 @@ struct DeviceSpace {
     }
 };
 
-// A timed-out spin of the fused Jacobi -> residual kernel (never expected: its queues drain by
-// construction) leaves the error word set; the synchronous entry points report it.
-static int check_jr_err(pamg_hier* H) {
-    const pamg_mat* A0 = H->A[0];
-    if (!A0->sym.d_jr_err) return PAMG_OK;
-    unsigned e = 0;
-    HIPC(hipMemcpy(&e, A0->sym.d_jr_err, sizeof(unsigned), hipMemcpyDeviceToHost));
-    if (e) return fail(PAMG_E_STATE, "vcycle: the fused Jacobi-residual kernel timed out waiting for a unit "
-                                     "(set option jr_fuse=0)");
-    return PAMG_OK;
-}
-
 static int vcycle_common(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int ncycles) {
     if (!ctx || !H || !x || !b || ncycles < 0 || H->ctx != ctx) return fail(PAMG_E_ARG, "vcycle: bad args");
     const pamg_mat* A0 = H->A[0];
@@ -2455,7 +2429,7 @@ int pamg_vcycle(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int
     if (!res_hist) {
         CHECK(vcycle_common(ctx, H, x, b, ncycles));
         HIPC(hipStreamSynchronize(ctx->s_comp));
-        return check_jr_err(H);
+        return PAMG_OK;
     }
     if (!ctx || !H || !x || !b || ncycles < 0 || H->ctx != ctx) return fail(PAMG_E_ARG, "vcycle: bad args");
     if (H->L < 1 || (!H->t[0] && H->L > 1)) return fail(PAMG_E_ARG, "vcycle: bad hierarchy");
@@ -2481,7 +2455,7 @@ int pamg_vcycle(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, int
     }
     d.finish(x);
     HIPC(hipStreamSynchronize(ctx->s_comp));
-    return check_jr_err(H);
+    return PAMG_OK;
 }
 
 // Preconditioned CG with one V-cycle from a zero guess as M^-1 (SPEC §S8). The V(1,1) cycle
@@ -2629,7 +2603,7 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
     *avg_ms = ms / reps;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    return check_jr_err(H);
+    return PAMG_OK;
 }
 
 int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, const pamg_vec* b,

@@ -951,15 +951,20 @@ def test_sym_dia_vcycle_same_bits_either_layout(ctx):
     assert np.array_equal(bits(out[0][1]), bits(out[1][1]))
 
 
-@pytest.mark.parametrize("kind,n", [("poisson3d", 128), ("aniso3d", 128), ("poisson3d", 256)])
-def test_jacobi_residual_op_bit_exact(ctx, kind, n):
-    """pamg_jacobi_residual: the fused pass (k_sym_jr) against the two separate sweeps on
-    random x, b — t and r bit for bit, repeated (a hand-off hazard shows as scattered units)."""
+@pytest.mark.parametrize("kind,shape", [("poisson3d", (128, 128, 128)), ("aniso3d", (128, 128, 128)),
+                                        ("poisson3d", (256, 256, 256)), ("poisson3d", (64, 32, 40)),
+                                        ("aniso3d", (192, 48, 7))])
+def test_jacobi_residual_op_bit_exact(ctx, kind, shape):
+    """pamg_jacobi_residual: the temporally blocked pass (k_sym_tb, S = 2) against the two
+    separate sweeps on random x, b — t and r bit for bit, repeated; grids whose tiles split the
+    planes into z chunks, and a grid with fewer planes than a chunk."""
+    from parallel_amg_amd._lib import layout_of
     from parallel_amg_amd.partitioned import jacobi_residual
-    Ao = O.generate(kind, n, n, n)
+    Ao = O.generate(kind, *shape)
     Ad, _h = upload(ctx, Ao)
+    assert layout_of(Ad)["jr_fused"]
     rng = np.random.default_rng(7)
-    N = n ** 3
+    N = Ao.nrows
     x = PVector(ctx, N, 0, rng.standard_normal(N))
     b = PVector(ctx, N, 0, rng.standard_normal(N))
     out = {}
