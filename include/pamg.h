@@ -215,8 +215,10 @@ int pamg_hier_profile(pamg_hier* H, int enable);
 int pamg_hier_profile_read(pamg_hier* H, double* ms_per_level_op /* nlevels*6 */);
 
 /* Micro-benchmark hook: `reps` back-to-back launches of one row operation of A (op 0 SpMV,
- * 1 residual, 2 Jacobi, 3 prolongate-add; no exchange), returning the average time per
- * launch in ms measured with HIP events on the launch stream. */
+ * 1 residual, 2 Jacobi, 3 prolongate-add; no exchange; 4 / 5: the temporally blocked
+ * Jacobi -> residual and Jacobi -> Jacobi -> residual passes, first output in y, where
+ * pamg_mat_layout out[9] bit 5 is set), returning the average time per launch in ms measured
+ * with HIP events on the launch stream. */
 int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, const pamg_vec* b,
                      pamg_vec* y, double omega, int reps, double* avg_ms);
 

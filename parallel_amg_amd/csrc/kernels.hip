@@ -774,31 +774,38 @@ struct TbShape {
 struct TbCoef {        // one row pair on one plane: the 7 values in ascending class order, b, masks
     double v[2][7];
     double b[2];
-    uint32_t m[2];
+    uint16_t mw;       // the two rows' mask bytes as loaded (split at use, not right after the load)
 };
 
 __device__ __forceinline__ int tb_mod3(int k) { return ((k % 3) + 3) % 3; }
 
+// An aligned pair p[j], p[j+1] (j even) through ONE 16-B load; a pair outside [0, n) is read at
+// the nearest end instead: its values only ever meet mask bits that are clear (no row of the
+// grid reaches outside it), so they are discarded.
+__device__ __forceinline__ double2 tb_pair(const double* __restrict__ p, int64_t j, int64_t n) {
+    j = j < 0 ? 0 : (j > n - 2 ? n - 2 : j);
+    return *reinterpret_cast<const double2*>(p + j);
+}
+
 __device__ __forceinline__ void tb_load(TbCoef& c, const uint8_t* __restrict__ mask, const double* __restrict__ dg,
                                         const double* __restrict__ up, int64_t ld, const SymDia& sd,
                                         const double* __restrict__ b, int64_t i, int64_t n) {
-    SymMask<3>::two(mask, i, c.m);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {  // lower classes -off[2], -off[1], -off[0] from the mirrors
-        const int o = sd.off[2 - q];
-        const double2 a = ld_pair(up + (size_t)(2 - q) * ld, i - o, n, (o & 1) == 0);
-        c.v[0][q] = a.x;
-        c.v[1][q] = a.y;
-    }
+    c.mw = *reinterpret_cast<const uint16_t*>(mask + i);
+    // ascending classes -M, -nx, -1, 0, +1, +nx, +M; the lower values from the mirrors
+    const double2 u0 = *reinterpret_cast<const double2*>(up + i);
+    const double2 u1 = *reinterpret_cast<const double2*>(up + ld + i);
+    const double2 u2 = *reinterpret_cast<const double2*>(up + 2 * ld + i);
+    const double2 m2 = tb_pair(up + 2 * ld, i - sd.off[2], n);
+    const double2 m1 = tb_pair(up + ld, i - sd.off[1], n);
+    const double2 m0 = tb_pair(up, i - 2, n);  // U0[i-1] = a(i, i-1); row i+1's is U0[i]
     const double2 d = *reinterpret_cast<const double2*>(dg + i);
-    c.v[0][3] = d.x;
-    c.v[1][3] = d.y;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        const double2 a = *reinterpret_cast<const double2*>(up + (size_t)q * ld + i);
-        c.v[0][4 + q] = a.x;
-        c.v[1][4 + q] = a.y;
-    }
+    c.v[0][0] = m2.x; c.v[1][0] = m2.y;
+    c.v[0][1] = m1.x; c.v[1][1] = m1.y;
+    c.v[0][2] = m0.y; c.v[1][2] = u0.x;
+    c.v[0][3] = d.x;  c.v[1][3] = d.y;
+    c.v[0][4] = u0.x; c.v[1][4] = u0.y;
+    c.v[0][5] = u1.x; c.v[1][5] = u1.y;
+    c.v[0][6] = u2.x; c.v[1][6] = u2.y;
     const double2 bb = *reinterpret_cast<const double2*>(b + i);
     c.b[0] = bb.x;
     c.b[1] = bb.y;
@@ -809,12 +816,13 @@ __device__ __forceinline__ void tb_rows(const TbCoef& c, const double (&xv)[2][7
                                         double (&out)[2]) {
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
+        const uint32_t m = r == 0 ? ((uint32_t)c.mw & 0xffu) : ((uint32_t)c.mw >> 8);
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
             const double p = c.v[r][k] * xv[r][k];
             const double t = s + p;
-            s = ((c.m[r] >> k) & 1u) ? t : s;
+            s = ((m >> k) & 1u) ? t : s;
         }
         if (resid) {
             out[r] = c.b[r] - s;
@@ -873,18 +881,18 @@ __device__ __forceinline__ void tb_step(int k, TbCoef& cA, TbCoef& cB, TbCoef& c
             tb_load(cA, mask, dg, up, ld, sd, ta.b, i, t.n);
             double xv[2][7];
             const double* x = ta.in0;
-            const double2 zl = ld_pair(x, i - t.M, t.n, true);
-            const double2 dn = ld_pair(x, i - t.nx, t.n, true);
-            const double2 lf = ld_pair(x, i - 1, t.n, false);
+            const double2 zl = tb_pair(x, i - t.M, t.n);
+            const double2 dn = tb_pair(x, i - t.nx, t.n);
+            const double2 lf = tb_pair(x, i - 2, t.n);
             const double2 ow = *reinterpret_cast<const double2*>(x + i);
-            const double2 rg = ld_pair(x, i + 1, t.n, false);
-            const double2 upl = ld_pair(x, i + t.nx, t.n, true);
-            const double2 zh = ld_pair(x, i + t.M, t.n, true);
+            const double2 rg = tb_pair(x, i + 2, t.n);
+            const double2 upl = tb_pair(x, i + t.nx, t.n);
+            const double2 zh = tb_pair(x, i + t.M, t.n);
             xv[0][0] = zl.x;  xv[1][0] = zl.y;
             xv[0][1] = dn.x;  xv[1][1] = dn.y;
-            xv[0][2] = lf.x;  xv[1][2] = lf.y;
+            xv[0][2] = lf.y;  xv[1][2] = ow.x;
             xv[0][3] = ow.x;  xv[1][3] = ow.y;
-            xv[0][4] = rg.x;  xv[1][4] = rg.y;
+            xv[0][4] = ow.y;  xv[1][4] = rg.x;
             xv[0][5] = upl.x; xv[1][5] = upl.y;
             xv[0][6] = zh.x;  xv[1][6] = zh.y;
             tb_rows(cA, xv, S == 1 && ta.last_resid, ta.omega, o);

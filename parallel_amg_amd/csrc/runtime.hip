@@ -2608,25 +2608,48 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
 
 int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, const pamg_vec* b,
                      pamg_vec* y, double omega, int reps, double* avg_ms) {
-    if (!ctx || !A || !x || !y || reps < 1 || !avg_ms || op < 0 || op > 3)
+    if (!ctx || !A || !x || !y || reps < 1 || !avg_ms || op < 0 || op > 5)
         return fail(PAMG_E_ARG, "bench_rowop: bad args");
-    if ((op == pamg::OP_RESID || op == pamg::OP_JACOBI) && !b) return fail(PAMG_E_ARG, "bench_rowop: b needed");
-    if (op == pamg::OP_JACOBI && !A->d_diag) return fail(PAMG_E_SETUP, "bench_rowop: jacobi needs a square matrix");
+    if ((op == pamg::OP_RESID || op == pamg::OP_JACOBI || op >= 4) && !b) return fail(PAMG_E_ARG, "bench_rowop: b needed");
+    if ((op == pamg::OP_JACOBI || op >= 4) && !A->d_diag)
+        return fail(PAMG_E_SETUP, "bench_rowop: jacobi needs a square matrix");
+    if (op >= 4 && !(A->interior.sym && A->sym.tb_ok))
+        return fail(PAMG_E_STATE, "bench_rowop: op %d needs the temporally blocked layout (pamg_mat_layout bit 5)", op);
     if (x == y) return fail(PAMG_E_ARG, "bench_rowop: x and y must differ");
     CHECK(check_vec_for(A, x, "bench_rowop"));
     CHECK(set_device(ctx));
+    // ops 4 / 5: the temporally blocked passes k_sym_tb<2> (Jacobi -> residual) and <3>
+    // (Jacobi -> Jacobi -> residual), the first output into y, the others into scratch
+    double* scratch[2] = {nullptr, nullptr};
+    if (op >= 4)
+        for (double*& p : scratch) {
+            CHECK(dalloc(&p, A->nrows + kVecPad));
+        }
+    pamg::TbArgs ta;
+    ta.nstages = op - 2;
+    ta.last_resid = true;
+    ta.in0 = x->d;
+    ta.out[0] = y->d;
+    ta.out[1] = scratch[0];
+    ta.out[2] = scratch[1];
+    ta.b = b ? b->d : nullptr;
+    ta.omega = omega;
     hipEvent_t e0, e1;
     HIPC(hipEventCreate(&e0));
     HIPC(hipEventCreate(&e1));
     hipStream_t s = ctx->s_comp;
     const double* bd = b ? b->d : nullptr;
-    pamg::launch_rows(*A, A->interior, op, x->d, bd, x->d, y->d, omega, s);
-    pamg::launch_rows(*A, A->boundary, op, x->d, bd, x->d, y->d, omega, s);
+    auto once = [&]() {
+        if (op >= 4) {
+            pamg::launch_sym_tb(*A, ta, s);
+        } else {
+            pamg::launch_rows(*A, A->interior, op, x->d, bd, x->d, y->d, omega, s);
+            pamg::launch_rows(*A, A->boundary, op, x->d, bd, x->d, y->d, omega, s);
+        }
+    };
+    once();
     HIPC(hipEventRecord(e0, s));
-    for (int k = 0; k < reps; ++k) {
-        pamg::launch_rows(*A, A->interior, op, x->d, bd, x->d, y->d, omega, s);
-        pamg::launch_rows(*A, A->boundary, op, x->d, bd, x->d, y->d, omega, s);
-    }
+    for (int k = 0; k < reps; ++k) once();
     HIPC(hipEventRecord(e1, s));
     HIPC(hipEventSynchronize(e1));
     float ms = 0.f;
@@ -2634,6 +2657,7 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
     *avg_ms = ms / reps;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    for (double* p : scratch) dfree(p);
     return PAMG_OK;
 }
 

@@ -29,7 +29,7 @@ from parallel_amg_amd._lib import call, layout_of  # noqa: E402
 from parallel_amg_amd.partitioned import Context, PSparseMatrix, PVector  # noqa: E402
 from parallel_amg_amd.solver import AMGSolver  # noqa: E402
 
-OPNAME = {0: "spmv", 1: "residual", 2: "jacobi", 3: "prolong"}
+OPNAME = {0: "spmv", 1: "residual", 2: "jacobi", 3: "prolong", 4: "jacobi_residual_tb", 5: "chain3_tb"}
 
 
 def set_opts(**kw):
@@ -44,7 +44,7 @@ def bench(ctx, M, op, reps):
     ms = C.c_double()
     call("pamg_bench_rowop", ctx.handle, M.handle, op, x.handle, b.handle, y.handle, 0.6, reps,
          C.byref(ms))
-    extra = {0: 0, 1: 1, 2: 1, 3: 1}[op]
+    extra = {0: 0, 1: 1, 2: 1, 3: 1, 4: 2, 5: 3}[op]  # fused: b + the other outputs, matrix once
     return ms.value, AMGSolver.csr_bytes(M, extra), AMGSolver.rowsum_bytes(M, extra)
 
 
@@ -96,7 +96,9 @@ def main():
                 continue
             D = PSparseMatrix(ctx, M, plan)
             for op in ops:
-                if op == 2 and not name.startswith("A"):
+                if op in (2, 4, 5) and not name.startswith("A"):
+                    continue
+                if op >= 4 and not layout_of(D).get("jr_fused"):
                     continue
                 if op == 3 and not name.startswith("P"):
                     continue

@@ -16,7 +16,7 @@ echo "bench done"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv \
     -- python3 -u bench.py --steps 5 --cpu-baseline off > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.log"
 echo "kernel trace done"
-KB="tools/kbench.py --n 512 --levels 1 --ops 0,2 --reps 3 --configs 1024"
+KB="tools/kbench.py --n 512 --levels 1 --ops 0,2,5 --reps 3 --configs 1024"
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o fetch --output-format csv \
     -- python3 -u $KB > "$OUT/pmc_fetch.jsonl" 2> "$OUT/pmc_fetch.err"
 echo "fetch pass done"
@@ -29,4 +29,6 @@ mkdir -p "$OUT/pmc"
 K=${PMCKERNEL:-k_rows_sym2}
 python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --kernel "$K<2" > "$OUT/pmc/traffic_jacobi.json"
 python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --kernel "$K<0" > "$OUT/pmc/traffic_spmv.json"
+# the pipelined cycles' level-0 chain (k_sym_tb<3>, the timed region's dominant kernel)
+python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --kernel "k_sym_tb<3>" > "$OUT/pmc/traffic_chain.json"
 echo "traffic records in $OUT/pmc (copy to profiles/pmc/ to let bench.py report them)"
