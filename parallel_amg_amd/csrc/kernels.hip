@@ -942,12 +942,13 @@ __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tb(int nrows, const
     __shared__ __attribute__((aligned(16))) double l0[3][Sh::RY][kTbLW];
     __shared__ __attribute__((aligned(16))) double l1[S == 3 ? 3 : 1][Sh::RY][kTbLW];
     const TbGeom& g = sd.tb;
-    // tile: consecutive tiles (shared halos) on one XCD (block b runs on XCD b % 8; speed only)
+    // tile: consecutive tiles on one XCD (block b runs on XCD b % 8; speed only), ordered y-fastest
+    // so that the tiles sharing the wide y halos (kTbX + 4 points x S-1 lines) sit on one XCD
     const int ntiles = g.tiles_x * g.tiles_y * g.zchunks;
     const int per = (ntiles + 7) / 8;
     const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
     if (lin >= ntiles) return;  // the whole workgroup, before any barrier
-    const int tx = lin % g.tiles_x, ty = (lin / g.tiles_x) % g.tiles_y, zc = lin / (g.tiles_x * g.tiles_y);
+    const int ty = lin % g.tiles_y, tx = (lin / g.tiles_y) % g.tiles_x, zc = lin / (g.tiles_x * g.tiles_y);
     const int x0 = tx * kTbX, y0 = ty * kTbY;
     TbCtx<S> t;
     t.nx = g.nx;
