@@ -769,6 +769,8 @@ struct TbShape {
     static constexpr int RY = kTbY + 2 * H;      // grid lines of stage 0
     static constexpr int NT = kTbPX * RY;        // threads with a row pair
     static constexpr int threads = (NT + 63) / 64 * 64;
+    static constexpr int XL = RY + 2;            // lines of the in0 window (stage 0's region + 1)
+    static constexpr int XPAIRS = XL * (kTbLW / 2);  // its row pairs: x0-4 .. x0+kTbX+3
 };
 
 struct TbCoef {        // one row pair on one plane: the 7 values in ascending class order, b, masks
@@ -787,15 +789,18 @@ __device__ __forceinline__ double2 tb_pair(const double* __restrict__ p, int64_t
     return *reinterpret_cast<const double2*>(p + j);
 }
 
-__device__ __forceinline__ void tb_load(TbCoef& c, const uint8_t* __restrict__ mask, const double* __restrict__ dg,
-                                        const double* __restrict__ up, int64_t ld, const SymDia& sd,
-                                        const double* __restrict__ b, int64_t i, int64_t n) {
+// prev: the same pair's values one plane down (held in the register ring): its U2 is this
+// plane's -M mirror, so only the first plane of a workgroup loads that mirror
+template <bool FIRST>
+__device__ __forceinline__ void tb_load(TbCoef& c, const TbCoef& prev, const uint8_t* __restrict__ mask,
+                                        const double* __restrict__ dg, const double* __restrict__ up, int64_t ld,
+                                        const SymDia& sd, const double* __restrict__ b, int64_t i, int64_t n) {
     c.mw = *reinterpret_cast<const uint16_t*>(mask + i);
     // ascending classes -M, -nx, -1, 0, +1, +nx, +M; the lower values from the mirrors
     const double2 u0 = *reinterpret_cast<const double2*>(up + i);
     const double2 u1 = *reinterpret_cast<const double2*>(up + ld + i);
     const double2 u2 = *reinterpret_cast<const double2*>(up + 2 * ld + i);
-    const double2 m2 = tb_pair(up + 2 * ld, i - sd.off[2], n);
+    const double2 m2 = FIRST ? tb_pair(up + 2 * ld, i - sd.off[2], n) : make_double2(prev.v[0][6], prev.v[1][6]);
     const double2 m1 = tb_pair(up + ld, i - sd.off[1], n);
     const double2 m0 = tb_pair(up, i - 2, n);  // U0[i-1] = a(i, i-1); row i+1's is U0[i]
     const double2 d = *reinterpret_cast<const double2*>(dg + i);
@@ -842,7 +847,40 @@ struct TbCtx {
     int ry, col;
     int64_t ixy;          // y * nx + x of the pair's first row
     bool pos_ok, own_xy;
+    int x0, y0;           // the tile's first grid point
 };
+
+// The in0 window of plane q (stage 0's region + one point / line around it, zeros outside the
+// grid), as the pairs thread tid moves: loads issued now (clamped addresses, no branch), stored
+// into the LDS ring later (tb_win_store) so their latency overlaps the step's other work.
+template <int S>
+struct TbWin {
+    double2 v[2];
+    bool ok[2];
+};
+template <int S>
+__device__ __forceinline__ void tb_win_load(TbWin<S>& w, const TbCtx<S>& t, const double* __restrict__ in0, int q) {
+    using Sh = TbShape<S>;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int p = threadIdx.x + h * Sh::threads;
+        const int line = p / (kTbLW / 2), pc = p % (kTbLW / 2);
+        const int x = t.x0 - 4 + 2 * pc, y = t.y0 - Sh::H - 1 + line;
+        w.ok[h] = p < Sh::XPAIRS && x >= 0 && x < t.nx && y >= 0 && y < t.ny && q >= 0 && q < t.nz;
+        w.v[h] = tb_pair(in0, (int64_t)q * t.M + (int64_t)y * t.nx + x, t.n);
+    }
+}
+template <int S>
+__device__ __forceinline__ void tb_win_store(const TbWin<S>& w, double (*xin)[TbShape<S>::XL][kTbLW], int slot) {
+    using Sh = TbShape<S>;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int p = threadIdx.x + h * Sh::threads;
+        if (p < Sh::XPAIRS)
+            *reinterpret_cast<double2*>(&xin[slot][p / (kTbLW / 2)][2 * (p % (kTbLW / 2))]) =
+                w.ok[h] ? w.v[h] : make_double2(0.0, 0.0);
+    }
+}
 
 // the 7 neighbour values of a row pair from an LDS plane ring (planes p-1, p, p+1 in slots
 // sm, s0, sp; lines ry-1, ry, ry+1)
@@ -865,36 +903,32 @@ __device__ __forceinline__ void tb_gather_lds(const double (*ring)[RY][kTbLW], i
     xv[0][6] = zh.x;  xv[1][6] = zh.y;
 }
 
-template <int S>
+template <int S, bool FIRST>
 __device__ __forceinline__ void tb_step(int k, TbCoef& cA, TbCoef& cB, TbCoef& cC, const TbCtx<S>& t,
                                         const uint8_t* __restrict__ mask, const double* __restrict__ dg,
                                         const double* __restrict__ up, int64_t ld, const SymDia& sd,
                                         const TbArgs& ta, double (*l0)[TbShape<S>::RY][kTbLW],
-                                        double (*l1)[TbShape<S>::RY][kTbLW]) {
+                                        double (*l1)[TbShape<S>::RY][kTbLW],
+                                        double (*xin)[TbShape<S>::XL][kTbLW]) {
     using Sh = TbShape<S>;
     if (k >= t.kend) return;  // uniform: the whole workgroup
-    // ---- stage 0 on plane k: a Jacobi sweep from in0 (global: never written in this launch)
+    // ---- stage 0 on plane k: a Jacobi sweep from in0 (its window ring in LDS: planes k-1..k+1)
     {
         double o[2] = {0.0, 0.0};
-        if (t.pos_ok && k >= 0 && k < t.nz) {
-            const int64_t i = (int64_t)k * t.M + t.ixy;
-            tb_load(cA, mask, dg, up, ld, sd, ta.b, i, t.n);
+        const bool act0 = t.pos_ok && k >= 0 && k < t.nz;
+        const int64_t i = (int64_t)k * t.M + t.ixy;
+        // the in0 window of plane k+1 into the slot of plane k-2 (last read by the previous
+        // step's stage 0), its loads issued with this plane's operator loads (one latency)
+        {
+            TbWin<S> win;
+            if (act0) tb_load<FIRST>(cA, cB, mask, dg, up, ld, sd, ta.b, i, t.n);
+            tb_win_load<S>(win, t, ta.in0, k + 1);
+            tb_win_store<S>(win, xin, tb_mod3(k + 1));
+        }
+        __syncthreads();
+        if (act0) {
             double xv[2][7];
-            const double* x = ta.in0;
-            const double2 zl = tb_pair(x, i - t.M, t.n);
-            const double2 dn = tb_pair(x, i - t.nx, t.n);
-            const double2 lf = tb_pair(x, i - 2, t.n);
-            const double2 ow = *reinterpret_cast<const double2*>(x + i);
-            const double2 rg = tb_pair(x, i + 2, t.n);
-            const double2 upl = tb_pair(x, i + t.nx, t.n);
-            const double2 zh = tb_pair(x, i + t.M, t.n);
-            xv[0][0] = zl.x;  xv[1][0] = zl.y;
-            xv[0][1] = dn.x;  xv[1][1] = dn.y;
-            xv[0][2] = lf.y;  xv[1][2] = ow.x;
-            xv[0][3] = ow.x;  xv[1][3] = ow.y;
-            xv[0][4] = ow.y;  xv[1][4] = rg.x;
-            xv[0][5] = upl.x; xv[1][5] = upl.y;
-            xv[0][6] = zh.x;  xv[1][6] = zh.y;
+            tb_gather_lds<Sh::XL>(xin, tb_mod3(k - 1), tb_mod3(k), tb_mod3(k + 1), t.ry + 1, t.col, xv);
             tb_rows(cA, xv, S == 1 && ta.last_resid, ta.omega, o);
             if (t.own_xy && k >= t.zs && k < t.ze) *reinterpret_cast<double2*>(ta.out[0] + i) = make_double2(o[0], o[1]);
         }
@@ -941,6 +975,7 @@ __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tb(int nrows, const
     using Sh = TbShape<S>;
     __shared__ __attribute__((aligned(16))) double l0[3][Sh::RY][kTbLW];
     __shared__ __attribute__((aligned(16))) double l1[S == 3 ? 3 : 1][Sh::RY][kTbLW];
+    __shared__ __attribute__((aligned(16))) double xin[3][Sh::XL][kTbLW];
     const TbGeom& g = sd.tb;
     // tile: consecutive tiles on one XCD (block b runs on XCD b % 8; speed only), ordered y-fastest
     // so that the tiles sharing the wide y halos (kTbX + 4 points x S-1 lines) sit on one XCD
@@ -951,6 +986,8 @@ __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tb(int nrows, const
     const int ty = lin % g.tiles_y, tx = (lin / g.tiles_y) % g.tiles_x, zc = lin / (g.tiles_x * g.tiles_y);
     const int x0 = tx * kTbX, y0 = ty * kTbY;
     TbCtx<S> t;
+    t.x0 = x0;
+    t.y0 = y0;
     t.nx = g.nx;
     t.ny = g.ny;
     t.nz = g.nz;
@@ -969,10 +1006,27 @@ __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tb(int nrows, const
     t.pos_ok = has && x >= 0 && x < g.nx && y >= 0 && y < g.ny;
     t.own_xy = t.pos_ok && px >= 1 && px <= kTbX / 2 && y >= y0 && y < y0 + kTbY;
     TbCoef c0, c1, c2;  // planes k, k-1, k-2 at step k (rotated by the unrolled loop)
-    for (int k = t.zs - Sh::H; k < t.kend; k += 3) {
-        tb_step<S>(k, c0, c2, c1, t, mask, dg, up, ld, sd, ta, l0, l1);
-        tb_step<S>(k + 1, c1, c0, c2, t, mask, dg, up, ld, sd, ta, l0, l1);
-        tb_step<S>(k + 2, c2, c1, c0, t, mask, dg, up, ld, sd, ta, l0, l1);
+    const int k0 = t.zs - Sh::H;
+    {  // the in0 windows of planes k0-1 and k0 (each step loads the one above its plane)
+        TbWin<S> w;
+#pragma unroll
+        for (int q = -1; q <= 0; ++q) {
+            tb_win_load<S>(w, t, ta.in0, k0 + q);
+            tb_win_store<S>(w, xin, tb_mod3(k0 + q));
+        }
+    }
+    tb_step<S, true>(k0, c0, c2, c1, t, mask, dg, up, ld, sd, ta, l0, l1, xin);
+    if constexpr (S == 2) {  // two planes of operator values live: a 2-way rotation
+        for (int k = k0 + 1; k < t.kend; k += 2) {
+            tb_step<S, false>(k, c1, c0, c0, t, mask, dg, up, ld, sd, ta, l0, l1, xin);
+            tb_step<S, false>(k + 1, c0, c1, c1, t, mask, dg, up, ld, sd, ta, l0, l1, xin);
+        }
+    } else {
+        for (int k = k0 + 1; k < t.kend; k += 3) {
+            tb_step<S, false>(k, c1, c0, c2, t, mask, dg, up, ld, sd, ta, l0, l1, xin);
+            tb_step<S, false>(k + 1, c2, c1, c0, t, mask, dg, up, ld, sd, ta, l0, l1, xin);
+            tb_step<S, false>(k + 2, c0, c2, c1, t, mask, dg, up, ld, sd, ta, l0, l1, xin);
+        }
     }
 }
 

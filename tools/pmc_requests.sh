@@ -11,7 +11,7 @@ TAG=${1:-r02_req}
 MATS=${MATS:-A0,R0,P0,A1}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-KB="tools/kbench.py --n 512 --levels 2 --mats $MATS --ops 0,2,3 --reps 2 --configs 1024"
+KB="tools/kbench.py --n 512 --levels ${LEVELS:-2} --mats $MATS --ops ${OPS:-0,2,3} --reps 2 --configs 1024"
 timeout -s KILL 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
     -d "$OUT/pass1" -o p1 --output-format csv -- python3 -u $KB > "$OUT/pass1.jsonl" 2> "$OUT/pass1.err"
 echo "pass 1 done"

@@ -13,5 +13,8 @@ for bp in 25 50 100 200; do
 done
 timeout -k 10 300 python3 -u $KB --configs 1024:0 >> "$OUT/kb_r1.jsonl" 2>> "$OUT/kb.err"
 echo "natural order done"
-MATS=R1,P1,A1 timeout -k 10 900 bash tools/pmc_requests.sh $TAG/req
+MATS=R1,P1,A1 timeout -k 10 700 bash tools/pmc_requests.sh $TAG/req
 echo "requests done"
+# the temporally blocked level-0 passes beside the separate sweeps: DRAM reads vs fabric reads
+MATS=A0 LEVELS=1 OPS=1,2,4,5 timeout -k 10 400 bash tools/pmc_requests.sh $TAG/req_tb
+echo "tb requests done"
