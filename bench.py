@@ -67,9 +67,9 @@ def main():
     ap.add_argument("--sweeps", default="1,1", help="nu1,nu2 of the V(nu1,nu2) cycle (SPEC S6)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="libpamg tuning option for an A/B run (pamg_set_option; INTEGRATION.md table)")
-    ap.add_argument("--value-dict", action="store_true",
-                    help="opt-in per-tile 4-bit value dictionaries where a tile has <= 16 distinct "
-                         "values (exact; not the default layout)")
+    ap.add_argument("--value-dict", type=int, choices=[0, 1], default=1,
+                    help="per-tile 4-bit value dictionaries where a tile has <= 16 distinct values (1, the "
+                         "library default) or never (0)")
     ap.add_argument("--setup", choices=["gpu", "host"], default="gpu",
                     help="where the Galerkin products of the setup run (same bits either way)")
     ap.add_argument("--permute", type=int, default=None, metavar="SEED",

@@ -396,9 +396,13 @@ def _replicated_tail(backend, A: dict, offs, levels: list, params: SAParams, log
     from .backend import SequentialBackend
     n = int(offs[-1])
     full = _gather_full(backend, A, offs)
+    # the tail (<= agglomerate rows) is set up on the host: its products are small, and the one
+    # failure seen of a device product (23 rows of one rank's tail level without a diagonal,
+    # 8 ranks sharing one GPU in the full GPU suite; not reproduced alone) was in these
+    # wide-row products (Correctness tooling)
     sub = build_hierarchy(SequentialBackend(1), {0: full}, np.array([0, n], np.int64),
                           replace(params, agglomerate=0, max_levels=params.max_levels - len(levels)),
-                          (lambda m: log(m + " (whole on every part)")) if log else None, device,
+                          (lambda m: log(m + " (whole on every part)")) if log else None, None,
                           _level0=len(levels))
     for p in backend.parts:  # the prolongation into the tail reads the whole vector
         levels[-1][p].planP = None

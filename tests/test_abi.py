@@ -109,7 +109,7 @@ def test_load_order_binds_opt_rocm_runtime(built):
 # every pamg_set_option key with its default and another legal value (include/pamg.h, the
 # INTEGRATION.md option table)
 OPTION_DEFAULTS = {"tile_nnz": (1024, 4096), "tile_order": (1, 0), "col24": (1, 0), "long_tiles": (1, 0),
-                   "long_tiles_min": (24, 48), "row_len8": (1, 0), "value_dict": (0, 1), "col_dict": (1, 0),
+                   "long_tiles_min": (24, 48), "row_len8": (1, 0), "value_dict": (1, 0), "col_dict": (1, 0),
                    "col_dict_anchor": (1, 0), "col_dict_tile": (1, 0), "x_stage": (1, 0), "tm_tile_dicts": (1, 0),
                    "band_pct": (100, 50), "band_pct_restrict": (50, 100), "tile_major": (1, 2), "poison_ghosts": (0, 1),
                    "sym_dia": (1, 0), "sym_rows": (2, 1), "jr_fuse": (1, 0)}

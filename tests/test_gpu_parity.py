@@ -19,6 +19,19 @@ def bits(a):
     return np.asarray(a, np.float64).view(np.int64)
 
 
+@pytest.fixture
+def novd():
+    """Value dictionaries off (the library default is on): for tests that assert which column
+    layout an upload picks on matrices with few distinct values."""
+    import ctypes
+    from parallel_amg_amd._lib import call
+    v = ctypes.c_int64()
+    call("pamg_get_option", b"value_dict", ctypes.byref(v))
+    call("pamg_set_option", b"value_dict", 0)
+    yield
+    call("pamg_set_option", b"value_dict", v.value)
+
+
 def random_csr(rng, lengths, ncols, square=False, palette=None):
     rows, cols, vals = [0], [], []
     for i, m in enumerate(lengths):
@@ -181,7 +194,7 @@ COLDICT_CASES = [("stencil7", None, [7]), ("d15", 15, [1, 16, 5, 9]), ("d16", 16
 
 @pytest.mark.parametrize("name,ndist,lengths", COLDICT_CASES, ids=[c[0] for c in COLDICT_CASES])
 @pytest.mark.parametrize("tnnz", [1024, 4096])
-def test_column_dictionary_bit_exact(ctx, name, ndist, lengths, tnnz):
+def test_column_dictionary_bit_exact(ctx, novd, name, ndist, lengths, tnnz):
     """col_dict: columns rebuilt as row + table[index] give the very bits of the oracle for
     SpMV, residual, prolongate-add and Jacobi (in-tile diagonal and stored diagonal), and the
     layout engages exactly when the matrix has <= 256 distinct row-relative offsets."""
@@ -408,7 +421,7 @@ def test_vcycle_sweeps_bit_exact(ctx, nu1, nu2):
         S.set_sweeps(0, 1)
 
 
-def test_stream_bytes_layout(ctx):
+def test_stream_bytes_layout(ctx, novd):
     """pamg_mat_stream_bytes: 12 B/nnz + row pointers + 16-B tile descriptors in the 32-bit
     layout; 3-B columns (+ a 4-B base per tile) in the 24-bit one; 1 B per row instead of a
     4-B row pointer with 8-bit row lengths (roofline byte model)."""
@@ -476,7 +489,7 @@ def anchored_csr(rng, nrows, ncols, nshape, maxlen):
 
 @pytest.mark.parametrize("nshape,maxlen,tnnz", [(12, 12, 1024), (75, 40, 1024), (75, 255, 1024),
                                                 (256, 60, 4096), (257, 60, 1024)])
-def test_anchored_dictionary_bit_exact(ctx, nshape, maxlen, tnnz):
+def test_anchored_dictionary_bit_exact(ctx, novd, nshape, maxlen, tnnz):
     """Anchored column dictionaries (column = the row's first column + table[index], anchors in
     the tile-major slots; the layout of the level-0 restriction): SpMV, residual and
     prolongate-add give the oracle's bits; 257 offsets fall back to 24-bit columns."""
@@ -573,7 +586,7 @@ def drift_csr(rng, n, ncols, anchored, nset=12, every=200, step=37):
 
 @pytest.mark.parametrize("anchored,tnnz,tm", [(False, 1024, 0), (False, 4096, 0), (True, 1024, 0), (True, 2048, 0),
                                              (False, 1024, 1), (False, 4096, 1), (True, 1024, 1)])
-def test_per_tile_dictionaries_bit_exact(ctx, anchored, tnnz, tm):
+def test_per_tile_dictionaries_bit_exact(ctx, novd, anchored, tnnz, tm):
     """col_dict_tile: no table fits the whole matrix (> 256 offsets) but every tile's fits —
     per-tile row-relative tables (coarse-operator shape) or per-tile anchored ones with 16-bit
     anchors (prolongator shape) in the descriptor kernel; SpMV / residual / prolongate-add (and
@@ -611,7 +624,7 @@ def test_hierarchy_operators_any_dictionary_bit_exact(ctx):
 
 @pytest.mark.parametrize("name,ndist,lengths", [("d300", 300, [30, 1, 7, 64]), ("d2000", 2000, [9, 3, 40]),
                                                 ("wide_ragged", 600, [1, 255, 2, 17])])
-def test_per_tile_dictionaries_random(ctx, name, ndist, lengths):
+def test_per_tile_dictionaries_random(ctx, novd, name, ndist, lengths):
     """Random offset patterns too wide for one table: per-tile tables where they stream less
     than 24-bit columns (else 24-bit), bit-exact either way."""
     from parallel_amg_amd._lib import layout_of
@@ -668,7 +681,7 @@ def _xs_case(name):
 @pytest.mark.parametrize("name", ["poisson3d_24", "poisson2d_64", "aniso3d_20", "elastic3d_12", "ragged",
                                   "clusters13", "wide_run"])
 @pytest.mark.parametrize("x_stage", [1, 0])
-def test_x_stage_bit_exact(ctx, name, x_stage):
+def test_x_stage_bit_exact(ctx, novd, name, x_stage):
     """x_stage: row-relative dictionary tiles read x from LDS copies of the runs their offset
     clusters cover (loaded coalesced at entry) instead of gathering it; SpMV / residual /
     prolongate-add / Jacobi (diagonal = offset 0's entry) give the oracle's bits either way,
@@ -683,7 +696,7 @@ def test_x_stage_bit_exact(ctx, name, x_stage):
     assert lay["x_stage"] == (staged and x_stage == 1), lay
 
 
-def test_restriction_takes_anchored_dictionary(ctx):
+def test_restriction_takes_anchored_dictionary(ctx, novd):
     """The level-0 restriction of the 7-point Poisson hierarchy (5x5x5 neighbourhoods of the
     aggregate roots) is uploaded with an anchored 8-bit dictionary in tile-major slots."""
     from parallel_amg_amd._lib import layout_of
