@@ -375,14 +375,17 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
 // PT (Options::tm_tile_dicts): per-tile row-relative dictionaries (TileSet::pt) in tile-major
 // slots — this tile's table is ctab[t * ctab_n ...], addressed from the block index like
 // every other pre-gather load.
-template <int OP, int TNNZ, int CD, bool ANC = false, bool XS = false, bool PT = false>
+// VD8 (TileSet::tm_vt): values through the tile's 8-bit dictionary — a byte per nonzero in the
+// slot and the tile's table (vt entries, staged into LDS at entry) instead of 8-B values.
+template <int OP, int TNNZ, int CD, bool ANC = false, bool XS = false, bool PT = false, bool VD8 = false>
 __global__ __launch_bounds__(kBlock) void k_rows_tm(
     const int4* __restrict__ tiles, const double* __restrict__ tval,
     const uint8_t* __restrict__ tcidx, const uint16_t* __restrict__ tclo,
     const uint8_t* __restrict__ tchi, const int* __restrict__ tbase,
     const uint8_t* __restrict__ trlen, int rs, const int* __restrict__ ctab, int ctab_n,
     const double* __restrict__ x, const double* __restrict__ b, double* __restrict__ y,
-    double omega, const int* __restrict__ tanc = nullptr, const XStage xst = XStage{}) {
+    double omega, const int* __restrict__ tanc = nullptr, const XStage xst = XStage{},
+    const uint8_t* __restrict__ tvidx = nullptr, const double* __restrict__ tvtab = nullptr, int vt = 0) {
     // ANC (anchored dictionary): column = the row's first column (slot anchors, tanc) +
     // table[index] instead of row + table[index]
     static_assert(!ANC || CD != 0, "anchored columns are dictionary columns");
@@ -401,6 +404,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     __shared__ __attribute__((aligned(4))) uint8_t lrow[TNNZ + 8];
     __shared__ int lanc[ANC ? BS : 1];
     __shared__ double lxs[XS ? kXsCap + 1 : 1];  // + 1: the dump slot of lanes past a run
+    __shared__ double lvt[VD8 ? kBlock : 1];     // the tile's value table (vt <= 256 entries)
 
     const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int4 d = tiles[t];
@@ -420,7 +424,10 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     const size_t rsl = (size_t)t * rs + (tid < rs ? tid : rs - 1);
     if constexpr (ANC) ancv = tanc[rsl];
     const int rlv = (int)trlen[rsl];
+    double vtv = 0.0;
+    if constexpr (VD8) vtv = tvtab[(size_t)t * vt + (tid < vt ? tid : vt - 1)];
     double2 va[G], vb[G];
+    uint32_t vi[G];
     uint32_t cn[G];
     ushort4 clo4[G];
     int cb = 0;
@@ -462,10 +469,15 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
 #pragma unroll
     for (int j = 0; j < G; ++j) {
         const size_t q = sb + 4 * (tid + j * BS);
-        va[j] = *reinterpret_cast<const double2*>(tval + q);
-        vb[j] = *reinterpret_cast<const double2*>(tval + q + 2);
+        if constexpr (VD8) {
+            vi[j] = *reinterpret_cast<const uint32_t*>(tvidx + q);
+        } else {
+            va[j] = *reinterpret_cast<const double2*>(tval + q);
+            vb[j] = *reinterpret_cast<const double2*>(tval + q + 2);
+        }
     }
     int rl_len = tid < rs ? rlv : 0;
+    if constexpr (VD8) lvt[tid] = vtv;  // every lane (lanes past vt repeat the last entry)
     // every lane stores its entry (unconditionally: a conditional store lets the compiler sink
     // the table load into the branch, behind the value stream)
     if constexpr (XS) ltab[tid < NTAB ? tid : NTAB - 1] = tabv;  // lanes past NTAB rewrite the last entry's value
@@ -491,6 +503,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     // follow the stream loads with no barrier in between.
     constexpr bool NEED_ROWS = CD != 0 || OP == OP_JACOBI;
     int re = 0;
+    if constexpr (VD8 && !NEED_ROWS) __syncthreads();  // lvt
     if constexpr (NEED_ROWS) {
         __syncthreads();  // lwt, ltab
         re = row_end();
@@ -540,7 +553,16 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
         const int q = 4 * (tid + j * BS);
         uint32_t rw = 0u;
         if constexpr (NEED_ROWS) rw = q < cnt ? *reinterpret_cast<const uint32_t*>(&lrow[q]) : 0u;
-        const double vv[4] = {va[j].x, va[j].y, vb[j].x, vb[j].y};
+        double vv[4];
+        if constexpr (VD8) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) vv[e] = lvt[(vi[j] >> (8 * e)) & 255u];
+        } else {
+            vv[0] = va[j].x;
+            vv[1] = va[j].y;
+            vv[2] = vb[j].x;
+            vv[3] = vb[j].y;
+        }
         double p[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1236,49 +1258,60 @@ void launch_tile2_cd(const pamg_mat& A, const TileSet& ts, const double* x, cons
     }
 }
 
+template <int OP, int TNNZ, bool VD8>
+void launch_tm(const pamg_mat& A, const TileSet& ts, const double* x, const double* b, double* y, double omega,
+               hipStream_t s) {
+    (void)A;
+    const int n = ts.n_short;
+    if (ts.anc && ts.cd == 4)
+        k_rows_tm<OP, TNNZ, 4, true, false, false, VD8><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
+                                                         nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n,
+                                                         x, b, y, omega, ts.d_tm_anc, XStage{}, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt);
+    else if (ts.anc)
+        k_rows_tm<OP, TNNZ, 8, true, false, false, VD8><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
+                                                         nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n,
+                                                         x, b, y, omega, ts.d_tm_anc, XStage{}, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt);
+    else if (ts.pt && ts.cd == 4)
+        k_rows_tm<OP, TNNZ, 4, false, false, true, VD8><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx,
+                                                                      nullptr, nullptr, nullptr, ts.d_tm_rlen,
+                                                                      ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y,
+                                                                      omega, nullptr, XStage{}, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt);
+    else if (ts.pt)
+        k_rows_tm<OP, TNNZ, 8, false, false, true, VD8><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx,
+                                                                      nullptr, nullptr, nullptr, ts.d_tm_rlen,
+                                                                      ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y,
+                                                                      omega, nullptr, XStage{}, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt);
+    else if (ts.xs && ts.cd == 4)
+        k_rows_tm<OP, TNNZ, 4, false, true, false, VD8><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr,
+                                                               nullptr, nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab,
+                                                               ts.ctab_n, x, b, y, omega, nullptr, ts.xst, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt);
+    else if (ts.xs)
+        k_rows_tm<OP, TNNZ, 8, false, true, false, VD8><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr,
+                                                               nullptr, nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab,
+                                                               ts.ctab_n, x, b, y, omega, nullptr, ts.xst, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt);
+    else if (ts.cd == 4)
+        k_rows_tm<OP, TNNZ, 4, false, false, false, VD8><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
+                                                   nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n, x,
+                                                   b, y, omega, nullptr, XStage{}, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt);
+    else if (ts.cd == 8)
+        k_rows_tm<OP, TNNZ, 8, false, false, false, VD8><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
+                                                   nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n, x,
+                                                   b, y, omega, nullptr, XStage{}, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt);
+    else
+        k_rows_tm<OP, TNNZ, 0, false, false, false, VD8><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, nullptr, ts.d_tm_clo,
+                                                   ts.d_tm_chi, ts.d_base, ts.d_tm_rlen, ts.tm_rs, nullptr,
+                                                   0, x, b, y, omega, nullptr, XStage{}, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt);
+}
+
 template <int OP, int TNNZ>
 void launch_tile(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
                  double* y, double omega, hipStream_t s) {
     const int n = ts.n_short;
     if (ts.tm) {
-        if (ts.anc && ts.cd == 4)
-            k_rows_tm<OP, TNNZ, 4, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
-                                                             nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n,
-                                                             x, b, y, omega, ts.d_tm_anc);
-        else if (ts.anc)
-            k_rows_tm<OP, TNNZ, 8, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
-                                                             nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n,
-                                                             x, b, y, omega, ts.d_tm_anc);
-        else if (ts.pt && ts.cd == 4)
-            k_rows_tm<OP, TNNZ, 4, false, false, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx,
-                                                                          nullptr, nullptr, nullptr, ts.d_tm_rlen,
-                                                                          ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y,
-                                                                          omega);
-        else if (ts.pt)
-            k_rows_tm<OP, TNNZ, 8, false, false, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx,
-                                                                          nullptr, nullptr, nullptr, ts.d_tm_rlen,
-                                                                          ts.tm_rs, ts.d_ctab, ts.ctab_n, x, b, y,
-                                                                          omega);
-        else if (ts.xs && ts.cd == 4)
-            k_rows_tm<OP, TNNZ, 4, false, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr,
-                                                                   nullptr, nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab,
-                                                                   ts.ctab_n, x, b, y, omega, nullptr, ts.xst);
-        else if (ts.xs)
-            k_rows_tm<OP, TNNZ, 8, false, true><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr,
-                                                                   nullptr, nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab,
-                                                                   ts.ctab_n, x, b, y, omega, nullptr, ts.xst);
-        else if (ts.cd == 4)
-            k_rows_tm<OP, TNNZ, 4><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
-                                                       nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n, x,
-                                                       b, y, omega);
-        else if (ts.cd == 8)
-            k_rows_tm<OP, TNNZ, 8><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, ts.d_tm_cidx, nullptr, nullptr,
-                                                       nullptr, ts.d_tm_rlen, ts.tm_rs, ts.d_ctab, ts.ctab_n, x,
-                                                       b, y, omega);
+        if (ts.tm_vt)
+            launch_tm<OP, TNNZ, true>(A, ts, x, b, y, omega, s);
         else
-            k_rows_tm<OP, TNNZ, 0><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_val, nullptr, ts.d_tm_clo,
-                                                       ts.d_tm_chi, ts.d_base, ts.d_tm_rlen, ts.tm_rs, nullptr,
-                                                       0, x, b, y, omega);
+            launch_tm<OP, TNNZ, false>(A, ts, x, b, y, omega, s);
     } else if (ts.cd && A.d_cidx && ts.rl8 && A.d_rlen) {
         if (ts.pt)
             launch_tile2_cd<OP, TNNZ, true>(A, ts, x, b, y, omega, s);

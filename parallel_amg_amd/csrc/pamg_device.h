@@ -83,6 +83,12 @@ struct TileSet {
     uint8_t* d_tm_chi = nullptr;   //   high 8 bits
     uint8_t* d_tm_rlen = nullptr;
     int* d_tm_anc = nullptr;       // anchored dictionary: each row's first column (tm_rs per tile)
+    // 8-bit per-tile value dictionaries in tile-major slots (Options::value_dict, where every
+    // tile of the set has <= 256 distinct values and the 4-bit ones do not fit): value = tile
+    // t's table d_tm_vtab[t * tm_vt + index], index d_tm_vidx[t * tile_nnz + k]; d_tm_val unused
+    int tm_vt = 0;                 // table entries per tile (0: plain values)
+    uint8_t* d_tm_vidx = nullptr;
+    double* d_tm_vtab = nullptr;
     // symmetric diagonal-class layout (Options::sym_dia; interior set of a square operator,
     // pamg_mat::sym): the set's rows run in k_rows_sym instead of tiles
     bool sym = false;

@@ -683,7 +683,30 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
         // every slot is written whole (nonzeros, then zero padding) by the thread that owns its
         // tile, so the buffers need no serial zero fill
         const int cdw = ts->cd;
-        std::unique_ptr<double[]> tv(new double[nt * tn + kVecPad]);
+        // 8-bit per-tile value dictionaries (value_dict): every tile <= 256 distinct values
+        // (bit patterns: +0.0 and -0.0 stay distinct)
+        int vt = 0;
+        if (opt.value_dict) {
+            std::atomic<int> vmax{0};
+            std::atomic<bool> over{false};
+            par_for(nt, [&](int64_t a, int64_t b) {
+                std::vector<uint64_t> u;
+                for (int64_t i = a; i < b && !over; ++i) {
+                    const int4 t = tiles[i];
+                    u.assign(reinterpret_cast<const uint64_t*>(val) + t.z, reinterpret_cast<const uint64_t*>(val) + t.w);
+                    std::sort(u.begin(), u.end());
+                    const int d = (int)(std::unique(u.begin(), u.end()) - u.begin());
+                    if (d > 256) over = true;
+                    int m = vmax.load();
+                    while (d > m && !vmax.compare_exchange_weak(m, d)) {
+                    }
+                }
+            });
+            if (!over) vt = std::max(4, (vmax.load() + 3) & ~3);
+        }
+        std::unique_ptr<double[]> tv(vt ? nullptr : new double[nt * tn + kVecPad]);
+        std::unique_ptr<uint8_t[]> tvi(vt ? new uint8_t[nt * tn + kVecPad] : nullptr);
+        std::unique_ptr<double[]> tvt(vt ? new double[nt * vt + kVecPad] : nullptr);
         std::unique_ptr<uint8_t[]> trl(new uint8_t[nt * rs + kVecPad]);
         const int64_t ncb = cdw == 4 ? tn / 2 : tn;  // column-stream bytes per slot (cd / chi)
         std::unique_ptr<uint8_t[]> tci(new uint8_t[nt * ncb + kVecPad]);
@@ -700,9 +723,32 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
                         const int row = t.x + r;
                         tan[i * rs + r] = row < t.y && rp[row + 1] > rp[row] ? ci[rp[row]] : 0;
                     }
-                double* v = &tv[i * tn];
-                std::memcpy(v, val + t.z, sizeof(double) * cnt);
-                std::fill(v + cnt, v + tn, 0.0);
+                if (vt) {  // the tile's table in first-occurrence order, indices per nonzero
+                    double* tab = &tvt[i * vt];
+                    uint8_t* vi = &tvi[i * tn];
+                    uint64_t hk[512];
+                    int16_t hv[512];
+                    std::fill(hv, hv + 512, (int16_t)-1);
+                    int nd = 0;
+                    for (int k = 0; k < cnt; ++k) {
+                        uint64_t key;
+                        std::memcpy(&key, &val[t.z + k], sizeof(key));
+                        uint32_t h = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 55);  // 9 bits
+                        while (hv[h] >= 0 && hk[h] != key) h = (h + 1) & 511;
+                        if (hv[h] < 0) {
+                            hk[h] = key;
+                            hv[h] = (int16_t)nd;
+                            std::memcpy(&tab[nd++], &key, sizeof(key));
+                        }
+                        vi[k] = (uint8_t)hv[h];
+                    }
+                    std::fill(tab + nd, tab + vt, 0.0);
+                    std::fill(vi + cnt, vi + tn, (uint8_t)0);
+                } else {
+                    double* v = &tv[i * tn];
+                    std::memcpy(v, val + t.z, sizeof(double) * cnt);
+                    std::fill(v + cnt, v + tn, 0.0);
+                }
                 uint8_t* c = &tci[i * ncb];
                 if (cdw == 4) {
                     std::fill(c, c + ncb, (uint8_t)0);
@@ -719,7 +765,7 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
                 }
             }
         });
-        std::fill(&tv[nt * tn], &tv[nt * tn] + kVecPad, 0.0);
+        if (tv) std::fill(&tv[nt * tn], &tv[nt * tn] + kVecPad, 0.0);
         std::fill(&trl[nt * rs], &trl[nt * rs] + kVecPad, (uint8_t)0);
         std::fill(&tci[nt * ncb], &tci[nt * ncb] + kVecPad, (uint8_t)0);
         if (tcl) std::fill(&tcl[nt * tn], &tcl[nt * tn] + kVecPad, (uint16_t)0);
@@ -728,8 +774,18 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
             CHECK(dalloc(&ts->d_tm_anc, nt * rs + kVecPad));
             CHECK(h2d(A->ctx, ts->d_tm_anc, tan.get(), sizeof(int) * (nt * rs + kVecPad)));
         }
-        CHECK(dalloc(&ts->d_tm_val, nt * tn + kVecPad));
-        CHECK(h2d(A->ctx, ts->d_tm_val, tv.get(), sizeof(double) * (nt * tn + kVecPad)));
+        if (vt) {
+            std::fill(&tvi[nt * tn], &tvi[nt * tn] + kVecPad, (uint8_t)0);
+            std::fill(&tvt[nt * vt], &tvt[nt * vt] + kVecPad, 0.0);
+            CHECK(dalloc(&ts->d_tm_vidx, nt * tn + kVecPad));
+            CHECK(h2d(A->ctx, ts->d_tm_vidx, tvi.get(), nt * tn + kVecPad));
+            CHECK(dalloc(&ts->d_tm_vtab, nt * vt + kVecPad));
+            CHECK(h2d(A->ctx, ts->d_tm_vtab, tvt.get(), sizeof(double) * (nt * vt + kVecPad)));
+        } else {
+            CHECK(dalloc(&ts->d_tm_val, nt * tn + kVecPad));
+            CHECK(h2d(A->ctx, ts->d_tm_val, tv.get(), sizeof(double) * (nt * tn + kVecPad)));
+        }
+        ts->tm_vt = vt;
         CHECK(dalloc(&ts->d_tm_rlen, nt * rs + kVecPad));
         CHECK(h2d(A->ctx, ts->d_tm_rlen, trl.get(), nt * rs + kVecPad));
         if (cdw) {
@@ -919,6 +975,9 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_tm_chi);
     dfree(ts.d_tm_rlen);
     dfree(ts.d_tm_anc);
+    dfree(ts.d_tm_vidx);
+    dfree(ts.d_tm_vtab);
+    ts.tm_vt = 0;
     dfree(ts.d_abase);
     ts.anc = ts.pt = ts.xs = false;
     ts.tm = false;
@@ -1772,7 +1831,8 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         if (t->tm) {  // whole padded slots: tile_nnz values + column entries + tm_rs lengths
             const int64_t tn = t->tile_nnz;
             const int64_t rowb = t->tm_rs;
-            b += ns * (rowb * (t->anc ? 5 : 1) + 8 * tn + (t->cd ? t->cd * tn / 8 : 3 * tn) + 16 + (base ? 4 : 0)) +
+            const int64_t valb = t->tm_vt ? tn + 8 * (int64_t)t->tm_vt : 8 * tn;  // 8-bit indices + table
+            b += ns * (rowb * (t->anc ? 5 : 1) + valb + (t->cd ? t->cd * tn / 8 : 3 * tn) + 16 + (base ? 4 : 0)) +
                  (t->cd ? 4 * t->ctab_n * (t->pt ? ns : 1) : 0);
         } else {
             b += (t->rl8 ? 1 : 4) * t->rows_short;
@@ -1910,7 +1970,7 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[7] = t.tile_nnz;
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
-             (t.sym && A->sym.tb_ok ? 32 : 0);
+             (t.sym && A->sym.tb_ok ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0);
     if (t.sym) {  // the symmetric diagonal-class layout: upper classes, k_rows_sym's grid
         out[4] = A->sym.nu;
         out[8] = A->sym.nbands * 8 * A->sym.eighth;

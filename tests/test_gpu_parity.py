@@ -964,6 +964,33 @@ def test_sym_dia_vcycle_same_bits_either_layout(ctx):
     assert np.array_equal(bits(out[0][1]), bits(out[1][1]))
 
 
+@pytest.mark.parametrize("npal,tnnz,lengths", [(40, 1024, [7, 31, 2]), (60, 4096, [31]), (17, 2048, [9]),
+                                               (1000, 1024, [31, 7])])
+def test_tile_major_value_dictionary_bit_exact(ctx, npal, tnnz, lengths):
+    """8-bit per-tile value dictionaries in tile-major slots (value_dict, where the 4-bit ones do
+    not fit and every tile has <= 256 distinct values — the 512^3 level-1 operator's case): SpMV,
+    residual, Jacobi and prolongate-add bit-exact with the oracle; a palette too large for a
+    tile keeps plain values."""
+    from parallel_amg_amd._lib import layout_of
+    rng = np.random.default_rng(npal + tnnz)
+    pal = rng.standard_normal(npal)
+    M = offset_csr(rng, 3000, [-57, -9, -3, -1, 1, 2, 3, 9, 11, 57, 130, -130], lengths, palette=pal)
+    with _with_option("tile_nnz", tnnz), _with_option("tile_major", 2):
+        A, _h = upload(ctx, M)
+    lay = layout_of(A)
+    assert lay["tm"] and lay["tm_vd"] == (npal <= 256 and npal > 16), lay
+    xh, bh, yh = (rng.standard_normal(M.nrows) for _ in range(3))
+    x, b = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh)
+    y = PVector(ctx, M.nrows)
+    mul(y, A, x)
+    assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
+    residual(y, A, x, b)
+    assert np.array_equal(bits(y.own_values()), bits(O.residual(M, xh, bh)))
+    t = PVector(ctx, M.nrows)
+    jacobi(x, A, b, t, 0.61, 1)
+    assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, xh, bh, 0.61)))
+
+
 @pytest.mark.parametrize("kind,shape", [("poisson3d", (128, 128, 128)), ("aniso3d", (128, 128, 128)),
                                         ("poisson3d", (256, 256, 256)), ("poisson3d", (64, 32, 40)),
                                         ("aniso3d", (192, 48, 7))])
