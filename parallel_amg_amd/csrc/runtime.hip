@@ -318,8 +318,12 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows, bo
             ts->c24 = true;
         }
     }
+    // 4-bit per-tile value dictionaries for the rectangular operators (R, P: -12 % at 512^3,
+    // profiles/r03_vd/); square operators keep their column dictionaries in tile-major slots,
+    // with 8-bit value dictionaries there (build_tile_major: elastic3d 80^3 A0 0.206 ms that way
+    // vs 0.237 ms with 24-bit columns + 4-bit values, profiles/r03_e80/)
     ts->vd = false;
-    if (opt.value_dict && ts->c24 && val)
+    if (opt.value_dict && ts->c24 && val && !square)
         CHECK(build_value_dict(tiles, val, ts, vidx, (ci.size() + 1) / 2 + 8));
     ts->rl8 = opt.row_len8 && ts->c24 && !ts->vd && ts->max_short_len <= 255 && ts->n_short > 0 &&
               ts->nnz_short <= 16 * ts->rows_short;

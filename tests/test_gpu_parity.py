@@ -458,8 +458,14 @@ def _stream_bytes_tiles(ctx, M, stream_bytes):
     assert rem == 0 and nt > 0
     assert stream_bytes(col24=1, row_len8=0, col_dict=0, tile_major=0) == 11 * nnz + 4 * (n + 1) + 20 * nt
     assert stream_bytes(col24=1, row_len8=1, col_dict=0, tile_major=0) == 11 * nnz + n + 4 + 20 * nt
-    # 2 distinct values: every tile takes a value dictionary (which keeps the row pointers)
-    assert stream_bytes(value_dict=1) == 3 * nnz + nnz // 2 + 4 * (n + 1) + (20 + 128) * nt
+    # 2 distinct values: a square operator keeps its column dictionary in tile-major slots and
+    # takes 8-bit value dictionaries there (a byte per slot + a 4-entry table per tile instead
+    # of 8 B per slot); 4-bit value dictionaries are for rectangular operators
+    A1, _h1 = _with_options({"value_dict": 1}, lambda: upload(ctx, M))
+    l1 = layout_of(A1)
+    assert l1["tm"] and l1["tm_vd"] and not l1["vd"]
+    tn = l1["tile_nnz"]
+    assert stream_bytes() - A1.stream_bytes == l1["tiles"] * (8 * tn - (tn + 8 * 4))
     # column dictionary: 7 offsets -> 4-bit indices + the 28-B table, 8-bit row lengths, no
     # per-tile base
     assert stream_bytes(tile_major=0) == 8 * nnz + (nnz + 1) // 2 + 4 * 7 + n + 4 + 16 * nt
