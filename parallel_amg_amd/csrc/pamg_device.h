@@ -107,7 +107,8 @@ struct Options {
     int long_tiles = 1;        // 1: 4096-nonzero tiles for square operators with long rows (build_tiles)
     int long_tiles_min = 24;   // nonzeros per row from which long_tiles applies to sets of >= 64 M nonzeros
     int row_len8 = 1;          // 1: 8-bit row lengths instead of 32-bit row pointers where they fit
-    int value_dict = 1;        // 1: 4-bit per-tile value dictionaries where a tile has <= 16 distinct values
+    int value_dict = 1;        // 1: per-tile value dictionaries (4-bit for rectangular operators where a tile has
+                               //    <= 16 distinct values, 8-bit in tile-major slots); 2: 8-bit ones only
     int col_dict = 1;          // 1: row-relative column dictionaries (4/8-bit) where they fit
     int tile_major = 1;        // tile-major padded copies (variant 4): 1 where measured faster, 2 all eligible
     int col_dict_tile = 1;     // 1: per-tile column dictionaries where no global table fits (and they beat 24-bit)

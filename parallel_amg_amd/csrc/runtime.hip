@@ -220,7 +220,7 @@ int build_value_dict(const std::vector<int4>& tiles, const double* val, pamg::Ti
 int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows, bool square,
                 pamg::TileSet* ts, int64_t band, const std::vector<int>& ci,
                 std::vector<uint16_t>* lo, std::vector<uint8_t>* hi, const double* val,
-                std::vector<uint8_t>* vidx, std::vector<int4>* tiles_out) {
+                std::vector<uint8_t>* vidx, std::vector<int4>* tiles_out, bool tall = false) {
     const auto& opt = pamg::options();
     int tnnz = opt.tile_nnz;
     const int trows = pamg::kTileRows;
@@ -318,12 +318,13 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows, bo
             ts->c24 = true;
         }
     }
-    // 4-bit per-tile value dictionaries for the rectangular operators (R, P: -12 % at 512^3,
-    // profiles/r03_vd/); square operators keep their column dictionaries in tile-major slots,
-    // with 8-bit value dictionaries there (build_tile_major: elastic3d 80^3 A0 0.206 ms that way
-    // vs 0.237 ms with 24-bit columns + 4-bit values, profiles/r03_e80/)
+    // 4-bit per-tile value dictionaries for the prolongations (more rows than columns: P0
+    // 1.21 ms vs 1.40 with 8-bit column dictionaries, 512^3, profiles/r03_r0/); the other
+    // operators keep their column dictionaries in tile-major slots with 8-bit value
+    // dictionaries there (build_tile_major: R0 1.06 vs 1.12 ms, elastic3d 80^3 A0 0.206 vs
+    // 0.237 ms, profiles/r03_r0/, profiles/r03_e80/)
     ts->vd = false;
-    if (opt.value_dict && ts->c24 && val && !square)
+    if (opt.value_dict == 1 && ts->c24 && val && tall)
         CHECK(build_value_dict(tiles, val, ts, vidx, (ci.size() + 1) / 2 + 8));
     ts->rl8 = opt.row_len8 && ts->c24 && !ts->vd && ts->max_short_len <= 255 && ts->n_short > 0 &&
               ts->nnz_short <= 16 * ts->rows_short;
@@ -1796,8 +1797,9 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     {
         std::vector<int4> t_in, t_bd;
         const bool square = n_own_cols == nrows;
-        CHECK(build_tiles(rp, inner, square, &A->interior, band, ci, &lo, &hi, val, &vidx, &t_in));
-        CHECK(build_tiles(rp, bnd, square, &A->boundary, band, ci, &lo, &hi, val, &vidx, &t_bd));
+        const bool tall = n_own_cols < nrows;  // a prolongation's shape
+        CHECK(build_tiles(rp, inner, square, &A->interior, band, ci, &lo, &hi, val, &vidx, &t_in, tall));
+        CHECK(build_tiles(rp, bnd, square, &A->boundary, band, ci, &lo, &hi, val, &vidx, &t_bd, tall));
         tr.mark("tiles");
         std::vector<uint8_t> idx8;
         CHECK(build_col_dicts(A.get(), rp, ci, t_in, t_bd, &idx8));
@@ -2598,7 +2600,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "col24" && (value == 0 || value == 1)) o.col24 = (int)value;
     else if (k == "long_tiles" && (value == 0 || value == 1)) o.long_tiles = (int)value;
     else if (k == "row_len8" && (value == 0 || value == 1)) o.row_len8 = (int)value;
-    else if (k == "value_dict" && (value == 0 || value == 1)) o.value_dict = (int)value;
+    else if (k == "value_dict" && value >= 0 && value <= 2) o.value_dict = (int)value;
     else if (k == "col_dict" && (value == 0 || value == 1)) o.col_dict = (int)value;
     else if (k == "tile_major" && value >= 0 && value <= 2) o.tile_major = (int)value;
     else if (k == "col_dict_anchor" && (value == 0 || value == 1)) o.col_dict_anchor = (int)value;
