@@ -150,8 +150,9 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * set runs in the symmetric diagonal-class layout (sym_dia: diagonal + upper values per row,
  * lower values read from their mirrors; then out[4] = the upper offset classes and out[8] =
  * the kernel's grid); bit 4: that kernel takes two rows per lane (sym_rows 2); bit 5: the
- * level-0 pre-smoothing sweep and residual of a V-cycle run fused in one pipelined pass
- * (jr_fuse) on this matrix. */
+ * matrix is a 7-point grid stencil the temporally blocked passes run on (k_sym_tb: the
+ * level-0 Jacobi -> residual, and the pipelined cycles' post -> pre -> residual chain; jr_fuse);
+ * bit 6: the tile-major set carries 8-bit per-tile value dictionaries (value_dict). */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[10]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
@@ -163,9 +164,10 @@ int pamg_residual(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec*
 int pamg_jacobi(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec* b,
                 pamg_vec* tmp, double omega, int nsweeps);
 /* One weighted-Jacobi sweep and the residual of its result: t = x + omega D^-1 (b - A x),
- * r = b - A t (the level-0 pre-smoothing + residual of a V-cycle). On one part in the symmetric
- * layout with jr_fuse on, both run in one pipelined pass (*fused = 1); otherwise two sweeps.
- * The bits are the same either way. fused may be NULL. */
+ * r = b - A t (the level-0 pre-smoothing + residual of a V-cycle). On one part, for a 7-point
+ * grid stencil in the symmetric layout (pamg_mat_layout bit 5) with jr_fuse on, both run in one
+ * temporally blocked pass over the matrix (*fused = 1); otherwise two sweeps. The bits are the
+ * same either way. fused may be NULL. */
 int pamg_jacobi_residual(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pamg_vec* b,
                          pamg_vec* t, pamg_vec* r, double omega, int* fused);
 
@@ -223,17 +225,19 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
                      pamg_vec* y, double omega, int reps, double* avg_ms);
 
 /* Micro-benchmark hook of the cross-cycle pipeline: `reps` launches of its level-0 chain kernel
- * (post-smoothing -> next pre-smoothing -> residual, k_sym_chain) on the hierarchy's own level-0
+ * (post-smoothing -> next pre-smoothing -> residual, k_sym_tb<3>) on the hierarchy's own level-0
  * buffers and the given x / b (x is overwritten); average ms per launch (HIP events).
- * PAMG_E_STATE when the hierarchy does not qualify (one part, V(1,1), symmetric level 0). */
+ * PAMG_E_STATE when the hierarchy does not qualify (one part, V(1,1), jr_fuse, level 0 with
+ * pamg_mat_layout bit 5). */
 int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps, double* avg_ms);
 
 /* Process-wide knobs. Applied to later pamg_mat_upload calls: "tile_nnz" (1024 | 2048 | 4096,
  * nonzero budget of a 256-row tile), "tile_order" (0 natural | 1 banded XCD-blocked), "col24",
- * "long_tiles", "row_len8", "value_dict", "col_dict", "col_dict_anchor", "col_dict_tile", "x_stage", "tm_tile_dicts" (0 | 1
+ * "long_tiles", "row_len8", "value_dict" (0 | 1 | 2), "col_dict", "col_dict_anchor", "col_dict_tile", "x_stage", "tm_tile_dicts" (0 | 1
  * layout features; "sym_dia": symmetric diagonal-class layout of a square operator's interior
- * rows where they qualify; "sym_rows" 1 | 2: rows per lane of its kernel; "jr_fuse": the fused
- * level-0 Jacobi -> residual pass of the V-cycle, read at graph capture), "long_tiles_min" (1..255 nonzeros per row from which sets of >= 64 M
+ * rows where they qualify; "sym_rows" 1 | 2: rows per lane of its kernel; "jr_fuse": the
+ * temporally blocked level-0 passes of the V-cycle and the cross-cycle pipeline, read at graph
+ * capture), "long_tiles_min" (1..255 nonzeros per row from which sets of >= 64 M
  * nonzeros take long tiles), "band_pct" / "band_pct_restrict" (percent scale of the banded
  * order's band; the second for operators with fewer rows than columns), "tile_major" (0 | 1 where measured faster | 2 every eligible set). Applied at
  * every exchange:
