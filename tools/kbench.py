@@ -87,7 +87,7 @@ def main():
     ops = [int(o) for o in args.ops.split(",")]
     for cfg in args.configs.split(","):
         given = [int(v) for v in cfg.split(":")]
-        vals = given + [1024, 1, 1, 0, 1, 1, 1, 1, 1, 1, 1, 1][len(given):]  # defaults for missing fields
+        vals = given + [1024, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1][len(given):]  # library defaults for missing fields
         tnnz, order, c24, vd, lt, rl8, cd, tm, anc, ptd, xst, tmpt = vals[:12]
         set_opts(tile_nnz=tnnz, tile_order=order, col24=c24, value_dict=vd, long_tiles=lt, row_len8=rl8,
                  col_dict=cd, tile_major=tm, col_dict_anchor=anc, col_dict_tile=ptd, x_stage=xst, tm_tile_dicts=tmpt)
