@@ -635,7 +635,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_sym(
     const double* __restrict__ b, double* __restrict__ y, double omega) {
     const int bid = blockIdx.x, tid = threadIdx.x;
     const int xcd = bid & 7, j = bid >> 3;
-    const int plane = j / sd.eighth, blk = xcd * sd.eighth + j % sd.eighth;
+    const int plane = sd.plane0 + j / sd.eighth, blk = xcd * sd.eighth + j % sd.eighth;
     const int64_t lo = (int64_t)plane * sd.band;
     const int64_t i64 = lo + (int64_t)blk * kBlock + tid;
     const int64_t hi = lo + sd.band < nrows ? lo + sd.band : nrows;
@@ -698,7 +698,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_sym2(
     constexpr int RB = 2 * kBlock;  // rows per block
     const int bid = blockIdx.x, tid = threadIdx.x;
     const int xcd = bid & 7, j = bid >> 3;
-    const int plane = j / sd.eighth, blk = xcd * sd.eighth + j % sd.eighth;
+    const int plane = sd.plane0 + j / sd.eighth, blk = xcd * sd.eighth + j % sd.eighth;
     const int64_t lo = (int64_t)plane * sd.band;
     const int64_t i0 = lo + (int64_t)blk * RB + 2 * tid;
     const int64_t hi = lo + sd.band < nrows ? lo + sd.band : nrows;
@@ -1006,6 +1006,7 @@ __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tb(int nrows, const
     const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
     if (lin >= ntiles) return;  // the whole workgroup, before any barrier
     const int ty = lin % g.tiles_y, tx = (lin / g.tiles_y) % g.tiles_x, zc = lin / (g.tiles_x * g.tiles_y);
+    if (g.zlo + zc * g.zlen >= g.zhi) return;  // (a chunk past the output range: uniform)
     const int x0 = tx * kTbX, y0 = ty * kTbY;
     TbCtx<S> t;
     t.x0 = x0;
@@ -1013,8 +1014,8 @@ __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tb(int nrows, const
     t.nx = g.nx;
     t.ny = g.ny;
     t.nz = g.nz;
-    t.zs = zc * g.zlen;
-    t.ze = min(t.zs + g.zlen, g.nz);
+    t.zs = g.zlo + zc * g.zlen;
+    t.ze = min(t.zs + g.zlen, g.zhi);
     t.kend = t.ze + Sh::H;
     t.M = (int64_t)g.nx * g.ny;
     t.n = nrows;
@@ -1381,13 +1382,36 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
 }  // namespace
 
 void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s) {
-    const SymDia& sd = A.sym;
-    const int ntiles = sd.tb.tiles_x * sd.tb.tiles_y * sd.tb.zchunks;
+    SymDia sd = A.sym;
+    // output planes: all of a one-part operator's; a part's planes S planes in from a neighbour
+    // part, whose stage-0 halo rows stay in the set and in0 planes in the part
+    TbGeom& g = sd.tb;
+    g.zlo = sd.part_lo == 0 ? 0 : sd.part_lo + ta.nstages - 1;
+    g.zhi = sd.part_hi == g.nz ? g.nz : sd.part_hi - (ta.nstages - 1);
+    const int span = g.zhi - g.zlo;
+    if (span <= 0) return;
+    g.zchunks = std::max(1, std::min(g.zchunks, span / 2 > 0 ? span / 2 : 1));
+    g.zlen = (span + g.zchunks - 1) / g.zchunks;
+    g.zchunks = (span + g.zlen - 1) / g.zlen;
+    const int ntiles = g.tiles_x * g.tiles_y * g.zchunks;
     const int grid = (ntiles + 7) / 8 * 8;
     if (ta.nstages == 2)
         k_sym_tb<2><<<grid, TbShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, ta);
     else
         k_sym_tb<3><<<grid, TbShape<3>::threads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, ta);
+}
+
+void launch_sym_planes(const pamg_mat& A, int op, int p0, int p1, const double* x, const double* b, double* y,
+                       double omega, hipStream_t s) {
+    if (p1 <= p0) return;
+    pamg_mat B = A;  // shallow: the same device arrays, a plane window
+    B.sym.plane0 = p0;
+    B.sym.nbands = p1 - p0;
+    switch (op) {
+        case OP_RESID: launch_sym<OP_RESID>(B, x, b, y, omega, s); break;
+        case OP_JACOBI: launch_sym<OP_JACOBI>(B, x, b, y, omega, s); break;
+        default: launch_sym<OP_SPMV>(B, x, b, y, omega, s); break;
+    }
 }
 
 void launch_rows(const pamg_mat& A, const TileSet& ts, int op, const double* x, const double* b,

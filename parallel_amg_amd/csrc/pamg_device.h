@@ -142,6 +142,7 @@ struct TbGeom {
     int nx = 0, ny = 0, nz = 0;
     int tiles_x = 0, tiles_y = 0;   // kTbX x kTbY tiles of a plane
     int zchunks = 1, zlen = 0;      // planes per workgroup (the last chunk may be shorter)
+    int zlo = 0, zhi = 0;           // output planes [zlo, zhi) of a launch (set by launch_sym_tb)
 };
 struct SymDia {
     int nu = 0;                     // upper offset classes
@@ -151,6 +152,13 @@ struct SymDia {
     int rpl = 1;                    // rows per lane (k_rows_sym / k_rows_sym2)
     // temporally blocked sweeps (Options::jr_fuse; one part, every row in the set, nu = 3)
     bool tb_ok = false;
+    // one part of several (z-slab of whole planes; a plane next to another part reads ghosts,
+    // the set is the other planes): the blocked passes run on the planes whose halo stays inside
+    // the set (S planes from a neighbour part) and the separate sweeps (with their exchanges) on
+    // the rest (runtime.hip jr_part)
+    bool tb_part = false;
+    int part_lo = 0, part_hi = 0;   // the set's planes [part_lo, part_hi) (the others read ghosts)
+    int plane0 = 0;                 // first plane of a plane-range launch of k_rows_sym / sym2
     TbGeom tb;
     uint8_t* d_mask = nullptr;      // nrows (+ pad) masks of 1 byte (2 nu + 1 <= 7) or 2 bytes
     int mask_bytes = 2;
@@ -246,6 +254,9 @@ struct TbArgs {
 };
 constexpr int kTbX = 64, kTbY = 16;  // output tile of a workgroup (grid points in x, y)
 void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s);
+// a row operation of the symmetric set on the grid planes [p0, p1) only (band = one plane)
+void launch_sym_planes(const pamg_mat& A, int op, int p0, int p1, const double* x, const double* b, double* y,
+                       double omega, hipStream_t s);
 // dst[i] = src[perm[i]] (gather), or dst[perm[i]] = src[i] (scatter)
 void launch_permute(int64_t n, const int* perm, const double* src, double* dst, bool scatter, hipStream_t s);
 void launch_axpby(int64_t n, double a, const double* x, double b, double* y, hipStream_t s);

@@ -904,8 +904,24 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
         }
     });
     if (bad) return PAMG_OK;
+    // A part of several (a z-slab of whole planes, SymDia::tb_part): the set must be exactly its
+    // planes 1 .. nz-2 (the first and last plane read ghosts); its bands are whole planes, so
+    // the separate sweeps can run on plane windows (launch_sym_planes)
+    const int64_t Mp = nu == 3 ? sd.off[2] : 0;
+    const bool whole = A->ncols == n && (int64_t)inner.size() == n;
+    bool part = false;
+    int plo = 0, phi = 0;
+    if (!whole && nu == 3 && Mp > 0 && n % Mp == 0 && n / Mp >= 6 && !inner.empty() && inner.size() % Mp == 0 &&
+        inner.front() % Mp == 0) {
+        const int nzp = (int)(n / Mp);
+        plo = (int)(inner.front() / Mp);
+        phi = plo + (int)(inner.size() / Mp);
+        part = (plo == 0 || plo == 1) && (phi == nzp || phi == nzp - 1) && phi - plo < nzp;
+        for (size_t q = 0; q < inner.size() && part; ++q) part = inner[q] == inner.front() + (int64_t)q;
+    }
     // XCD-banded block order (natural order: one band)
     int64_t bd = (pamg::options().tile_order == 1 && band >= 8 * pamg::kBlock) ? band : n;
+    if (part && Mp >= 8 * pamg::kBlock) bd = Mp;
     sd.band = (int)bd;
     sd.rpl = pamg::options().sym_rows;
     const int64_t rows_per_block = (int64_t)pamg::kBlock * sd.rpl;
@@ -928,8 +944,8 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
     // 7-point grid stencil in natural order (classes 1, nx, nx*ny; n = nx*ny*nz) whose rows
     // never reach across a grid line (the -1 / +1 / -nx / +nx classes absent at x = 0 / nx-1 /
     // y = 0 / ny-1), tiles of kTbX x kTbY
-    if (nu == 3 && mb == 1 && A->ncols == n && (int64_t)inner.size() == n && sd.off[0] == 1 &&
-        sd.off[2] % sd.off[1] == 0 && n % sd.off[2] == 0) {
+    part = part && sd.band == Mp;
+    if (nu == 3 && mb == 1 && (whole || part) && sd.off[0] == 1 && sd.off[2] % sd.off[1] == 0 && n % sd.off[2] == 0) {
         const int nx = sd.off[1], ny = sd.off[2] / sd.off[1];
         const int nz = (int)(n / sd.off[2]);
         bool ok = nx % pamg::kTbX == 0 && ny % pamg::kTbY == 0;
@@ -958,7 +974,12 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
             g.zchunks = std::max(1, std::min(want, nz / 4 > 0 ? nz / 4 : 1));
             g.zlen = (nz + g.zchunks - 1) / g.zchunks;
             g.zchunks = (nz + g.zlen - 1) / g.zlen;
-            sd.tb_ok = true;
+            g.zlo = 0;
+            g.zhi = nz;
+            sd.tb_ok = whole;
+            sd.tb_part = part;
+            sd.part_lo = part ? plo : 0;
+            sd.part_hi = part ? phi : nz;
         }
     }
     A->sym = sd;
@@ -1062,6 +1083,62 @@ int apply(pamg_ctx* ctx, const pamg_mat* A, int op, double* x, const double* b, 
     pamg::launch_rows(*A, A->boundary, op, x, b, x, y, omega, s);
     HIPC(hipGetLastError());
     return PAMG_OK;
+}
+
+// t = Jacobi(x), r = b - A t on one part of several whose level is a z-slab in the symmetric
+// layout (SymDia::tb_part): the blocked pass k_sym_tb<2> covers the output planes that need no
+// ghost (two planes in from a neighbour part) and runs while x's ghosts travel; the set's
+// planes next to them then take the separate Jacobi, the planes with ghost columns (the
+// boundary tiles) theirs after the exchange; t's ghosts travel while the set's planes take the
+// residual, then the boundary planes theirs. Every row's value is the separate sweeps' (SPEC
+// §S3 bits).
+int jr_part(pamg_ctx* ctx, const pamg_mat* A, double* x, const double* b, double* t, double* r, double omega) {
+    hipStream_t s = ctx->s_comp;
+    const pamg::SymDia& sd = A->sym;
+    const int nz = sd.tb.nz;
+    // the blocked pass's output planes (launch_sym_tb): S = 2 planes in from a neighbour part
+    const int zlo = sd.part_lo == 0 ? 0 : sd.part_lo + 1, zhi = sd.part_hi == nz ? nz : sd.part_hi - 1;
+    auto stage = [&](double* v, auto&& overlapped, auto&& after) -> int {
+        bool comm = A->plan && !A->plan->nbr.empty();
+        if (comm && ctx->host_fn) {  // debug transport: exchange first, no overlap
+            CHECK(exchange_on(A->plan, v, s));
+            comm = false;
+        }
+        if (comm) {
+            HIPC(hipEventRecord(ctx->ev_fork, s));
+            HIPC(hipStreamWaitEvent(ctx->s_comm, ctx->ev_fork, 0));
+            CHECK(exchange_on(A->plan, v, ctx->s_comm));
+            HIPC(hipEventRecord(ctx->ev_join, ctx->s_comm));
+        }
+        overlapped();
+        if (comm) HIPC(hipStreamWaitEvent(s, ctx->ev_join, 0));
+        after();
+        HIPC(hipGetLastError());
+        return PAMG_OK;
+    };
+    pamg::TbArgs ta;
+    ta.nstages = 2;
+    ta.last_resid = true;
+    ta.in0 = x;
+    ta.out[0] = t;
+    ta.out[1] = r;
+    ta.b = b;
+    ta.omega = omega;
+    CHECK(stage(
+        x,
+        [&]() {
+            pamg::launch_sym_tb(*A, ta, s);
+            pamg::launch_sym_planes(*A, pamg::OP_JACOBI, sd.part_lo, zlo, x, b, t, omega, s);
+            pamg::launch_sym_planes(*A, pamg::OP_JACOBI, zhi, sd.part_hi, x, b, t, omega, s);
+        },
+        [&]() { pamg::launch_rows(*A, A->boundary, pamg::OP_JACOBI, x, b, x, t, omega, s); }));
+    return stage(
+        t,
+        [&]() {
+            pamg::launch_sym_planes(*A, pamg::OP_RESID, sd.part_lo, zlo, t, b, r, 0.0, s);
+            pamg::launch_sym_planes(*A, pamg::OP_RESID, zhi, sd.part_hi, t, b, r, 0.0, s);
+        },
+        [&]() { pamg::launch_rows(*A, A->boundary, pamg::OP_RESID, t, b, t, r, 0.0, s); });
 }
 
 // The deterministic dot x.y over the own rows of every rank (fixed-grid partials, then the
@@ -1254,7 +1331,13 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false,
         // temporally blocked pass (k_sym_tb, S = 2; both timed as jacobi_pre)
         const bool fuse = l == 0 && !zero0 && H->nu1 == 1 && pamg::options().jr_fuse && A->interior.sym &&
                           A->sym.tb_ok && !(A->plan && !A->plan->nbr.empty());
-        if (fuse) {
+        // one part of several: the blocked pass on the slab's inner planes (jr_part)
+        const bool fuse_part = !fuse && l == 0 && !zero0 && H->nu1 == 1 && pamg::options().jr_fuse &&
+                               A->interior.sym && A->sym.tb_part;
+        if (fuse_part) {
+            ProfScope p(H, l, 0, s);
+            CHECK(jr_part(ctx, A, H->x[0], H->b[0], c, o, H->omega[0]));
+        } else if (fuse) {
             ProfScope p(H, l, 0, s);
             pamg::TbArgs ta;
             ta.nstages = 2;
@@ -1279,7 +1362,7 @@ int vcycle_enqueue(pamg_hier* H, double* x, const double* b, bool zero0 = false,
         }
         cur[l] = c;
         spare[l] = o;
-        if (!fuse) {
+        if (!fuse && !fuse_part) {
             ProfScope p(H, l, 1, s);
             CHECK(apply(ctx, A, pamg::OP_RESID, c, H->b[l], o, 0.0));
         }
@@ -1976,7 +2059,7 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[7] = t.tile_nnz;
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
-             (t.sym && A->sym.tb_ok ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0);
+             (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0);
     if (t.sym) {  // the symmetric diagonal-class layout: upper classes, k_rows_sym's grid
         out[4] = A->sym.nu;
         out[8] = A->sym.nbands * 8 * A->sym.eighth;
@@ -2051,7 +2134,10 @@ int pamg_jacobi_residual(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pa
         return fail(PAMG_E_ARG, "jacobi_residual: size mismatch or aliasing");
     CHECK(set_device(ctx));
     const bool fuse = pamg::options().jr_fuse && A->interior.sym && A->sym.tb_ok && !(A->plan && !A->plan->nbr.empty());
-    if (fuse) {
+    const bool fuse_part = !fuse && pamg::options().jr_fuse && A->interior.sym && A->sym.tb_part;
+    if (fuse_part) {
+        CHECK(jr_part(ctx, A, x->d, b->d, t->d, r->d, omega));
+    } else if (fuse) {
         pamg::TbArgs ta;
         ta.nstages = 2;
         ta.last_resid = true;
@@ -2066,7 +2152,7 @@ int pamg_jacobi_residual(pamg_ctx* ctx, const pamg_mat* A, pamg_vec* x, const pa
         CHECK(apply(ctx, A, pamg::OP_JACOBI, x->d, b->d, t->d, omega));
         CHECK(apply(ctx, A, pamg::OP_RESID, t->d, b->d, r->d, 0.0));
     }
-    if (fused) *fused = fuse ? 1 : 0;
+    if (fused) *fused = (fuse || fuse_part) ? 1 : 0;
     HIPC(hipStreamSynchronize(ctx->s_comp));
     return PAMG_OK;
 }
