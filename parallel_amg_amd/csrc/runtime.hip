@@ -1085,19 +1085,20 @@ int apply(pamg_ctx* ctx, const pamg_mat* A, int op, double* x, const double* b, 
     return PAMG_OK;
 }
 
-// t = Jacobi(x), r = b - A t on one part of several whose level is a z-slab in the symmetric
-// layout (SymDia::tb_part): the blocked pass k_sym_tb<2> covers the output planes that need no
-// ghost (two planes in from a neighbour part) and runs while x's ghosts travel; the set's
-// planes next to them then take the separate Jacobi, the planes with ghost columns (the
-// boundary tiles) theirs after the exchange; t's ghosts travel while the set's planes take the
-// residual, then the boundary planes theirs. Every row's value is the separate sweeps' (SPEC
-// §S3 bits).
-int jr_part(pamg_ctx* ctx, const pamg_mat* A, double* x, const double* b, double* t, double* r, double omega) {
+// S dependent sweeps (S = 2: Jacobi -> residual; S = 3: Jacobi -> Jacobi -> residual, the
+// pipeline's chain) on one part of several whose level is a z-slab in the symmetric layout
+// (SymDia::tb_part): the blocked pass k_sym_tb<S> covers the output planes that need no ghost
+// (S-1 planes in from a neighbour part) and runs while in0's ghosts travel; the set's planes
+// next to them then take the separate sweep, the planes with ghost columns (the boundary
+// tiles) theirs after the exchange; each later stage exchanges its input's ghosts while the
+// set's planes take the separate sweep, then the boundary planes. Every row's value is the
+// separate sweeps' (SPEC §S3 bits).
+int sweeps_part(pamg_ctx* ctx, const pamg_mat* A, int S, const double* in0, double* const* out, const double* b,
+                double omega) {
     hipStream_t s = ctx->s_comp;
     const pamg::SymDia& sd = A->sym;
     const int nz = sd.tb.nz;
-    // the blocked pass's output planes (launch_sym_tb): S = 2 planes in from a neighbour part
-    const int zlo = sd.part_lo == 0 ? 0 : sd.part_lo + 1, zhi = sd.part_hi == nz ? nz : sd.part_hi - 1;
+    const int zlo = sd.part_lo == 0 ? 0 : sd.part_lo + S - 1, zhi = sd.part_hi == nz ? nz : sd.part_hi - (S - 1);
     auto stage = [&](double* v, auto&& overlapped, auto&& after) -> int {
         bool comm = A->plan && !A->plan->nbr.empty();
         if (comm && ctx->host_fn) {  // debug transport: exchange first, no overlap
@@ -1117,28 +1118,31 @@ int jr_part(pamg_ctx* ctx, const pamg_mat* A, double* x, const double* b, double
         return PAMG_OK;
     };
     pamg::TbArgs ta;
-    ta.nstages = 2;
+    ta.nstages = S;
     ta.last_resid = true;
-    ta.in0 = x;
-    ta.out[0] = t;
-    ta.out[1] = r;
+    ta.in0 = in0;
+    for (int q = 0; q < S; ++q) ta.out[q] = out[q];
     ta.b = b;
     ta.omega = omega;
-    CHECK(stage(
-        x,
-        [&]() {
-            pamg::launch_sym_tb(*A, ta, s);
-            pamg::launch_sym_planes(*A, pamg::OP_JACOBI, sd.part_lo, zlo, x, b, t, omega, s);
-            pamg::launch_sym_planes(*A, pamg::OP_JACOBI, zhi, sd.part_hi, x, b, t, omega, s);
-        },
-        [&]() { pamg::launch_rows(*A, A->boundary, pamg::OP_JACOBI, x, b, x, t, omega, s); }));
-    return stage(
-        t,
-        [&]() {
-            pamg::launch_sym_planes(*A, pamg::OP_RESID, sd.part_lo, zlo, t, b, r, 0.0, s);
-            pamg::launch_sym_planes(*A, pamg::OP_RESID, zhi, sd.part_hi, t, b, r, 0.0, s);
-        },
-        [&]() { pamg::launch_rows(*A, A->boundary, pamg::OP_RESID, t, b, t, r, 0.0, s); });
+    for (int q = 0; q < S; ++q) {
+        const int op = q == S - 1 ? pamg::OP_RESID : pamg::OP_JACOBI;
+        const double w = q == S - 1 ? 0.0 : omega;
+        double* v = const_cast<double*>(q == 0 ? in0 : out[q - 1]);
+        CHECK(stage(
+            v,
+            [&]() {
+                if (q == 0) pamg::launch_sym_tb(*A, ta, s);
+                pamg::launch_sym_planes(*A, op, sd.part_lo, zlo, v, b, out[q], w, s);
+                pamg::launch_sym_planes(*A, op, zhi, sd.part_hi, v, b, out[q], w, s);
+            },
+            [&]() { pamg::launch_rows(*A, A->boundary, op, v, b, v, out[q], w, s); }));
+    }
+    return PAMG_OK;
+}
+
+int jr_part(pamg_ctx* ctx, const pamg_mat* A, double* x, const double* b, double* t, double* r, double omega) {
+    double* out[2] = {t, r};
+    return sweeps_part(ctx, A, 2, x, out, b, omega);
 }
 
 // The deterministic dot x.y over the own rows of every rank (fixed-grid partials, then the
@@ -2399,8 +2403,12 @@ int pamg_hier_profile_read(pamg_hier* H, double* out) {
 // keyed on the vector addresses and the zero-guess flag).
 // The k_sym_chain launch of a steady segment: the previous cycle's level-0 post-smoothing
 // (t_prev -> x), this cycle's pre-smoothing (x -> t_next) and residual (t_next -> r[0]).
-static void launch_chain3(pamg_hier* H, double* x, const double* b, const double* t_prev, double* t_next) {
+static int launch_chain3(pamg_hier* H, double* x, const double* b, const double* t_prev, double* t_next) {
     const pamg_mat* A = H->A[0];
+    if (A->sym.tb_part) {  // one part of several: the blocked pass on the slab's inner planes
+        double* out[3] = {x, t_next, H->r[0]};
+        return sweeps_part(H->ctx, A, 3, t_prev, out, b, H->omega[0]);
+    }
     pamg::TbArgs ta;
     ta.nstages = 3;
     ta.last_resid = true;
@@ -2411,6 +2419,8 @@ static void launch_chain3(pamg_hier* H, double* x, const double* b, const double
     ta.b = b;
     ta.omega = H->omega[0];
     pamg::launch_sym_tb(*A, ta, H->ctx->s_comp);
+    HIPC(hipGetLastError());
+    return PAMG_OK;
 }
 
 // Segments of the cross-cycle pipeline. seg 0: head (first cycle, no level-0 post-smoothing,
@@ -2427,7 +2437,7 @@ static int pipe_enqueue(pamg_hier* H, double* x, const double* b, int seg) {
         double* next = seg == 1 ? u0 : t0;
         {
             ProfScope p(H, 0, 0, H->ctx->s_comp);
-            launch_chain3(H, x, b, prev, next);
+            CHECK(launch_chain3(H, x, b, prev, next));
         }
         sg.given = true;
         sg.t0 = next;
@@ -2444,7 +2454,8 @@ static bool pipe_ok(const pamg_hier* H, int ncycles, bool zero0) {
     if (zero0 || ncycles < 2 || H->L < 2 || H->prof || !pamg::options().jr_fuse || H->nu1 != 1 || H->nu2 != 1)
         return false;
     const pamg_mat* A = H->A[0];
-    return H->ctx->nranks == 1 && A->interior.sym && A->sym.tb_ok && !(A->plan && !A->plan->nbr.empty());
+    if (!A->interior.sym) return false;
+    return (H->ctx->nranks == 1 && A->sym.tb_ok && !(A->plan && !A->plan->nbr.empty())) || A->sym.tb_part;
 }
 
 static int vcycle_pipe(pamg_hier* H, double* x, const double* b, int ncycles) {
@@ -2737,7 +2748,7 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
     CHECK(check_vec_for(H->A[0], x, "hier_bench_chain"));
     CHECK(set_device(ctx));
     if (!H->u0) {
-        const int64_t n = H->nown[0] + kVecPad;
+        const int64_t n = H->nown[0] + (H->A[0]->plan ? H->A[0]->plan->n_ghost : 0) + kVecPad;
         CHECK(dalloc(&H->u0, n));
         HIPC(hipMemset(H->u0, 0, sizeof(double) * n));
     }
@@ -2745,9 +2756,9 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
     HIPC(hipEventCreate(&e0));
     HIPC(hipEventCreate(&e1));
     hipStream_t s = ctx->s_comp;
-    launch_chain3(H, x->d, b->d, H->t[0], H->u0);
+    CHECK(launch_chain3(H, x->d, b->d, H->t[0], H->u0));
     HIPC(hipEventRecord(e0, s));
-    for (int k = 0; k < reps; ++k) launch_chain3(H, x->d, b->d, (k & 1) ? H->u0 : H->t[0], (k & 1) ? H->t[0] : H->u0);
+    for (int k = 0; k < reps; ++k) CHECK(launch_chain3(H, x->d, b->d, (k & 1) ? H->u0 : H->t[0], (k & 1) ? H->t[0] : H->u0));
     HIPC(hipEventRecord(e1, s));
     HIPC(hipEventSynchronize(e1));
     float ms = 0.f;

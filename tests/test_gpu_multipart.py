@@ -89,6 +89,11 @@ def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, poison
         mul(b, A0, xst)
         x = S.new_vector()
         hist = S.vcycle(x, b, ncycles, res_hist=True)
+        # the same cycles as one stationary run: the cross-cycle pipeline where the parts qualify
+        # (z-slabs of whole planes), separate cycles otherwise — the same bits either way
+        xp = S.new_vector()
+        S.vcycle(xp, b, ncycles)
+        same_pipe = bool(np.array_equal(xp.own_values().view(np.int64), x.own_values().view(np.int64)))
         # consistent!(x) split (exchange_begin/_end) == the synchronous exchange == the
         # owners' values at the ghost ids
         ghosts = None
@@ -102,11 +107,11 @@ def _worker(rank, world, port, kind, n, max_coarse, agglomerate, ncycles, poison
             ga, gb = va.ghost_values(), vb.ghost_values()
             assert np.array_equal(ga.view(np.int64), gb.view(np.int64))
             ghosts = (np.asarray(pl.ghost_ids, np.int64), ga)
-        out = (rank, "ok", b.own_values(), x.own_values(), hist, ghosts, _lib.layout_of(S.A[0])["jr_fused"])
+        out = (rank, "ok", b.own_values(), x.own_values(), hist, ghosts, _lib.layout_of(S.A[0])["jr_fused"], same_pipe)
         q.put(out)
     except Exception:
         import traceback
-        q.put((rank, traceback.format_exc(), None, None, None, None, None))
+        q.put((rank, traceback.format_exc(), None, None, None, None, None, None))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
@@ -152,6 +157,7 @@ def test_multipart_vcycle_bit_exact(world, kind, n, max_coarse, agglomerate, poi
         # every part is a z-slab of whole planes: the level-0 Jacobi -> residual runs as the
         # blocked pass on the slab's inner planes (SymDia::tb_part) — the bits above are its
         assert all(res[r][6] for r in range(world)), [res[r][6] for r in range(world)]
+    assert all(res[r][7] for r in range(world)), [res[r][7] for r in range(world)]
     for r in range(world):
         np.testing.assert_allclose(res[r][4], ho, rtol=1e-12)
         if res[r][5] is not None:
