@@ -294,7 +294,7 @@ def main():
         kname = f"k_rows_tile2<2, {tn}, false, false, true, {cd}, {tf(lay['per_tile'])}, {tf(lay['anchored'])}>"
     else:
         c24 = lay["c24"]
-        kname = (f"k_rows_tile2<2, {tn}, {tf(c24)}, {tf(lay['vd'])}, {tf(lay['rl8'] and c24 and not lay['vd'])}, "
+        kname = (f"k_rows_tile2<2, {tn}, {tf(c24)}, {tf(lay['vd'])}, {tf(lay['rl8'] and c24)}, "
                  f"0, false, false>")
     workload_key = f"{args.matrix or args.kind}:{args.grid}:p{world}:perm{args.permute}" + (":rcm" if args.rcm else "")
     src = kernel_source_sha()

@@ -1318,6 +1318,10 @@ void launch_tile(const pamg_mat& A, const TileSet& ts, const double* x, const do
             launch_tile2_cd<OP, TNNZ, true>(A, ts, x, b, y, omega, s);
         else
             launch_tile2_cd<OP, TNNZ, false>(A, ts, x, b, y, omega, s);
+    } else if (ts.c24 && A.d_clo && ts.vd && A.d_vidx && ts.rl8 && A.d_rlen) {
+        k_rows_tile2<OP, TNNZ, true, true, true><<<n, kBlock, 0, s>>>(ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b,
+                                                                     y, omega, A.d_clo, A.d_chi, ts.d_base,
+                                                                     A.d_vidx, ts.d_vtab, A.d_rlen);
     } else if (ts.c24 && A.d_clo && ts.vd && A.d_vidx) {
         k_rows_tile2<OP, TNNZ, true, true><<<n, kBlock, 0, s>>>(ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y,
                                                                omega, A.d_clo, A.d_chi, ts.d_base, A.d_vidx,

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -181,40 +182,135 @@ static std::vector<int4> xcd_band_order(const std::vector<int4>& tiles, int64_t 
     return out;
 }
 
-// Opt-in value dictionaries of a 24-bit tile set: every tile holds <= 16 distinct values
-// (bit patterns, so -0.0 / NaN payloads survive); indices go to vidx (4 bits per entry).
+// Value dictionaries of a 24-bit tile set: every tile holds <= 16 distinct values (bit
+// patterns, so -0.0 / NaN payloads survive); indices go to vidx (4 bits per entry). Tiles are
+// independent (tables in parallel); the indices go through a byte per nonzero and are packed by
+// byte afterwards, since two tiles can share the byte of an odd boundary.
 int build_value_dict(const std::vector<int4>& tiles, const double* val, pamg::TileSet* ts,
                      std::vector<uint8_t>* vidx, size_t nslots) {
+    const int64_t nt = (int64_t)tiles.size();
     std::vector<double> tab(tiles.size() * 16, 0.0);
-    std::vector<uint8_t> slot;
-    for (size_t t = 0; t < tiles.size(); ++t) {
-        uint64_t key[16];
-        int nk = 0;
-        for (int k = tiles[t].z; k < tiles[t].w; ++k) {
-            uint64_t b;
-            std::memcpy(&b, &val[k], 8);
-            int j = 0;
-            while (j < nk && key[j] != b) ++j;
-            if (j == nk) {
-                if (nk == 16) return PAMG_OK;  // does not fit: plain values for this set
-                key[nk++] = b;
-                tab[t * 16 + j] = val[k];
+    std::atomic<bool> over{false};
+    par_for(nt, [&](int64_t a, int64_t b) {
+        for (int64_t t = a; t < b && !over; ++t) {
+            uint64_t key[16];
+            int nk = 0;
+            for (int k = tiles[t].z; k < tiles[t].w; ++k) {
+                uint64_t u;
+                std::memcpy(&u, &val[k], 8);
+                int j = 0;
+                while (j < nk && key[j] != u) ++j;
+                if (j == nk) {
+                    if (nk == 16) {  // does not fit: plain values for this set
+                        over = true;
+                        return;
+                    }
+                    key[nk++] = u;
+                    tab[t * 16 + j] = val[k];
+                }
             }
         }
-    }
-    if (vidx->empty()) vidx->assign(nslots, 0);
-    for (size_t t = 0; t < tiles.size(); ++t) {
-        const double* tt = &tab[t * 16];
-        for (int k = tiles[t].z; k < tiles[t].w; ++k) {
-            int j = 0;
-            while (std::memcmp(&tt[j], &val[k], 8) != 0) ++j;
-            (*vidx)[k >> 1] |= (uint8_t)(j << (4 * (k & 1)));
+    });
+    if (over) return PAMG_OK;
+    std::vector<uint8_t> one(2 * nslots, 0);  // nonzeros outside every tile (long rows) keep 0
+    par_for(nt, [&](int64_t a, int64_t b) {
+        for (int64_t t = a; t < b; ++t) {
+            const double* tt = &tab[t * 16];
+            for (int k = tiles[t].z; k < tiles[t].w; ++k) {
+                int j = 0;
+                while (std::memcmp(&tt[j], &val[k], 8) != 0) ++j;
+                one[k] = (uint8_t)j;
+            }
         }
-    }
+    });
+    if (vidx->empty()) vidx->assign(nslots, 0);
+    par_for((int64_t)nslots, [&](int64_t a, int64_t b) {
+        for (int64_t q = a; q < b; ++q) (*vidx)[q] |= (uint8_t)(one[2 * q] | (one[2 * q + 1] << 4));
+    });
     CHECK(dalloc(&ts->d_vtab, (int64_t)tab.size()));
     HIPC(hipMemcpy(ts->d_vtab, tab.data(), sizeof(double) * tab.size(), hipMemcpyHostToDevice));
     ts->vd = true;
     return PAMG_OK;
+}
+
+// Per own column: the largest gap between consecutive rows that read it (0 if fewer than two
+// do). Row chunks in parallel, each over the column range its rows touch (first / last reader
+// and the largest gap inside the chunk), then merged per column in chunk order: the values of
+// one sequential pass. A matrix whose chunks together span more than ~2x the columns (no band
+// structure) takes the sequential pass.
+std::vector<int> column_reuse_gaps(const std::vector<int64_t>& rp, const std::vector<int>& ci, int64_t nrows,
+                                   int64_t ncols) {
+    std::vector<int> gap(ncols, 0);
+    const int nch = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, nrows / 65536));
+    std::vector<int64_t> r0(nch + 1);
+    for (int t = 0; t <= nch; ++t) r0[t] = nrows * t / nch;
+    // one thread per chunk (par_for would keep a handful of items on one thread)
+    auto each_chunk = [nch](const std::function<void(int)>& f) {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nch; ++t) th.emplace_back([&f, t] { f(t); });
+        for (auto& x : th) x.join();
+    };
+    std::vector<int> lo(nch, INT32_MAX), hi(nch, -1);
+    each_chunk([&](int t) {
+        int a = INT32_MAX, b = -1;
+        for (int64_t k = rp[r0[t]]; k < rp[r0[t + 1]]; ++k)
+            if (ci[k] < ncols) {
+                a = std::min(a, ci[k]);
+                b = std::max(b, ci[k]);
+            }
+        lo[t] = a;
+        hi[t] = b;
+    });
+    int64_t span = 0;
+    for (int t = 0; t < nch; ++t) span += hi[t] >= lo[t] ? (int64_t)hi[t] - lo[t] + 1 : 0;
+    if (nch == 1 || span > 2 * ncols + 65536) {
+        std::vector<int> last(ncols, -1);
+        for (int64_t i = 0; i < nrows; ++i)
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                const int c = ci[k];
+                if (c < ncols) {
+                    if (last[c] >= 0) gap[c] = std::max(gap[c], (int)i - last[c]);
+                    last[c] = (int)i;
+                }
+            }
+        return gap;
+    }
+    // per chunk, over [lo, hi]: first reader, last reader, largest gap inside the chunk
+    std::vector<std::vector<int>> first(nch), last(nch), cgap(nch);
+    each_chunk([&](int t) {
+        if (hi[t] < lo[t]) return;
+        const int64_t w = (int64_t)hi[t] - lo[t] + 1;
+        first[t].assign(w, -1);
+        last[t].assign(w, -1);
+        cgap[t].assign(w, 0);
+        int* f = first[t].data();
+        int* l = last[t].data();
+        int* g = cgap[t].data();
+        for (int64_t i = r0[t]; i < r0[t + 1]; ++i)
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                const int c = ci[k];
+                if (c >= ncols) continue;
+                const int j = c - lo[t];
+                if (l[j] >= 0) g[j] = std::max(g[j], (int)i - l[j]);
+                else f[j] = (int)i;
+                l[j] = (int)i;
+            }
+    });
+    par_for(ncols, [&](int64_t a, int64_t b) {
+        for (int64_t c = a; c < b; ++c) {
+            int g = 0, prev = -1;
+            for (int t = 0; t < nch; ++t) {
+                if (c < lo[t] || c > hi[t]) continue;
+                const int64_t j = c - lo[t];
+                if (first[t][j] < 0) continue;
+                if (prev >= 0) g = std::max(g, first[t][j] - prev);
+                g = std::max(g, cgap[t][j]);
+                prev = last[t][j];
+            }
+            gap[c] = g;
+        }
+    });
+    return gap;
 }
 
 int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows, bool square,
@@ -326,11 +422,11 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows, bo
     ts->vd = false;
     if (opt.value_dict == 1 && ts->c24 && val && tall)
         CHECK(build_value_dict(tiles, val, ts, vidx, (ci.size() + 1) / 2 + 8));
-    ts->rl8 = opt.row_len8 && ts->c24 && !ts->vd && ts->max_short_len <= 255 && ts->n_short > 0 &&
+    ts->rl8 = opt.row_len8 && ts->c24 && ts->max_short_len <= 255 && ts->n_short > 0 &&
               ts->nnz_short <= 16 * ts->rows_short;
     // ^ short rows only: the 3 B/row saved are 3-8 % of a 4-7-nonzero row (A0 SpMV -2 %, P0
     //   -5..-8 %) but ~1 % of a 30-nonzero row, where the scan's latency costs more (R0, A1
-    //   +2..3 %; profiles/r01_kbench_512_rl8.jsonl)
+    //   +2..3 %; profiles/r01_kbench_512_rl8.jsonl); with the value dictionaries too (P0)
     if (ts->n_short)
         HIPC(hipMemcpy(ts->d_short, tiles.data(), sizeof(int4) * tiles.size(), hipMemcpyHostToDevice));
     if (ts->n_long)
@@ -1835,16 +1931,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     // columns. (Sequential: the gaps depend on the row order.)
     int64_t band = 0;
     {
-        std::vector<int> last_row(n_own_cols, -1), max_gap(n_own_cols, 0);
-        for (int64_t i = 0; i < nrows; ++i)
-            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-                const int c = ci[k];
-                if (c < n_own_cols) {
-                    if (last_row[c] >= 0) max_gap[c] = std::max(max_gap[c], (int)i - last_row[c]);
-                    last_row[c] = (int)i;
-                }
-            }
-        std::vector<int>().swap(last_row);
+        std::vector<int> max_gap = column_reuse_gaps(rp, ci, nrows, n_own_cols);
         auto end = std::remove(max_gap.begin(), max_gap.end(), 0);
         const size_t m = (size_t)(end - max_gap.begin());
         if (m > 0) {

@@ -997,6 +997,23 @@ def test_tile_major_value_dictionary_bit_exact(ctx, npal, tnnz, lengths):
     assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, xh, bh, 0.61)))
 
 
+@pytest.mark.parametrize("rl8", [0, 1])
+@pytest.mark.parametrize("lengths", [[3, 4, 1, 5, 0, 9, 2], [4], [255, 2, 1]])
+def test_prolongator_value_dictionary_row_lengths_bit_exact(ctx, rl8, lengths):
+    """Tall operators (the prolongators' shape) take 4-bit per-tile value dictionaries in the
+    descriptor kernel, with 8-bit row lengths where the rows are short (row_len8) or row
+    pointers: SpMV, residual and prolongate-add bit-exact with the oracle, ragged and empty
+    rows and a 255-nonzero row included."""
+    from parallel_amg_amd._lib import layout_of
+    rng = np.random.default_rng(len(lengths) + 10 * rl8)
+    M = random_csr(rng, (lengths * 6000)[:6000], 900, palette=PALETTES["few"])
+    with _with_option("row_len8", rl8), _with_option("value_dict", 1), _with_option("col24", 1):
+        A = _layout_ops_match_oracle(ctx, M, rng)
+    lay = layout_of(A)
+    short = M.rowptr[-1] <= 16 * M.nrows
+    assert lay["vd"] and lay["c24"] and lay["rl8"] == bool(rl8 and short), lay
+
+
 @pytest.mark.parametrize("kind,shape", [("poisson3d", (128, 128, 128)), ("aniso3d", (128, 128, 128)),
                                         ("poisson3d", (256, 256, 256)), ("poisson3d", (64, 32, 40)),
                                         ("aniso3d", (192, 48, 7))])
