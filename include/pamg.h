@@ -237,8 +237,8 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
  * layout features; "sym_dia": symmetric diagonal-class layout of a square operator's interior
  * rows where they qualify; "sym_rows" 1 | 2: rows per lane of its kernel; "jr_fuse": the
  * temporally blocked level-0 passes of the V-cycle and the cross-cycle pipeline, read at graph
- * capture), "long_tiles_min" (1..255 nonzeros per row from which sets of >= 64 M
- * nonzeros take long tiles), "band_pct" / "band_pct_restrict" (percent scale of the banded
+ * capture), "long_tiles_min" (1..255 nonzeros per row from which sets of >= 32 x 4096
+ * nonzeros per CU take 2048-nonzero tiles), "band_pct" / "band_pct_restrict" (percent scale of the banded
  * order's band; the second for operators with fewer rows than columns), "tile_major" (0 | 1 where measured faster | 2 every eligible set). Applied at
  * every exchange:
  * "poison_ghosts" (0 | 1, debug: NaN-fill the ghost slots before each exchange). */

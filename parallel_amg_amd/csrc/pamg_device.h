@@ -105,7 +105,7 @@ struct Options {
     int tile_order = 1;        // 1: banded XCD-blocked tile order (see build_tiles)
     int col24 = 1;             // 1: 3-byte column stream where every tile's span fits 2^24
     int long_tiles = 1;        // 1: 4096-nonzero tiles for square operators with long rows (build_tiles)
-    int long_tiles_min = 24;   // nonzeros per row from which long_tiles applies to sets of >= 64 M nonzeros
+    int long_tiles_min = 24;   // nonzeros per row from which sets of >= 32 x 4096 nonzeros per CU take 2048-nonzero tiles
     int row_len8 = 1;          // 1: 8-bit row lengths instead of 32-bit row pointers where they fit
     int value_dict = 1;        // 1: per-tile value dictionaries (4-bit for rectangular operators where a tile has
                                //    <= 16 distinct values, 8-bit in tile-major slots); 2: 8-bit ones only

@@ -336,9 +336,14 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows, bo
         // the 6 M-nonzero A1 of 128^3, 6 per CU, is 9 % slower with them,
         // profiles/r02_exp/bench_long_tiles_min_ab/). Keyed on the CU count, not on a fixed
         // nonzero count, so a part of an 8-GPU run takes the layout one GPU takes.
+        // Round 3 (8-bit per-tile value dictionaries): the set under the second rule (512^3 A1)
+        // takes 2048-nonzero tiles — residual + Jacobi 1.85 -> 1.80 ms on one box; 3072 1.83
+        // (profiles/r03_jdiag/kb.jsonl) — A2 (>= 48 per row) stays at 4096 (2048: Jacobi +5 %).
         const int64_t nr = (int64_t)rows.size();
-        if (nz >= 48 * nr || (nz >= (int64_t)opt.long_tiles_min * nr && nz >= int64_t(32) * 4096 * device_cus()))
+        if (nz >= 48 * nr)
             tnnz = 4096;
+        else if (nz >= (int64_t)opt.long_tiles_min * nr && nz >= int64_t(32) * 4096 * device_cus())
+            tnnz = 2048;
     }
     ts->tile_nnz = tnnz;
     std::vector<int4> tiles;
