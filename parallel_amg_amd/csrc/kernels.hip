@@ -399,12 +399,16 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     __shared__ int lwt[BS / 64];
     // XS keeps only the table's LDS positions (kXsIoff + index): 16 / 128 entries, so the
     // staged runs fit beside Jacobi's arrays at 8 blocks per CU
-    constexpr int NTAB = CD == 0 ? 1 : !XS ? BS : CD == 4 ? 16 : kXsIoff;
+    // 2048-nonzero tiles keep per-tile tables of <= kTmSmallTab entries (checked at upload,
+    // build_tile_major), so one more block fits per CU (512^3 A1: residual 7 -> 8, Jacobi 6 -> 7
+    // waves per SIMD; -2.4 % / -4.6 %, profiles/r03_lds/)
+    constexpr int NTAB = CD == 0 ? 1 : XS ? (CD == 4 ? 16 : kXsIoff) : PT && TNNZ == 2048 ? kTmSmallTab : BS;
+    constexpr int NVT = TNNZ == 2048 ? kTmSmallTab : BS;
     __shared__ int ltab[NTAB];
     __shared__ __attribute__((aligned(4))) uint8_t lrow[TNNZ + 8];
     __shared__ int lanc[ANC ? BS : 1];
     __shared__ double lxs[XS ? kXsCap + 1 : 1];  // + 1: the dump slot of lanes past a run
-    __shared__ double lvt[VD8 ? kBlock : 1];     // the tile's value table (vt <= 256 entries)
+    __shared__ double lvt[VD8 ? NVT : 1];        // the tile's value table (vt <= NVT entries)
 
     const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int4 d = tiles[t];
@@ -477,11 +481,11 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
         }
     }
     int rl_len = tid < rs ? rlv : 0;
-    if constexpr (VD8) lvt[tid] = vtv;  // every lane (lanes past vt repeat the last entry)
+    if constexpr (VD8) lvt[tid < NVT ? tid : NVT - 1] = vtv;  // every lane (lanes past vt repeat the last entry)
     // every lane stores its entry (unconditionally: a conditional store lets the compiler sink
     // the table load into the branch, behind the value stream)
     if constexpr (XS) ltab[tid < NTAB ? tid : NTAB - 1] = tabv;  // lanes past NTAB rewrite the last entry's value
-    else if constexpr (CD != 0) ltab[tid] = tabv;
+    else if constexpr (CD != 0) ltab[tid < NTAB ? tid : NTAB - 1] = tabv;  // (lanes past ctab_n: the last entry)
     if constexpr (ANC) lanc[tid] = tid < rs ? ancv : 0;
     if constexpr (XS) {
 #pragma unroll

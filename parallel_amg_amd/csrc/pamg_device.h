@@ -25,6 +25,8 @@ constexpr int kTileRows = 256;
 // gathers. The dictionary table holds, at kXsIoff + index, each offset's LDS position
 // c * stride + offset - omin_c.
 constexpr int kXsMaxClusters = 12;
+// tile-major sets of 2048-nonzero tiles: per-tile column / value tables of <= this many entries
+constexpr int kTmSmallTab = 128;
 constexpr int kXsCap = 1088;   // LDS doubles (8.5 KiB; 512^3 7-point: 5 runs x 210)
 constexpr int kXsIoff = 128;   // table entries [128, 256): the LDS positions of offsets [0, 128)
 constexpr int kXsGap = 48;

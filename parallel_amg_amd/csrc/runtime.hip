@@ -783,6 +783,9 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
         }
         const std::vector<int4>& tiles = *tl[q];
         const int64_t nt = (int64_t)tiles.size(), tn = ts->tile_nnz;
+        // k_rows_tm keeps per-tile tables of <= kTmSmallTab entries in LDS for 2048-nonzero tiles:
+        // a set with longer per-tile column tables stays in the descriptor kernel
+        if (ts->pt && tn == 2048 && ts->ctab_n > pamg::kTmSmallTab) continue;
         int rs = 0;
         for (const int4& t : tiles) rs = std::max(rs, t.y - t.x);
         rs = (rs + 3) & ~3;
@@ -809,6 +812,7 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
                 }
             });
             if (!over) vt = std::max(4, (vmax.load() + 3) & ~3);
+            if (tn == 2048 && vt > pamg::kTmSmallTab) vt = 0;  // (the kernel's LDS table, see above)
         }
         std::unique_ptr<double[]> tv(vt ? nullptr : new double[nt * tn + kVecPad]);
         std::unique_ptr<uint8_t[]> tvi(vt ? new uint8_t[nt * tn + kVecPad] : nullptr);

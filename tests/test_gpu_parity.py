@@ -971,12 +971,12 @@ def test_sym_dia_vcycle_same_bits_either_layout(ctx):
 
 
 @pytest.mark.parametrize("npal,tnnz,lengths", [(40, 1024, [7, 31, 2]), (60, 4096, [31]), (17, 2048, [9]),
-                                               (1000, 1024, [31, 7])])
+                                               (60, 2048, [31]), (150, 2048, [31]), (1000, 1024, [31, 7])])
 def test_tile_major_value_dictionary_bit_exact(ctx, npal, tnnz, lengths):
     """8-bit per-tile value dictionaries in tile-major slots (value_dict, where the 4-bit ones do
     not fit and every tile has <= 256 distinct values — the 512^3 level-1 operator's case): SpMV,
     residual, Jacobi and prolongate-add bit-exact with the oracle; a palette too large for a
-    tile keeps plain values."""
+    tile keeps plain values (2048-nonzero tiles: > 128 values per tile, the kernel's LDS table)."""
     from parallel_amg_amd._lib import layout_of
     rng = np.random.default_rng(npal + tnnz)
     pal = rng.standard_normal(npal)
@@ -984,7 +984,7 @@ def test_tile_major_value_dictionary_bit_exact(ctx, npal, tnnz, lengths):
     with _with_option("tile_nnz", tnnz), _with_option("tile_major", 2):
         A, _h = upload(ctx, M)
     lay = layout_of(A)
-    assert lay["tm"] and lay["tm_vd"] == (npal <= 256 and npal > 16), lay
+    assert lay["tm"] and lay["tm_vd"] == (npal <= (128 if tnnz == 2048 else 256) and npal > 16), lay
     xh, bh, yh = (rng.standard_normal(M.nrows) for _ in range(3))
     x, b = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh)
     y = PVector(ctx, M.nrows)
