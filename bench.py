@@ -78,6 +78,11 @@ def main():
     ap.add_argument("--reorder", choices=["auto", "off", "on"], default="auto",
                     help="locality permutation of the level operators inside the device layout "
                          "(AMGSolver reorder; one part; bits unchanged)")
+    ap.add_argument("--pmc", choices=["auto", "committed", "off"], default="auto",
+                    help="HBM traffic of the dominant kernel and the fine SpMV: auto = two rocprofv3 --pmc "
+                         "passes (FETCH_SIZE, WRITE_SIZE) over tools/kbench.py's launches of the same "
+                         "kernels on the same operator, run as child processes before this process touches "
+                         "the GPU (N = 1, generated problems); committed = the records in profiles/pmc/ only")
     ap.add_argument("--pcg-rtol", type=float, default=1e-8,
                     help="time-to-solution leg: PCG with the V-cycle preconditioner to this "
                          "relative residual from x = 0 (0: skip)")
@@ -88,6 +93,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # counters first: the profiled child runs start before this process makes any HIP call
+    live_pmc = None
+    if args.pmc == "auto" and world == 1 and not args.matrix and args.permute is None and not args.rcm:
+        live_pmc = pmc_live(args)
 
     # libpamg first: it then binds to /opt/rocm's HIP 7.2 / RCCL 2.27.7 rather than the copies
     # the torch wheel bundles (HIP 7.0 / RCCL 2.26.6, same sonames; _lib.runtime_providers).
@@ -154,7 +163,7 @@ def main():
             f"{[S.span[l] for l in S.reordered]})")
     nu1, nu2 = (int(v) for v in args.sweeps.split(","))
     S.set_sweeps(nu1, nu2)
-    A0 = S.A[0]
+    A0 = S.A_dev[0]  # the hierarchy's own level-0 operator (device numbering where permuted)
     Af = S.fine_operator()  # the caller's numbering (b = A x* as the caller forms it)
     xst = PVector(ctx, Af.n_own_cols, Af.n_ghost, xs[rank])
     b = PVector(ctx, Af.nrows)
@@ -298,12 +307,17 @@ def main():
                  f"0, false, false>")
     workload_key = f"{args.matrix or args.kind}:{args.grid}:p{world}:perm{args.permute}" + (":rcm" if args.rcm else "")
     src = kernel_source_sha()
-    # (k_sym_tb's grid is its tile count, not the layout's: matched on name, workload and source)
-    traffic = pmc_lookup("traffic_chain.json" if pipelined else "traffic_jacobi.json", kname,
-                         None if pipelined else lay["tiles"], workload_key, src)
     spmv_kname = (f"k_rows_sym{'2' if lay['sym_rows'] == 2 else ''}<0, {lay['cd_offsets']}>" if pipelined
                   else kname.replace("<2,", "<0,", 1))
-    spmv_traffic = pmc_lookup("traffic_spmv.json", spmv_kname, lay["tiles"], workload_key, src)
+    traffic = spmv_traffic = None
+    if live_pmc and pipelined:  # this run's own counters (the child ran op 5 = k_sym_tb<3>, op 0 = SpMV)
+        traffic = live_pmc.get(kname)
+        spmv_traffic = live_pmc.get(spmv_kname)
+    if args.pmc != "off":
+        # (k_sym_tb's grid is its tile count, not the layout's: matched on name, workload and source)
+        traffic = traffic or pmc_lookup("traffic_chain.json" if pipelined else "traffic_jacobi.json", kname,
+                                        None if pipelined else lay["tiles"], workload_key, src)
+        spmv_traffic = spmv_traffic or pmc_lookup("traffic_spmv.json", spmv_kname, lay["tiles"], workload_key, src)
     spmv_traffic_gbps = (round(spmv_traffic["traffic_bytes"] / (spmv_ms * 1e-3) / 1e9, 1)
                          if spmv_traffic else None)
 
@@ -343,10 +357,17 @@ def main():
             },
             # level-0 fused passes (Options::jr_fuse) beside the separate sweeps they replace
             "fused_level0": fused,
-            "fine_spmv_GBps": round(spmv_gbps, 1),
-            "fine_spmv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
-            # HBM bytes actually moved (PMC record of this kernel/layout/source) per second
+            # fine SpMV (k_rows_sym2<0, 3>, one launch = y = A0 x): HBM bytes it moved (rocprofv3
+            # counters: (2 FETCH_SIZE + WRITE_SIZE) per launch) / its launch time, and that over the
+            # 8 TB/s peak — the metric's "fine-SpMV HBM GB/s"
             "fine_spmv_traffic_GBps": spmv_traffic_gbps,
+            "fine_spmv_hbm_frac": round(spmv_traffic_gbps / HBM_PEAK_GBPS, 4) if spmv_traffic_gbps else None,
+            "fine_spmv_traffic_source": spmv_traffic["source"] if spmv_traffic else None,
+            "fine_spmv_ms": round(spmv_ms, 4),
+            # NOT HBM bytes: SURVEY 8(d)'s plain-CSR bytes (12 B/nnz) over the same time. The symmetric
+            # layout streams about half of that, so this "CSR-equivalent" rate may exceed the peak
+            "fine_spmv_csr_equiv_GBps": round(spmv_gbps, 1),
+            "fine_spmv_csr_equiv_frac": round(spmv_gbps / HBM_PEAK_GBPS, 4),
             "samples_ms_per_step": [round(t / args.steps * 1e3, 4) for t in times],
             "roofline": {
                 "kernel": kname + (" (level-0 chain of the pipelined cycles, one launch per cycle: post-smoothing "
@@ -403,7 +424,7 @@ def exchange_times(ctx, S, be, nu1, nu2, reps=20) -> dict:
     out, total = [], 0.0
     for l in range(S.L):
         rec = {}
-        mats = [("A", S.A[l])] + ([("R", S.R[l]), ("P", S.P[l])] if l < S.L - 1 else [])
+        mats = [("A", S.A_dev[l])] + ([("R", S.R[l]), ("P", S.P[l])] if l < S.L - 1 else [])
         for name, M in mats:
             if M.plan is None:
                 continue
@@ -483,6 +504,72 @@ def option(name, value):
     return cm()
 
 
+def pmc_live(args):
+    """HBM bytes per launch of the pipelined cycles' chain kernel (k_sym_tb<3>) and the fine SpMV
+    on this run's operator, from two rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE: one
+    counter per run, MI355X_MICROARCH.md §HBM) over tools/kbench.py, which uploads the same
+    level-0 operator with the same options and launches exactly those kernels (ops 5 and 0).
+    Called before this process makes any HIP call: the children are separate programs started
+    from a process that has not initialised the GPU. Returns {kernel: {"traffic_bytes", ...}}
+    (bytes = (2 FETCH_SIZE + WRITE_SIZE) KiB x 1024, the gfx950 correction for 16-B/lane
+    streams), or None if a pass fails (the committed records are used then)."""
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        log("pmc: rocprofv3 not found")
+        return None
+    tmp = tempfile.mkdtemp(prefix="pamg_pmc_")
+    kb = [sys.executable, "-u", os.path.join(ROOT, "tools", "kbench.py"), "--n", str(args.grid), "--kind", args.kind,
+          "--levels", "1", "--ops", "0,5", "--reps", "3", "--configs", f"1024:1:1:{int(args.value_dict)}",
+          ]
+    for kv in args.set:
+        kb += ["--set", kv]
+    agg = {}
+    t0 = time.time()
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = ["timeout", "-s", "KILL", "240", prof, "--pmc", counter, "-d", d, "-o", "p",
+                   "--output-format", "csv", "--"] + kb
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+            if r.returncode != 0:
+                log(f"pmc: {counter} pass failed (rc {r.returncode}): {r.stderr[-400:]}")
+                return None
+            for (name, _blocks), vals in pmc_csv(d, counter).items():
+                agg.setdefault(name, {})[counter] = sum(vals) / len(vals)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    out = {}
+    for name, c in agg.items():
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            out[name] = {"traffic_bytes": (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0,
+                         "fetch_kib": c["FETCH_SIZE"], "write_kib": c["WRITE_SIZE"],
+                         "source": "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/kbench.py "
+                                   "(bench.py child runs), (2 FETCH + WRITE) x 1 KiB per launch"}
+    log(f"pmc: live passes in {time.time() - t0:.0f}s: "
+        + ", ".join(f"{k} {v['traffic_bytes'] / 1e9:.2f} GB" for k, v in out.items()))
+    return out
+
+
+def pmc_csv(path, counter):
+    """{(kernel name, blocks): [values]} of one counter from a rocprofv3 -d directory's csv."""
+    import collections
+    import csv
+    import glob
+    import re
+    agg = collections.defaultdict(list)
+    for f in sorted(glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"].replace("pamg::(anonymous namespace)::", "").replace("void ", "")
+            name = re.sub(r"\(.*", "", name)
+            agg[(name, int(r["Grid_Size"]) // max(1, int(r["Workgroup_Size"])))].append(float(r["Counter_Value"]))
+    return agg
+
+
 def pmc_lookup(fname, kname, tiles, workload_key, src):
     """The committed PMC traffic record (profiles/pmc/<fname>, tools/pmc_traffic.py) of this
     kernel instance on this workload, tile count and kernels.hip source; None otherwise."""
@@ -530,7 +617,8 @@ def host_cpu_info() -> dict:
 def cpu_baseline(H, xstar, ncycles, log, sweeps=(1, 1)):
     """Time the CPU oracle's V-cycle (oracle/pamg_oracle.c, OpenMP) on the same hierarchy, on
     every core of this process's affinity set (all host cores), plus the CPU
-    fine-level SpMV rate on the same algorithmic bytes as the GPU's fine_spmv_GBps."""
+    fine-level SpMV rate on the same algorithmic bytes as the GPU's fine_spmv_csr_equiv_GBps
+    (plain CSR, 12 B/nnz; the oracle's int64 columns stream more than that)."""
     from oracle import oracle as O
     info = host_cpu_info()
     # every core this process may use: the affinity set, capped by the cgroup CPU quota (a
@@ -564,7 +652,7 @@ def cpu_baseline(H, xstar, ncycles, log, sweeps=(1, 1)):
     log(f"cpu baseline: {ncycles} V-cycle(s) in {dt:.2f}s, fine SpMV {ts * 1e3:.1f} ms on {threads} threads "
         f"(affinity {cores}, nproc {info['nproc']}, quota {info['cgroup_quota_cores']}; {info['cpu_model']})")
     return {"value": round(ncycles / dt, 5), "unit": "V-cycles/s", "cores": threads, "kind": "port",
-            "fine_spmv_GBps": round(spmv_bytes / ts / 1e9, 2), "fine_spmv_ms": round(ts * 1e3, 2),
+            "fine_spmv_csr_GBps": round(spmv_bytes / ts / 1e9, 2), "fine_spmv_ms": round(ts * 1e3, 2),
             "affinity_cores": cores, "nproc": info["nproc"], "omp_num_threads_env": info["omp_num_threads"],
             "cgroup_quota_cores": info["cgroup_quota_cores"], "cpu_model": info["cpu_model"],
             "sample": f"{ncycles} full V-cycle(s) of the same {A0.nrows}-row hierarchy by the C "

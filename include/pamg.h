@@ -196,8 +196,10 @@ int pamg_hier_set_sweeps(pamg_hier* H, int nu1, int nu2);
 /* Level-0 numbering of a hierarchy whose operators were uploaded with pamg_mat_upload_perm
  * (one part only): device row i of level 0 is caller row perm[i]. pamg_vcycle(_async) and
  * pamg_pcg then take x and b in the caller's numbering — gathered into the device numbering at
- * entry, x scattered back at exit — and return the bits of the unpermuted hierarchy's cycle.
- * perm = NULL (or n = 0) removes it. */
+ * entry, x scattered back at exit. x after stationary V-cycles has the bits of the unpermuted
+ * hierarchy's cycles (every row sum keeps its storage order). Reductions run in the device
+ * order: pamg_vcycle's res_hist norms and pamg_pcg's dot products — hence its iterates — match
+ * the unpermuted run to rounding only, not bit for bit. perm = NULL (or n = 0) removes it. */
 int pamg_hier_set_perm(pamg_hier* H, int64_t n, const int64_t* perm);
 /* enabled: graph replay currently on; captured: a graph exists; failed: a capture failed. */
 int pamg_hier_graph_state(const pamg_hier* H, int* enabled, int* captured, int* failed);

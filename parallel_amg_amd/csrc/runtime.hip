@@ -785,7 +785,13 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
         const int64_t nt = (int64_t)tiles.size(), tn = ts->tile_nnz;
         // k_rows_tm keeps per-tile tables of <= kTmSmallTab entries in LDS for 2048-nonzero tiles:
         // a set with longer per-tile column tables stays in the descriptor kernel
-        if (ts->pt && tn == 2048 && ts->ctab_n > pamg::kTmSmallTab) continue;
+        if (ts->pt && tn == 2048 && ts->ctab_n > pamg::kTmSmallTab) {
+            if (UploadTrace{}.on)
+                std::fprintf(stderr, "[pamg upload nnz=%lld] set %d: per-tile column tables of %d > %d entries on "
+                             "2048-nonzero tiles: descriptor kernel instead of tile-major slots\n",
+                             (long long)A->nnz, q, ts->ctab_n, pamg::kTmSmallTab);
+            continue;
+        }
         int rs = 0;
         for (const int4& t : tiles) rs = std::max(rs, t.y - t.x);
         rs = (rs + 3) & ~3;
@@ -812,7 +818,16 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
                 }
             });
             if (!over) vt = std::max(4, (vmax.load() + 3) & ~3);
-            if (tn == 2048 && vt > pamg::kTmSmallTab) vt = 0;  // (the kernel's LDS table, see above)
+            if (tn == 2048 && vt > pamg::kTmSmallTab) {  // (the kernel's LDS table, see above)
+                if (UploadTrace{}.on)
+                    std::fprintf(stderr, "[pamg upload nnz=%lld] set %d: a 2048-nonzero tile has %d > %d distinct "
+                                 "values: 8-B values instead of the 8-bit value dictionary\n",
+                                 (long long)A->nnz, q, vmax.load(), pamg::kTmSmallTab);
+                vt = 0;
+            }
+            if (over && UploadTrace{}.on)
+                std::fprintf(stderr, "[pamg upload nnz=%lld] set %d: a tile has > 256 distinct values: 8-B values\n",
+                             (long long)A->nnz, q);
         }
         std::unique_ptr<double[]> tv(vt ? nullptr : new double[nt * tn + kVecPad]);
         std::unique_ptr<uint8_t[]> tvi(vt ? new uint8_t[nt * tn + kVecPad] : nullptr);

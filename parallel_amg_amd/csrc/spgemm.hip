@@ -471,11 +471,17 @@ int dev_spgemm(pamg_ctx* ctx, const pamg_hcsr* X, int64_t y0, const pamg_hcsr* Y
     HIPC(hipMemcpyAsync(&novf, d_novf, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     std::vector<int32_t> hovf(novf);
+    // The global tables' offsets go to the device by an asynchronous copy that k_sg_glob reads on
+    // the stream, so their host copy must outlive the copy: it lives until the final stream
+    // synchronisation below. (It was a local of this if-block once: freed while the copy from
+    // pageable memory could still be pending, which under contention — 8 ranks sharing one GPU —
+    // gave k_sg_glob garbage table bounds and a tail level without its diagonal; DESIGN.md.)
+    std::vector<int64_t> wo;
     if (novf > 0) {
         HIPC(hipMemcpy(hovf.data(), ovf.p, 4 * (size_t)novf, hipMemcpyDeviceToHost));
         std::vector<int64_t> hm(n);
         HIPC(hipMemcpy(hm.data(), m.p, 8 * (size_t)n, hipMemcpyDeviceToHost));
-        std::vector<int64_t> wo(novf + 1, 0);
+        wo.assign(novf + 1, 0);
         for (int r = 0; r < novf; ++r)
             wo[r + 1] = wo[r] + (int64_t)next_pow2(2 * (uint64_t)std::min(hm[hovf[r]], nc));
         CHECK(h2d(woff, wo.data(), novf + 1, s));

@@ -396,13 +396,14 @@ def _replicated_tail(backend, A: dict, offs, levels: list, params: SAParams, log
     from .backend import SequentialBackend
     n = int(offs[-1])
     full = _gather_full(backend, A, offs)
-    # the tail (<= agglomerate rows) is set up on the host: its products are small, and the one
-    # failure seen of a device product (23 rows of one rank's tail level without a diagonal,
-    # 8 ranks sharing one GPU in the full GPU suite; not reproduced alone) was in these
-    # wide-row products (Correctness tooling)
+    # the tail's products run where the rest of the setup's do (device or host: the same bits).
+    # Round 3 kept them on the host after a tail level came out without its diagonal (8 ranks
+    # sharing one GPU); the cause was spgemm.hip's overflow-row path, whose table offsets were
+    # copied asynchronously from a host vector freed before the copy had run (fixed; DESIGN.md,
+    # Correctness tooling) — these wide rows are the ones that overflow the LDS tables
     sub = build_hierarchy(SequentialBackend(1), {0: full}, np.array([0, n], np.int64),
                           replace(params, agglomerate=0, max_levels=params.max_levels - len(levels)),
-                          (lambda m: log(m + " (whole on every part)")) if log else None, None,
+                          (lambda m: log(m + " (whole on every part)")) if log else None, device,
                           _level0=len(levels))
     for p in backend.parts:  # the prolongation into the tail reads the whole vector
         levels[-1][p].planP = None

@@ -31,7 +31,10 @@ class AMGSolver:
         in its storage order, and the V-cycle gathers / scatters the caller's level-0 vectors
         (pamg_hier_set_perm), so every result keeps the unpermuted hierarchy's bits."""
         self.ctx, self.part, self.L = ctx, part, H.nlevels
-        self.A, self.P, self.R, self.omega = [], [], [], []
+        # the level operators as the hierarchy holds them (device numbering where permuted);
+        # ``A`` (below) gives level 0 in the caller's numbering
+        self.A_dev, self.P, self.R, self.omega = [], [], [], []
+        self._A0_caller = None
         self._H = H
         # levels >= rep are whole on every part (agglomerated tail / coarsest level): the
         # prolongation into rep - 1 reads that whole vector, so its columns stay global
@@ -54,7 +57,7 @@ class AMGSolver:
             lp = H.levels[l][part]
             pl = self.perm[l]
             pn = self.perm[l + 1] if l + 1 < H.nlevels else None
-            self.A.append(PSparseMatrix(ctx, lp.A, lp.planA, row_perm=pl, col_perm=pl))
+            self.A_dev.append(PSparseMatrix(ctx, lp.A, lp.planA, row_perm=pl, col_perm=pl))
             self.omega.append(lp.omega)
             if l < H.nlevels - 1:
                 self.P.append(PSparseMatrix(ctx, lp.P, None if l + 1 >= rep else lp.planP,
@@ -63,7 +66,7 @@ class AMGSolver:
         self.level_rows = [int(H.levels[l][part].A.nrows) for l in range(H.nlevels)]
         self.n_coarse = H.n_coarse
         L = self.L
-        arrA = (C.c_void_p * L)(*[a.handle for a in self.A])
+        arrA = (C.c_void_p * L)(*[a.handle for a in self.A_dev])
         arrP = (C.c_void_p * L)(*([p.handle for p in self.P] + [None]))
         arrR = (C.c_void_p * L)(*([r.handle for r in self.R] + [None]))
         om = np.asarray(self.omega, np.float64)
@@ -81,18 +84,28 @@ class AMGSolver:
             self.set_graph(graph)
 
     @property
+    def A(self) -> list:
+        """The level operators, level 0 in the CALLER's numbering (b = A[0] x, residuals of the
+        caller's vectors): the hierarchy's own A_0 when level 0 is not permuted, else an
+        unpermuted upload made on first use (``fine_operator``). Levels >= 1 are internal to the
+        cycle and listed as the hierarchy holds them (``A_dev``)."""
+        return [self.fine_operator()] + self.A_dev[1:]
+
+    @property
     def reordered(self) -> list:
         """Levels whose device layout carries a locality permutation."""
         return [l for l, p in enumerate(self.perm) if p is not None]
 
     def fine_operator(self) -> PSparseMatrix:
         """The level-0 operator in the caller's numbering (for b = A x and residuals of the
-        caller's vectors): the hierarchy's own A_0 when level 0 is not permuted, else a fresh
-        unpermuted upload."""
+        caller's vectors): the hierarchy's own A_0 when level 0 is not permuted, else an
+        unpermuted upload (made once, kept)."""
         if self.perm[0] is None:
-            return self.A[0]
-        lp = self._H.levels[0][self.part]
-        return PSparseMatrix(self.ctx, lp.A, lp.planA)
+            return self.A_dev[0]
+        if self._A0_caller is None:
+            lp = self._H.levels[0][self.part]
+            self._A0_caller = PSparseMatrix(self.ctx, lp.A, lp.planA)
+        return self._A0_caller
 
     @property
     def handle(self):
@@ -112,7 +125,7 @@ class AMGSolver:
 
     def new_vector(self) -> PVector:
         """A level-0 vector with room for the fine-level ghosts."""
-        return self.A[0].new_input_vector()
+        return self.A_dev[0].new_input_vector()
 
     def vcycle(self, x: PVector, b: PVector, ncycles: int = 1, res_hist: bool = False):
         if res_hist:
@@ -186,7 +199,7 @@ class AMGSolver:
                 nc = self.n_coarse
                 out[l, 5] = 8 * nc * n + 8 * nc + 8 * n
                 continue
-            A, P, R = self.A[l], self.P[l], self.R[l]
+            A, P, R = self.A_dev[l], self.P[l], self.R[l]
             # jacobi: x (read once), b, x' ; zero-guess form on l >= 1 reads b, diag, writes x'
             out[l, 0] = rb(A, 1) if l == 0 else 24 * n
             out[l, 1] = rb(A, 1)

@@ -166,10 +166,12 @@ def test_jacobi_bit_exact(ctx, case, palette, tile_cfg):
     assert np.array_equal(bits(x.own_values()), bits(ref))
 
 
-def offset_csr(rng, n, offsets, lengths, palette=None):
+def offset_csr(rng, n, offsets, lengths, palette=None, diag_from_palette=False):
     """Square matrix whose row i holds the diagonal plus columns i + o for o drawn from
     `offsets` (those inside [0, n)): at most len(offsets) + 1 distinct row-relative offsets,
-    the layout the column dictionaries (col_dict) compress."""
+    the layout the column dictionaries (col_dict) compress. The diagonal is 4 + row length +
+    |value| (dominant), or with diag_from_palette a palette value too, so that every value of
+    the matrix is one of the palette's."""
     offsets = np.asarray(offsets, np.int64)
     rows, cols, vals = [0], [], []
     for i in range(n):
@@ -178,7 +180,8 @@ def offset_csr(rng, n, offsets, lengths, palette=None):
         cand = cand[(cand >= 0) & (cand < n) & (cand != i)]
         c = np.sort(np.concatenate([[i], rng.choice(cand, size=min(max(m - 1, 0), len(cand)), replace=False)]))
         v = rng.standard_normal(len(c)) if palette is None else rng.choice(palette, len(c))
-        v[c == i] = 4.0 + len(c) + abs(v[c == i])
+        if not diag_from_palette:
+            v[c == i] = 4.0 + len(c) + abs(v[c == i])
         cols.append(c)
         vals.append(v)
         rows.append(rows[-1] + len(c))
@@ -766,6 +769,31 @@ def test_vcycle_permuted_bit_exact(ctx, kind, n, seed):
     np.testing.assert_allclose(hist, ho, rtol=1e-12)
 
 
+def test_default_solver_fine_operator_is_caller_numbered(ctx):
+    """with the default reorder="auto", a scattered problem of >= 4096 rows gets a
+    locality-permuted level 0 inside the hierarchy, yet S.A[0] stays the caller's operator:
+    b = S.A[0] x* through the default constructor equals the oracle's A x* on the caller's
+    numbering, and the V-cycle from that b keeps the oracle's bits."""
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 20)
+    A, xs = pa.permute_problem(A, xs, 5)
+    M = A[0]
+    assert M.nrows >= 4096
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=100), device=ctx)
+    S = AMGSolver(ctx, H)                      # default constructor (reorder="auto")
+    assert 0 in S.reordered
+    b = PVector(ctx, M.nrows)
+    mul(b, S.A[0], PVector(ctx, M.nrows, 0, xs[0]))
+    Ao = O.CSR(M.rowptr.copy(), M.col.astype(np.int64), M.val.copy(), M.ncols)
+    bo = O.spmv(Ao, xs[0])
+    assert np.array_equal(bits(b.own_values()), bits(bo))
+    Ho = O.setup(Ao, max_coarse=100)
+    xo = Ho.solve(bo, 4)
+    x = S.new_vector()
+    S.vcycle(x, b, 4)
+    assert np.array_equal(bits(x.own_values()), bits(xo))
+
+
 # ---------------------------------------------------------------- locality permutation (reorder)
 def test_upload_perm_rows_and_columns_bit_exact(ctx):
     """pamg_mat_upload_perm: device row i = row perm[i], device column k = column perm[k], each
@@ -971,20 +999,28 @@ def test_sym_dia_vcycle_same_bits_either_layout(ctx):
 
 
 @pytest.mark.parametrize("npal,tnnz,lengths", [(40, 1024, [7, 31, 2]), (60, 4096, [31]), (17, 2048, [9]),
-                                               (17, 2048, [31]), (150, 2048, [31]), (1000, 1024, [31, 7])])
+                                               (17, 2048, [31]), (60, 2048, [31]), (128, 2048, [31]),
+                                               (129, 2048, [31]), (150, 2048, [31]), (256, 1024, [31]),
+                                               (1000, 1024, [31, 7])])
 def test_tile_major_value_dictionary_bit_exact(ctx, npal, tnnz, lengths):
     """8-bit per-tile value dictionaries in tile-major slots (value_dict, where the 4-bit ones do
     not fit and every tile has <= 256 distinct values — the 512^3 level-1 operator's case): SpMV,
-    residual, Jacobi and prolongate-add bit-exact with the oracle; a palette too large for a
-    tile keeps plain values (2048-nonzero tiles: > 128 values per tile, the kernel's LDS table)."""
+    residual, Jacobi and prolongate-add bit-exact with the oracle. The rule (runtime.hip
+    build_tile_major): the set takes them when its widest tile has 17..256 distinct values
+    (bit patterns), <= 128 on 2048-nonzero tiles (the kernel's LDS table), rounded up to 4.
+    Every value here (the diagonal too) is a palette value, and each tile draws ~2000 of them,
+    so a tile holds the whole palette: npal is the widest tile's count, and the cases sit on
+    both sides of each limit (128 / 129 on 2048-nonzero tiles, 256 on 1024)."""
     from parallel_amg_amd._lib import layout_of
     rng = np.random.default_rng(npal + tnnz)
     pal = rng.standard_normal(npal)
-    M = offset_csr(rng, 3000, [-57, -9, -3, -1, 1, 2, 3, 9, 11, 57, 130, -130], lengths, palette=pal)
+    M = offset_csr(rng, 3000, [-57, -9, -3, -1, 1, 2, 3, 9, 11, 57, 130, -130], lengths, palette=pal,
+                   diag_from_palette=True)
     with _with_option("tile_nnz", tnnz), _with_option("tile_major", 2):
         A, _h = upload(ctx, M)
     lay = layout_of(A)
-    assert lay["tm"] and lay["tm_vd"] == (npal <= (128 if tnnz == 2048 else 256) and npal > 16), lay
+    limit = 128 if tnnz == 2048 else 256
+    assert lay["tm"] and lay["tm_vd"] == (16 < npal <= limit), lay
     xh, bh, yh = (rng.standard_normal(M.nrows) for _ in range(3))
     x, b = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh)
     y = PVector(ctx, M.nrows)

@@ -1,0 +1,115 @@
+"""The bench's timed path at the bench's size: 3D 7-point Poisson 512^3, one
+part, the library defaults.
+
+bench.py times ``S.vcycle_async(x, b, K)``: with jr_fuse on, stationary runs of K >= 2 cycles
+take the cross-cycle pipeline (``vcycle_pipe``: one ``k_sym_tb<3>`` launch per cycle boundary —
+the level-0 post-smoothing of cycle k, the pre-smoothing and residual of cycle k + 1 — five
+captured graphs, the iterate alternating between ``t[0]`` and ``u0``). At 512^3 that kernel runs
+a geometry no smaller test reaches (8 x 32 xy tiles, one z chunk of all 512 planes per
+workgroup, 256 workgroups), so these tests pin it against separate, unfused cycles at this size:
+
+* K pipelined cycles through graph replay == K separate cycles (jr_fuse off, eager), bit for
+  bit, from x = 0 and continued from a non-zero iterate (the bench's warm-up then timed runs);
+* the temporally blocked pre-smoothing pass ``k_sym_tb<2>`` == Jacobi then residual, bit for bit.
+
+The separate cycles are themselves oracle-bit-exact at 128^3 (test_gpu_parity.py); no oracle
+run is possible at 134M rows in a test's time budget.
+"""
+import contextlib
+import ctypes
+
+import numpy as np
+import pytest
+
+import parallel_amg_amd as pa
+from parallel_amg_amd._lib import call, layout_of
+from parallel_amg_amd.partitioned import PVector, jacobi_residual, mul
+from parallel_amg_amd.solver import AMGSolver
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.asarray(a, np.float64).view(np.int64)
+
+
+@contextlib.contextmanager
+def option(key, value):
+    v = ctypes.c_int64()
+    call("pamg_get_option", key.encode(), ctypes.byref(v))
+    call("pamg_set_option", key.encode(), int(value))
+    try:
+        yield
+    finally:
+        call("pamg_set_option", key.encode(), v.value)
+
+
+@pytest.fixture(scope="module")
+def h512(ctx):
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 512)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=ctx)
+    del A
+    S = AMGSolver(ctx, H)
+    b = PVector(ctx, S.A[0].nrows)
+    mul(b, S.A[0], PVector(ctx, S.A[0].nrows, 0, xs[0]))
+    yield S, b
+    del S, b
+
+
+def test_timed_path_geometry(h512):
+    """The 512^3 level-0 operator takes the symmetric layout with the blocked passes (the
+    layout whose kernels the bench times)."""
+    S, _b = h512
+    lay = layout_of(S.A[0])
+    assert lay["sym"] and lay["jr_fused"] and lay["cd_offsets"] == 3, lay
+    assert S.L == 6
+
+
+def test_pipelined_cycles_512_bit_exact(ctx, h512):
+    S, b = h512
+    n = S.A[0].nrows
+    ref = {}
+    with option("jr_fuse", 0):
+        S.set_graph(False)
+        x = S.new_vector()
+        for k in range(1, 6):
+            S.vcycle(x, b, 1)
+            if k in (3, 5):
+                ref[k] = x.own_values()
+    assert not np.array_equal(bits(ref[3]), bits(ref[5]))
+    with option("jr_fuse", 1):
+        S.set_graph(False)
+        S.set_graph(True)
+        x = S.new_vector()
+        S.vcycle_async(x, b, 3)          # what bench.py times (graph replay, pipelined)
+        ctx.sync()
+        assert S.graph_state()["captured"]
+        got3 = x.own_values()
+        S.vcycle_async(x, b, 2)          # continued from a non-zero iterate
+        ctx.sync()
+        got5 = x.own_values()
+    d3 = np.flatnonzero(bits(got3) != bits(ref[3]))
+    assert d3.size == 0, (d3.size, d3[:8], n)
+    d5 = np.flatnonzero(bits(got5) != bits(ref[5]))
+    assert d5.size == 0, (d5.size, d5[:8], n)
+
+
+def test_blocked_pre_smoothing_512_bit_exact(ctx, h512):
+    """k_sym_tb<2> (Jacobi -> residual in one pass) == the two separate sweeps, random x, b."""
+    S, _b = h512
+    A0 = S.A[0]
+    n = A0.nrows
+    rng = np.random.default_rng(11)
+    x = PVector(ctx, n, 0, rng.standard_normal(n))
+    b = PVector(ctx, n, 0, rng.standard_normal(n))
+    out = []
+    for fuse in (1, 0):
+        t, r = PVector(ctx, n), PVector(ctx, n)
+        with option("jr_fuse", fuse):
+            ran = jacobi_residual(t, r, A0, x, b, S.omega[0])
+        assert ran == bool(fuse)
+        out.append((t.own_values(), r.own_values()))
+        del t, r
+    assert np.array_equal(bits(out[0][0]), bits(out[1][0]))
+    assert np.array_equal(bits(out[0][1]), bits(out[1][1]))

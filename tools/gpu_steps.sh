@@ -1,0 +1,63 @@
+#!/bin/bash
+# GPU-box steps of a round (run through gpurun), one launcher instead of per-experiment scripts:
+#
+#   gpurun -- 'bash tools/gpu_steps.sh TAG step [step ...]'
+#
+# steps (each GPU step under its own time limit; the first failure ends the script):
+#   tests      the whole -m gpu suite (one process)
+#   timed      the 512^3 timed-path tests + the parity file (faster than `tests`)
+#   bench      the default bench line (live PMC passes included) -> TAG/bench.json, bench.log
+#   trace      rocprofv3 --kernel-trace --stats of bench.py (5 steps, no CPU leg, no PMC)
+#   anatomy    counter anatomy of the level-0/1 row operators (A0 chain/SpMV, R0, P0, A1, R1, P1):
+#              three --pmc passes (requests by size; DRAM / L2 hits / writes; SQ wave-cycle split)
+#   kbench     tools/kbench.py --n 512 --levels 2 timings (KB_ARGS overrides)
+# Output: gpurun_out/TAG/.
+set -euo pipefail
+export TMPDIR=/tmp
+TAG=$1
+shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+PYT="python -u -m pytest -x -q --timeout 600 --timeout-method thread"
+KBA=${KB_ARGS:-"--n 512 --levels 2 --mats A0,R0,P0,A1,R1,P1 --ops 0,1,2,3,5 --reps 3 --configs 1024"}
+for step in "$@"; do
+    case $step in
+    tests)
+        timeout -k 10 1000 $PYT tests -m gpu > "$OUT/tests.log" 2>&1
+        ;;
+    timed)
+        timeout -k 10 700 $PYT tests/test_gpu_timed_path.py tests/test_gpu_parity.py -m gpu > "$OUT/timed.log" 2>&1
+        ;;
+    bench)
+        timeout -k 10 700 python3 -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log"
+        ;;
+    trace)
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv \
+            -- python3 -u bench.py --steps 5 --cpu-baseline off --pmc off > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.log"
+        ;;
+    anatomy)
+        timeout -s KILL 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
+            -d "$OUT/an1" -o p --output-format csv -- python3 -u tools/kbench.py $KBA > "$OUT/an1.jsonl" 2> "$OUT/an1.err"
+        echo "anatomy pass 1 done"
+        timeout -s KILL 300 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_WRREQ_sum \
+            -d "$OUT/an2" -o p --output-format csv -- python3 -u tools/kbench.py $KBA > "$OUT/an2.jsonl" 2> "$OUT/an2.err"
+        echo "anatomy pass 2 done"
+        timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+            SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS \
+            -d "$OUT/an3" -o p --output-format csv -- python3 -u tools/kbench.py $KBA > "$OUT/an3.jsonl" 2> "$OUT/an3.err"
+        echo "anatomy pass 3 done"
+        timeout -s KILL 300 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum \
+            -d "$OUT/an4" -o p --output-format csv -- python3 -u tools/kbench.py $KBA > "$OUT/an4.jsonl" 2> "$OUT/an4.err"
+        echo "anatomy pass 4 done"
+        python3 tools/pmc_anatomy.py "$OUT/an1" "$OUT/an2" "$OUT/an3" "$OUT/an4" > "$OUT/anatomy.json"
+        ;;
+    kbench)
+        timeout -k 10 400 python3 -u tools/kbench.py $KBA > "$OUT/kbench.jsonl" 2> "$OUT/kbench.err"
+        ;;
+    *)
+        echo "unknown step $step" >&2
+        exit 2
+        ;;
+    esac
+    echo "$step done"
+done
