@@ -289,13 +289,13 @@ def main():
     # the instance name as rocprofv3 demangles it (every template argument, defaults included)
     tf = lambda v: "true" if v else "false"  # noqa: E731
     if pipelined:
-        kname = "k_sym_tb<3>"
+        kname = "k_sym_tbd<3>" if lay.get("sym_vd") else "k_sym_tb<3>"
         post_ms = float(fused["chain3_ms"])
         post_bytes = float(S.csr_bytes(A0, 3))       # matrix once + in0 + b + 3 outputs
         post_fbytes = float(S.rowsum_bytes(A0, 3))
         achieved = post_bytes / (post_ms * 1e-3) / 1e9
     elif lay.get("sym"):
-        kname = f"k_rows_sym{'2' if lay['sym_rows'] == 2 else ''}<2, {lay['cd_offsets']}>"
+        kname = f"k_rows_sym{'d' if lay.get('sym_vd') else '2' if lay['sym_rows'] == 2 else ''}<2, {lay['cd_offsets']}>"
     elif tm:
         kname = (f"k_rows_tm<2, {tn}, {cd}, {tf(lay['anchored'])}, {tf(lay['x_stage'])}, "
                  f"{tf(lay['per_tile'])}>")
@@ -307,7 +307,8 @@ def main():
                  f"0, false, false>")
     workload_key = f"{args.matrix or args.kind}:{args.grid}:p{world}:perm{args.permute}" + (":rcm" if args.rcm else "")
     src = kernel_source_sha()
-    spmv_kname = (f"k_rows_sym{'2' if lay['sym_rows'] == 2 else ''}<0, {lay['cd_offsets']}>" if pipelined
+    spmv_kname = (f"k_rows_sym{'d' if lay.get('sym_vd') else '2' if lay['sym_rows'] == 2 else ''}<0, {lay['cd_offsets']}>"
+                  if pipelined
                   else kname.replace("<2,", "<0,", 1))
     traffic = spmv_traffic = None
     if live_pmc and pipelined:  # this run's own counters (the child ran op 5 = k_sym_tb<3>, op 0 = SpMV)
@@ -372,7 +373,9 @@ def main():
             "roofline": {
                 "kernel": kname + (" (level-0 chain of the pipelined cycles, one launch per cycle: post-smoothing "
                                    "Jacobi -> next pre-smoothing Jacobi -> residual, temporally blocked over the "
-                                   "symmetric diagonal-class layout, the matrix streamed once)" if pipelined else
+                                   "symmetric diagonal-class layout" + (" with its row-class dictionary" if lay.get("sym_vd")
+                                                                        else "") +
+                                   ", the matrix streamed once)" if pipelined else
                                    " (level-0 post-smoothing Jacobi, symmetric diagonal-class layout: "
                                    "diagonal + upper values per row, lower values from their mirrors)"
                                    if lay.get("sym") else " (level-0 post-smoothing Jacobi"

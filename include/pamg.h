@@ -80,6 +80,29 @@ typedef int (*pamg_host_comm_fn)(void* user, int op, int n, const int32_t* peer,
                                  const int64_t* send_counts, const double* sendbuf,
                                  const int64_t* recv_counts, double* recvbuf);
 int pamg_comm_init_host(pamg_ctx* ctx, int nranks, int rank, pamg_host_comm_fn fn, void* user);
+/* In-process transport (PartitionedArrays with_debug: all parts in one process): a world of
+ * nparts sibling contexts, each registered under its rank and driven by its own host thread
+ * (a context is not re-entrant). Ghost exchanges, the agglomeration all-gather and all-reduces
+ * rendezvous in the world and move data by device-to-device copies along the plans' send/recv
+ * lists — straight from the sibling's vector into the ghost slots (hipMemcpyAsync with peer
+ * access across GPUs; siblings may share one GPU). Synchronous like the host transport: no
+ * overlap, no graph capture. A rank that does not arrive within 300 s fails the collective
+ * (PAMG_E_STATE) on every rank. The world lives until it and all its contexts are destroyed. */
+typedef struct pamg_world pamg_world;
+int pamg_world_create(int nparts, pamg_world** out);
+int pamg_world_destroy(pamg_world* w);
+int pamg_comm_init_local(pamg_ctx* ctx, pamg_world* w, int rank);
+/* All parts of a world at once (one host thread per part inside, each on its own context; for
+ * callers with one host thread, e.g. PartitionedArrays with_debug's map over the parts): the
+ * per-part arrays are indexed by rank. The result of a failed part is returned with its message
+ * ("part r: ..."). res_hist / iters receive rank 0's (every rank's are the same). */
+int pamg_world_spmv(pamg_world* w, pamg_mat* const* A, pamg_vec* const* x, pamg_vec* const* y);
+int pamg_world_exchange(pamg_world* w, pamg_plan* const* plan, pamg_vec* const* x);
+int pamg_world_dot(pamg_world* w, pamg_vec* const* x, pamg_vec* const* y, double* out);
+int pamg_world_vcycle(pamg_world* w, pamg_hier* const* H, pamg_vec* const* x, pamg_vec* const* b, int ncycles,
+                      double* res_hist);
+int pamg_world_pcg(pamg_world* w, pamg_hier* const* H, pamg_vec* const* x, pamg_vec* const* b, double rtol,
+                   int maxit, int* iters, double* res_hist);
 
 /* ------------------------------------------------------------------ exchange plan */
 /* Replaces PRange / ExchangeGraph: ghosts [n_own, n_own+n_ghost) grouped by neighbour in
@@ -152,7 +175,9 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * the kernel's grid); bit 4: that kernel takes two rows per lane (sym_rows 2); bit 5: the
  * matrix is a 7-point grid stencil the temporally blocked passes run on (k_sym_tb: the
  * level-0 Jacobi -> residual, and the pipelined cycles' post -> pre -> residual chain; jr_fuse);
- * bit 6: the tile-major set carries 8-bit per-tile value dictionaries (value_dict). */
+ * bit 6: the tile-major set carries 8-bit per-tile value dictionaries (value_dict);
+ * bit 7: the symmetric layout stores a 1-byte row class per row, its values in a table of
+ * <= 64 (mask, diagonal, upper values) tuples (sym_vd). */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[10]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */

@@ -22,8 +22,16 @@
 #   copyto!(x, x_d)               # own values back into the PartitionedArrays vector
 #
 # `ctxs` is a PartitionedArrays array of PamgHIP.Context, one per part, made with `map` over
-# the parts (with_mpi: one rank = one part = one GPU, each context comm_init!'ed; with_debug:
-# all parts in one process, e.g. Context(0) for each, no communicator).
+# the parts:
+#   with_mpi:   one rank = one part = one GPU, each context comm_init!'ed (RCCL);
+#   with_debug: all parts in one process — the contexts of one PamgHIP.World,
+#               `w = World(nparts); ctxs = map(p -> w.ctxs[p], LinearIndices((nparts,)))`
+#               (libpamg's in-process transport: ghosts copied device to device from the
+#               sibling parts' vectors; parts may share one GPU). A part's exchange waits for its
+#               neighbours' inside the library, so the methods below run every exchanging
+#               operation (mul!, consistent!, dot, ldiv!) for all parts in ONE call
+#               (world_spmv!, world_exchange!, world_dot, world_vcycle!: a thread per part
+#               inside libpamg) instead of a sequential map; local operations stay a map.
 #
 # Layout mapping. PartitionedArrays numbers a part's local indices own-first for the
 # OwnAndGhostIndices it builds (uniform_partition + ghosts), with ghosts in the order of
@@ -207,8 +215,20 @@ end
 
 Base.similar(x::HIPPVector) = HIPPVector(map(similar, x.parts), x.layouts, x.plans)
 
-LinearAlgebra.mul!(y::HIPPVector, A::HIPPSparseMatrix, x::HIPPVector) =
-    (foreach(mul!, y.parts, A.parts, x.parts); y)
+# the World of a debug-backend distribution (every part's context in one), or nothing
+function _world(parts)
+    ps = collect(parts)
+    w = first(ps).ctx.world
+    (w === nothing || length(ps) < 2) && return nothing
+    w
+end
+
+function LinearAlgebra.mul!(y::HIPPVector, A::HIPPSparseMatrix, x::HIPPVector)
+    w = _world(x.parts)
+    w === nothing ? foreach(mul!, y.parts, A.parts, x.parts) :
+        PamgHIP.world_spmv!(w, collect(y.parts), collect(A.parts), collect(x.parts))
+    y
+end
 
 """
 consistent!(x): PartitionedArrays' contract — start the ghost exchange and return a task;
@@ -216,6 +236,11 @@ consistent!(x): PartitionedArrays' contract — start the ghost exchange and ret
 part's comm stream (pamg_exchange_begin); the Task joins them (pamg_exchange_end).
 """
 function PartitionedArrays.consistent!(x::HIPPVector)
+    w = _world(x.parts)
+    if w !== nothing  # in-process transport: synchronous, all parts in one call
+        PamgHIP.world_exchange!(w, collect(x.parts), collect(x.plans))
+        return @async x
+    end
     tasks = map(PamgHIP.exchange_begin, x.parts, x.plans)
     @async begin
         foreach(wait, tasks)
@@ -223,15 +248,13 @@ function PartitionedArrays.consistent!(x::HIPPVector)
     end
 end
 
-# Reductions: with an RCCL communicator every part's pamg_vec_dot already returns the global
-# sum (all-reduce inside libpamg); without one (debug backend, parts in one process) the part
-# sums are added here.
-function _global(ctxs, vals)
-    r, n = PamgHIP.comm_rank(first(ctxs))
-    n > 1 ? first(vals) : sum(vals)
+# Reductions: every part's pamg_vec_dot returns the global sum (the all-reduce inside libpamg:
+# RCCL, or the in-process world's rank-order sum, which is collective — all parts in one call).
+function LinearAlgebra.dot(x::HIPPVector, y::HIPPVector)
+    w = _world(x.parts)
+    w === nothing || return PamgHIP.world_dot(w, collect(x.parts), collect(y.parts))
+    getany(map(dot, x.parts, y.parts))
 end
-LinearAlgebra.dot(x::HIPPVector, y::HIPPVector) =
-    _global(map(p -> p.ctx, x.parts), collect(map(dot, x.parts, y.parts)))
 LinearAlgebra.norm(x::HIPPVector) = sqrt(dot(x, x))
 LinearAlgebra.axpy!(a::Real, x::HIPPVector, y::HIPPVector) = (foreach((xp, yp) -> axpy!(a, xp, yp), x.parts, y.parts); y)
 LinearAlgebra.axpby!(a::Real, x::HIPPVector, b::Real, y::HIPPVector) =
@@ -455,7 +478,16 @@ end
 struct HIPPVCycle{A}
     parts::A
 end
-LinearAlgebra.ldiv!(x::HIPPVector, M::HIPPVCycle, b::HIPPVector) =
-    (foreach(ldiv!, x.parts, M.parts, b.parts); x)
+function LinearAlgebra.ldiv!(x::HIPPVector, M::HIPPVCycle, b::HIPPVector)
+    w = _world(x.parts)
+    if w === nothing
+        foreach(ldiv!, x.parts, M.parts, b.parts)
+    else  # one V-cycle from zero per ldiv! (the preconditioner), all parts in one call
+        xs = collect(x.parts)
+        foreach(v -> fill!(v, 0.0), xs)
+        PamgHIP.world_vcycle!(w, xs, collect(M.parts), collect(b.parts); ncycles = first(collect(M.parts)).ncycles)
+    end
+    x
+end
 
 end # module

@@ -25,7 +25,8 @@ using SparseArrays
 export Context, ExchangePlan, DeviceVector, DeviceMatrix, HostCSR, VCycle, ExchangeTask, PamgError,
        download_own, download_ghosts, exchange_begin, residual!, jacobi!, jacobi_residual!, vcycle!, pcg!, set_sweeps!,
        set_perm!, setup_hierarchy, gen_grid, gen_xstar, read_mtx, rcm_order, locality_order, unique_id,
-       comm_init!, runtime_versions, hip
+       comm_init!, runtime_versions, hip, World, world_spmv!, world_exchange!, world_dot, world_vcycle!,
+       world_pcg!
 
 """
     hip(ctxs, A::PSparseMatrix) / hip(ctxs, x::PVector)
@@ -62,11 +63,12 @@ end
 mutable struct Context
     h::Ptr{Cvoid}
     device::Int
+    world::Any     # the World this context is a part of (in-process transport), or nothing
 end
 function Context(device::Integer = 0)
     h = Ref{Ptr{Cvoid}}(C_NULL)
     check(ccall((:pamg_ctx_create, libpamg), Cint, (Cint, Ptr{Ptr{Cvoid}}), device, h))
-    ctx = Context(h[], device)
+    ctx = Context(h[], device, nothing)
     finalizer(close, ctx)
 end
 function Base.close(c::Context)
@@ -106,6 +108,76 @@ function comm_rank(ctx::Context)
     r, n = Ref{Cint}(0), Ref{Cint}(1)
     check(ccall((:pamg_comm_rank, libpamg), Cint, (Ptr{Cvoid}, Ptr{Cint}, Ptr{Cint}), ctx.h, r, n))
     (Int(r[]), Int(n[]))
+end
+
+# ------------------------------------------------------------------ in-process world (with_debug)
+"""
+    World(nparts; devices = [0])
+
+PartitionedArrays `with_debug` on the device: `nparts` contexts in this process (part p on
+`devices[mod1(p, end)]`; parts may share a GPU), registered in one libpamg world, so ghost
+exchanges move data by device-to-device copies straight from the sibling parts' vectors
+(pamg_comm_init_local). A part's exchange waits for its neighbours' inside the library, so an
+operation that exchanges runs for all parts at once: `world_spmv!`, `world_exchange!`,
+`world_dot`, `world_vcycle!`, `world_pcg!` (one host thread per part inside libpamg; the
+PartitionedArrays extension calls them from its with_debug methods).
+"""
+mutable struct World
+    h::Ptr{Cvoid}
+    ctxs::Vector{Context}
+end
+function World(nparts::Integer; devices::AbstractVector{<:Integer} = [0])
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:pamg_world_create, libpamg), Cint, (Cint, Ptr{Ptr{Cvoid}}), nparts, h))
+    w = World(h[], Context[])
+    finalizer(close, w)
+    for r in 0:nparts-1
+        c = Context(devices[mod1(r + 1, length(devices))])
+        check(ccall((:pamg_comm_init_local, libpamg), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Cint), c.h, w.h, r))
+        c.world = w
+        push!(w.ctxs, c)
+    end
+    w
+end
+"Drop the world handle (libpamg keeps the world until its last context is destroyed too)."
+function Base.close(w::World)
+    w.h == C_NULL && return nothing
+    ccall((:pamg_world_destroy, libpamg), Cint, (Ptr{Cvoid},), w.h)
+    w.h = C_NULL
+    nothing
+end
+_handles(objs) = Ptr{Cvoid}[o.h for o in objs]
+"ys[p] = As[p] xs[p] for every part (the exchanges between siblings included)."
+world_spmv!(w::World, ys, As, xs) =
+    check(ccall((:pamg_world_spmv, libpamg), Cint, (Ptr{Cvoid}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}),
+                w.h, _handles(As), _handles(xs), _handles(ys)))
+"consistent!(x) |> wait for every part: the owners' values into the ghost slots."
+world_exchange!(w::World, xs, plans) =
+    check(ccall((:pamg_world_exchange, libpamg), Cint, (Ptr{Cvoid}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}),
+                w.h, _handles(plans), _handles(xs)))
+"dot over the own entries of every part."
+function world_dot(w::World, xs, ys)
+    out = Ref{Cdouble}(0.0)
+    check(ccall((:pamg_world_dot, libpamg), Cint, (Ptr{Cvoid}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Ptr{Cdouble}),
+                w.h, _handles(xs), _handles(ys), out))
+    out[]
+end
+"ncycles V-cycles on every part's hierarchy; returns the residual history (part 1's = all parts')."
+function world_vcycle!(w::World, xs, Ms, bs; ncycles::Integer = 1)
+    hist = zeros(Float64, ncycles)
+    check(ccall((:pamg_world_vcycle, libpamg), Cint,
+                (Ptr{Cvoid}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Cint, Ptr{Float64}),
+                w.h, _handles(Ms), _handles(xs), _handles(bs), ncycles, hist))
+    hist
+end
+"PCG with the V-cycle preconditioner on every part; returns (iterations, residual history)."
+function world_pcg!(w::World, xs, Ms, bs; rtol::Real = 1e-8, maxit::Integer = 100)
+    it = Ref{Cint}(0)
+    hist = zeros(Float64, maxit + 1)
+    check(ccall((:pamg_world_pcg, libpamg), Cint,
+                (Ptr{Cvoid}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Cdouble, Cint, Ptr{Cint}, Ptr{Float64}),
+                w.h, _handles(Ms), _handles(xs), _handles(bs), rtol, maxit, it, hist))
+    (Int(it[]), hist[1:Int(it[])+1])
 end
 
 # ------------------------------------------------------------------ exchange plan (PRange part)

@@ -45,6 +45,14 @@ SIGNATURES = {
     "pamg_comm_rank": [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "pamg_runtime_versions": [C.POINTER(C.c_int)] * 4,
     "pamg_comm_init_host": [vp, i32, i32, vp, vp],
+    "pamg_world_create": [i32, pvp],
+    "pamg_world_destroy": [vp],
+    "pamg_comm_init_local": [vp, vp, i32],
+    "pamg_world_spmv": [vp, vp, vp, vp],
+    "pamg_world_exchange": [vp, vp, vp],
+    "pamg_world_dot": [vp, vp, vp, pdbl],
+    "pamg_world_vcycle": [vp, vp, vp, vp, i32, vp],
+    "pamg_world_pcg": [vp, vp, vp, vp, dbl, i32, C.POINTER(C.c_int), vp],
     "pamg_plan_create": [vp, i64, i64, i32, vp, vp, vp, vp, pvp],
     "pamg_plan_destroy": [vp],
     "pamg_vec_create": [vp, i64, i64, pvp],
@@ -180,7 +188,7 @@ def layout_of(M, part_set: int = 0) -> dict:
             "cd_offsets": int(out[4]), "tm": bool(out[5]), "tm_rs": int(out[6]),
             "tile_nnz": int(out[7]), "tiles": int(out[8]), "anchored": bool(out[9] & 1), "per_tile": bool(out[9] & 2),
             "x_stage": bool(out[9] & 4), "sym": bool(out[9] & 8), "sym_rows": 2 if out[9] & 16 else 1,
-            "jr_fused": bool(out[9] & 32), "tm_vd": bool(out[9] & 64)}
+            "jr_fused": bool(out[9] & 32), "tm_vd": bool(out[9] & 64), "sym_vd": bool(out[9] & 128)}
 
 
 def last_error() -> str:

@@ -768,6 +768,107 @@ __global__ __launch_bounds__(kBlock) void k_rows_sym2(
     }
 }
 
+// k_rows_symd: k_rows_sym2 over the row-class dictionary (SymDia::vd_n): a row's mask, diagonal
+// and upper values are its class's (table in LDS), a lower value a(i, i - o_c) is U_c of the
+// class of row i - o_c — so the matrix streams one byte per row (its class id; the mirror rows'
+// ids are the same bytes a block o_c rows earlier read, cache hits) instead of 33. The products
+// and their order are k_rows_sym2's, so are the bits.
+template <int NU>
+struct SymTab {  // the class table in LDS: values (D, U_0 .. U_{NU-1}) per class, and masks
+    double v[kSymVdMax][NU + 1];
+    uint32_t m[kSymVdMax];
+};
+
+template <int NU>
+__device__ __forceinline__ void symtab_fill(SymTab<NU>& t, const double* __restrict__ vtab,
+                                            const uint32_t* __restrict__ mtab, int nv) {
+    for (int e = threadIdx.x; e < nv * (NU + 1); e += blockDim.x) (&t.v[0][0])[e] = vtab[e];
+    for (int e = threadIdx.x; e < nv; e += blockDim.x) t.m[e] = mtab[e];
+}
+
+__device__ __forceinline__ uint32_t tid_at(const uint8_t* __restrict__ tid, int64_t j, int64_t n) {
+    return tid[j >= 0 && j < n ? j : 0];
+}
+
+template <int OP, int NU>
+__global__ __launch_bounds__(kBlock) void k_rows_symd(
+    int nrows, int ncols, const uint8_t* __restrict__ tid, const double* __restrict__ vtab,
+    const uint32_t* __restrict__ mtab, int nv, const SymDia sd, const double* __restrict__ x,
+    const double* __restrict__ b, double* __restrict__ y, double omega) {
+    constexpr int RB = 2 * kBlock;  // rows per block
+    __shared__ SymTab<NU> tab;
+    const int bid = blockIdx.x, tidx = threadIdx.x;
+    const int xcd = bid & 7, j = bid >> 3;
+    const int plane = sd.plane0 + j / sd.eighth, blk = xcd * sd.eighth + j % sd.eighth;
+    const int64_t lo = (int64_t)plane * sd.band;
+    const int64_t i0 = lo + (int64_t)blk * RB + 2 * tidx;
+    const int64_t hi = lo + sd.band < nrows ? lo + sd.band : nrows;
+    const bool blk_ok = blk < sd.band_blocks;
+    const bool in0 = blk_ok && i0 < hi, in1 = blk_ok && i0 + 1 < hi;
+    const int64_t n = nrows;
+    const int64_t ib = in0 ? i0 : 0;  // even
+    // every global load first (ids, mirror ids, x, b), then the table, one barrier
+    const uint32_t tw = *reinterpret_cast<const uint16_t*>(tid + ib);
+    uint32_t tl[2][NU];
+    double xv[2][2 * NU + 1];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+        const int o = sd.off[NU - 1 - c];
+        tl[0][c] = tid_at(tid, ib - o, n);
+        tl[1][c] = tid_at(tid, ib + 1 - o, n);
+        const double2 xx = ld_pair(x, ib - o, ncols, (o & 1) == 0);
+        xv[0][c] = xx.x;
+        xv[1][c] = xx.y;
+    }
+    {
+        const double2 xx = ld_pair(x, ib, ncols, true);
+        xv[0][NU] = xx.x;
+        xv[1][NU] = xx.y;
+    }
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+        const int o = sd.off[c];
+        const double2 xx = ld_pair(x, ib + o, ncols, (o & 1) == 0);
+        xv[0][NU + 1 + c] = xx.x;
+        xv[1][NU + 1 + c] = xx.y;
+    }
+    double2 pb = make_double2(0.0, 0.0);
+    if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = ld_pair(b, ib, n, true);
+    const double pbv[2] = {pb.x, pb.y};
+    symtab_fill<NU>(tab, vtab, mtab, nv);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const uint32_t t = r == 0 ? (tw & 0xffu) : (tw >> 8);
+        const uint32_t m = tab.m[t];
+        double v[2 * NU + 1];
+#pragma unroll
+        for (int c = 0; c < NU; ++c) v[c] = tab.v[tl[r][c]][1 + (NU - 1 - c)];
+        v[NU] = tab.v[t][0];
+#pragma unroll
+        for (int c = 0; c < NU; ++c) v[NU + 1 + c] = tab.v[t][1 + c];
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 2 * NU + 1; ++k) {
+            const double p = v[k] * xv[r][k];
+            const double u = s + p;
+            s = ((m >> k) & 1u) ? u : s;
+        }
+        double out;
+        if constexpr (OP == OP_SPMV) {
+            out = s;
+        } else if constexpr (OP == OP_RESID) {
+            out = pbv[r] - s;
+        } else {
+            const double u = pbv[r] - s;
+            const double w = omega * u;
+            const double q = w / v[NU];
+            out = xv[r][NU] + q;
+        }
+        if ((r == 0 ? in0 : in1) && (m & SymMask<NU>::kIn)) y[ib + r] = out;
+    }
+}
+
 // ------------------------------------------------------------------ temporally blocked sweeps
 // k_sym_tb<S>: S dependent sweeps (Jacobi, [Jacobi,] then Jacobi or the residual) over a 7-point
 // grid stencil held in the symmetric layout, in ONE pass over the matrix (Options::jr_fuse):
@@ -875,6 +976,42 @@ struct TbCtx {
     bool pos_ok, own_xy;
     int x0, y0;           // the tile's first grid point
 };
+
+// The workgroup's tile and the thread's row pair (k_sym_tb / k_sym_tbd); false: no tile (the
+// whole workgroup returns before any barrier). Tiles: consecutive tiles on one XCD (block b runs
+// on XCD b % 8; speed only), ordered y-fastest so that the tiles sharing the wide y halos
+// (kTbX + 4 points x S-1 lines) sit on one XCD.
+template <int S>
+__device__ __forceinline__ bool tb_ctx_init(TbCtx<S>& t, const TbGeom& g, int nrows) {
+    using Sh = TbShape<S>;
+    const int ntiles = g.tiles_x * g.tiles_y * g.zchunks;
+    const int per = (ntiles + 7) / 8;
+    const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (lin >= ntiles) return false;
+    const int ty = lin % g.tiles_y, tx = (lin / g.tiles_y) % g.tiles_x, zc = lin / (g.tiles_x * g.tiles_y);
+    if (g.zlo + zc * g.zlen >= g.zhi) return false;  // (a chunk past the output range: uniform)
+    const int x0 = tx * kTbX, y0 = ty * kTbY;
+    t.x0 = x0;
+    t.y0 = y0;
+    t.nx = g.nx;
+    t.ny = g.ny;
+    t.nz = g.nz;
+    t.zs = g.zlo + zc * g.zlen;
+    t.ze = min(t.zs + g.zlen, g.zhi);
+    t.kend = t.ze + Sh::H;
+    t.M = (int64_t)g.nx * g.ny;
+    t.n = nrows;
+    const int tid = threadIdx.x;
+    const bool has = tid < Sh::NT;
+    const int px = has ? tid % kTbPX : 0;
+    t.ry = has ? tid / kTbPX : -1;
+    const int x = x0 - 2 + 2 * px, y = y0 - Sh::H + (has ? t.ry : 0);
+    t.col = 2 * px + 2;
+    t.ixy = (int64_t)y * g.nx + x;
+    t.pos_ok = has && x >= 0 && x < g.nx && y >= 0 && y < g.ny;
+    t.own_xy = t.pos_ok && px >= 1 && px <= kTbX / 2 && y >= y0 && y < y0 + kTbY;
+    return true;
+}
 
 // The in0 window of plane q (stage 0's region + one point / line around it, zeros outside the
 // grid), as the pairs thread tid moves: loads issued now (clamped addresses, no branch), stored
@@ -1002,36 +1139,8 @@ __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tb(int nrows, const
     __shared__ __attribute__((aligned(16))) double l0[3][Sh::RY][kTbLW];
     __shared__ __attribute__((aligned(16))) double l1[S == 3 ? 3 : 1][Sh::RY][kTbLW];
     __shared__ __attribute__((aligned(16))) double xin[3][Sh::XL][kTbLW];
-    const TbGeom& g = sd.tb;
-    // tile: consecutive tiles on one XCD (block b runs on XCD b % 8; speed only), ordered y-fastest
-    // so that the tiles sharing the wide y halos (kTbX + 4 points x S-1 lines) sit on one XCD
-    const int ntiles = g.tiles_x * g.tiles_y * g.zchunks;
-    const int per = (ntiles + 7) / 8;
-    const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (lin >= ntiles) return;  // the whole workgroup, before any barrier
-    const int ty = lin % g.tiles_y, tx = (lin / g.tiles_y) % g.tiles_x, zc = lin / (g.tiles_x * g.tiles_y);
-    if (g.zlo + zc * g.zlen >= g.zhi) return;  // (a chunk past the output range: uniform)
-    const int x0 = tx * kTbX, y0 = ty * kTbY;
     TbCtx<S> t;
-    t.x0 = x0;
-    t.y0 = y0;
-    t.nx = g.nx;
-    t.ny = g.ny;
-    t.nz = g.nz;
-    t.zs = g.zlo + zc * g.zlen;
-    t.ze = min(t.zs + g.zlen, g.zhi);
-    t.kend = t.ze + Sh::H;
-    t.M = (int64_t)g.nx * g.ny;
-    t.n = nrows;
-    const int tid = threadIdx.x;
-    const bool has = tid < Sh::NT;
-    const int px = has ? tid % kTbPX : 0;
-    t.ry = has ? tid / kTbPX : -1;
-    const int x = x0 - 2 + 2 * px, y = y0 - Sh::H + (has ? t.ry : 0);
-    t.col = 2 * px + 2;
-    t.ixy = (int64_t)y * g.nx + x;
-    t.pos_ok = has && x >= 0 && x < g.nx && y >= 0 && y < g.ny;
-    t.own_xy = t.pos_ok && px >= 1 && px <= kTbX / 2 && y >= y0 && y < y0 + kTbY;
+    if (!tb_ctx_init<S>(t, sd.tb, nrows)) return;  // the whole workgroup, before any barrier
     TbCoef c0, c1, c2;  // planes k, k-1, k-2 at step k (rotated by the unrolled loop)
     const int k0 = t.zs - Sh::H;
     {  // the in0 windows of planes k0-1 and k0 (each step loads the one above its plane)
@@ -1053,6 +1162,189 @@ __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tb(int nrows, const
             tb_step<S, false>(k, c1, c0, c2, t, mask, dg, up, ld, sd, ta, l0, l1, xin);
             tb_step<S, false>(k + 1, c2, c1, c0, t, mask, dg, up, ld, sd, ta, l0, l1, xin);
             tb_step<S, false>(k + 2, c0, c2, c1, t, mask, dg, up, ld, sd, ta, l0, l1, xin);
+        }
+    }
+}
+
+// ---- k_sym_tbd<S>: k_sym_tb over the row-class dictionary (SymDia::vd_n). Same tiles, halos,
+// LDS rings and row expressions (so the same bits); what differs is what a thread holds per plane
+// and when it loads it. Per row pair and plane it holds the two class ids, the mirror rows' ids
+// (i-1; i-nx, i+1-nx; i-M, i+1-M: the pair's ids one plane down) and b — 5 registers instead of
+// k_sym_tb's 17 doubles — so the plane ring runs one plane ahead of the computation. At step k a
+// thread stores the in0 window of plane k+1 (loaded during step k-1), then issues the loads of
+// plane k+1's ids and b and of plane k+2's window; none of them is consumed in this step (they are
+// kept as loaded, unpacked), so the HBM latency overlaps the three stages of the current plane
+// (k_sym_tb waits for its own loads before its first barrier: one full latency per plane).
+// Values come from the class table in LDS at use.
+struct TbdRow {    // one row pair on one plane, as loaded (narrow types: widened at use, so no
+    uint16_t own;  // instruction touches a load's result before the step that consumes it)
+    uint8_t m0;    // class ids: own = row i (bits 0-7), row i+1 (8-15); m0 = row i-1;
+    uint16_t m1;   // m1 = rows i-nx (0-7), i+1-nx (8-15)
+    double b[2];
+};
+
+__device__ __forceinline__ uint16_t tbd_pair_ids(const uint8_t* __restrict__ tid, int64_t j, int64_t n) {
+    j = j < 0 ? 0 : (j > n - 2 ? n - 2 : j);  // (even j; clamped ones meet clear mask bits only)
+    return *reinterpret_cast<const uint16_t*>(tid + j);
+}
+
+// plane p's entry of the pair at i (even; 0 when the pair or plane is inactive)
+__device__ __forceinline__ void tbd_load(TbdRow& c, const uint8_t* __restrict__ tid, const double* __restrict__ b,
+                                         const SymDia& sd, int64_t i, int64_t n) {
+    c.own = *reinterpret_cast<const uint16_t*>(tid + i);
+    c.m0 = tid[i >= 1 ? i - 1 : 0];
+    c.m1 = tbd_pair_ids(tid, i - sd.off[1], n);
+    const double2 bb = *reinterpret_cast<const double2*>(b + i);
+    c.b[0] = bb.x;
+    c.b[1] = bb.y;
+}
+
+// the pair's outputs: k_rows_symd's values for the 7 classes -M, -nx, -1, 0, +1, +nx, +M (m2: the
+// pair's ids one plane down, whose U_2 are this plane's -M values), then tb_rows' arithmetic
+__device__ __forceinline__ void tbd_rows(const SymTab<3>& tab, const TbdRow& c, uint32_t m2, const double (&xv)[2][7],
+                                         bool resid, double omega, double (&out)[2]) {
+    const uint32_t t0 = c.own & 0xffu, t1 = (c.own >> 8) & 0xffu;
+    const uint32_t tr[2] = {t0, t1}, l0[2] = {c.m0 & 0xffu, t0};
+    const uint32_t l1[2] = {c.m1 & 0xffu, (c.m1 >> 8) & 0xffu}, l2[2] = {m2 & 0xffu, (m2 >> 8) & 0xffu};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const uint32_t t = tr[r];
+        const uint32_t m = tab.m[t];
+        double v[7];
+        v[0] = tab.v[l2[r]][3];  // a(i, i-M)  = U_2 of row i-M
+        v[1] = tab.v[l1[r]][2];  // a(i, i-nx) = U_1 of row i-nx
+        v[2] = tab.v[l0[r]][1];  // a(i, i-1)  = U_0 of row i-1
+        v[3] = tab.v[t][0];
+        v[4] = tab.v[t][1];
+        v[5] = tab.v[t][2];
+        v[6] = tab.v[t][3];
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const double p = v[k] * xv[r][k];
+            const double u = s + p;
+            s = ((m >> k) & 1u) ? u : s;
+        }
+        if (resid) {
+            out[r] = c.b[r] - s;
+        } else {
+            const double u = c.b[r] - s;
+            const double w = omega * u;
+            const double q = w / v[3];
+            out[r] = xv[r][3] + q;
+        }
+    }
+}
+
+// one step k: En <- plane k+1 (loads issued), E0 = plane k (stage 0), E1 = k-1 (stage 1),
+// E2 = k-2 (stage 2, S = 3), E3 = k-3 (the -M ids of stage 2; of stage 1 when S = 2 it is E2);
+// win holds plane k+1's window on entry, plane k+2's on exit
+template <int S>
+__device__ __forceinline__ void tbd_step(int k, TbdRow& En, const TbdRow& E0, const TbdRow& E1, const TbdRow& E2,
+                                         const TbdRow& E3, TbWin<S>& win, const TbCtx<S>& t,
+                                         const uint8_t* __restrict__ tid, const SymDia& sd, const TbArgs& ta,
+                                         const SymTab<3>& tab, double (*l0)[TbShape<S>::RY][kTbLW],
+                                         double (*l1)[TbShape<S>::RY][kTbLW], double (*xin)[TbShape<S>::XL][kTbLW]) {
+    using Sh = TbShape<S>;
+    if (k >= t.kend) return;  // uniform: the whole workgroup
+    tb_win_store<S>(win, xin, tb_mod3(k + 1));  // loaded during the previous step
+    tb_win_load<S>(win, t, ta.in0, k + 2);
+    {
+        const int p = k + 1;
+        const bool ok = t.pos_ok && p >= 0 && p < t.nz;
+        tbd_load(En, tid, ta.b, sd, ok ? (int64_t)p * t.M + t.ixy : 0, t.n);
+    }
+    __syncthreads();  // xin (planes k-1 .. k+1)
+    // ---- stage 0 on plane k: a Jacobi sweep from in0
+    {
+        double o[2] = {0.0, 0.0};
+        if (t.pos_ok && k >= 0 && k < t.nz) {
+            double xv[2][7];
+            tb_gather_lds<Sh::XL>(xin, tb_mod3(k - 1), tb_mod3(k), tb_mod3(k + 1), t.ry + 1, t.col, xv);
+            tbd_rows(tab, E0, E1.own, xv, S == 1 && ta.last_resid, ta.omega, o);
+            if (t.own_xy && k >= t.zs && k < t.ze)
+                *reinterpret_cast<double2*>(ta.out[0] + (int64_t)k * t.M + t.ixy) = make_double2(o[0], o[1]);
+        }
+        if (t.ry >= 0) *reinterpret_cast<double2*>(&l0[tb_mod3(k)][t.ry][t.col]) = make_double2(o[0], o[1]);
+    }
+    __syncthreads();
+    // ---- stage 1 on plane k-1 from stage 0's ring
+    {
+        const int p = k - 1;
+        constexpr bool last = S == 2;
+        constexpr int hz = Sh::H - 1;
+        double o[2] = {0.0, 0.0};
+        const bool act = t.pos_ok && t.ry >= 1 && t.ry < Sh::RY - 1 && p >= 0 && p < t.nz && p >= t.zs - hz &&
+                         p < t.ze + hz && (!last || t.own_xy);
+        if (act) {
+            double xv[2][7];
+            tb_gather_lds<Sh::RY>(l0, tb_mod3(p - 1), tb_mod3(p), tb_mod3(p + 1), t.ry, t.col, xv);
+            tbd_rows(tab, E1, E2.own, xv, last && ta.last_resid, ta.omega, o);
+            if (t.own_xy && p >= t.zs && p < t.ze)
+                *reinterpret_cast<double2*>(ta.out[1] + (int64_t)p * t.M + t.ixy) = make_double2(o[0], o[1]);
+        }
+        if constexpr (S == 3) {
+            if (t.ry >= 0) *reinterpret_cast<double2*>(&l1[tb_mod3(p)][t.ry][t.col]) = make_double2(o[0], o[1]);
+        }
+    }
+    __syncthreads();  // S = 3: stage 2 reads l1; S = 2: the next step's stage 0 rewrites l0
+    // ---- stage 2 on plane k-2 from stage 1's ring (S = 3)
+    if constexpr (S == 3) {
+        const int p = k - 2;
+        if (t.own_xy && t.ry >= 2 && t.ry < Sh::RY - 2 && p >= t.zs && p < t.ze) {
+            double xv[2][7], o[2];
+            tb_gather_lds<Sh::RY>(l1, tb_mod3(p - 1), tb_mod3(p), tb_mod3(p + 1), t.ry, t.col, xv);
+            tbd_rows(tab, E2, E3.own, xv, ta.last_resid, ta.omega, o);
+            *reinterpret_cast<double2*>(ta.out[2] + (int64_t)p * t.M + t.ixy) = make_double2(o[0], o[1]);
+        }
+    }
+}
+
+template <int S>
+__global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tbd(int nrows, const uint8_t* __restrict__ tid,
+                                                                  const double* __restrict__ vtab,
+                                                                  const uint32_t* __restrict__ mtab, int nv,
+                                                                  const SymDia sd, const TbArgs ta) {
+    using Sh = TbShape<S>;
+    __shared__ __attribute__((aligned(16))) double l0[3][Sh::RY][kTbLW];
+    __shared__ __attribute__((aligned(16))) double l1[S == 3 ? 3 : 1][Sh::RY][kTbLW];
+    __shared__ __attribute__((aligned(16))) double xin[3][Sh::XL][kTbLW];
+    __shared__ __attribute__((aligned(16))) SymTab<3> tab;
+    TbCtx<S> t;
+    if (!tb_ctx_init<S>(t, sd.tb, nrows)) return;  // the whole workgroup, before any barrier
+    symtab_fill<3>(tab, vtab, mtab, nv);           // (read after the first step's barrier)
+    const int k0 = t.zs - Sh::H;
+    TbWin<S> win;
+    {  // the in0 windows of planes k0-1 and k0; plane k0+1's stays in registers for step k0
+#pragma unroll
+        for (int q = -1; q <= 0; ++q) {
+            tb_win_load<S>(win, t, ta.in0, k0 + q);
+            tb_win_store<S>(win, xin, tb_mod3(k0 + q));
+        }
+        tb_win_load<S>(win, t, ta.in0, k0 + 1);
+    }
+    // the plane ring (planes k+1 .. k-S), rotated by the unrolled loop; planes k0-1 and k0 first
+    TbdRow e0{}, e1{}, e2{}, e3{}, e4{};
+#pragma unroll
+    for (int q = -1; q <= 0; ++q) {
+        const int p = k0 + q;
+        const bool ok = t.pos_ok && p >= 0 && p < t.nz;
+        tbd_load(q == 0 ? e0 : (S == 3 ? e4 : e3), tid, ta.b, sd, ok ? (int64_t)p * t.M + t.ixy : 0, t.n);
+    }
+    if constexpr (S == 2) {  // planes k+1, k, k-1, k-2 live: e0 = k0, e3 = k0-1
+        for (int k = k0; k < t.kend; k += 4) {
+            tbd_step<S>(k, e1, e0, e3, e2, e2, win, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S>(k + 1, e2, e1, e0, e3, e3, win, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S>(k + 2, e3, e2, e1, e0, e0, win, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S>(k + 3, e0, e3, e2, e1, e1, win, t, tid, sd, ta, tab, l0, l1, xin);
+        }
+    } else {  // planes k+1, k, k-1, k-2, k-3 live: e0 = k0, e4 = k0-1
+        for (int k = k0; k < t.kend; k += 5) {
+            tbd_step<S>(k, e1, e0, e4, e3, e2, win, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S>(k + 1, e2, e1, e0, e4, e3, win, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S>(k + 2, e3, e2, e1, e0, e4, win, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S>(k + 3, e4, e3, e2, e1, e0, win, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S>(k + 4, e0, e4, e3, e2, e1, win, t, tid, sd, ta, tab, l0, l1, xin);
         }
     }
 }
@@ -1346,6 +1638,11 @@ template <int OP, int NU>
 void launch_sym_nu(const pamg_mat& A, const double* x, const double* b, double* y, double omega, hipStream_t s) {
     const SymDia& sd = A.sym;
     const int grid = sd.nbands * 8 * sd.eighth;
+    if (sd.vd_n) {  // (the upload builds the dictionary only with two rows per lane)
+        k_rows_symd<OP, NU><<<grid, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab,
+                                                  sd.vd_n, sd, x, b, y, omega);
+        return;
+    }
     if (sd.rpl == 2) {
         k_rows_sym2<OP, NU><<<grid, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper,
                                                   sd.ld, sd, x, b, y, omega);
@@ -1403,6 +1700,15 @@ void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s) {
     g.zchunks = (span + g.zlen - 1) / g.zlen;
     const int ntiles = g.tiles_x * g.tiles_y * g.zchunks;
     const int grid = (ntiles + 7) / 8 * 8;
+    if (sd.vd_n) {
+        if (ta.nstages == 2)
+            k_sym_tbd<2><<<grid, TbShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
+                                                              sd, ta);
+        else
+            k_sym_tbd<3><<<grid, TbShape<3>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
+                                                              sd, ta);
+        return;
+    }
     if (ta.nstages == 2)
         k_sym_tb<2><<<grid, TbShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_mask, sd.d_diag, sd.d_upper, sd.ld, sd, ta);
     else

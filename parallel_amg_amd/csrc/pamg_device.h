@@ -124,6 +124,8 @@ struct Options {
     int sym_rows = 2;          // rows per lane of its kernel (1 | 2)
     int jr_fuse = 1;           // 1: temporally blocked level-0 Jacobi -> residual / cross-cycle pipeline where the
                                //    operator is a grid stencil (k_sym_tb)
+    int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
+                               //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
 };
 
 // Symmetric diagonal-class layout (k_rows_sym): a square operator whose interior rows use at
@@ -135,6 +137,10 @@ struct Options {
 // NU+1 values per row instead of 2*NU+1, with no column stream at all. (Where 2*NU+1 <= 7 the
 // mask is one byte, the set flag in bit 7.)
 constexpr int kSymMaxU = 7;
+// Row-class dictionary of the symmetric layout (Options::sym_vd): at most this many distinct
+// (mask, D, U_0 .. U_{nu-1}) bit tuples over the own rows; each row then stores its class id
+// (1 byte) instead of mask + diagonal + nu upper values, the table sits in LDS
+constexpr int kSymVdMax = 64;
 // Temporal blocking of S dependent row sweeps (kernels.hip k_sym_tb): the operator is a 7-point
 // grid stencil in natural order — classes {1, nx, nx*ny}, n = nx*ny*nz, and no row reaching
 // across a grid line or plane (checked at upload) — so a workgroup owns a kTbX x kTbY column of
@@ -166,6 +172,13 @@ struct SymDia {
     int mask_bytes = 2;
     double* d_diag = nullptr;       // nrows (+ pad)
     double* d_upper = nullptr;      // nu * ld
+    // row-class dictionary (vd_n > 0; then d_mask / d_diag / d_upper are not allocated): row i's
+    // class d_tid[i]; class e's values d_vtab[e * (nu + 1) + {0: D, 1 + c: U_c}], mask d_mtab[e]
+    // (the in-set flag included); the lower value a(i, i - o_c) is U_c of class d_tid[i - o_c]
+    int vd_n = 0;
+    uint8_t* d_tid = nullptr;       // nrows (+ pad)
+    double* d_vtab = nullptr;
+    uint32_t* d_mtab = nullptr;
 };
 Options& options();
 
@@ -180,6 +193,8 @@ struct pamg_ctx {
     int rank = 0, nranks = 1;
     pamg_host_comm_fn host_fn = nullptr;  // debug transport (pamg_comm_init_host)
     void* host_user = nullptr;
+    pamg_world* world = nullptr;           // in-process transport (pamg_comm_init_local)
+    hipEvent_t ev_ready = nullptr;         //   "the vector I posted is written" (on s_comp / s_comm)
     std::vector<double> h_send, h_recv;   // staging for the debug transport
     double* d_red = nullptr;  // reduction workspace (partials + result)
     int red_cap = 0;

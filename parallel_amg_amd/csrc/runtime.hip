@@ -6,9 +6,12 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <functional>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1049,17 +1052,98 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
     sd.eighth = (sd.band_blocks + 7) / 8;
     sd.nbands = (int)((n + bd - 1) / bd);
     sd.mask_bytes = mb;
-    CHECK(dalloc(&sd.d_mask, (n + kVecPad) * mb));
-    CHECK(dalloc(&sd.d_diag, n + kVecPad));
-    CHECK(dalloc(&sd.d_upper, (int64_t)nu * sd.ld));
-    if (mb == 1) {
-        std::vector<uint8_t> m8(mask.begin(), mask.end());
-        CHECK(h2d(A->ctx, sd.d_mask, m8.data(), m8.size()));
-    } else {
-        CHECK(h2d(A->ctx, sd.d_mask, mask.data(), sizeof(uint16_t) * mask.size()));
+    // Row-class dictionary (Options::sym_vd, two rows per lane): the distinct (mask, D, U_0 ..
+    // U_{nu-1}) bit tuples of the own rows in first-occurrence order (chunks scanned in
+    // parallel, merged in chunk order — the table one sequential pass builds); a constant-
+    // coefficient stencil has one per boundary case (512^3 Poisson: 27)
+    std::vector<uint8_t> tid;
+    std::vector<double> vtab;
+    std::vector<uint32_t> mtab;
+    if (pamg::options().sym_vd && sd.rpl == 2) {
+        using Key = std::array<uint64_t, 2 + kSymMaxU>;
+        auto key_of = [&](int64_t i) {
+            Key k{};
+            k[0] = mask[i];
+            std::memcpy(&k[1], &dg[i], 8);
+            for (int c = 0; c < nu; ++c) std::memcpy(&k[2 + c], &up[(size_t)c * sd.ld + i], 8);
+            return k;
+        };
+        const int nch = std::max(1, std::min<int>(host_threads(), (int)(n / 65536)));
+        std::vector<std::vector<Key>> firsts(nch);
+        std::atomic<bool> over{false};
+        {
+            std::vector<std::thread> th;
+            for (int c = 0; c < nch; ++c)
+                th.emplace_back([&, c] {
+                    std::vector<Key>& f = firsts[c];
+                    int last = -1;
+                    for (int64_t i = n * c / nch, e = n * (c + 1) / nch; i < e && !over; ++i) {
+                        const Key k = key_of(i);
+                        if (last >= 0 && f[last] == k) continue;
+                        last = -1;
+                        for (int q = 0; q < (int)f.size() && last < 0; ++q)
+                            if (f[q] == k) last = q;
+                        if (last >= 0) continue;
+                        if ((int)f.size() == pamg::kSymVdMax) {
+                            over = true;
+                            break;
+                        }
+                        f.push_back(k);
+                        last = (int)f.size() - 1;
+                    }
+                });
+            for (auto& x : th) x.join();
+        }
+        std::vector<Key> tab;
+        for (int c = 0; c < nch && !over; ++c)
+            for (const Key& k : firsts[c]) {
+                if (std::find(tab.begin(), tab.end(), k) != tab.end()) continue;
+                if ((int)tab.size() == pamg::kSymVdMax) {
+                    over = true;
+                    break;
+                }
+                tab.push_back(k);
+            }
+        if (!over && !tab.empty()) {
+            tid.assign(n + kVecPad, 0);
+            par_for(n, [&](int64_t a, int64_t b) {
+                int last = 0;
+                for (int64_t i = a; i < b; ++i) {
+                    const Key k = key_of(i);
+                    if (tab[last] != k) last = (int)(std::find(tab.begin(), tab.end(), k) - tab.begin());
+                    tid[i] = (uint8_t)last;
+                }
+            });
+            const int nv = (int)tab.size();
+            vtab.assign((size_t)nv * (nu + 1) + kVecPad, 0.0);
+            mtab.assign(nv + kVecPad, 0u);
+            for (int e = 0; e < nv; ++e) {
+                mtab[e] = (uint32_t)tab[e][0];
+                for (int c = 0; c <= nu; ++c) std::memcpy(&vtab[(size_t)e * (nu + 1) + c], &tab[e][1 + c], 8);
+            }
+            sd.vd_n = nv;
+        }
     }
-    CHECK(h2d(A->ctx, sd.d_diag, dg.data(), sizeof(double) * dg.size()));
-    CHECK(h2d(A->ctx, sd.d_upper, up.data(), sizeof(double) * up.size()));
+    if (sd.vd_n) {
+        CHECK(dalloc(&sd.d_tid, (int64_t)tid.size()));
+        CHECK(h2d(A->ctx, sd.d_tid, tid.data(), tid.size()));
+        CHECK(dalloc(&sd.d_vtab, (int64_t)vtab.size()));
+        CHECK(h2d(A->ctx, sd.d_vtab, vtab.data(), sizeof(double) * vtab.size()));
+        CHECK(dalloc(&sd.d_mtab, (int64_t)mtab.size()));
+        CHECK(h2d(A->ctx, sd.d_mtab, mtab.data(), sizeof(uint32_t) * mtab.size()));
+    } else {
+        CHECK(dalloc(&sd.d_mask, (n + kVecPad) * mb));
+        CHECK(dalloc(&sd.d_diag, n + kVecPad));
+        CHECK(dalloc(&sd.d_upper, (int64_t)nu * sd.ld));
+        if (mb == 1) {
+            std::vector<uint8_t> m8(mask.begin(), mask.end());
+            CHECK(h2d(A->ctx, sd.d_mask, m8.data(), m8.size()));
+        } else {
+            CHECK(h2d(A->ctx, sd.d_mask, mask.data(), sizeof(uint16_t) * mask.size()));
+        }
+        CHECK(h2d(A->ctx, sd.d_diag, dg.data(), sizeof(double) * dg.size()));
+        CHECK(h2d(A->ctx, sd.d_upper, up.data(), sizeof(double) * up.size()));
+    }
     // temporally blocked sweeps (kernels.hip k_sym_tb): one part with every row in the set, a
     // 7-point grid stencil in natural order (classes 1, nx, nx*ny; n = nx*ny*nz) whose rows
     // never reach across a grid line (the -1 / +1 / -nx / +nx classes absent at x = 0 / nx-1 /
@@ -1134,18 +1218,152 @@ void free_tiles(pamg::TileSet& ts) {
     ts.n_short = ts.n_long = 0;
 }
 
+}  // namespace
+
+// In-process world of sibling contexts (pamg_comm_init_local): a generation barrier over the
+// rank threads and one posting slot per rank. Collectives post, meet, read the siblings' posts
+// (device-to-device copies on the reader's stream, after the poster's ready event), sync their
+// stream and meet again, so no post is overwritten while a sibling still reads it.
+struct pamg_world {
+    int n = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    bool broken = false;
+    int refs = 1;  // the creator's + one per registered context
+    struct Slot {
+        const double* x = nullptr;        // the posted vector / buffer
+        const pamg_plan* plan = nullptr;  // exchanges: the poster's plan
+        hipEvent_t ready = nullptr;       // recorded after the work that wrote x
+        double scalar = 0.0;              // all-reduce operand
+    };
+    std::vector<Slot> slot;
+    std::vector<pamg_ctx*> ctx;
+    // false when a rank does not come within 300 s (or an earlier meeting failed): every
+    // waiting rank then fails instead of hanging
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (broken) return false;
+        const uint64_t g = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        if (!cv.wait_for(lk, std::chrono::seconds(300), [&] { return gen != g || broken; }) || broken) {
+            broken = true;
+            cv.notify_all();
+            return false;
+        }
+        return true;
+    }
+    void release() {
+        bool last;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            last = --refs == 0;
+        }
+        if (last) delete this;
+    }
+};
+
+namespace {
+
+// a synchronous transport (host staging or the in-process world): exchanges complete inside
+// the call, so nothing overlaps them and nothing can be graph-captured
+bool sync_transport(const pamg_ctx* ctx) { return ctx->host_fn != nullptr || ctx->world != nullptr; }
+
+// The in-process exchange: every rank posts (x, plan, ready event), the ranks meet, each copies
+// the segments its neighbours' send lists hold for it straight from their vectors into its
+// ghost slots — a contiguous run by one copy, any other list by a gather kernel reading the
+// sibling's vector — waits for its copies, and the ranks meet again.
+int exchange_local(const pamg_plan* plan, double* x, hipStream_t s) {
+    pamg_ctx* ctx = plan->ctx;
+    pamg_world* w = ctx->world;
+    const int me = ctx->rank, nn = (int)plan->nbr.size();
+    w->slot[me].x = x;
+    w->slot[me].plan = plan;
+    w->slot[me].ready = ctx->ev_ready;
+    HIPC(hipEventRecord(ctx->ev_ready, s));
+    if (!w->barrier()) return fail(PAMG_E_STATE, "local exchange: a sibling part did not arrive");
+    int rc = PAMG_OK;
+    for (int k = 0; k < nn && rc == PAMG_OK; ++k) {
+        const int64_t cnt = plan->recv_off[k + 1] - plan->recv_off[k];
+        if (cnt == 0) continue;
+        const int q = plan->nbr[k];
+        const pamg_world::Slot& sq = w->slot[q];
+        const pamg_plan* pq = sq.plan;
+        int kq = -1;
+        for (int j = 0; pq && j < (int)pq->nbr.size(); ++j)
+            if (pq->nbr[j] == me) kq = j;
+        if (kq < 0 || pq->send_off[kq + 1] - pq->send_off[kq] != cnt) {
+            rc = fail(PAMG_E_ARG, "local exchange: part %d expects %lld ghosts from part %d, which sends %lld", me,
+                      (long long)cnt, q, kq < 0 ? 0LL : (long long)(pq->send_off[kq + 1] - pq->send_off[kq]));
+            break;
+        }
+        double* dst = x + plan->n_own + plan->recv_off[k];
+        if (hipStreamWaitEvent(s, sq.ready, 0) != hipSuccess) {
+            rc = fail(PAMG_E_HIP, "local exchange: stream wait failed");
+            break;
+        }
+        if (pq->send_run[kq] >= 0) {
+            if (hipMemcpyAsync(dst, sq.x + pq->send_run[kq], sizeof(double) * cnt, hipMemcpyDefault, s) != hipSuccess)
+                rc = fail(PAMG_E_HIP, "local exchange: copy from part %d failed", q);
+        } else {
+            pamg::launch_pack(cnt, pq->d_send_idx + pq->send_off[kq], sq.x, dst, s);
+        }
+    }
+    if (rc == PAMG_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PAMG_E_HIP, "local exchange: sync failed");
+    if (!w->barrier() && rc == PAMG_OK) rc = fail(PAMG_E_STATE, "local exchange: a sibling part did not arrive");
+    return rc;
+}
+
+// sum of the ranks' *v in rank order, on every rank
+int allreduce_local(pamg_ctx* ctx, double* v) {
+    pamg_world* w = ctx->world;
+    w->slot[ctx->rank].scalar = *v;
+    if (!w->barrier()) return fail(PAMG_E_STATE, "local all-reduce: a sibling part did not arrive");
+    double sum = 0.0;
+    for (int q = 0; q < w->n; ++q) sum += w->slot[q].scalar;
+    if (!w->barrier()) return fail(PAMG_E_STATE, "local all-reduce: a sibling part did not arrive");
+    *v = sum;
+    return PAMG_OK;
+}
+
+// every rank's cnt doubles at its src, in rank order, into dst (cnt per rank)
+int allgather_local(pamg_ctx* ctx, const double* src, int64_t cnt, double* dst, hipStream_t s) {
+    pamg_world* w = ctx->world;
+    const int me = ctx->rank;
+    w->slot[me].x = src;
+    w->slot[me].ready = ctx->ev_ready;
+    HIPC(hipEventRecord(ctx->ev_ready, s));
+    if (!w->barrier()) return fail(PAMG_E_STATE, "local all-gather: a sibling part did not arrive");
+    int rc = PAMG_OK;
+    for (int q = 0; q < w->n && rc == PAMG_OK && cnt > 0; ++q) {
+        if (hipStreamWaitEvent(s, w->slot[q].ready, 0) != hipSuccess ||
+            hipMemcpyAsync(dst + (size_t)q * cnt, w->slot[q].x, sizeof(double) * cnt, hipMemcpyDefault, s) != hipSuccess)
+            rc = fail(PAMG_E_HIP, "local all-gather: copy from part %d failed", q);
+    }
+    if (rc == PAMG_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PAMG_E_HIP, "local all-gather: sync failed");
+    if (!w->barrier() && rc == PAMG_OK) rc = fail(PAMG_E_STATE, "local all-gather: a sibling part did not arrive");
+    return rc;
+}
+
 // Ghost exchange of plan on stream s: pack own values, grouped RCCL send/recv straight into
 // the ghost slots [n_own + recv_off[k], ...).
 int exchange_on(const pamg_plan* plan, double* x, hipStream_t s) {
     pamg_ctx* ctx = plan->ctx;
     const int nn = (int)plan->nbr.size();
     if (nn == 0) return PAMG_OK;
-    if (!ctx->comm && !ctx->host_fn)
+    if (!ctx->comm && !sync_transport(ctx))
         return fail(PAMG_E_STATE, "exchange: plan has neighbours but no communicator");
     // debug (SURVEY §5 race detection): NaN in the ghost slots before every exchange, so a
     // row that reads a ghost before the exchange has landed shows up as NaN
     if (pamg::options().poison_ghosts)
         pamg::launch_fill(plan->recv_off[nn], __builtin_nan(""), x + plan->n_own, s);
+    if (ctx->world) return exchange_local(plan, x, s);
     // contiguous send lists go straight from x; the others are packed first
     if (!plan->all_contig)
         pamg::launch_pack(plan->send_off[nn], plan->d_send_idx, x, plan->d_sendbuf, s);
@@ -1188,7 +1406,7 @@ int apply(pamg_ctx* ctx, const pamg_mat* A, int op, double* x, const double* b, 
           double omega) {
     hipStream_t s = ctx->s_comp;
     bool comm = A->plan && !A->plan->nbr.empty();
-    if (comm && ctx->host_fn) {  // debug transport: exchange first, no overlap
+    if (comm && sync_transport(ctx)) {  // debug / in-process transport: exchange first, no overlap
         CHECK(exchange_on(A->plan, x, s));
         comm = false;
     }
@@ -1221,7 +1439,7 @@ int sweeps_part(pamg_ctx* ctx, const pamg_mat* A, int S, const double* in0, doub
     const int zlo = sd.part_lo == 0 ? 0 : sd.part_lo + S - 1, zhi = sd.part_hi == nz ? nz : sd.part_hi - (S - 1);
     auto stage = [&](double* v, auto&& overlapped, auto&& after) -> int {
         bool comm = A->plan && !A->plan->nbr.empty();
-        if (comm && ctx->host_fn) {  // debug transport: exchange first, no overlap
+        if (comm && sync_transport(ctx)) {  // debug / in-process transport: exchange first, no overlap
             CHECK(exchange_on(A->plan, v, s));
             comm = false;
         }
@@ -1278,6 +1496,7 @@ int reduce_with(pamg_ctx* ctx, int64_t n, double* out, F partial) {
     HIPC(hipMemcpyAsync(ctx->h_red, res, sizeof(double), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     *out = *ctx->h_red;
+    if (ctx->world && ctx->nranks > 1) CHECK(allreduce_local(ctx, out));
     if (ctx->host_fn && ctx->nranks > 1) {
         const int64_t one = 1;
         double sum = 0.0;
@@ -1362,6 +1581,8 @@ int gather_rep(pamg_hier* H, double* dst, hipStream_t s) {
         if (ctx->host_fn(ctx->host_user, 1, nr, nullptr, &cnt, ctx->h_send.data(), &tot, ctx->h_recv.data()) != 0)
             return fail(PAMG_E_RCCL, "allgather: host transport failed");
         HIPC(hipMemcpyAsync(H->d_bgather, ctx->h_recv.data(), sizeof(double) * tot, hipMemcpyHostToDevice, s));
+    } else if (ctx->world) {
+        CHECK(allgather_local(ctx, H->d_bsend, H->cmax, H->d_bgather, s));
     } else {
         NCCLC(ncclAllGather(H->d_bsend, H->d_bgather, (size_t)H->cmax, ncclDouble, ctx->comm, s));
     }
@@ -1557,6 +1778,14 @@ int pamg_ctx_destroy(pamg_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->s_comp);
     (void)hipStreamSynchronize(ctx->s_comm);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
+    if (ctx->world) {
+        {
+            std::lock_guard<std::mutex> lk(ctx->world->mu);
+            ctx->world->ctx[ctx->rank] = nullptr;
+        }
+        ctx->world->release();
+    }
+    if (ctx->ev_ready) (void)hipEventDestroy(ctx->ev_ready);
     dfree(ctx->d_red);
     if (ctx->h_red) (void)hipHostFree(ctx->h_red);
     for (int k = 0; k < 2; ++k) {
@@ -1648,6 +1877,116 @@ int pamg_comm_init_host(pamg_ctx* ctx, int nranks, int rank, pamg_host_comm_fn f
     ctx->rank = rank;
     ctx->nranks = nranks;
     return PAMG_OK;
+}
+
+int pamg_world_create(int nparts, pamg_world** out) {
+    if (!out || nparts < 1) return fail(PAMG_E_ARG, "world_create: bad args");
+    auto w = new pamg_world();
+    w->n = nparts;
+    w->slot.resize(nparts);
+    w->ctx.assign(nparts, nullptr);
+    *out = w;
+    return PAMG_OK;
+}
+
+int pamg_world_destroy(pamg_world* w) {
+    if (w) w->release();
+    return PAMG_OK;
+}
+
+int pamg_comm_init_local(pamg_ctx* ctx, pamg_world* w, int rank) {
+    if (!ctx || !w || rank < 0 || rank >= w->n) return fail(PAMG_E_ARG, "comm_init_local: bad args");
+    if (ctx->comm || ctx->host_fn || ctx->world)
+        return fail(PAMG_E_STATE, "comm_init_local: the context already has a transport");
+    CHECK(set_device(ctx));
+    {
+        std::lock_guard<std::mutex> lk(w->mu);
+        if (w->ctx[rank]) return fail(PAMG_E_STATE, "comm_init_local: rank %d is taken", rank);
+        // siblings on other GPUs read this one's vectors and it reads theirs (peer access; an
+        // already enabled pair is fine)
+        for (pamg_ctx* o : w->ctx) {
+            if (!o || o->device == ctx->device) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, ctx->device, o->device) != hipSuccess || !can)
+                return fail(PAMG_E_HIP, "comm_init_local: devices %d and %d cannot access each other", ctx->device,
+                            o->device);
+            for (int d = 0; d < 2; ++d) {
+                (void)hipSetDevice(d == 0 ? ctx->device : o->device);
+                const hipError_t e = hipDeviceEnablePeerAccess(d == 0 ? o->device : ctx->device, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                    return fail(PAMG_E_HIP, "comm_init_local: peer access %d <-> %d: %s", ctx->device, o->device,
+                                hipGetErrorString(e));
+                (void)hipGetLastError();
+            }
+            CHECK(set_device(ctx));
+        }
+        w->ctx[rank] = ctx;
+        ++w->refs;
+    }
+    if (!ctx->ev_ready) HIPC(hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming));
+    ctx->world = w;
+    ctx->rank = rank;
+    ctx->nranks = w->n;
+    return PAMG_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// f(r) for every rank r of w, each on its own host thread (the world's contexts meet inside);
+// the first failure's code, with the failing part's message in this thread's error state
+template <class F>
+int world_each(pamg_world* w, F&& f) {
+    if (!w) return fail(PAMG_E_ARG, "world: NULL");
+    for (int r = 0; r < w->n; ++r)
+        if (!w->ctx[r]) return fail(PAMG_E_STATE, "world: rank %d has no context", r);
+    std::vector<int> rc(w->n, PAMG_OK);
+    std::vector<std::string> msg(w->n);
+    std::vector<std::thread> th;
+    for (int r = 0; r < w->n; ++r)
+        th.emplace_back([&, r] {
+            rc[r] = f(r);
+            if (rc[r] != PAMG_OK) msg[r] = pamg::last_error();
+        });
+    for (auto& t : th) t.join();
+    for (int r = 0; r < w->n; ++r)
+        if (rc[r] != PAMG_OK) return fail(rc[r], "part %d: %s", r, msg[r].c_str());
+    return PAMG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int pamg_world_spmv(pamg_world* w, pamg_mat* const* A, pamg_vec* const* x, pamg_vec* const* y) {
+    if (!A || !x || !y) return fail(PAMG_E_ARG, "world_spmv: bad args");
+    return world_each(w, [&](int r) { return pamg_spmv(w->ctx[r], A[r], x[r], y[r]); });
+}
+
+int pamg_world_exchange(pamg_world* w, pamg_plan* const* plan, pamg_vec* const* x) {
+    if (!plan || !x) return fail(PAMG_E_ARG, "world_exchange: bad args");
+    return world_each(w, [&](int r) { return pamg_exchange(w->ctx[r], plan[r], x[r]); });
+}
+
+int pamg_world_dot(pamg_world* w, pamg_vec* const* x, pamg_vec* const* y, double* out) {
+    if (!x || !y || !out || !w) return fail(PAMG_E_ARG, "world_dot: bad args");
+    std::vector<double> v(w->n, 0.0);
+    CHECK(world_each(w, [&](int r) { return pamg_vec_dot(w->ctx[r], x[r], y[r], &v[r]); }));
+    *out = v[0];  // (every rank holds the same sum)
+    return PAMG_OK;
+}
+
+int pamg_world_vcycle(pamg_world* w, pamg_hier* const* H, pamg_vec* const* x, pamg_vec* const* b, int ncycles,
+                      double* res_hist) {
+    if (!H || !x || !b || !w) return fail(PAMG_E_ARG, "world_vcycle: bad args");
+    return world_each(w, [&](int r) { return pamg_vcycle(w->ctx[r], H[r], x[r], b[r], ncycles, r == 0 ? res_hist : nullptr); });
+}
+
+int pamg_world_pcg(pamg_world* w, pamg_hier* const* H, pamg_vec* const* x, pamg_vec* const* b, double rtol,
+                   int maxit, int* iters, double* res_hist) {
+    if (!H || !x || !b || !w) return fail(PAMG_E_ARG, "world_pcg: bad args");
+    return world_each(w, [&](int r) {
+        return pamg_pcg(w->ctx[r], H[r], x[r], b[r], rtol, maxit, r == 0 ? iters : nullptr, r == 0 ? res_hist : nullptr);
+    });
 }
 
 int pamg_comm_rank(const pamg_ctx* ctx, int* rank, int* nranks) {
@@ -1844,7 +2183,7 @@ int pamg_exchange_begin(pamg_ctx* ctx, pamg_plan* plan, pamg_vec* x) {
         return fail(PAMG_E_ARG, "exchange_begin: vector does not fit the plan");
     if (plan->in_flight) return fail(PAMG_E_STATE, "exchange_begin: the plan has an exchange in flight");
     CHECK(set_device(ctx));
-    if (ctx->host_fn) {
+    if (sync_transport(ctx)) {
         CHECK(exchange_on(plan, x->d, ctx->s_comp));
         plan->in_flight = x;
         return PAMG_OK;
@@ -1863,7 +2202,7 @@ int pamg_exchange_end(pamg_ctx* ctx, pamg_plan* plan, pamg_vec* x) {
     if (plan->in_flight != x) return fail(PAMG_E_STATE, "exchange_end: no exchange of this vector in flight");
     CHECK(set_device(ctx));
     plan->in_flight = nullptr;
-    if (!ctx->host_fn) {
+    if (!sync_transport(ctx)) {
         HIPC(hipStreamWaitEvent(ctx->s_comp, plan->ev_done, 0));
         HIPC(hipEventSynchronize(plan->ev_done));
     }
@@ -2026,7 +2365,9 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     A->stream_bytes = 4;
     // symmetric diagonal-class layout: 8/16-bit mask, diagonal and nu upper values per row (the
     // mirrored lower values are the same lines, re-read from cache)
-    if (A->interior.sym) A->stream_bytes += nrows * (A->sym.mask_bytes + 8 + 8 * (int64_t)A->sym.nu);
+    if (A->interior.sym)
+        A->stream_bytes += A->sym.vd_n ? nrows + (int64_t)A->sym.vd_n * (8 * (A->sym.nu + 1) + 4)
+                                       : nrows * (A->sym.mask_bytes + 8 + 8 * (int64_t)A->sym.nu);
     for (const pamg::TileSet* t : {&A->interior, &A->boundary}) {
         if (t->sym) continue;  // counted above
         const int64_t ns = t->n_short, nz = t->nnz_short;
@@ -2141,6 +2482,9 @@ int pamg_mat_destroy(pamg_mat* A) {
     dfree(A->sym.d_mask);
     dfree(A->sym.d_diag);
     dfree(A->sym.d_upper);
+    dfree(A->sym.d_tid);
+    dfree(A->sym.d_vtab);
+    dfree(A->sym.d_mtab);
     free_tiles(A->interior);
     free_tiles(A->boundary);
     delete A;
@@ -2174,7 +2518,8 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[7] = t.tile_nnz;
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
-             (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0);
+             (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0) |
+             (t.sym && A->sym.vd_n ? 128 : 0);
     if (t.sym) {  // the symmetric diagonal-class layout: upper classes, k_rows_sym's grid
         out[4] = A->sym.nu;
         out[8] = A->sym.nbands * 8 * A->sym.eighth;
@@ -2430,8 +2775,8 @@ int pamg_hier_destroy(pamg_hier* H) {
 
 int pamg_hier_set_graph(pamg_hier* H, int enable) {
     if (!H) return fail(PAMG_E_ARG, "hier_set_graph: NULL");
-    if (enable && H->ctx->host_fn)
-        return fail(PAMG_E_STATE, "hier_set_graph: the host debug transport cannot be graph-captured");
+    if (enable && sync_transport(H->ctx))
+        return fail(PAMG_E_STATE, "hier_set_graph: the host debug / in-process transports cannot be graph-captured");
     H->use_graph = enable != 0;
     if (!H->use_graph) drop_graph(H);
     return PAMG_OK;
@@ -2821,6 +3166,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "sym_dia" && (value == 0 || value == 1)) o.sym_dia = (int)value;
     else if (k == "sym_rows" && (value == 1 || value == 2)) o.sym_rows = (int)value;
     else if (k == "jr_fuse" && (value == 0 || value == 1)) o.jr_fuse = (int)value;
+    else if (k == "sym_vd" && (value == 0 || value == 1)) o.sym_vd = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -2848,6 +3194,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "sym_dia") *value = o.sym_dia;
     else if (k == "sym_rows") *value = o.sym_rows;
     else if (k == "jr_fuse") *value = o.jr_fuse;
+    else if (k == "sym_vd") *value = o.sym_vd;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

@@ -16,7 +16,9 @@ PartitionedArrays.jl names → this module:
 
 One process drives one GPU and one part (the ``with_mpi`` shape); with more than one part
 the context owns an RCCL communicator and ``mul`` overlaps the RCCL ghost exchange with the
-interior rows. Everything here calls the C-ABI; there is no host fallback.
+interior rows. ``LocalWorld`` is the ``with_debug`` shape: every part in this process, one
+context per part (on one GPU or several), exchanges by device-to-device copies between sibling
+vectors. Everything here calls the C-ABI; there is no host fallback.
 """
 from __future__ import annotations
 
@@ -152,6 +154,65 @@ class Context:
 
     def close(self):
         _release(self, "pamg_ctx_destroy")
+
+    def __del__(self):
+        self.close()
+
+
+class LocalWorld:
+    """PartitionedArrays ``with_debug`` on the device (pamg_world, pamg_comm_init_local): the
+    parts of a ``SequentialBackend(n)`` in this process, part p on ``ctxs[p]`` (devices[p %
+    len(devices)]; several parts may share a GPU). A collective operation (``mul``, ``vcycle``,
+    ``pcg``, dots, exchanges) is issued for all parts at once with ``run``, one host thread per
+    part: each thread drives its own context (libpamg calls release the GIL) and the parts meet
+    inside the library at every exchange."""
+
+    def __init__(self, nparts: int, devices=(0,)):
+        h = C.c_void_p()
+        call("pamg_world_create", int(nparts), C.byref(h))
+        self._h = h
+        self.nparts = nparts
+        self.ctxs = []
+        try:
+            for r in range(nparts):
+                c = Context(devices[r % len(devices)])
+                call("pamg_comm_init_local", c.handle, h, r)
+                c.rank, c.nranks = r, nparts
+                self.ctxs.append(c)
+        except Exception:
+            for c in self.ctxs:
+                c.close()
+            self.close()
+            raise
+
+    def run(self, fn, parts=None):
+        """[fn(p) for p in parts], one thread per part, concurrently; the first exception of any
+        part is raised after every thread has ended."""
+        import threading
+        parts = list(range(self.nparts)) if parts is None else list(parts)
+        out, err = {}, {}
+
+        def body(p):
+            try:
+                out[p] = fn(p)
+            except BaseException as e:  # noqa: BLE001 - re-raised below
+                err[p] = e
+
+        th = [threading.Thread(target=body, args=(p,), daemon=True) for p in parts]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if err:
+            p = min(err)
+            raise RuntimeError(f"part {p}: {err[p]!r}") from err[p]
+        return [out[p] for p in parts]
+
+    def close(self):
+        # drop this object's references only: a context is destroyed when its last user (a
+        # vector, a matrix) is, and the library keeps the world until its last context is gone
+        self.ctxs = []
+        _release(self, "pamg_world_destroy")
 
     def __del__(self):
         self.close()

@@ -49,7 +49,8 @@ def test_fine_512_rowsums(ctx):
 
 def test_fine_512_layouts_agree(ctx):
     """The metric's level-0 Jacobi gives the same bits in every upload layout at full size:
-    the symmetric diagonal-class layout (default), tile-major slots + 4-bit column dictionary
+    the symmetric diagonal-class layout with its row-class dictionary (default) and without it,
+    tile-major slots + 4-bit column dictionary
     (+ x staging), variant 1 with the dictionary, 24-bit columns + 8-bit row lengths, plain
     32-bit CSR tiles, and the tile path's default (8-bit per-tile value dictionaries)."""
     import ctypes
@@ -63,11 +64,11 @@ def test_fine_512_layouts_agree(ctx):
     xh = rng.standard_normal(N)
     bh = rng.standard_normal(N)
     b = PVector(ctx, N, 0, bh)
-    layouts = [{}, {"sym_dia": 0, "value_dict": 0}, {"sym_dia": 0, "tile_major": 0, "value_dict": 0},
+    layouts = [{}, {"sym_vd": 0}, {"sym_dia": 0, "value_dict": 0}, {"sym_dia": 0, "tile_major": 0, "value_dict": 0},
                {"sym_dia": 0, "tile_major": 0, "col_dict": 0, "value_dict": 0},
                {"sym_dia": 0, "tile_major": 0, "col_dict": 0, "col24": 0, "row_len8": 0, "value_dict": 0},
                {"sym_dia": 0}]  # the tile path's default: 8-bit per-tile value dictionaries in tile-major slots
-    keys = ("sym_dia", "tile_major", "col_dict", "col24", "row_len8", "value_dict")
+    keys = ("sym_dia", "tile_major", "col_dict", "col24", "row_len8", "value_dict", "sym_vd")
     old = []
     for k in keys:
         v = ctypes.c_int64()
@@ -91,7 +92,9 @@ def test_fine_512_layouts_agree(ctx):
     finally:
         for k, v in zip(keys, old):
             call("pamg_set_option", k.encode(), v)
-    assert seen[0]["sym"] and seen[0]["cd_offsets"] == 3
+    assert seen[0]["sym"] and seen[0]["cd_offsets"] == 3 and seen[0]["sym_vd"]
+    assert seen[1]["sym"] and not seen[1]["sym_vd"]
+    seen = seen[1:]
     assert seen[1]["tm"] and seen[1]["cd"] == 4 and seen[1]["x_stage"] and not seen[2]["tm"] and seen[2]["cd"] == 4
     assert seen[3]["cd"] == 0 and seen[3]["c24"] and not seen[4]["c24"]
     assert seen[5]["tm"] and seen[5]["tm_vd"]

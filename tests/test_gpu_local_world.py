@@ -1,0 +1,124 @@
+"""PartitionedArrays ``with_debug`` on the device: every part of a
+``SequentialBackend(n)`` in ONE process on one GPU, one context per part registered in an
+in-process world (pamg_world / pamg_comm_init_local), ghosts moved by device-to-device copies
+from the sibling parts' vectors. The global-view oracle's multi-part setup (SPEC §S7) is the
+reference: b = A x*, x after V-cycles (bit for bit), residual histories and PCG (1e-12), with
+NaN-poisoned ghost slots before every exchange (a read before the copy landed would show)."""
+import contextlib
+import ctypes
+
+import numpy as np
+import pytest
+
+import parallel_amg_amd as pa
+from oracle import oracle as O
+from parallel_amg_amd._lib import call, layout_of
+from parallel_amg_amd.partitioned import LocalWorld, PVector, consistent, mul
+from parallel_amg_amd.solver import AMGSolver
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.asarray(a, np.float64).view(np.int64)
+
+
+@contextlib.contextmanager
+def option(key, value):
+    v = ctypes.c_int64()
+    call("pamg_get_option", key.encode(), ctypes.byref(v))
+    call("pamg_set_option", key.encode(), int(value))
+    try:
+        yield
+    finally:
+        call("pamg_set_option", key.encode(), v.value)
+
+
+@pytest.mark.parametrize("nparts,kind,n,max_coarse,agglomerate", [
+    (2, "poisson3d", 20, 100, 0),         # decoupled on every level, the coarsest gathered
+    (2, "poisson3d", 20, 100, 32768),     # agglomerated from level 1 on (one all-gather)
+    (3, "poisson2d", 60, 200, 0),
+    (4, "poisson3d", 24, 60, 0),          # interior parts with two neighbours
+    (2, "poisson2d", 20, 1000, 0),        # one level: the distributed coarsest solve
+    (8, "poisson3d", 64, 1000, 0),        # BASELINE.json configs[2]'s part count; z-slabs: the
+    (8, "aniso3d", 64, 1000, 32768),      # blocked level-0 passes run on every part (tb_part)
+])
+def test_local_world_vcycle_bit_exact(built, nparts, kind, n, max_coarse, agglomerate):
+    ncycles = 4
+    with option("poison_ghosts", 1):
+        W = LocalWorld(nparts)
+        try:
+            be = pa.SequentialBackend(nparts)
+            A, offs, xs = pa.generate_problem(be, kind, n)
+            H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse, agglomerate=agglomerate),
+                                   device=W.ctxs[0])
+            S = [AMGSolver(W.ctxs[p], H, part=p) for p in range(nparts)]
+            assert all(not s.graph_state()["enabled"] for s in S)   # synchronous transport: eager
+            A0 = [s.A[0] for s in S]
+            xst = [PVector(W.ctxs[p], A0[p].n_own_cols, A0[p].n_ghost, xs[p]) for p in range(nparts)]
+            b = [PVector(W.ctxs[p], A0[p].nrows) for p in range(nparts)]
+            W.run(lambda p: mul(b[p], A0[p], xst[p]))
+            x = [s.new_vector() for s in S]
+            hist = W.run(lambda p: S[p].vcycle(x[p], b[p], ncycles, res_hist=True))
+            # one stationary run of the same cycles (the cross-cycle pipeline where every part is
+            # a z-slab of whole planes) gives the same bits
+            xp = [s.new_vector() for s in S]
+            W.run(lambda p: S[p].vcycle(xp[p], b[p], ncycles))
+            same_pipe = [np.array_equal(bits(xp[p].own_values()), bits(x[p].own_values())) for p in range(nparts)]
+            # consistent!(x): the owners' values in every part's ghost slots
+            pl = [H.levels[0][p].planA for p in range(nparts)]
+            v = [PVector(W.ctxs[p], pl[p].n_own, pl[p].n_ghost, x[p].own_values()) for p in range(nparts)]
+            if A0[0].plan is not None:
+                W.run(lambda p: consistent(v[p], A0[p].plan))
+            pcg = W.run(lambda p: S[p].pcg(S[p].new_vector(), b[p], rtol=1e-8, maxit=60))
+            # the same cycles through the all-parts entry point (one call; the library runs a
+            # thread per part): what a single-threaded with_debug driver (Julia map) calls
+            xw = [s.new_vector() for s in S]
+            arr = lambda objs: (ctypes.c_void_p * nparts)(*[o.handle for o in objs])  # noqa: E731
+            hw = np.zeros(ncycles)
+            call("pamg_world_vcycle", W._h, arr(S), arr(xw), arr(b), ncycles, hw.ctypes.data_as(ctypes.c_void_p))
+            same_world = [np.array_equal(bits(xw[p].own_values()), bits(x[p].own_values())) for p in range(nparts)]
+            assert all(same_world) and np.array_equal(hw, hist[0]), same_world
+            fused = [layout_of(a)["jr_fused"] for a in A0]
+            got_b = np.concatenate([bb.own_values() for bb in b])
+            got_x = np.concatenate([xx.own_values() for xx in x])
+            ghosts = [(np.asarray(pl[p].ghost_ids, np.int64), v[p].ghost_values()) for p in range(nparts)]
+        finally:
+            del S
+            W.close()
+    Ao = O.generate(kind, *O.grid_shape(kind, n))
+    bo = O.spmv(Ao, O.xstar(Ao.nrows))
+    Ho = O.setup(Ao, nparts=nparts, max_coarse=max_coarse, agglomerate=agglomerate)
+    xo, ho = Ho.solve(bo, ncycles, res_hist=True)
+    _xpo, kpo, hpo = Ho.pcg(bo, rtol=1e-8, maxit=60)
+    assert np.array_equal(bits(got_b), bits(bo))
+    assert np.array_equal(bits(got_x), bits(xo))
+    assert all(same_pipe), same_pipe
+    if n == 64:
+        assert all(fused), fused
+    for p in range(nparts):
+        np.testing.assert_allclose(hist[p], ho, rtol=1e-12)
+        its, ph = pcg[p]
+        assert its == kpo
+        np.testing.assert_allclose(ph, hpo, rtol=1e-10)
+        gid, gv = ghosts[p]
+        if A0[0].plan is not None and len(gid):
+            assert np.array_equal(bits(gv), bits(got_x[gid]))
+
+
+def test_local_world_rejects_a_second_transport(built):
+    """A context joins one transport only; a world rank is taken once."""
+    from parallel_amg_amd._lib import PamgError
+    from parallel_amg_amd.partitioned import Context
+    W = LocalWorld(2)
+    try:
+        with pytest.raises(PamgError):
+            call("pamg_comm_init_local", W.ctxs[0].handle, W._h, 1)
+        c = Context(0)
+        with pytest.raises(PamgError):
+            call("pamg_comm_init_local", c.handle, W._h, 1)   # rank 1 is taken
+        c.close()
+        y = PVector(W.ctxs[0], 10, 0, np.arange(10.0))
+        assert np.array_equal(y.own_values(), np.arange(10.0))
+    finally:
+        W.close()

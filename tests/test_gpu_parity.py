@@ -924,16 +924,20 @@ def _sym_grid(kind, n, seed=None):
                                          ("poisson3d", 40, None), ("p9", 45, None)])
 @pytest.mark.parametrize("order", [0, 1])
 @pytest.mark.parametrize("rows", [1, 2])
-def test_sym_dia_bit_exact(ctx, kind, n, seed, order, rows):
+@pytest.mark.parametrize("vd", [0, 1])
+def test_sym_dia_bit_exact(ctx, kind, n, seed, order, rows, vd):
     """k_rows_sym / k_rows_sym2 (diagonal + upper values per row, lower values read from their
-    mirrors, no column stream; one or two rows per lane): SpMV, residual and Jacobi bit-exact
-    with the oracle, natural and XCD-banded block orders, odd and even row counts."""
+    mirrors, no column stream; one or two rows per lane) and k_rows_symd (the row-class
+    dictionary: a class id per row, values from the table; the SPEC grids, whose rows take a few
+    tuples): SpMV, residual and Jacobi bit-exact with the oracle, natural and XCD-banded block
+    orders, odd and even row counts."""
     from parallel_amg_amd._lib import layout_of
     M = _sym_grid(kind, n, seed)
-    with _with_option("tile_order", order), _with_option("sym_rows", rows):
+    with _with_option("tile_order", order), _with_option("sym_rows", rows), _with_option("sym_vd", vd):
         A, _h = upload(ctx, M)
     lay = layout_of(A)
     assert lay["sym"] and lay["cd_offsets"] == {"poisson2d": 2, "p9": 4}.get(kind, 3), lay
+    assert lay["sym_vd"] == bool(vd and rows == 2 and seed is None and kind != "p9"), lay
     rng = np.random.default_rng(n)
     xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
     x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
@@ -977,6 +981,48 @@ def test_sym_dia_declines_what_it_cannot_reproduce(ctx, breaker):
     x, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows)
     mul(y, A, x)
     assert np.array_equal(bits(y.own_values()), bits(O.spmv(M2, xh)))
+
+
+def _row_classes(M):
+    """The distinct (present offsets, diagonal, upper values) tuples of a square CSR matrix — what
+    the row-class dictionary (sym_vd) counts, on the host."""
+    keys = set()
+    for i in range(M.nrows):
+        a, e = int(M.rowptr[i]), int(M.rowptr[i + 1])
+        offs = tuple(int(c) - i for c in M.col[a:e])
+        vals = tuple(float(v).hex() for c, v in zip(M.col[a:e], M.val[a:e]) if c >= i)
+        keys.add((offs, vals))
+    return len(keys)
+
+
+@pytest.mark.parametrize("npal", [1, 7, 8])
+def test_sym_row_class_dictionary_limit(ctx, npal):
+    """The row-class dictionary holds <= 64 tuples: 2D Poisson (9 boundary cases) whose diagonal
+    takes npal values gives 9 npal classes — 9, 63 (dictionary) and 72 (f64 arrays) — and both
+    layouts are bit-exact with the oracle (SpMV, residual, two Jacobi sweeps)."""
+    from parallel_amg_amd._lib import layout_of
+    M = _sym_grid("poisson2d", 30)
+    val = M.val.copy()
+    rows = np.repeat(np.arange(M.nrows), np.diff(M.rowptr))
+    dg = M.col == rows
+    pal = 4.0 + np.arange(npal) / 8.0
+    val[dg] = pal[(np.arange(M.nrows) * 7) % npal]
+    M = O.CSR(M.rowptr.copy(), M.col.copy(), val, M.ncols)
+    ncl = _row_classes(M)
+    assert ncl == 9 * npal
+    A, _h = upload(ctx, M)
+    lay = layout_of(A)
+    assert lay["sym"] and lay["sym_vd"] == (ncl <= 64), (ncl, lay)
+    rng = np.random.default_rng(npal)
+    xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
+    x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
+    mul(y, A, x)
+    assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
+    residual(y, A, x, b)
+    assert np.array_equal(bits(y.own_values()), bits(O.residual(M, xh, bh)))
+    t = PVector(ctx, M.nrows)
+    jacobi(x, A, b, t, 0.57, 2)
+    assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.57), bh, 0.57)))
 
 
 def test_sym_dia_vcycle_same_bits_either_layout(ctx):
@@ -1053,15 +1099,18 @@ def test_prolongator_value_dictionary_row_lengths_bit_exact(ctx, rl8, lengths):
 @pytest.mark.parametrize("kind,shape", [("poisson3d", (128, 128, 128)), ("aniso3d", (128, 128, 128)),
                                         ("poisson3d", (256, 256, 256)), ("poisson3d", (64, 32, 40)),
                                         ("aniso3d", (192, 48, 7))])
-def test_jacobi_residual_op_bit_exact(ctx, kind, shape):
-    """pamg_jacobi_residual: the temporally blocked pass (k_sym_tb, S = 2) against the two
-    separate sweeps on random x, b — t and r bit for bit, repeated; grids whose tiles split the
-    planes into z chunks, and a grid with fewer planes than a chunk."""
+@pytest.mark.parametrize("vd", [1, 0])
+def test_jacobi_residual_op_bit_exact(ctx, kind, shape, vd):
+    """pamg_jacobi_residual: the temporally blocked pass (k_sym_tb, S = 2; k_sym_tbd over the
+    row-class dictionary) against the two separate sweeps on random x, b — t and r bit for bit,
+    repeated, and the separate sweeps against the oracle; grids whose tiles split the planes into
+    z chunks, and a grid with fewer planes than a chunk."""
     from parallel_amg_amd._lib import layout_of
     from parallel_amg_amd.partitioned import jacobi_residual
     Ao = O.generate(kind, *shape)
-    Ad, _h = upload(ctx, Ao)
-    assert layout_of(Ad)["jr_fused"]
+    with _with_option("sym_vd", vd):
+        Ad, _h = upload(ctx, Ao)
+    assert layout_of(Ad)["jr_fused"] and layout_of(Ad)["sym_vd"] == bool(vd)
     rng = np.random.default_rng(7)
     N = Ao.nrows
     x = PVector(ctx, N, 0, rng.standard_normal(N))
@@ -1076,6 +1125,9 @@ def test_jacobi_residual_op_bit_exact(ctx, kind, shape):
                 assert f == bool(fuse)
                 out[(fuse, rep)] = (t.own_values(), r.own_values())
     t0, r0 = out[(0, 0)]
+    to = O.jacobi(Ao, x.own_values(), b.own_values(), 0.66)
+    assert np.array_equal(bits(t0), bits(to))
+    assert np.array_equal(bits(r0), bits(O.residual(Ao, to, b.own_values())))
     for rep in range(3):
         t1, r1 = out[(1, rep)]
         bt = np.flatnonzero(bits(t1) != bits(t0))
@@ -1124,7 +1176,8 @@ def test_fused_jacobi_residual_bit_exact(ctx, kind, n):
 
 
 @pytest.mark.parametrize("kind", ["poisson3d", "aniso3d"])
-def test_pipelined_cycles_bit_exact(ctx, kind):
+@pytest.mark.parametrize("vd", [1, 0])
+def test_pipelined_cycles_bit_exact(ctx, kind, vd):
     """Stationary runs of K >= 2 cycles take the cross-cycle pipeline (one k_sym_chain launch per
     cycle boundary: the level-0 post-smoothing of cycle k, the pre-smoothing and residual of
     cycle k + 1; the iterate alternating between two level-0 buffers): x after K cycles has the
@@ -1133,7 +1186,10 @@ def test_pipelined_cycles_bit_exact(ctx, kind):
     n = 128
     A, offs, xs = pa.generate_problem(be, kind, n)
     H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=ctx)
-    S = AMGSolver(ctx, H)
+    with _with_option("sym_vd", vd):
+        S = AMGSolver(ctx, H)
+    from parallel_amg_amd._lib import layout_of
+    assert layout_of(S.A[0])["sym_vd"] == bool(vd)
     b = PVector(ctx, S.A[0].nrows)
     mul(b, S.A[0], PVector(ctx, S.A[0].nrows, 0, xs[0]))
     ref = {}

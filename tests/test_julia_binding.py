@@ -23,7 +23,7 @@ UNBOUND = {
     "pamg_comm_init_host",
 }
 
-OPAQUE = {"pamg_ctx", "pamg_plan", "pamg_vec", "pamg_mat", "pamg_hier", "pamg_hcsr"}
+OPAQUE = {"pamg_ctx", "pamg_plan", "pamg_vec", "pamg_mat", "pamg_hier", "pamg_hcsr", "pamg_world"}
 SCALAR = {"int": {"Cint", "Int32"}, "int32_t": {"Int32", "Cint"}, "int64_t": {"Int64"},
           "uint64_t": {"UInt64"}, "double": {"Cdouble", "Float64"}, "uint8_t": {"UInt8"},
           "unsigned char": {"UInt8"}, "char": {"UInt8", "Cchar"}}
