@@ -177,7 +177,8 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * level-0 Jacobi -> residual, and the pipelined cycles' post -> pre -> residual chain; jr_fuse);
  * bit 6: the tile-major set carries 8-bit per-tile value dictionaries (value_dict);
  * bit 7: the symmetric layout stores a 1-byte row class per row, its values in a table of
- * <= 64 (mask, diagonal, upper values) tuples (sym_vd). */
+ * <= 64 (mask, diagonal, upper values) tuples (sym_vd); bit 8: the tile-major set stages each
+ * tile's x runs in LDS and sums one row per lane (x_stage_tiles, k_rows_xsr). */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[10]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */

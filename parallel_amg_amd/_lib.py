@@ -188,7 +188,8 @@ def layout_of(M, part_set: int = 0) -> dict:
             "cd_offsets": int(out[4]), "tm": bool(out[5]), "tm_rs": int(out[6]),
             "tile_nnz": int(out[7]), "tiles": int(out[8]), "anchored": bool(out[9] & 1), "per_tile": bool(out[9] & 2),
             "x_stage": bool(out[9] & 4), "sym": bool(out[9] & 8), "sym_rows": 2 if out[9] & 16 else 1,
-            "jr_fused": bool(out[9] & 32), "tm_vd": bool(out[9] & 64), "sym_vd": bool(out[9] & 128)}
+            "jr_fused": bool(out[9] & 32), "tm_vd": bool(out[9] & 64), "sym_vd": bool(out[9] & 128),
+            "xsr": bool(out[9] & 256)}
 
 
 def last_error() -> str:

@@ -600,6 +600,150 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     }
     if (tid < nr) y[r0 + tid] = out;
 }
+// k_rows_xsr: tile-major slots with per-tile 8-bit column and value dictionaries (TileSet::xsr;
+// the 512^3 level-1 operator: 31 nonzeros per row, 567 distinct values), x staged in LDS, one
+// row per lane. A tile's loads are coalesced and issued at entry — its column- and value-index
+// streams (one byte each per nonzero), its dictionary tables (entry -> LDS position, index ->
+// value) and its run table — then, after one barrier, its x runs: staged element e of run c is
+// x[r0 + omin_c + e - base_c], a lane loads elements tid, tid + 256, ... After a second barrier
+// each lane walks its own row in storage order and reads everything from LDS: x of entry ix for
+// row tid at lxs[pos[ix] + tid]. No x gather from L2 (k_rows_tm's per-nonzero round trip: 2048
+// lines per tile for ~1250 staged doubles here), no row map, no product staging. Products
+// rounded, summed left to right from +0.0 in storage order (SPEC §S3): every row kernel's bits.
+template <int OP, int TNNZ>
+__global__ __launch_bounds__(kBlock) void k_rows_xsr(
+    const int4* __restrict__ tiles, const uint8_t* __restrict__ tcidx, const uint8_t* __restrict__ tvidx,
+    const double* __restrict__ tvtab, int vt, const uint8_t* __restrict__ trlen, int rs,
+    const uint16_t* __restrict__ xpos, int ctab_n, const int* __restrict__ xmeta, const double* __restrict__ x,
+    int64_t ncols, const double* __restrict__ b, double* __restrict__ y, double omega) {
+    constexpr int BS = kBlock;
+    constexpr int NB = TNNZ / BS;  // index-stream bytes per lane (8 or 16)
+    static_assert(NB == 8 || NB == 16, "2048- or 4096-nonzero tiles");
+    constexpr int NT = TNNZ == 2048 ? kTmSmallTab : BS;  // table entries (upload limit)
+    constexpr int CAP = TNNZ == 2048 ? kXsrCap2048 : kXsrCap4096;
+    constexpr int NE = (CAP + BS - 1) / BS;              // staged elements per lane
+    static_assert(kXsMeta <= BS, "one run-table entry per lane");
+    __shared__ __attribute__((aligned(16))) uint8_t lix[TNNZ];
+    __shared__ __attribute__((aligned(16))) uint8_t lvx[TNNZ];
+    __shared__ uint16_t lpos[NT];
+    __shared__ double lvt[NT];
+    __shared__ double lxs[CAP];
+    __shared__ int lmeta[kXsMeta];
+    __shared__ int lwt[BS / 64];
+
+    const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int4 d = tiles[t];
+    const int r0 = d.x, nr = d.y - d.x;
+    const size_t sb = (size_t)t * TNNZ;
+    // ---- every load that depends on no other one, the run table first
+    const int mv = xmeta[(size_t)t * kXsMeta + (tid < kXsMeta ? tid : 0)];
+    const int rlv = (int)trlen[(size_t)t * rs + (tid < rs ? tid : rs - 1)];
+    uint4 ci4, vi4;
+    uint2 ci2, vi2;
+    if constexpr (NB == 16) {
+        ci4 = *reinterpret_cast<const uint4*>(tcidx + sb + 16 * tid);
+        vi4 = *reinterpret_cast<const uint4*>(tvidx + sb + 16 * tid);
+    } else {
+        ci2 = *reinterpret_cast<const uint2*>(tcidx + sb + 8 * tid);
+        vi2 = *reinterpret_cast<const uint2*>(tvidx + sb + 8 * tid);
+    }
+    const uint16_t posv = xpos[(size_t)t * ctab_n + (tid < ctab_n ? tid : ctab_n - 1)];
+    const double vtv = tvtab[(size_t)t * vt + (tid < vt ? tid : vt - 1)];
+    double pb = 0.0, px = 0.0, py = 0.0;
+    {
+        const int r = r0 + (tid < nr ? tid : 0);
+        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[r];
+        if constexpr (OP == OP_JACOBI) px = x[r];
+        if constexpr (OP == OP_PROLONG) py = y[r];
+    }
+    if (tid < kXsMeta) lmeta[tid] = mv;
+    if constexpr (NB == 16) {
+        *reinterpret_cast<uint4*>(&lix[16 * tid]) = ci4;
+        *reinterpret_cast<uint4*>(&lvx[16 * tid]) = vi4;
+    } else {
+        *reinterpret_cast<uint2*>(&lix[8 * tid]) = ci2;
+        *reinterpret_cast<uint2*>(&lvx[8 * tid]) = vi2;
+    }
+    if (tid < NT) {
+        lpos[tid] = posv;
+        lvt[tid] = vtv;
+    }
+    const int rl_len = tid < nr ? rlv : 0;
+    const int rl_inc = wave_incl_scan(rl_len);
+    if (lane == 63) lwt[tid >> 6] = rl_inc;
+    __syncthreads();  // lmeta, lwt
+    // ---- the x runs: element e belongs to the last run whose base is <= e (binary search)
+    const int ncl = lmeta[0], zix = lmeta[1], tot = lmeta[2];
+    const int* __restrict__ omin = &lmeta[3];
+    const int* __restrict__ base = &lmeta[3 + kXsrMaxRuns];
+    double xe[NE];
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+        const int e = tid + j * BS;
+        int lo = 0, hi = ncl - 1;
+        while (lo < hi) {  // (uniform trip count per lane; <= 5 steps)
+            const int mid = (lo + hi + 1) >> 1;
+            if (base[mid] <= e) lo = mid;
+            else hi = mid - 1;
+        }
+        const int64_t g = (int64_t)r0 + omin[lo] + (e - base[lo]);
+        const bool ok = e < tot && g >= 0 && g < ncols;
+        xe[j] = x[ok ? g : 0];
+    }
+#pragma unroll
+    for (int j = 0; j < NE; ++j)
+        if (tid + j * BS < tot) lxs[tid + j * BS] = xe[j];
+    int pre = 0;
+#pragma unroll
+    for (int q = 0; q < BS / 64; ++q) pre += q < (tid >> 6) ? lwt[q] : 0;
+    const int ke = pre + rl_inc, kb = ke - rl_len;
+    __syncthreads();  // lxs
+    // ---- one row per lane, storage order; batches of 4 read ahead of the dependent adds
+    double s = 0.0, dg = 0.0;
+    int k = kb;
+    for (; k + 4 <= ke; k += 4) {
+        uint32_t ix[4], vx[4];
+        double xv[4], vv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            ix[e] = lix[k + e];
+            vx[e] = lvx[k + e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            xv[e] = lxs[lpos[ix[e]] + tid];
+            vv[e] = lvt[vx[e]];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const double p = vv[e] * xv[e];
+            s = s + p;
+            if constexpr (OP == OP_JACOBI) dg = (int)ix[e] == zix ? vv[e] : dg;
+        }
+    }
+    for (; k < ke; ++k) {
+        const uint32_t ix = lix[k];
+        const double vv = lvt[lvx[k]];
+        const double p = vv * lxs[lpos[ix] + tid];
+        s = s + p;
+        if constexpr (OP == OP_JACOBI) dg = (int)ix == zix ? vv : dg;
+    }
+    double out;
+    if constexpr (OP == OP_SPMV) {
+        out = s;
+    } else if constexpr (OP == OP_RESID) {
+        out = pb - s;
+    } else if constexpr (OP == OP_JACOBI) {
+        const double u = pb - s;
+        const double v = omega * u;
+        const double w = v / dg;
+        out = px + w;
+    } else {
+        out = py + s;
+    }
+    if (tid < nr) y[r0 + tid] = out;
+}
+
 // k_rows_sym: the symmetric diagonal-class layout (pamg::SymDia). One row per lane; every
 // operand is a coalesced stream over consecutive rows — the diagonal, the NU upper-value
 // arrays U_c[i], their mirrors U_c[i - o_c] (the lower values: the same lines a block o_c rows
@@ -1604,6 +1748,14 @@ template <int OP, int TNNZ>
 void launch_tile(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
                  double* y, double omega, hipStream_t s) {
     const int n = ts.n_short;
+    if constexpr (TNNZ == 2048 || TNNZ == 4096) {
+        if (ts.tm && ts.xsr) {
+            k_rows_xsr<OP, TNNZ><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_cidx, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt,
+                                                     ts.d_tm_rlen, ts.tm_rs, ts.d_xpos, ts.ctab_n, ts.d_xmeta, x,
+                                                     A.ncols, b, y, omega);
+            return;
+        }
+    }
     if (ts.tm) {
         if (ts.tm_vt)
             launch_tm<OP, TNNZ, true>(A, ts, x, b, y, omega, s);

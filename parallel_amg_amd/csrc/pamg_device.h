@@ -34,6 +34,16 @@ struct XStage {
     int ncl = 0, stride = 0, zix = -1, ncols = 0;
     int omin[kXsMaxClusters] = {}, wid[kXsMaxClusters] = {};
 };
+// Per-tile x staging with row lanes (TileSet::xsr; kernels.hip k_rows_xsr): for tile-major sets
+// with per-tile row-relative 8-bit dictionaries and 8-bit value dictionaries (the 512^3 level-1
+// operator), each tile's offsets are clustered into <= kXsrMaxRuns runs of x, staged in LDS by
+// coalesced loads (staged element e of run c is x[r0 + omin_c + e - base_c]); per tile:
+// [ncl, zix, tot, omin_0 .. omin_{R-1}, base_0 .. base_{R-1}] in d_xmeta (kXsMeta ints) and each
+// dictionary entry's LDS position in d_xpos (uint16).
+constexpr int kXsrMaxRuns = 32;
+constexpr int kXsMeta = 3 + 2 * kXsrMaxRuns;
+constexpr int kXsrCap2048 = 2048;   // staged doubles per tile (16 KiB), 2048-nonzero tiles
+constexpr int kXsrCap4096 = 2560;   //                                  4096-nonzero tiles
 
 enum RowOp : int {
     OP_SPMV = 0,     // y = A x
@@ -75,6 +85,10 @@ struct TileSet {
     // x staging (Options::x_stage): see XStage
     bool xs = false;
     XStage xst;
+    // per-tile x staging with row lanes (Options::x_stage_tiles): see kXsMeta
+    bool xsr = false;
+    int* d_xmeta = nullptr;
+    uint16_t* d_xpos = nullptr;
     // tile-major copies (Options::tile_major; kernels.hip k_rows_tm): tile t's values and
     // column stream at t * tile_nnz, its row lengths at t * tm_rs, zero-padded
     bool tm = false;
@@ -124,6 +138,7 @@ struct Options {
     int sym_rows = 2;          // rows per lane of its kernel (1 | 2)
     int jr_fuse = 1;           // 1: temporally blocked level-0 Jacobi -> residual / cross-cycle pipeline where the
                                //    operator is a grid stencil (k_sym_tb)
+    int x_stage_tiles = 1;     // 1: per-tile x staging with row lanes for per-tile dictionary sets (k_rows_xsr)
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
 };

@@ -750,6 +750,93 @@ int build_x_stage(pamg_mat* A, pamg::TileSet* ts, int rs) {
     return PAMG_OK;
 }
 
+// Per-tile x staging with row lanes (Options::x_stage_tiles, pamg::kXsMeta, k_rows_xsr) for a
+// tile-major set with per-tile row-relative 8-bit dictionaries and 8-bit value dictionaries: per
+// tile, the offsets its nonzeros use, sorted, split into runs where the gap exceeds kXsGap (a
+// run of offsets [a, b] stages x[r0 + a .. r0 + nr - 1 + b]: nr + b - a doubles), and each
+// entry's LDS position; declined (the set keeps k_rows_tm) when a tile needs more than
+// kXsrMaxRuns runs or more doubles than the kernel's LDS holds.
+int build_x_stage_tiles(pamg_mat* A, pamg::TileSet* ts, const std::vector<int64_t>& rp, const std::vector<int>& ci,
+                        const std::vector<int4>& tiles, const std::vector<uint8_t>& idx8) {
+    using pamg::kXsMeta;
+    using pamg::kXsrMaxRuns;
+    ts->xsr = false;
+    if (!pamg::options().x_stage_tiles || !ts->tm || !ts->pt || ts->anc || ts->cd != 8 || !ts->tm_vt ||
+        (ts->tile_nnz != 2048 && ts->tile_nnz != 4096) || ts->ctab_n > (ts->tile_nnz == 2048 ? pamg::kTmSmallTab : 256))
+        return PAMG_OK;
+    const int64_t nt = (int64_t)tiles.size();
+    const int cap = ts->tile_nnz == 2048 ? pamg::kXsrCap2048 : pamg::kXsrCap4096;
+    const int tn = ts->ctab_n;
+    std::vector<uint16_t> pos((size_t)nt * tn + kVecPad, 0);
+    std::vector<int> meta((size_t)nt * kXsMeta + kVecPad, 0);
+    std::atomic<int64_t> staged{0};
+    std::atomic<int> worst_runs{0}, worst_tot{0};
+    par_for(nt, [&](int64_t a, int64_t b) {
+        std::vector<std::pair<int, int>> ent;  // (offset, dictionary index) of the used entries
+        int wr = 0, wt = 0;
+        for (int64_t t = a; t < b; ++t) {
+            const int4 d = tiles[t];
+            const int nr = d.y - d.x;
+            int off[256];
+            bool used[256] = {};
+            for (int r = d.x; r < d.y; ++r)
+                for (int64_t k = rp[r]; k < rp[r + 1]; ++k) {
+                    const int ix = idx8[k];
+                    off[ix] = ci[k] - r;
+                    used[ix] = true;
+                }
+            ent.clear();
+            for (int ix = 0; ix < 256; ++ix)
+                if (used[ix]) ent.emplace_back(off[ix], ix);
+            std::sort(ent.begin(), ent.end());
+            int* m = &meta[(size_t)t * kXsMeta];
+            int ncl = 0, tot = 0, zix = -1, cmin = 0, cmax = 0;
+            for (size_t q = 0; q <= ent.size(); ++q) {
+                const bool brk = q == ent.size() || (q > 0 && ent[q].first - cmax > pamg::kXsGap);
+                if (q > 0 && brk) {  // close the run [cmin, cmax]
+                    if (ncl < kXsrMaxRuns) {
+                        m[3 + ncl] = cmin;
+                        m[3 + kXsrMaxRuns + ncl] = tot;
+                    }
+                    ++ncl;
+                    tot += nr + (cmax - cmin);
+                }
+                if (q == ent.size()) break;
+                const int o = ent[q].first;
+                if (q == 0 || brk) cmin = o;
+                cmax = o;
+                if (o == 0) zix = ent[q].second;
+                pos[(size_t)t * tn + ent[q].second] = (uint16_t)std::min(tot + (o - cmin), 65535);
+            }
+            m[0] = ncl;
+            m[1] = zix;
+            m[2] = tot;
+            wr = std::max(wr, ncl);
+            wt = std::max(wt, tot);
+            staged += tot;
+        }
+        int cur = worst_runs.load();
+        while (wr > cur && !worst_runs.compare_exchange_weak(cur, wr)) {
+        }
+        cur = worst_tot.load();
+        while (wt > cur && !worst_tot.compare_exchange_weak(cur, wt)) {
+        }
+    });
+    const bool fits = worst_runs.load() <= kXsrMaxRuns && worst_tot.load() <= cap;
+    if (UploadTrace{}.on)
+        std::fprintf(stderr, "[pamg upload nnz=%lld] per-tile x staging: %lld tiles, %.0f doubles per tile, worst "
+                     "tile %d runs / %d doubles (limits %d / %d) -> %s\n", (long long)A->nnz, (long long)nt,
+                     (double)staged.load() / (double)std::max<int64_t>(nt, 1), worst_runs.load(), worst_tot.load(),
+                     kXsrMaxRuns, cap, fits ? "staged" : "declined");
+    if (!fits) return PAMG_OK;
+    CHECK(dalloc(&ts->d_xmeta, (int64_t)meta.size()));
+    CHECK(h2d(A->ctx, ts->d_xmeta, meta.data(), sizeof(int) * meta.size()));
+    CHECK(dalloc(&ts->d_xpos, (int64_t)pos.size()));
+    CHECK(h2d(A->ctx, ts->d_xpos, pos.data(), sizeof(uint16_t) * pos.size()));
+    ts->xsr = true;
+    return PAMG_OK;
+}
+
 // Tile-major copies (Options::tile_major, kernel variant 4 k_rows_tm): for a tile set with
 // one row per lane (<= 256 rows per tile, rows <= 255 nonzeros) and 24-bit or dictionary
 // columns, tile t's values, column stream and row lengths are copied to fixed, zero-padded
@@ -928,6 +1015,7 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
         ts->tm_rs = rs;
         ts->tm = true;
         CHECK(build_x_stage(A, ts, rs));
+        CHECK(build_x_stage_tiles(A, ts, rp, ci, tiles, idx8));
     }
     return PAMG_OK;
 }
@@ -1209,6 +1297,9 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_tm_vtab);
     ts.tm_vt = 0;
     dfree(ts.d_abase);
+    dfree(ts.d_xmeta);
+    dfree(ts.d_xpos);
+    ts.xsr = false;
     ts.anc = ts.pt = ts.xs = false;
     ts.tm = false;
     ts.tm_rs = 0;
@@ -1431,14 +1522,16 @@ int apply(pamg_ctx* ctx, const pamg_mat* A, int op, double* x, const double* b, 
 // tiles) theirs after the exchange; each later stage exchanges its input's ghosts while the
 // set's planes take the separate sweep, then the boundary planes. Every row's value is the
 // separate sweeps' (SPEC §S3 bits).
+// exch = false (pamg_bench_rowop): the same launches without the exchanges, to time one part's
+// kernels alone (the per-part figures of the multi-GPU model)
 int sweeps_part(pamg_ctx* ctx, const pamg_mat* A, int S, const double* in0, double* const* out, const double* b,
-                double omega) {
+                double omega, bool exch = true) {
     hipStream_t s = ctx->s_comp;
     const pamg::SymDia& sd = A->sym;
     const int nz = sd.tb.nz;
     const int zlo = sd.part_lo == 0 ? 0 : sd.part_lo + S - 1, zhi = sd.part_hi == nz ? nz : sd.part_hi - (S - 1);
     auto stage = [&](double* v, auto&& overlapped, auto&& after) -> int {
-        bool comm = A->plan && !A->plan->nbr.empty();
+        bool comm = exch && A->plan && !A->plan->nbr.empty();
         if (comm && sync_transport(ctx)) {  // debug / in-process transport: exchange first, no overlap
             CHECK(exchange_on(A->plan, v, s));
             comm = false;
@@ -2519,7 +2612,7 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
              (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0) |
-             (t.sym && A->sym.vd_n ? 128 : 0);
+             (t.sym && A->sym.vd_n ? 128 : 0) | (t.tm && t.xsr ? 256 : 0);
     if (t.sym) {  // the symmetric diagonal-class layout: upper classes, k_rows_sym's grid
         out[4] = A->sym.nu;
         out[8] = A->sym.nbands * 8 * A->sym.eighth;
@@ -2906,6 +2999,13 @@ static int pipe_enqueue(pamg_hier* H, double* x, const double* b, int seg) {
 
 // Eligible for the cross-cycle pipeline: one part, V(1, 1), level 0 in the symmetric layout with
 // chain schedules, fusion on, a stationary run of >= 2 cycles from a given guess.
+// Invariant across ranks: the decision is per rank (A->sym.tb_part depends on the
+// part's shape), so ranks may disagree — one pipelining, its neighbour running separate cycles.
+// That is correct only because both schedules issue the same exchanges in the same order on
+// every level: pre-smoothing (A), residual (A), restriction (R), [tail all-gather], prolongation
+// (P), post-smoothing (A) — the pipeline's chain does post-smoothing(k) (A), pre-smoothing(k+1)
+// (A), residual(k+1) (A) through sweeps_part, one exchange per stage, in cycle order. Any change
+// to either schedule must keep that sequence (tests/test_gpu_multipart.py: mixed ranks).
 static bool pipe_ok(const pamg_hier* H, int ncycles, bool zero0) {
     if (zero0 || ncycles < 2 || H->L < 2 || H->prof || !pamg::options().jr_fuse || H->nu1 != 1 || H->nu2 != 1)
         return false;
@@ -3167,6 +3267,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "sym_rows" && (value == 1 || value == 2)) o.sym_rows = (int)value;
     else if (k == "jr_fuse" && (value == 0 || value == 1)) o.jr_fuse = (int)value;
     else if (k == "sym_vd" && (value == 0 || value == 1)) o.sym_vd = (int)value;
+    else if (k == "x_stage_tiles" && (value == 0 || value == 1)) o.x_stage_tiles = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -3195,6 +3296,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "sym_rows") *value = o.sym_rows;
     else if (k == "jr_fuse") *value = o.jr_fuse;
     else if (k == "sym_vd") *value = o.sym_vd;
+    else if (k == "x_stage_tiles") *value = o.x_stage_tiles;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }
@@ -3234,7 +3336,7 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
     if ((op == pamg::OP_RESID || op == pamg::OP_JACOBI || op >= 4) && !b) return fail(PAMG_E_ARG, "bench_rowop: b needed");
     if ((op == pamg::OP_JACOBI || op >= 4) && !A->d_diag)
         return fail(PAMG_E_SETUP, "bench_rowop: jacobi needs a square matrix");
-    if (op >= 4 && !(A->interior.sym && A->sym.tb_ok))
+    if (op >= 4 && !(A->interior.sym && (A->sym.tb_ok || A->sym.tb_part)))
         return fail(PAMG_E_STATE, "bench_rowop: op %d needs the temporally blocked layout (pamg_mat_layout bit 5)", op);
     if (x == y) return fail(PAMG_E_ARG, "bench_rowop: x and y must differ");
     CHECK(check_vec_for(A, x, "bench_rowop"));
@@ -3261,7 +3363,9 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
     hipStream_t s = ctx->s_comp;
     const double* bd = b ? b->d : nullptr;
     auto once = [&]() {
-        if (op >= 4) {
+        if (op >= 4 && A->sym.tb_part) {  // one part of several: its blocked pass + edge planes + boundary rows
+            (void)sweeps_part(ctx, A, op - 2, x->d, ta.out, ta.b, omega, false);
+        } else if (op >= 4) {
             pamg::launch_sym_tb(*A, ta, s);
         } else {
             pamg::launch_rows(*A, A->interior, op, x->d, bd, x->d, y->d, omega, s);

@@ -23,6 +23,7 @@ vectors. Everything here calls the C-ABI; there is no host fallback.
 from __future__ import annotations
 
 import ctypes as C
+import sys
 
 import numpy as np
 
@@ -33,9 +34,14 @@ from .hierarchy import HostPlan
 
 
 def _release(obj, fn):
-    """Destroy a libpamg handle once (safe during interpreter shutdown)."""
+    """Destroy a libpamg handle once. During interpreter shutdown nothing is called: the
+    process is ending, and objects a failed test's traceback kept alive are collected after the
+    HIP runtime has begun its own teardown (a destroy call then can abort the process)."""
     h = getattr(obj, "_h", None)
     lib = getattr(_L, "_lib", None) if _L is not None else None
+    if sys is None or sys.is_finalizing():
+        obj._h = None
+        return
     if h and lib is not None:
         try:
             getattr(lib, fn)(h)
@@ -118,7 +124,7 @@ class Context:
         self._hostfn = None
         if backend is not None and backend.nparts > 1:
             if not backend.distributed:
-                raise ValueError("device runs need one part per process (DistributedBackend)")
+                raise ValueError("several parts in one process: use LocalWorld(nparts) (one context per part)")
             if transport == "rccl":
                 self._init_comm(backend)
             elif transport == "host":

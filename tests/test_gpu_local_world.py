@@ -122,3 +122,52 @@ def test_local_world_rejects_a_second_transport(built):
         assert np.array_equal(y.own_values(), np.arange(10.0))
     finally:
         W.close()
+
+
+def test_ranks_disagreeing_on_the_pipeline_bit_exact(built):
+    """ADVICE r3: whether a rank pipelines its level-0 cycles (the blocked chain, SymDia::tb_part)
+    depends on its part's shape. Here part 0 is a z-slab of whole planes (it pipelines) and parts
+    1, 2 start or end inside a plane (separate cycles): the exchanges still pair up (both
+    schedules issue them in the same order), and x, the residual history and a stationary run
+    keep the oracle's bits."""
+    from parallel_amg_amd.hcsr import HCSR
+    n, plane = 64, 64 * 64
+    offs = np.array([0, 20 * plane, 40 * plane + 1000, n ** 3], np.int64)
+    whole, _o, wx = pa.generate_problem(pa.SequentialBackend(1), "poisson3d", n)
+    M = whole[0]
+    nparts = 3
+    A, xs = {}, {}
+    for p in range(nparts):
+        a, c = int(offs[p]), int(offs[p + 1])
+        lo, hi = int(M.rowptr[a]), int(M.rowptr[c])
+        A[p] = HCSR.from_arrays(M.rowptr[a:c + 1] - lo, M.col[lo:hi].copy(), M.val[lo:hi].copy(), M.ncols)
+        xs[p] = np.ascontiguousarray(wx[0][a:c])
+    ncycles = 4
+    with option("poison_ghosts", 1):
+        W = LocalWorld(nparts)
+        try:
+            be = pa.SequentialBackend(nparts)
+            H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000, agglomerate=0), device=W.ctxs[0])
+            S = [AMGSolver(W.ctxs[p], H, part=p) for p in range(nparts)]
+            fused = [layout_of(s.A[0])["jr_fused"] for s in S]
+            A0 = [s.A[0] for s in S]
+            xst = [PVector(W.ctxs[p], A0[p].n_own_cols, A0[p].n_ghost, xs[p]) for p in range(nparts)]
+            b = [PVector(W.ctxs[p], A0[p].nrows) for p in range(nparts)]
+            W.run(lambda p: mul(b[p], A0[p], xst[p]))
+            x = [s.new_vector() for s in S]
+            hist = W.run(lambda p: S[p].vcycle(x[p], b[p], ncycles, res_hist=True))
+            xp = [s.new_vector() for s in S]
+            W.run(lambda p: S[p].vcycle(xp[p], b[p], ncycles))
+            got_x = np.concatenate([v.own_values() for v in x])
+            got_xp = np.concatenate([v.own_values() for v in xp])
+        finally:
+            del S
+            W.close()
+    assert fused == [True, False, False], fused
+    Ao = O.CSR(M.rowptr.copy(), M.col.astype(np.int64), M.val.copy(), M.ncols)
+    Ho = O.setup(Ao, offsets=offs, max_coarse=1000, agglomerate=0)
+    xo, ho = Ho.solve(O.spmv(Ao, wx[0]), ncycles, res_hist=True)
+    assert np.array_equal(bits(got_x), bits(xo))
+    assert np.array_equal(bits(got_xp), bits(xo))
+    for p in range(nparts):
+        np.testing.assert_allclose(hist[p], ho, rtol=1e-12)

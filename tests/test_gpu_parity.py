@@ -1218,3 +1218,47 @@ def test_pipelined_cycles_bit_exact(ctx, kind, vd):
     Ho = O.setup(Ao, max_coarse=1000)
     xo, _ho = Ho.solve(O.spmv(Ao, O.xstar(Ao.nrows)), 4, res_hist=True)
     assert np.array_equal(bits(ref[4]), bits(xo))
+
+
+@pytest.fixture(scope="module")
+def level1_64(ctx):
+    """The level-1 operator of the 64^3 Poisson hierarchy (the 512^3 A1's kind: ~31 nonzeros per
+    row, offsets scattered over the coarse numbering, a few hundred distinct values)."""
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 64)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=ctx)
+    M = H.levels[1][0].A
+    return O.CSR(M.rowptr.copy(), M.col.astype(np.int64), M.val.copy(), M.ncols)
+
+
+@pytest.mark.parametrize("tnnz", [2048, 4096])
+def test_row_lane_x_staging_bit_exact(ctx, level1_64, tnnz):
+    """k_rows_xsr (per-tile x staging, one row per lane; x_stage_tiles) on a coarse AMG operator
+    in tile-major slots with per-tile column and value dictionaries: SpMV, residual, Jacobi
+    (in-row diagonal by the tile's offset-0 entry) and the oracle's bits; the same upload without
+    the staging (k_rows_tm) gives the same bits."""
+    from parallel_amg_amd._lib import layout_of
+    M = level1_64
+    rng = np.random.default_rng(tnnz)
+    xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
+    outs = []
+    for xst in (1, 0):
+        with _with_option("tile_nnz", tnnz), _with_option("tile_major", 2), _with_option("x_stage_tiles", xst):
+            A, _h = upload(ctx, M)
+        lay = layout_of(A)
+        assert lay["tm"] and lay["per_tile"] and lay["cd"] == 8 and lay["tm_vd"], lay
+        assert lay["xsr"] == bool(xst), lay
+        x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
+        mul(y, A, x)
+        sp = y.own_values()
+        residual(y, A, x, b)
+        rs = y.own_values()
+        t = PVector(ctx, M.nrows)
+        jacobi(x, A, b, t, 0.61, 2)
+        outs.append((sp, rs, x.own_values()))
+        del A
+    assert np.array_equal(bits(outs[0][0]), bits(O.spmv(M, xh)))
+    assert np.array_equal(bits(outs[0][1]), bits(O.residual(M, xh, bh)))
+    assert np.array_equal(bits(outs[0][2]), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.61), bh, 0.61)))
+    for a, c in zip(outs[0], outs[1]):
+        assert np.array_equal(bits(a), bits(c))

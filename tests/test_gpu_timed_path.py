@@ -113,3 +113,30 @@ def test_blocked_pre_smoothing_512_bit_exact(ctx, h512):
         del t, r
     assert np.array_equal(bits(out[0][0]), bits(out[1][0]))
     assert np.array_equal(bits(out[0][1]), bits(out[1][1]))
+
+
+def test_level1_row_lane_staging_512_bit_exact(ctx, h512):
+    """The 512^3 level-1 operator (16.8M rows, 517M nonzeros) runs k_rows_xsr in the bench; its
+    residual and Jacobi give the bits of the same operator uploaded without the staging
+    (k_rows_tm, oracle-pinned at smaller sizes)."""
+    S, _b = h512
+    A1 = S.A_dev[1]
+    assert layout_of(A1)["xsr"], layout_of(A1)
+    lp = S._H.levels[1][0]
+    with option("x_stage_tiles", 0):
+        from parallel_amg_amd.partitioned import PSparseMatrix
+        B1 = PSparseMatrix(ctx, lp.A, lp.planA)
+    assert not layout_of(B1)["xsr"]
+    from parallel_amg_amd.partitioned import jacobi, residual
+    n = A1.nrows
+    rng = np.random.default_rng(5)
+    xh, bh = rng.standard_normal(n), rng.standard_normal(n)
+    outs = []
+    for M in (A1, B1):
+        x, b, y, t = PVector(ctx, n, 0, xh), PVector(ctx, n, 0, bh), PVector(ctx, n), PVector(ctx, n)
+        residual(y, M, x, b)
+        jacobi(x, M, b, t, S.omega[1], 1)
+        outs.append((y.own_values(), x.own_values()))
+    del B1
+    assert np.array_equal(bits(outs[0][0]), bits(outs[1][0]))
+    assert np.array_equal(bits(outs[0][1]), bits(outs[1][1]))

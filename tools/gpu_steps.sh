@@ -10,6 +10,7 @@
 #   trace      rocprofv3 --kernel-trace --stats of bench.py (5 steps, no CPU leg, no PMC)
 #   anatomy    counter anatomy of the level-0/1 row operators (A0 chain/SpMV, R0, P0, A1, R1, P1):
 #              three --pmc passes (requests by size; DRAM / L2 hits / writes; SQ wave-cycle split)
+#   part       tools/part_bench.py: one part (3 of 8 z-slabs of 512^3) timed alone (the T_8 model)
 #   kbench     tools/kbench.py --n 512 --levels 2 timings (KB_ARGS overrides)
 # Output: gpurun_out/TAG/.
 set -euo pipefail
@@ -26,7 +27,13 @@ for step in "$@"; do
         timeout -k 10 1000 $PYT tests -m gpu > "$OUT/tests.log" 2>&1
         ;;
     timed)
-        timeout -k 10 700 $PYT tests/test_gpu_timed_path.py tests/test_gpu_parity.py -m gpu > "$OUT/timed.log" 2>&1
+        timeout -k 10 800 $PYT tests/test_gpu_timed_path.py tests/test_gpu_parity.py tests/test_gpu_local_world.py -m gpu > "$OUT/timed.log" 2>&1
+        ;;
+    world)
+        timeout -k 10 600 $PYT tests/test_gpu_local_world.py -m gpu > "$OUT/world.log" 2>&1
+        ;;
+    census)
+        timeout -k 10 300 python3 -u tools/xsr_census.py 512 > "$OUT/census.txt" 2>&1
         ;;
     bench)
         timeout -k 10 700 python3 -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log"
@@ -50,6 +57,9 @@ for step in "$@"; do
             -d "$OUT/an4" -o p --output-format csv -- python3 -u tools/kbench.py $KBA > "$OUT/an4.jsonl" 2> "$OUT/an4.err"
         echo "anatomy pass 4 done"
         python3 tools/pmc_anatomy.py "$OUT/an1" "$OUT/an2" "$OUT/an3" "$OUT/an4" > "$OUT/anatomy.json"
+        ;;
+    part)
+        timeout -k 10 600 python3 -u tools/part_bench.py --n 512 --parts 8 --part 3 > "$OUT/part.json" 2> "$OUT/part.err"
         ;;
     kbench)
         timeout -k 10 400 python3 -u tools/kbench.py $KBA > "$OUT/kbench.jsonl" 2> "$OUT/kbench.err"
