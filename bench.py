@@ -289,7 +289,7 @@ def main():
     # the instance name as rocprofv3 demangles it (every template argument, defaults included)
     tf = lambda v: "true" if v else "false"  # noqa: E731
     if pipelined:
-        kname = "k_sym_tbd<3>" if lay.get("sym_vd") else "k_sym_tb<3>"
+        kname = f"k_sym_tbd<3, {_tb_pd()}>" if lay.get("sym_vd") else "k_sym_tb<3>"
         post_ms = float(fused["chain3_ms"])
         post_bytes = float(S.csr_bytes(A0, 3))       # matrix once + in0 + b + 3 outputs
         post_fbytes = float(S.rowsum_bytes(A0, 3))
@@ -454,6 +454,14 @@ def exchange_times(ctx, S, be, nu1, nu2, reps=20) -> dict:
     return {"per_level": per, "ms_per_cycle_upper_bound": round(total, 4),
             "note": "synchronous consistent! per plan, max over ranks; the replicated tail's all-gather is "
                     "inside levels[rep-1].restrict"}
+
+
+def _tb_pd() -> int:
+    """The row-class chain's prefetch depth (libpamg option tb_pd, a template argument of k_sym_tbd)."""
+    from parallel_amg_amd import _lib
+    v = ctypes.c_int64()
+    _lib.call("pamg_get_option", b"tb_pd", ctypes.byref(v))
+    return int(v.value)
 
 
 def kernel_source_sha() -> str:

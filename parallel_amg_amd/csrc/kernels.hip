@@ -385,16 +385,25 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     const uint8_t* __restrict__ trlen, int rs, const int* __restrict__ ctab, int ctab_n,
     const double* __restrict__ x, const double* __restrict__ b, double* __restrict__ y,
     double omega, const int* __restrict__ tanc = nullptr, const XStage xst = XStage{},
-    const uint8_t* __restrict__ tvidx = nullptr, const double* __restrict__ tvtab = nullptr, int vt = 0) {
+    const uint8_t* __restrict__ tvidx = nullptr, const double* __restrict__ tvtab = nullptr, int vt = 0,
+    const uint16_t* __restrict__ xpos = nullptr, const int* __restrict__ xmeta = nullptr) {
     // ANC (anchored dictionary): column = the row's first column (slot anchors, tanc) +
     // table[index] instead of row + table[index]
     static_assert(!ANC || CD != 0, "anchored columns are dictionary columns");
     static_assert(!XS || (CD != 0 && !ANC), "x staging needs row-relative dictionary columns");
-    static_assert(!PT || (CD != 0 && !ANC && !XS), "per-tile tables: row-relative, gathered");
+    static_assert(!PT || (CD != 0 && !ANC), "per-tile tables: row-relative");
+    // XS && PT (TileSet::xsr, launched with Options::xsr_kernel = 1): per-tile x staging — the
+    // tile's run table (xmeta) and entry positions (xpos) from the upload, the runs loaded after
+    // the first barrier, products reading x from LDS (the k_rows_xsr staging inside this body)
+    constexpr bool XSP = XS && PT;
+    static_assert(!XSP || (CD == 8 && TNNZ == 2048), "per-tile staging: 8-bit tables, 2048-nonzero tiles");
     constexpr int BS = kBlock;
     constexpr int G = TNNZ / (4 * BS);
     static_assert(G >= 1 && TNNZ % (4 * BS) == 0, "tile budget must be a multiple of 4 x block");
-    __shared__ __attribute__((aligned(16))) double lprod[TNNZ + 8];
+    // XSP: the staged x runs and the products share one array (a barrier between the last x read
+    // and the first product store), so the staging costs no occupancy
+    constexpr int NPROD = XSP && kXsrCap2048 > TNNZ + 8 ? kXsrCap2048 : TNNZ + 8;
+    __shared__ __attribute__((aligned(16))) double lprod[NPROD];
     __shared__ double ldiag[OP == OP_JACOBI ? BS : 1];
     __shared__ int lwt[BS / 64];
     // XS keeps only the table's LDS positions (kXsIoff + index): 16 / 128 entries, so the
@@ -402,12 +411,15 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     // 2048-nonzero tiles keep per-tile tables of <= kTmSmallTab entries (checked at upload,
     // build_tile_major), so one more block fits per CU (512^3 A1: residual 7 -> 8, Jacobi 6 -> 7
     // waves per SIMD; -2.4 % / -4.6 %, profiles/r03_lds/)
-    constexpr int NTAB = CD == 0 ? 1 : XS ? (CD == 4 ? 16 : kXsIoff) : PT && TNNZ == 2048 ? kTmSmallTab : BS;
+    constexpr int NTAB = CD == 0 ? 1 : XSP ? kTmSmallTab : XS ? (CD == 4 ? 16 : kXsIoff)
+                       : PT && TNNZ == 2048 ? kTmSmallTab : BS;
     constexpr int NVT = TNNZ == 2048 ? kTmSmallTab : BS;
     __shared__ int ltab[NTAB];
     __shared__ __attribute__((aligned(4))) uint8_t lrow[TNNZ + 8];
     __shared__ int lanc[ANC ? BS : 1];
-    __shared__ double lxs[XS ? kXsCap + 1 : 1];  // + 1: the dump slot of lanes past a run
+    __shared__ double lxs_own[XS && !XSP ? kXsCap + 1 : 1];  // + 1: the dump slot of lanes past a run
+    double* const lxs = XSP ? lprod : lxs_own;
+    __shared__ int lmeta[XSP ? kXsMeta : 1];
     __shared__ double lvt[VD8 ? NVT : 1];        // the tile's value table (vt <= NVT entries)
 
     const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -421,8 +433,11 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     // value stream last: the scan, the row map and the x gathers then proceed while the
     // values are still in flight (previously the scan's wait on the row lengths also waited
     // for the whole value stream, and the gathers' wait on the columns for b / x).
-    int tabv = 0, ancv = 0;
-    if constexpr (XS) tabv = ctab[kXsIoff + (tid < NTAB ? tid : NTAB - 1)];
+    int tabv = 0, ancv = 0, mv = 0;
+    if constexpr (XSP) {
+        mv = xmeta[(size_t)t * kXsMeta + (tid < kXsMeta ? tid : 0)];
+        tabv = xpos[(size_t)t * ctab_n + (tid < ctab_n ? tid : ctab_n - 1)];
+    } else if constexpr (XS) tabv = ctab[kXsIoff + (tid < NTAB ? tid : NTAB - 1)];
     else if constexpr (PT) tabv = ctab[(size_t)t * ctab_n + (tid < ctab_n ? tid : ctab_n - 1)];
     else if constexpr (CD != 0) tabv = ctab[tid];  // the table is allocated with 256 entries
     const size_t rsl = (size_t)t * rs + (tid < rs ? tid : rs - 1);
@@ -456,7 +471,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
         if constexpr (OP == OP_PROLONG) py = y[r];
     }
     double xsv[XS ? kXsMaxClusters : 1];
-    if constexpr (XS) {
+    if constexpr (XS && !XSP) {
 #pragma unroll
         for (int c = 0; c < kXsMaxClusters; ++c) {
             xsv[c] = 0.0;
@@ -484,10 +499,13 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     if constexpr (VD8) lvt[tid < NVT ? tid : NVT - 1] = vtv;  // every lane (lanes past vt repeat the last entry)
     // every lane stores its entry (unconditionally: a conditional store lets the compiler sink
     // the table load into the branch, behind the value stream)
-    if constexpr (XS) ltab[tid < NTAB ? tid : NTAB - 1] = tabv;  // lanes past NTAB rewrite the last entry's value
+    if constexpr (XSP) {
+        if (tid < NTAB) ltab[tid] = tabv;
+        if (tid < kXsMeta) lmeta[tid] = mv;
+    } else if constexpr (XS) ltab[tid < NTAB ? tid : NTAB - 1] = tabv;  // lanes past NTAB rewrite the last entry's value
     else if constexpr (CD != 0) ltab[tid < NTAB ? tid : NTAB - 1] = tabv;  // (lanes past ctab_n: the last entry)
     if constexpr (ANC) lanc[tid] = tid < rs ? ancv : 0;
-    if constexpr (XS) {
+    if constexpr (XS && !XSP) {
 #pragma unroll
         for (int c = 0; c < kXsMaxClusters; ++c)
             if (c < xst.ncl) lxs[tid < xst.stride ? c * xst.stride + tid : kXsCap] = xsv[c];
@@ -508,12 +526,36 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     constexpr bool NEED_ROWS = CD != 0 || OP == OP_JACOBI;
     int re = 0;
     if constexpr (VD8 && !NEED_ROWS) __syncthreads();  // lvt
+    int xzix = -1;
     if constexpr (NEED_ROWS) {
-        __syncthreads();  // lwt, ltab
+        __syncthreads();  // lwt, ltab (, lmeta)
         re = row_end();
-        if (tid < nr)
+        if constexpr (XSP) {  // the x runs: staged element e of run c is x[r0 + omin_c + e - base_c]
+            constexpr int NE = (kXsrCap2048 + BS - 1) / BS;
+            const int ncl = lmeta[0], tot = lmeta[2];
+            xzix = lmeta[1];
+            double xe[NE];
+#pragma unroll
+            for (int j = 0; j < NE; ++j) {
+                const int e = tid + j * BS;
+                int lo = 0, hi = ncl - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (lmeta[3 + kXsrMaxRuns + mid] <= e) lo = mid;
+                    else hi = mid - 1;
+                }
+                const int64_t g = (int64_t)r0 + lmeta[3 + lo] + (e - lmeta[3 + kXsrMaxRuns + lo]);
+                xe[j] = x[e < tot && g >= 0 && g < xst.ncols ? g : 0];
+            }
+            if (tid < nr)
+                for (int p = re - rl_len; p < re; ++p) lrow[p] = (uint8_t)tid;
+#pragma unroll
+            for (int j = 0; j < NE; ++j)
+                if (tid + j * BS < tot) lxs[tid + j * BS] = xe[j];
+        } else if (tid < nr) {
             for (int p = re - rl_len; p < re; ++p) lrow[p] = (uint8_t)tid;
-        __syncthreads();  // lrow
+        }
+        __syncthreads();  // lrow (, lxs)
     }
 
     double xv[G][4];
@@ -531,7 +573,11 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
                 // product is discarded), so every LDS read stays inside lxs
                 const int rid = q + e < cnt ? (int)((rw >> (8 * e)) & 255u) : 0;
                 cc[j][e] = ix;
-                xv[j][e] = lxs[ltab[ix] + rid];
+                if constexpr (XSP) {  // padding bytes index no table entry: slot 0 for them too
+                    xv[j][e] = q + e < cnt ? lxs[ltab[ix] + rid] : 0.0;
+                } else {
+                    xv[j][e] = lxs[ltab[ix] + rid];
+                }
             }
             continue;
         }
@@ -552,6 +598,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
 #pragma unroll
         for (int e = 0; e < 4; ++e) xv[j][e] = x[q + e < cnt ? cc[j][e] : 0];
     }
+    if constexpr (XSP) __syncthreads();  // every staged x read before the products overwrite it
 #pragma unroll
     for (int j = 0; j < G; ++j) {
         const int q = 4 * (tid + j * BS);
@@ -574,7 +621,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
             p[e] = ok ? vv[e] * xv[j][e] : 0.0;
             if constexpr (OP == OP_JACOBI) {
                 const int rl = (int)((rw >> (8 * e)) & 255u);
-                if (ok && (XS ? cc[j][e] == xst.zix : cc[j][e] - r0 == rl)) ldiag[rl] = vv[e];
+                if (ok && (XSP ? cc[j][e] == xzix : XS ? cc[j][e] == xst.zix : cc[j][e] - r0 == rl)) ldiag[rl] = vv[e];
             }
         }
         *reinterpret_cast<double2*>(&lprod[q]) = make_double2(p[0], p[1]);
@@ -1380,10 +1427,10 @@ __device__ __forceinline__ void tbd_rows(const SymTab<3>& tab, const TbdRow& c, 
     }
 }
 
-// one step k: En <- plane k+1 (loads issued), E0 = plane k (stage 0), E1 = k-1 (stage 1),
+// one step k: En <- plane k+PD (loads issued), E0 = plane k (stage 0), E1 = k-1 (stage 1),
 // E2 = k-2 (stage 2, S = 3), E3 = k-3 (the -M ids of stage 2; of stage 1 when S = 2 it is E2);
-// win holds plane k+1's window on entry, plane k+2's on exit
-template <int S>
+// win holds plane k+1's window on entry (loaded PD steps earlier), plane k+1+PD's on exit
+template <int S, int PD>
 __device__ __forceinline__ void tbd_step(int k, TbdRow& En, const TbdRow& E0, const TbdRow& E1, const TbdRow& E2,
                                          const TbdRow& E3, TbWin<S>& win, const TbCtx<S>& t,
                                          const uint8_t* __restrict__ tid, const SymDia& sd, const TbArgs& ta,
@@ -1391,10 +1438,10 @@ __device__ __forceinline__ void tbd_step(int k, TbdRow& En, const TbdRow& E0, co
                                          double (*l1)[TbShape<S>::RY][kTbLW], double (*xin)[TbShape<S>::XL][kTbLW]) {
     using Sh = TbShape<S>;
     if (k >= t.kend) return;  // uniform: the whole workgroup
-    tb_win_store<S>(win, xin, tb_mod3(k + 1));  // loaded during the previous step
-    tb_win_load<S>(win, t, ta.in0, k + 2);
+    tb_win_store<S>(win, xin, tb_mod3(k + 1));  // loaded PD steps ago
+    tb_win_load<S>(win, t, ta.in0, k + 1 + PD);
     {
-        const int p = k + 1;
+        const int p = k + PD;
         const bool ok = t.pos_ok && p >= 0 && p < t.nz;
         tbd_load(En, tid, ta.b, sd, ok ? (int64_t)p * t.M + t.ixy : 0, t.n);
     }
@@ -1444,12 +1491,15 @@ __device__ __forceinline__ void tbd_step(int k, TbdRow& En, const TbdRow& E0, co
     }
 }
 
-template <int S>
+// PD (Options::tb_pd): how many planes ahead the loads run — 1: a ring of S + 2 planes and one
+// window register set; 2: S + 3 planes and two window sets used in alternation
+template <int S, int PD>
 __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tbd(int nrows, const uint8_t* __restrict__ tid,
                                                                   const double* __restrict__ vtab,
                                                                   const uint32_t* __restrict__ mtab, int nv,
                                                                   const SymDia sd, const TbArgs ta) {
     using Sh = TbShape<S>;
+    static_assert(PD == 1 || PD == 2, "one or two planes ahead");
     __shared__ __attribute__((aligned(16))) double l0[3][Sh::RY][kTbLW];
     __shared__ __attribute__((aligned(16))) double l1[S == 3 ? 3 : 1][Sh::RY][kTbLW];
     __shared__ __attribute__((aligned(16))) double xin[3][Sh::XL][kTbLW];
@@ -1458,37 +1508,62 @@ __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tbd(int nrows, cons
     if (!tb_ctx_init<S>(t, sd.tb, nrows)) return;  // the whole workgroup, before any barrier
     symtab_fill<3>(tab, vtab, mtab, nv);           // (read after the first step's barrier)
     const int k0 = t.zs - Sh::H;
-    TbWin<S> win;
-    {  // the in0 windows of planes k0-1 and k0; plane k0+1's stays in registers for step k0
+    TbWin<S> wa, wb;
+    {  // the in0 windows of planes k0-1 and k0; planes k0+1 (.. k0+PD) stay in registers
 #pragma unroll
         for (int q = -1; q <= 0; ++q) {
-            tb_win_load<S>(win, t, ta.in0, k0 + q);
-            tb_win_store<S>(win, xin, tb_mod3(k0 + q));
+            tb_win_load<S>(wa, t, ta.in0, k0 + q);
+            tb_win_store<S>(wa, xin, tb_mod3(k0 + q));
         }
-        tb_win_load<S>(win, t, ta.in0, k0 + 1);
+        tb_win_load<S>(wa, t, ta.in0, k0 + 1);
+        if constexpr (PD == 2) tb_win_load<S>(wb, t, ta.in0, k0 + 2);
     }
-    // the plane ring (planes k+1 .. k-S), rotated by the unrolled loop; planes k0-1 and k0 first
-    TbdRow e0{}, e1{}, e2{}, e3{}, e4{};
-#pragma unroll
-    for (int q = -1; q <= 0; ++q) {
-        const int p = k0 + q;
+    // the plane ring (planes k+PD .. k-S), rotated by the unrolled loop; planes k0-1 .. k0+PD-1 first
+    TbdRow e0{}, e1{}, e2{}, e3{}, e4{}, e5{};
+    auto load = [&](TbdRow& e, int p) {
         const bool ok = t.pos_ok && p >= 0 && p < t.nz;
-        tbd_load(q == 0 ? e0 : (S == 3 ? e4 : e3), tid, ta.b, sd, ok ? (int64_t)p * t.M + t.ixy : 0, t.n);
-    }
-    if constexpr (S == 2) {  // planes k+1, k, k-1, k-2 live: e0 = k0, e3 = k0-1
+        tbd_load(e, tid, ta.b, sd, ok ? (int64_t)p * t.M + t.ixy : 0, t.n);
+    };
+    constexpr int R = PD + S + 1;  // ring entries
+    load(R == 4 ? e3 : R == 5 ? e4 : e5, k0 - 1);
+    load(e0, k0);
+    if constexpr (PD == 2) load(e1, k0 + 1);
+    if constexpr (S == 2 && PD == 1) {  // planes k+1, k, k-1, k-2
         for (int k = k0; k < t.kend; k += 4) {
-            tbd_step<S>(k, e1, e0, e3, e2, e2, win, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S>(k + 1, e2, e1, e0, e3, e3, win, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S>(k + 2, e3, e2, e1, e0, e0, win, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S>(k + 3, e0, e3, e2, e1, e1, win, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k, e1, e0, e3, e2, e2, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 1, e2, e1, e0, e3, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 2, e3, e2, e1, e0, e0, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 3, e0, e3, e2, e1, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
         }
-    } else {  // planes k+1, k, k-1, k-2, k-3 live: e0 = k0, e4 = k0-1
+    } else if constexpr (S == 3 && PD == 1) {  // planes k+1, k, k-1, k-2, k-3
         for (int k = k0; k < t.kend; k += 5) {
-            tbd_step<S>(k, e1, e0, e4, e3, e2, win, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S>(k + 1, e2, e1, e0, e4, e3, win, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S>(k + 2, e3, e2, e1, e0, e4, win, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S>(k + 3, e4, e3, e2, e1, e0, win, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S>(k + 4, e0, e4, e3, e2, e1, win, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k, e1, e0, e4, e3, e2, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 1, e2, e1, e0, e4, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 2, e3, e2, e1, e0, e4, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 3, e4, e3, e2, e1, e0, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 4, e0, e4, e3, e2, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
+        }
+    } else if constexpr (S == 2) {  // PD 2: planes k+2, k+1, k, k-1, k-2; windows wa / wb alternate
+        for (int k = k0; k < t.kend; k += 10) {
+            tbd_step<S, PD>(k, e2, e0, e4, e3, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 1, e3, e1, e0, e4, e4, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 2, e4, e2, e1, e0, e0, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 3, e0, e3, e2, e1, e1, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 4, e1, e4, e3, e2, e2, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 5, e2, e0, e4, e3, e3, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 6, e3, e1, e0, e4, e4, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 7, e4, e2, e1, e0, e0, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 8, e0, e3, e2, e1, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 9, e1, e4, e3, e2, e2, wb, t, tid, sd, ta, tab, l0, l1, xin);
+        }
+    } else {  // S 3, PD 2: planes k+2, k+1, k, k-1, k-2, k-3; windows wa / wb alternate
+        for (int k = k0; k < t.kend; k += 6) {
+            tbd_step<S, PD>(k, e2, e0, e5, e4, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 1, e3, e1, e0, e5, e4, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 2, e4, e2, e1, e0, e5, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 3, e5, e3, e2, e1, e0, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 4, e0, e4, e3, e2, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD>(k + 5, e1, e5, e4, e3, e2, wb, t, tid, sd, ta, tab, l0, l1, xin);
         }
     }
 }
@@ -1749,6 +1824,15 @@ void launch_tile(const pamg_mat& A, const TileSet& ts, const double* x, const do
                  double* y, double omega, hipStream_t s) {
     const int n = ts.n_short;
     if constexpr (TNNZ == 2048 || TNNZ == 4096) {
+        if (ts.tm && ts.xsr && TNNZ == 2048 && options().xsr_kernel == 1 && ts.pt && ts.cd == 8 && ts.tm_vt) {
+            XStage xs{};
+            xs.ncols = (int)A.ncols;
+            k_rows_tm<OP, 2048, 8, false, true, true, true><<<n, kBlock, 0, s>>>(
+                ts.d_short, nullptr, ts.d_tm_cidx, nullptr, nullptr, nullptr, ts.d_tm_rlen, ts.tm_rs, nullptr,
+                ts.ctab_n, x, b, y, omega, nullptr, xs, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt, ts.d_xpos,
+                ts.d_xmeta);
+            return;
+        }
         if (ts.tm && ts.xsr) {
             k_rows_xsr<OP, TNNZ><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_cidx, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt,
                                                      ts.d_tm_rlen, ts.tm_rs, ts.d_xpos, ts.ctab_n, ts.d_xmeta, x,
@@ -1853,12 +1937,19 @@ void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s) {
     const int ntiles = g.tiles_x * g.tiles_y * g.zchunks;
     const int grid = (ntiles + 7) / 8 * 8;
     if (sd.vd_n) {
-        if (ta.nstages == 2)
-            k_sym_tbd<2><<<grid, TbShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
-                                                              sd, ta);
+        const bool pd2 = options().tb_pd == 2;
+        if (ta.nstages == 2 && pd2)
+            k_sym_tbd<2, 2><<<grid, TbShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
+                                                                 sd, ta);
+        else if (ta.nstages == 2)
+            k_sym_tbd<2, 1><<<grid, TbShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
+                                                                 sd, ta);
+        else if (pd2)
+            k_sym_tbd<3, 2><<<grid, TbShape<3>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
+                                                                 sd, ta);
         else
-            k_sym_tbd<3><<<grid, TbShape<3>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
-                                                              sd, ta);
+            k_sym_tbd<3, 1><<<grid, TbShape<3>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
+                                                                 sd, ta);
         return;
     }
     if (ta.nstages == 2)

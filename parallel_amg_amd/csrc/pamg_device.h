@@ -40,9 +40,9 @@ struct XStage {
 // coalesced loads (staged element e of run c is x[r0 + omin_c + e - base_c]); per tile:
 // [ncl, zix, tot, omin_0 .. omin_{R-1}, base_0 .. base_{R-1}] in d_xmeta (kXsMeta ints) and each
 // dictionary entry's LDS position in d_xpos (uint16).
-constexpr int kXsrMaxRuns = 32;
+constexpr int kXsrMaxRuns = 40;
 constexpr int kXsMeta = 3 + 2 * kXsrMaxRuns;
-constexpr int kXsrCap2048 = 2048;   // staged doubles per tile (16 KiB), 2048-nonzero tiles
+constexpr int kXsrCap2048 = 2200;   // staged doubles per tile (17 KiB: 7 blocks per CU), 2048-nonzero tiles
 constexpr int kXsrCap4096 = 2560;   //                                  4096-nonzero tiles
 
 enum RowOp : int {
@@ -138,7 +138,9 @@ struct Options {
     int sym_rows = 2;          // rows per lane of its kernel (1 | 2)
     int jr_fuse = 1;           // 1: temporally blocked level-0 Jacobi -> residual / cross-cycle pipeline where the
                                //    operator is a grid stencil (k_sym_tb)
-    int x_stage_tiles = 1;     // 1: per-tile x staging with row lanes for per-tile dictionary sets (k_rows_xsr)
+    int tb_pd = 1;             // planes the row-class chain's loads run ahead (k_sym_tbd<S, PD>: 1 or 2)
+    int x_stage_tiles = 0;     // 1: per-tile x staging with row lanes for per-tile dictionary sets (k_rows_xsr)
+    int xsr_kernel = 0;        // staged sets: 0 row lanes (k_rows_xsr), 1 nonzero lanes (k_rows_tm, 2048-nonzero tiles)
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
 };

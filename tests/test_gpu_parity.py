@@ -443,8 +443,12 @@ def test_stream_bytes_layout(ctx, novd):
                 call("pamg_set_option", k.encode(), 0 if k == "value_dict" else 1)
 
     from parallel_amg_amd._lib import layout_of
-    # the symmetric diagonal-class layout: 1-B mask + diagonal + 3 upper values per row
+    # the symmetric diagonal-class layout with its row-class dictionary (default): a 1-B class id
+    # per row + 27 classes of (diagonal, 3 upper values, mask); without it: 1-B mask + diagonal +
+    # 3 upper values per row
     A, _h = upload(ctx, M)
+    assert layout_of(A)["sym"] and layout_of(A)["sym_vd"] and A.stream_bytes == n + 27 * (32 + 4) + 4
+    A, _h = _with_options({"sym_vd": 0}, lambda: upload(ctx, M))
     assert layout_of(A)["sym"] and A.stream_bytes == n * (1 + 8 + 24) + 4
     call("pamg_set_option", b"sym_dia", 0)
     try:
@@ -1231,12 +1235,13 @@ def level1_64(ctx):
     return O.CSR(M.rowptr.copy(), M.col.astype(np.int64), M.val.copy(), M.ncols)
 
 
-@pytest.mark.parametrize("tnnz", [2048, 4096])
-def test_row_lane_x_staging_bit_exact(ctx, level1_64, tnnz):
-    """k_rows_xsr (per-tile x staging, one row per lane; x_stage_tiles) on a coarse AMG operator
-    in tile-major slots with per-tile column and value dictionaries: SpMV, residual, Jacobi
-    (in-row diagonal by the tile's offset-0 entry) and the oracle's bits; the same upload without
-    the staging (k_rows_tm) gives the same bits."""
+@pytest.mark.parametrize("tnnz,xk", [(2048, 0), (4096, 0), (2048, 1)])
+def test_row_lane_x_staging_bit_exact(ctx, level1_64, tnnz, xk):
+    """Per-tile x staging (x_stage_tiles) on a coarse AMG operator in tile-major slots with
+    per-tile column and value dictionaries — row lanes (k_rows_xsr, xsr_kernel 0) or nonzero
+    lanes (k_rows_tm with the staged runs, xsr_kernel 1): SpMV, residual, Jacobi (in-row diagonal
+    by the tile's offset-0 entry) and the oracle's bits; the same upload without the staging
+    (k_rows_tm gathering x) gives the same bits."""
     from parallel_amg_amd._lib import layout_of
     M = level1_64
     rng = np.random.default_rng(tnnz)
@@ -1249,12 +1254,13 @@ def test_row_lane_x_staging_bit_exact(ctx, level1_64, tnnz):
         assert lay["tm"] and lay["per_tile"] and lay["cd"] == 8 and lay["tm_vd"], lay
         assert lay["xsr"] == bool(xst), lay
         x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
-        mul(y, A, x)
-        sp = y.own_values()
-        residual(y, A, x, b)
-        rs = y.own_values()
-        t = PVector(ctx, M.nrows)
-        jacobi(x, A, b, t, 0.61, 2)
+        with _with_option("xsr_kernel", xk):
+            mul(y, A, x)
+            sp = y.own_values()
+            residual(y, A, x, b)
+            rs = y.own_values()
+            t = PVector(ctx, M.nrows)
+            jacobi(x, A, b, t, 0.61, 2)
         outs.append((sp, rs, x.own_values()))
         del A
     assert np.array_equal(bits(outs[0][0]), bits(O.spmv(M, xh)))
@@ -1262,3 +1268,35 @@ def test_row_lane_x_staging_bit_exact(ctx, level1_64, tnnz):
     assert np.array_equal(bits(outs[0][2]), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.61), bh, 0.61)))
     for a, c in zip(outs[0], outs[1]):
         assert np.array_equal(bits(a), bits(c))
+
+
+@pytest.mark.parametrize("kind", ["poisson3d", "aniso3d"])
+def test_chain_two_planes_ahead_bit_exact(ctx, kind):
+    """tb_pd = 2 (k_sym_tbd<S, 2>: the chain's loads two planes ahead, two window register sets in
+    alternation): the fused pre-smoothing pass and pipelined cycles keep the oracle's bits."""
+    from parallel_amg_amd._lib import layout_of
+    from parallel_amg_amd.partitioned import jacobi_residual
+    be = pa.SequentialBackend(1)
+    n = 128
+    A, offs, xs = pa.generate_problem(be, kind, n)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=ctx)
+    S = AMGSolver(ctx, H)
+    assert layout_of(S.A[0])["sym_vd"]
+    b = PVector(ctx, S.A[0].nrows)
+    mul(b, S.A[0], PVector(ctx, S.A[0].nrows, 0, xs[0]))
+    Ao = O.generate(kind, n, n, n)
+    rng = np.random.default_rng(2)
+    xh, bh = rng.standard_normal(Ao.nrows), rng.standard_normal(Ao.nrows)
+    with _with_option("tb_pd", 2):
+        t, r = PVector(ctx, Ao.nrows), PVector(ctx, Ao.nrows)
+        assert jacobi_residual(t, r, S.A[0], PVector(ctx, Ao.nrows, 0, xh), PVector(ctx, Ao.nrows, 0, bh), 0.66)
+        S.set_graph(False)
+        S.set_graph(True)
+        x = S.new_vector()
+        S.vcycle(x, b, 5)
+    to = O.jacobi(Ao, xh, bh, 0.66)
+    assert np.array_equal(bits(t.own_values()), bits(to))
+    assert np.array_equal(bits(r.own_values()), bits(O.residual(Ao, to, bh)))
+    Ho = O.setup(Ao, max_coarse=1000)
+    xo = Ho.solve(O.spmv(Ao, O.xstar(Ao.nrows)), 5)
+    assert np.array_equal(bits(x.own_values()), bits(xo))

@@ -116,17 +116,17 @@ def test_blocked_pre_smoothing_512_bit_exact(ctx, h512):
 
 
 def test_level1_row_lane_staging_512_bit_exact(ctx, h512):
-    """The 512^3 level-1 operator (16.8M rows, 517M nonzeros) runs k_rows_xsr in the bench; its
-    residual and Jacobi give the bits of the same operator uploaded without the staging
-    (k_rows_tm, oracle-pinned at smaller sizes)."""
+    """The 512^3 level-1 operator (16.8M rows, 517M nonzeros) with per-tile x staging and row
+    lanes (k_rows_xsr, x_stage_tiles; off by default: measured slower): its residual
+    and Jacobi give the bits of the bench's layout (k_rows_tm, oracle-pinned at smaller sizes)."""
     S, _b = h512
     A1 = S.A_dev[1]
-    assert layout_of(A1)["xsr"], layout_of(A1)
+    assert not layout_of(A1)["xsr"], layout_of(A1)
     lp = S._H.levels[1][0]
-    with option("x_stage_tiles", 0):
+    with option("x_stage_tiles", 1):
         from parallel_amg_amd.partitioned import PSparseMatrix
         B1 = PSparseMatrix(ctx, lp.A, lp.planA)
-    assert not layout_of(B1)["xsr"]
+    assert layout_of(B1)["xsr"]
     from parallel_amg_amd.partitioned import jacobi, residual
     n = A1.nrows
     rng = np.random.default_rng(5)

@@ -62,10 +62,16 @@ def main():
     ap.add_argument("--ops", default="0,2")
     ap.add_argument("--mats", default=None, help="comma list of level matrices to run (e.g. R0,A1); default all")
     ap.add_argument("--ab", default=None,
-                    help="launch-time option to A/B on the same upload (e.g. stream_nt): runs 0,1,0,1")
+                    help="launch-time option to A/B on the same upload: KEY (values 0,1,0,1) or KEY=a,b "
+                         "(a,b,a,b; e.g. tb_pd=1,2)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="extra pamg_set_option before the uploads (e.g. band_pct=50)")
     args = ap.parse_args()
+    ab_vals = (0, 1, 0, 1)
+    if args.ab and "=" in args.ab:
+        args.ab, vs = args.ab.split("=")
+        a_, b_ = (int(v) for v in vs.split(","))
+        ab_vals = (a_, b_, a_, b_)
     for kv in args.set:
         k, v = kv.split("=")
         set_opts(**{k: int(v)})
@@ -102,7 +108,7 @@ def main():
                     continue
                 if op == 3 and not name.startswith("P"):
                     continue
-                for abv in ((0, 1, 0, 1) if args.ab else (None,)):
+                for abv in (ab_vals if args.ab else (None,)):
                     if abv is not None:
                         set_opts(**{args.ab: abv})
                     ms, byt, fbyt = bench(ctx, D, op, args.reps)
@@ -114,7 +120,7 @@ def main():
                         rec[args.ab] = abv
                     print(json.dumps(rec), flush=True)
                 if args.ab:
-                    set_opts(**{args.ab: 0})
+                    set_opts(**{args.ab: ab_vals[0]})
             del D
 
 
