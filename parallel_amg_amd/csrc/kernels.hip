@@ -981,82 +981,104 @@ __device__ __forceinline__ uint32_t tid_at(const uint8_t* __restrict__ tid, int6
     return tid[j >= 0 && j < n ? j : 0];
 }
 
-template <int OP, int NU>
+// CH (Options::symd_chunks): a block takes CH consecutive 512-row units of its XCD's eighths
+// (unit u = (blockIdx / 8) CH + k, the banded order of k_rows_sym2 otherwise unchanged), so the
+// class table is filled and waited for once per CH units; the units' loads go out two at a time.
+template <int OP, int NU, int CH = 1>
 __global__ __launch_bounds__(kBlock) void k_rows_symd(
     int nrows, int ncols, const uint8_t* __restrict__ tid, const double* __restrict__ vtab,
     const uint32_t* __restrict__ mtab, int nv, const SymDia sd, const double* __restrict__ x,
     const double* __restrict__ b, double* __restrict__ y, double omega) {
-    constexpr int RB = 2 * kBlock;  // rows per block
+    constexpr int RB = 2 * kBlock;  // rows per unit
+    constexpr int P = CH < 2 ? CH : 2;
+    static_assert(CH % P == 0, "units in pairs");
     __shared__ SymTab<NU> tab;
     const int bid = blockIdx.x, tidx = threadIdx.x;
-    const int xcd = bid & 7, j = bid >> 3;
-    const int plane = sd.plane0 + j / sd.eighth, blk = xcd * sd.eighth + j % sd.eighth;
-    const int64_t lo = (int64_t)plane * sd.band;
-    const int64_t i0 = lo + (int64_t)blk * RB + 2 * tidx;
-    const int64_t hi = lo + sd.band < nrows ? lo + sd.band : nrows;
-    const bool blk_ok = blk < sd.band_blocks;
-    const bool in0 = blk_ok && i0 < hi, in1 = blk_ok && i0 + 1 < hi;
+    const int xcd = bid & 7, u0 = (bid >> 3) * CH;
+    const int nunits = sd.nbands * sd.eighth;
     const int64_t n = nrows;
-    const int64_t ib = in0 ? i0 : 0;  // even
-    // every global load first (ids, mirror ids, x, b), then the table, one barrier
-    const uint32_t tw = *reinterpret_cast<const uint16_t*>(tid + ib);
-    uint32_t tl[2][NU];
-    double xv[2][2 * NU + 1];
+#pragma unroll 1
+    for (int k0 = 0; k0 < CH; k0 += P) {
+        int64_t ib[P];
+        bool in0[P], in1[P];
+        uint32_t tw[P], tl[P][2][NU];
+        double xv[P][2][2 * NU + 1], pbv[P][2];
 #pragma unroll
-    for (int c = 0; c < NU; ++c) {
-        const int o = sd.off[NU - 1 - c];
-        tl[0][c] = tid_at(tid, ib - o, n);
-        tl[1][c] = tid_at(tid, ib + 1 - o, n);
-        const double2 xx = ld_pair(x, ib - o, ncols, (o & 1) == 0);
-        xv[0][c] = xx.x;
-        xv[1][c] = xx.y;
-    }
-    {
-        const double2 xx = ld_pair(x, ib, ncols, true);
-        xv[0][NU] = xx.x;
-        xv[1][NU] = xx.y;
-    }
+        for (int q = 0; q < P; ++q) {
+            const int u = u0 + k0 + q;
+            const int plane = sd.plane0 + u / sd.eighth, blk = xcd * sd.eighth + u % sd.eighth;
+            const int64_t lo = (int64_t)plane * sd.band;
+            const int64_t i0 = lo + (int64_t)blk * RB + 2 * tidx;
+            const int64_t hi = lo + sd.band < nrows ? lo + sd.band : nrows;
+            const bool ok = u < nunits && blk < sd.band_blocks;
+            in0[q] = ok && i0 < hi;
+            in1[q] = ok && i0 + 1 < hi;
+            ib[q] = in0[q] ? i0 : 0;  // even
+            // every global load first (ids, mirror ids, x, b), then the table, one barrier
+            tw[q] = *reinterpret_cast<const uint16_t*>(tid + ib[q]);
 #pragma unroll
-    for (int c = 0; c < NU; ++c) {
-        const int o = sd.off[c];
-        const double2 xx = ld_pair(x, ib + o, ncols, (o & 1) == 0);
-        xv[0][NU + 1 + c] = xx.x;
-        xv[1][NU + 1 + c] = xx.y;
-    }
-    double2 pb = make_double2(0.0, 0.0);
-    if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = ld_pair(b, ib, n, true);
-    const double pbv[2] = {pb.x, pb.y};
-    symtab_fill<NU>(tab, vtab, mtab, nv);
-    __syncthreads();
+            for (int c = 0; c < NU; ++c) {
+                const int o = sd.off[NU - 1 - c];
+                tl[q][0][c] = tid_at(tid, ib[q] - o, n);
+                tl[q][1][c] = tid_at(tid, ib[q] + 1 - o, n);
+                const double2 xx = ld_pair(x, ib[q] - o, ncols, (o & 1) == 0);
+                xv[q][0][c] = xx.x;
+                xv[q][1][c] = xx.y;
+            }
+            {
+                const double2 xx = ld_pair(x, ib[q], ncols, true);
+                xv[q][0][NU] = xx.x;
+                xv[q][1][NU] = xx.y;
+            }
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const uint32_t t = r == 0 ? (tw & 0xffu) : (tw >> 8);
-        const uint32_t m = tab.m[t];
-        double v[2 * NU + 1];
-#pragma unroll
-        for (int c = 0; c < NU; ++c) v[c] = tab.v[tl[r][c]][1 + (NU - 1 - c)];
-        v[NU] = tab.v[t][0];
-#pragma unroll
-        for (int c = 0; c < NU; ++c) v[NU + 1 + c] = tab.v[t][1 + c];
-        double s = 0.0;
-#pragma unroll
-        for (int k = 0; k < 2 * NU + 1; ++k) {
-            const double p = v[k] * xv[r][k];
-            const double u = s + p;
-            s = ((m >> k) & 1u) ? u : s;
+            for (int c = 0; c < NU; ++c) {
+                const int o = sd.off[c];
+                const double2 xx = ld_pair(x, ib[q] + o, ncols, (o & 1) == 0);
+                xv[q][0][NU + 1 + c] = xx.x;
+                xv[q][1][NU + 1 + c] = xx.y;
+            }
+            double2 pb = make_double2(0.0, 0.0);
+            if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = ld_pair(b, ib[q], n, true);
+            pbv[q][0] = pb.x;
+            pbv[q][1] = pb.y;
         }
-        double out;
-        if constexpr (OP == OP_SPMV) {
-            out = s;
-        } else if constexpr (OP == OP_RESID) {
-            out = pbv[r] - s;
-        } else {
-            const double u = pbv[r] - s;
-            const double w = omega * u;
-            const double q = w / v[NU];
-            out = xv[r][NU] + q;
+        if (k0 == 0) {  // (uniform)
+            symtab_fill<NU>(tab, vtab, mtab, nv);
+            __syncthreads();
         }
-        if ((r == 0 ? in0 : in1) && (m & SymMask<NU>::kIn)) y[ib + r] = out;
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const uint32_t t = r == 0 ? (tw[q] & 0xffu) : (tw[q] >> 8);
+                const uint32_t m = tab.m[t];
+                double v[2 * NU + 1];
+#pragma unroll
+                for (int c = 0; c < NU; ++c) v[c] = tab.v[tl[q][r][c]][1 + (NU - 1 - c)];
+                v[NU] = tab.v[t][0];
+#pragma unroll
+                for (int c = 0; c < NU; ++c) v[NU + 1 + c] = tab.v[t][1 + c];
+                double s = 0.0;
+#pragma unroll
+                for (int k = 0; k < 2 * NU + 1; ++k) {
+                    const double p = v[k] * xv[q][r][k];
+                    const double w = s + p;
+                    s = ((m >> k) & 1u) ? w : s;
+                }
+                double out;
+                if constexpr (OP == OP_SPMV) {
+                    out = s;
+                } else if constexpr (OP == OP_RESID) {
+                    out = pbv[q][r] - s;
+                } else {
+                    const double w0 = pbv[q][r] - s;
+                    const double w = omega * w0;
+                    const double w2 = w / v[NU];
+                    out = xv[q][r][NU] + w2;
+                }
+                if ((r == 0 ? in0[q] : in1[q]) && (m & SymMask<NU>::kIn)) y[ib[q] + r] = out;
+            }
+        }
     }
 }
 
@@ -1875,6 +1897,20 @@ void launch_sym_nu(const pamg_mat& A, const double* x, const double* b, double* 
     const SymDia& sd = A.sym;
     const int grid = sd.nbands * 8 * sd.eighth;
     if (sd.vd_n) {  // (the upload builds the dictionary only with two rows per lane)
+        const int ch = NU <= 3 ? options().symd_chunks : 1;
+        const int g = 8 * ((sd.nbands * sd.eighth + ch - 1) / ch);
+        if constexpr (NU <= 3) {
+            if (ch == 2) {
+                k_rows_symd<OP, NU, 2><<<g, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab,
+                                                            sd.d_mtab, sd.vd_n, sd, x, b, y, omega);
+                return;
+            }
+            if (ch == 4) {
+                k_rows_symd<OP, NU, 4><<<g, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab,
+                                                            sd.d_mtab, sd.vd_n, sd, x, b, y, omega);
+                return;
+            }
+        }
         k_rows_symd<OP, NU><<<grid, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab,
                                                   sd.vd_n, sd, x, b, y, omega);
         return;

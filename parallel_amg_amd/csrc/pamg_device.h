@@ -140,6 +140,7 @@ struct Options {
                                //    operator is a grid stencil (k_sym_tb)
     int tb_pd = 1;             // planes the row-class chain's loads run ahead (k_sym_tbd<S, PD>: 1 or 2)
     int x_stage_tiles = 0;     // 1: per-tile x staging with row lanes for per-tile dictionary sets (k_rows_xsr)
+    int symd_chunks = 1;       // 512-row units per block of k_rows_symd (1, 2 or 4)
     int xsr_kernel = 0;        // staged sets: 0 row lanes (k_rows_xsr), 1 nonzero lanes (k_rows_tm, 2048-nonzero tiles)
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)

@@ -954,6 +954,32 @@ def test_sym_dia_bit_exact(ctx, kind, n, seed, order, rows, vd):
     assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.57), bh, 0.57)))
 
 
+@pytest.mark.parametrize("kind,n", [("poisson3d", 40), ("poisson2d", 80), ("aniso3d", 20), ("poisson3d", 7),
+                                    ("poisson3d", 33)])
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("ch", [2, 4])
+def test_symd_units_per_block_bit_exact(ctx, kind, n, order, ch):
+    """k_rows_symd with CH 512-row units per block (symd_chunks; a unit count that CH does not
+    divide leaves the last block's tail units idle): SpMV, residual, Jacobi bit-exact with the
+    oracle."""
+    from parallel_amg_amd._lib import layout_of
+    M = _sym_grid(kind, n)
+    with _with_option("tile_order", order), _with_option("sym_rows", 2), _with_option("sym_vd", 1):
+        A, _h = upload(ctx, M)
+    assert layout_of(A)["sym_vd"], layout_of(A)
+    rng = np.random.default_rng(n + ch)
+    xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
+    x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
+    with _with_option("symd_chunks", ch):
+        mul(y, A, x)
+        assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
+        residual(y, A, x, b)
+        assert np.array_equal(bits(y.own_values()), bits(O.residual(M, xh, bh)))
+        t = PVector(ctx, M.nrows)
+        jacobi(x, A, b, t, 0.57, 2)
+    assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.57), bh, 0.57)))
+
+
 @pytest.mark.parametrize("breaker", ["asym_value", "signed_zero", "unsorted_row", "diagonal_only"])
 def test_sym_dia_declines_what_it_cannot_reproduce(ctx, breaker):
     """A mirror that differs in one bit (or +0.0 against -0.0), a row whose storage order is
@@ -999,21 +1025,24 @@ def _row_classes(M):
     return len(keys)
 
 
-@pytest.mark.parametrize("npal", [1, 7, 8])
+@pytest.mark.parametrize("npal", [1, 12, 13])
 def test_sym_row_class_dictionary_limit(ctx, npal):
-    """The row-class dictionary holds <= 64 tuples: 2D Poisson (9 boundary cases) whose diagonal
-    takes npal values gives 9 npal classes — 9, 63 (dictionary) and 72 (f64 arrays) — and both
-    layouts are bit-exact with the oracle (SpMV, residual, two Jacobi sweeps)."""
+    """The row-class dictionary holds <= 64 tuples: 2D Poisson on a 30 x 30 grid (9 boundary
+    cases: interior, 4 edges, 4 single-row corners) whose diagonal at grid point (r, c) is
+    palette entry (r + c) % npal gives 5 npal + 4 classes — 9, 64 (dictionary, at the limit) and
+    69 (f64 arrays) — and both layouts are bit-exact with the oracle (SpMV, residual, two Jacobi
+    sweeps)."""
     from parallel_amg_amd._lib import layout_of
     M = _sym_grid("poisson2d", 30)
     val = M.val.copy()
     rows = np.repeat(np.arange(M.nrows), np.diff(M.rowptr))
     dg = M.col == rows
     pal = 4.0 + np.arange(npal) / 8.0
-    val[dg] = pal[(np.arange(M.nrows) * 7) % npal]
+    i = np.arange(M.nrows)
+    val[dg] = pal[(i // 30 + i % 30) % npal]
     M = O.CSR(M.rowptr.copy(), M.col.copy(), val, M.ncols)
     ncl = _row_classes(M)
-    assert ncl == 9 * npal
+    assert ncl == 5 * npal + 4
     A, _h = upload(ctx, M)
     lay = layout_of(A)
     assert lay["sym"] and lay["sym_vd"] == (ncl <= 64), (ncl, lay)
@@ -1225,25 +1254,28 @@ def test_pipelined_cycles_bit_exact(ctx, kind, vd):
 
 
 @pytest.fixture(scope="module")
-def level1_64(ctx):
-    """The level-1 operator of the 64^3 Poisson hierarchy (the 512^3 A1's kind: ~31 nonzeros per
-    row, offsets scattered over the coarse numbering, a few hundred distinct values)."""
+def level1_128(ctx):
+    """The level-1 operator of the 128^3 Poisson hierarchy (the 512^3 A1's kind: ~30 nonzeros per
+    row, <= 73 distinct row-relative offsets per 2048-nonzero tile, a few hundred distinct values;
+    64^3's level 1 is too irregular for per-tile 8-bit tables: up to 486 offsets per tile)."""
     be = pa.SequentialBackend(1)
-    A, offs, xs = pa.generate_problem(be, "poisson3d", 64)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 128)
     H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=ctx)
     M = H.levels[1][0].A
     return O.CSR(M.rowptr.copy(), M.col.astype(np.int64), M.val.copy(), M.ncols)
 
 
-@pytest.mark.parametrize("tnnz,xk", [(2048, 0), (4096, 0), (2048, 1)])
-def test_row_lane_x_staging_bit_exact(ctx, level1_64, tnnz, xk):
+# (4096-nonzero tiles of this operator exceed the staging caps — kXsrCap4096 staged values — and
+# keep the gathering kernel; the 512^3 A1 runs 2048-nonzero tiles)
+@pytest.mark.parametrize("tnnz,xk", [(2048, 0), (2048, 1)])
+def test_row_lane_x_staging_bit_exact(ctx, level1_128, tnnz, xk):
     """Per-tile x staging (x_stage_tiles) on a coarse AMG operator in tile-major slots with
     per-tile column and value dictionaries — row lanes (k_rows_xsr, xsr_kernel 0) or nonzero
     lanes (k_rows_tm with the staged runs, xsr_kernel 1): SpMV, residual, Jacobi (in-row diagonal
     by the tile's offset-0 entry) and the oracle's bits; the same upload without the staging
     (k_rows_tm gathering x) gives the same bits."""
     from parallel_amg_amd._lib import layout_of
-    M = level1_64
+    M = level1_128
     rng = np.random.default_rng(tnnz)
     xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
     outs = []
