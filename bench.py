@@ -295,7 +295,7 @@ def main():
         post_fbytes = float(S.rowsum_bytes(A0, 3))
         achieved = post_bytes / (post_ms * 1e-3) / 1e9
     elif lay.get("sym"):
-        kname = f"k_rows_sym{'d' if lay.get('sym_vd') else '2' if lay['sym_rows'] == 2 else ''}<2, {lay['cd_offsets']}>"
+        kname = _sym_kname(2, lay)
     elif tm:
         kname = (f"k_rows_tm<2, {tn}, {cd}, {tf(lay['anchored'])}, {tf(lay['x_stage'])}, "
                  f"{tf(lay['per_tile'])}>")
@@ -307,9 +307,7 @@ def main():
                  f"0, false, false>")
     workload_key = f"{args.matrix or args.kind}:{args.grid}:p{world}:perm{args.permute}" + (":rcm" if args.rcm else "")
     src = kernel_source_sha()
-    spmv_kname = (f"k_rows_sym{'d' if lay.get('sym_vd') else '2' if lay['sym_rows'] == 2 else ''}<0, {lay['cd_offsets']}>"
-                  if pipelined
-                  else kname.replace("<2,", "<0,", 1))
+    spmv_kname = _sym_kname(0, lay) if lay.get("sym") else kname.replace("<2,", "<0,", 1)
     traffic = spmv_traffic = None
     if live_pmc and pipelined:  # this run's own counters (the child ran op 5 = k_sym_tb<3>, op 0 = SpMV)
         traffic = live_pmc.get(kname)
@@ -456,12 +454,25 @@ def exchange_times(ctx, S, be, nu1, nu2, reps=20) -> dict:
                     "inside levels[rep-1].restrict"}
 
 
-def _tb_pd() -> int:
-    """The row-class chain's prefetch depth (libpamg option tb_pd, a template argument of k_sym_tbd)."""
+def _option(key: str) -> int:
     from parallel_amg_amd import _lib
     v = ctypes.c_int64()
-    _lib.call("pamg_get_option", b"tb_pd", ctypes.byref(v))
+    _lib.call("pamg_get_option", key.encode(), ctypes.byref(v))
     return int(v.value)
+
+
+def _tb_pd() -> int:
+    """The row-class chain's prefetch depth (libpamg option tb_pd, a template argument of k_sym_tbd)."""
+    return _option("tb_pd")
+
+
+def _sym_kname(op: int, lay: dict) -> str:
+    """The symmetric-layout row kernel's instance name as rocprofv3 demangles it: k_rows_symd<OP,
+    NU, CH> (row-class dictionary; CH = symd_chunks for NU <= 3), k_rows_sym2 / k_rows_sym<OP, NU>."""
+    nu = lay["cd_offsets"]
+    if lay.get("sym_vd"):
+        return f"k_rows_symd<{op}, {nu}, {_option('symd_chunks') if nu <= 3 else 1}>"
+    return f"k_rows_sym{'2' if lay['sym_rows'] == 2 else ''}<{op}, {nu}>"
 
 
 def kernel_source_sha() -> str:

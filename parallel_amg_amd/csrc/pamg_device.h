@@ -138,9 +138,11 @@ struct Options {
     int sym_rows = 2;          // rows per lane of its kernel (1 | 2)
     int jr_fuse = 1;           // 1: temporally blocked level-0 Jacobi -> residual / cross-cycle pipeline where the
                                //    operator is a grid stencil (k_sym_tb)
-    int tb_pd = 1;             // planes the row-class chain's loads run ahead (k_sym_tbd<S, PD>: 1 or 2)
+    int tb_pd = 2;             // planes the row-class chain's loads run ahead (k_sym_tbd<S, PD>: 1 or 2;
+                               // 2: -0.5 % chain time, same-box A/B profiles/r04_g_pd/)
     int x_stage_tiles = 0;     // 1: per-tile x staging with row lanes for per-tile dictionary sets (k_rows_xsr)
-    int symd_chunks = 1;       // 512-row units per block of k_rows_symd (1, 2 or 4)
+    int symd_chunks = 2;       // 512-row units per block of k_rows_symd (1, 2 or 4; 2: SpMV -2 %, residual and
+                               // Jacobi -4..-5 %, 4: -1..-2 %; same-box A/B profiles/r04_g_c2/, r04_g_c4/)
     int xsr_kernel = 0;        // staged sets: 0 row lanes (k_rows_xsr), 1 nonzero lanes (k_rows_tm, 2048-nonzero tiles)
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)

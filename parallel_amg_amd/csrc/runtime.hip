@@ -2071,15 +2071,29 @@ int pamg_world_dot(pamg_world* w, pamg_vec* const* x, pamg_vec* const* y, double
 int pamg_world_vcycle(pamg_world* w, pamg_hier* const* H, pamg_vec* const* x, pamg_vec* const* b, int ncycles,
                       double* res_hist) {
     if (!H || !x || !b || !w) return fail(PAMG_E_ARG, "world_vcycle: bad args");
-    return world_each(w, [&](int r) { return pamg_vcycle(w->ctx[r], H[r], x[r], b[r], ncycles, r == 0 ? res_hist : nullptr); });
+    // every rank takes the same schedule: with a history each computes the norms (an all-reduce
+    // per cycle), so each gets a buffer of its own and rank 0's is returned
+    if (ncycles < 0) return fail(PAMG_E_ARG, "world_vcycle: ncycles < 0");
+    std::vector<std::vector<double>> hist(w->n, std::vector<double>(res_hist ? (size_t)ncycles : 0));
+    CHECK(world_each(w, [&](int r) {
+        return pamg_vcycle(w->ctx[r], H[r], x[r], b[r], ncycles, res_hist ? hist[r].data() : nullptr);
+    }));
+    if (res_hist) std::copy(hist[0].begin(), hist[0].end(), res_hist);
+    return PAMG_OK;
 }
 
 int pamg_world_pcg(pamg_world* w, pamg_hier* const* H, pamg_vec* const* x, pamg_vec* const* b, double rtol,
                    int maxit, int* iters, double* res_hist) {
     if (!H || !x || !b || !w) return fail(PAMG_E_ARG, "world_pcg: bad args");
-    return world_each(w, [&](int r) {
-        return pamg_pcg(w->ctx[r], H[r], x[r], b[r], rtol, maxit, r == 0 ? iters : nullptr, r == 0 ? res_hist : nullptr);
-    });
+    if (maxit < 0) return fail(PAMG_E_ARG, "world_pcg: maxit < 0");
+    std::vector<std::vector<double>> hist(w->n, std::vector<double>(res_hist ? (size_t)maxit + 1 : 0));
+    std::vector<int> it(w->n, 0);
+    CHECK(world_each(w, [&](int r) {
+        return pamg_pcg(w->ctx[r], H[r], x[r], b[r], rtol, maxit, &it[r], res_hist ? hist[r].data() : nullptr);
+    }));
+    if (iters) *iters = it[0];
+    if (res_hist) std::copy(hist[0].begin(), hist[0].end(), res_hist);
+    return PAMG_OK;
 }
 
 int pamg_comm_rank(const pamg_ctx* ctx, int* rank, int* nranks) {

@@ -79,6 +79,12 @@ def test_local_world_vcycle_bit_exact(built, nparts, kind, n, max_coarse, agglom
             call("pamg_world_vcycle", W._h, arr(S), arr(xw), arr(b), ncycles, hw.ctypes.data_as(ctypes.c_void_p))
             same_world = [np.array_equal(bits(xw[p].own_values()), bits(x[p].own_values())) for p in range(nparts)]
             assert all(same_world) and np.array_equal(hw, hist[0]), same_world
+            xq = [s.new_vector() for s in S]
+            itw, hq = ctypes.c_int(), np.zeros(61)
+            call("pamg_world_pcg", W._h, arr(S), arr(xq), arr(b), 1e-8, 60, ctypes.byref(itw),
+                 hq.ctypes.data_as(ctypes.c_void_p))
+            assert itw.value == pcg[0][0]
+            assert np.array_equal(hq[:itw.value + 1], np.asarray(pcg[0][1])[:itw.value + 1])
             fused = [layout_of(a)["jr_fused"] for a in A0]
             got_b = np.concatenate([bb.own_values() for bb in b])
             got_x = np.concatenate([xx.own_values() for xx in x])

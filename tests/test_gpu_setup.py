@@ -82,6 +82,20 @@ def test_dev_spgemm_ghost_rows(ctx):
                                                                Yg.val[:Yg.rowptr[10]], 4000), device=ctx)
 
 
+def test_dev_spgemm_overflow_repeated(ctx):
+    """The overflow path's host-side row offsets are copied asynchronously: the source must live
+    until the copy ran (it once went out of scope first, and a later allocation overwrote it).
+    Repeated products with host allocations in between keep the bits."""
+    rng = np.random.default_rng(11)
+    for k in range(12):
+        Y = rand_csr(rng, [50] * 400, 100_000)
+        X = rand_csr(rng, [300 + 7 * k] * (3 + k % 4) + [2] * 50, 400)
+        junk = [np.full(1 << 16, -1.0) for _ in range(8)]  # churn the host heap
+        got = HC.spgemm(X, 0, Y, device=ctx)
+        del junk
+        same(got, HC.spgemm(X, 0, Y))
+
+
 @pytest.mark.parametrize("rng_cols", [(0, 700), (100, 350), (0, 0), (650, 700)])
 def test_dev_transpose_bit_exact(ctx, rng_cols):
     rng = np.random.default_rng(9)
@@ -92,7 +106,12 @@ def test_dev_transpose_bit_exact(ctx, rng_cols):
 
 @pytest.mark.parametrize("kind,n,nparts,max_coarse", [("poisson3d", 24, 1, 100), ("aniso3d", 20, 1, 300),
                                                       ("elastic3d", 9, 1, 100), ("poisson3d", 16, 3, 60),
-                                                      ("poisson2d", 64, 2, 100)])
+                                                      ("poisson2d", 64, 2, 100),
+                                                      # the 8-part layout whose replicated
+                                                      # tail once lost its diagonal (an async copy
+                                                      # from a freed host vector in the overflow
+                                                      # path of pamg_dev_spgemm)
+                                                      ("poisson3d", 32, 8, 60)])
 def test_device_setup_matches_oracle(ctx, kind, n, nparts, max_coarse):
     be = pa.SequentialBackend(nparts)
     A, offs, _ = pa.generate_problem(be, kind, n)
