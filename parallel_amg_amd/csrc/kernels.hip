@@ -1590,6 +1590,141 @@ __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tbd(int nrows, cons
     }
 }
 
+// ---- k_sym_tbs<OP,PD>: ONE sweep (SpMV, residual or Jacobi) of the row-class dictionary operator
+// streamed plane by plane like k_sym_tbd (Options::sym_stream; one part, tb_ok): a 576-thread
+// workgroup owns a 64 x 16 column of the grid over a z-chunk, keeps the x window of planes
+// k-1 .. k+1 (tile + 1 line / 2 points around it) in a 4-slot LDS ring — so one barrier per plane —
+// and reads the 7 neighbour values of a row pair from LDS instead of 7 global loads. The loads of
+// plane k+PD's class ids and b and of plane k+1+PD's window are issued before the barrier of plane
+// k and consumed PD steps later. Every value is k_rows_symd's expression (same classes, same
+// order: SPEC §S3 bits). No halo recompute: the window's extra lines are L2 hits of the
+// neighbour tiles' lines.
+struct TbsRow {
+    uint16_t own;  // as TbdRow (narrow until use)
+    uint8_t m0;
+    uint16_t m1;
+    double b[2];
+};
+
+template <bool NEEDB>
+__device__ __forceinline__ void tbs_load(TbsRow& c, const uint8_t* __restrict__ tid, const double* __restrict__ b,
+                                         const SymDia& sd, int64_t i, int64_t n) {
+    c.own = *reinterpret_cast<const uint16_t*>(tid + i);
+    c.m0 = tid[i >= 1 ? i - 1 : 0];
+    c.m1 = tbd_pair_ids(tid, i - sd.off[1], n);
+    if constexpr (NEEDB) {
+        const double2 bb = *reinterpret_cast<const double2*>(b + i);
+        c.b[0] = bb.x;
+        c.b[1] = bb.y;
+    }
+}
+
+template <int OP, int PD>
+__device__ __forceinline__ void tbs_step(int k, TbsRow& En, const TbsRow& E0, const TbsRow& E1, TbWin<1>& win,
+                                         const TbCtx<1>& t, const uint8_t* __restrict__ tid, const SymDia& sd,
+                                         const SymTab<3>& tab, const double* __restrict__ x,
+                                         const double* __restrict__ b, double* __restrict__ y, double omega,
+                                         double (*xin)[TbShape<1>::XL][kTbLW]) {
+    using Sh = TbShape<1>;
+    if (k >= t.ze) return;  // uniform: the whole workgroup
+    tb_win_store<1>(win, xin, (k + 1) & 3);  // loaded PD steps ago
+    tb_win_load<1>(win, t, x, k + 1 + PD);
+    {
+        const int p = k + PD;
+        const bool ok = t.pos_ok && p < t.nz;
+        tbs_load<OP != OP_SPMV>(En, tid, b, sd, ok ? (int64_t)p * t.M + t.ixy : 0, t.n);
+    }
+    __syncthreads();  // xin (planes k-1 .. k+1); the slot stored next step was last read a step ago
+    if (t.own_xy) {
+        double xv[2][7];
+        tb_gather_lds<Sh::XL>(xin, (k - 1) & 3, k & 3, (k + 1) & 3, t.ry + 1, t.col, xv);
+        const uint32_t m2 = E1.own;  // the pair's ids one plane down: their U_2 are the -M values
+        const uint32_t t0 = E0.own & 0xffu, t1 = (E0.own >> 8) & 0xffu;
+        const uint32_t tr[2] = {t0, t1}, l0[2] = {E0.m0 & 0xffu, t0};
+        const uint32_t l1[2] = {E0.m1 & 0xffu, (E0.m1 >> 8) & 0xffu}, l2[2] = {m2 & 0xffu, (m2 >> 8) & 0xffu};
+        double o[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const uint32_t tc = tr[r];
+            const uint32_t m = tab.m[tc];
+            double v[7];
+            v[0] = tab.v[l2[r]][3];
+            v[1] = tab.v[l1[r]][2];
+            v[2] = tab.v[l0[r]][1];
+            v[3] = tab.v[tc][0];
+            v[4] = tab.v[tc][1];
+            v[5] = tab.v[tc][2];
+            v[6] = tab.v[tc][3];
+            double s = 0.0;
+#pragma unroll
+            for (int q = 0; q < 7; ++q) {
+                const double pr = v[q] * xv[r][q];
+                const double u = s + pr;
+                s = ((m >> q) & 1u) ? u : s;
+            }
+            if constexpr (OP == OP_SPMV) {
+                o[r] = s;
+            } else if constexpr (OP == OP_RESID) {
+                o[r] = E0.b[r] - s;
+            } else {
+                const double u = E0.b[r] - s;
+                const double w = omega * u;
+                const double q = w / v[3];
+                o[r] = xv[r][3] + q;
+            }
+        }
+        *reinterpret_cast<double2*>(y + (int64_t)k * t.M + t.ixy) = make_double2(o[0], o[1]);
+    }
+}
+
+template <int OP, int PD>
+__global__ __launch_bounds__(TbShape<1>::threads) void k_sym_tbs(int nrows, const uint8_t* __restrict__ tid,
+                                                                 const double* __restrict__ vtab,
+                                                                 const uint32_t* __restrict__ mtab, int nv,
+                                                                 const SymDia sd, const TbGeom g,
+                                                                 const double* __restrict__ x,
+                                                                 const double* __restrict__ b, double* __restrict__ y,
+                                                                 double omega) {
+    static_assert(PD == 1 || PD == 2, "one or two planes ahead");
+    __shared__ __attribute__((aligned(16))) double xin[4][TbShape<1>::XL][kTbLW];
+    __shared__ __attribute__((aligned(16))) SymTab<3> tab;
+    TbCtx<1> t;
+    if (!tb_ctx_init<1>(t, g, nrows)) return;  // the whole workgroup, before any barrier
+    symtab_fill<3>(tab, vtab, mtab, nv);       // (read after the first step's barrier)
+    const int k0 = t.zs;
+    TbWin<1> wa, wb;
+#pragma unroll
+    for (int q = -1; q <= 0; ++q) {
+        tb_win_load<1>(wa, t, x, k0 + q);
+        tb_win_store<1>(wa, xin, (k0 + q) & 3);
+    }
+    tb_win_load<1>(wa, t, x, k0 + 1);
+    if constexpr (PD == 2) tb_win_load<1>(wb, t, x, k0 + 2);
+    // the id ring: planes k+PD .. k-1
+    TbsRow e0{}, e1{}, e2{}, e3{};
+    auto load = [&](TbsRow& e, int p) {
+        const bool ok = t.pos_ok && p >= 0 && p < t.nz;
+        tbs_load<OP != OP_SPMV>(e, tid, b, sd, ok ? (int64_t)p * t.M + t.ixy : 0, t.n);
+    };
+    load(PD == 1 ? e2 : e3, k0 - 1);
+    load(e0, k0);
+    if constexpr (PD == 2) load(e1, k0 + 1);
+    if constexpr (PD == 1) {  // planes k+1, k, k-1
+        for (int k = k0; k < t.ze; k += 3) {
+            tbs_step<OP, PD>(k, e1, e0, e2, wa, t, tid, sd, tab, x, b, y, omega, xin);
+            tbs_step<OP, PD>(k + 1, e2, e1, e0, wa, t, tid, sd, tab, x, b, y, omega, xin);
+            tbs_step<OP, PD>(k + 2, e0, e2, e1, wa, t, tid, sd, tab, x, b, y, omega, xin);
+        }
+    } else {  // planes k+2, k+1, k, k-1; windows wa / wb alternate
+        for (int k = k0; k < t.ze; k += 4) {
+            tbs_step<OP, PD>(k, e2, e0, e3, wa, t, tid, sd, tab, x, b, y, omega, xin);
+            tbs_step<OP, PD>(k + 1, e3, e1, e0, wb, t, tid, sd, tab, x, b, y, omega, xin);
+            tbs_step<OP, PD>(k + 2, e0, e2, e1, wa, t, tid, sd, tab, x, b, y, omega, xin);
+            tbs_step<OP, PD>(k + 3, e1, e3, e2, wb, t, tid, sd, tab, x, b, y, omega, xin);
+        }
+    }
+}
+
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_rows_long(
     const int* __restrict__ rows, const int* __restrict__ rowptr, const int* __restrict__ col,
@@ -1896,6 +2031,22 @@ template <int OP, int NU>
 void launch_sym_nu(const pamg_mat& A, const double* x, const double* b, double* y, double omega, hipStream_t s) {
     const SymDia& sd = A.sym;
     const int grid = sd.nbands * 8 * sd.eighth;
+    if constexpr (NU == 3) {
+        // streamed one-sweep kernel (Options::sym_stream): the whole one-part grid operator
+        if (sd.vd_n && sd.tb_ok && !sd.tb_part && options().sym_stream > 0 && sd.plane0 == 0 &&
+            sd.nbands == sd.tb.nz && (int64_t)sd.band == (int64_t)sd.tb.nx * sd.tb.ny && A.nrows % 2 == 0) {
+            TbGeom g = sd.tb;
+            g.zlo = 0;
+            g.zhi = g.nz;
+            g.zchunks = std::max(1, std::min(options().sym_stream, g.nz));
+            g.zlen = (g.nz + g.zchunks - 1) / g.zchunks;
+            g.zchunks = (g.nz + g.zlen - 1) / g.zlen;
+            const int gr = (g.tiles_x * g.tiles_y * g.zchunks + 7) / 8 * 8;
+            k_sym_tbs<OP, 1><<<gr, TbShape<1>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab,
+                                                                sd.vd_n, sd, g, x, b, y, omega);
+            return;
+        }
+    }
     if (sd.vd_n) {  // (the upload builds the dictionary only with two rows per lane)
         const int ch = NU <= 3 ? options().symd_chunks : 1;
         const int g = 8 * ((sd.nbands * sd.eighth + ch - 1) / ch);

@@ -980,6 +980,32 @@ def test_symd_units_per_block_bit_exact(ctx, kind, n, order, ch):
     assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.57), bh, 0.57)))
 
 
+@pytest.mark.parametrize("kind,shape", [("poisson3d", (64, 64, 64)), ("aniso3d", (64, 64, 64)),
+                                        ("poisson3d", (128, 128, 128)), ("poisson3d", (64, 32, 40)),
+                                        ("aniso3d", (192, 48, 7))])
+@pytest.mark.parametrize("zch", [1, 3, 8])
+def test_sym_stream_bit_exact(ctx, kind, shape, zch):
+    """k_sym_tbs (sym_stream = z-chunks per tile column: one sweep streamed plane by plane, x from
+    a 4-slot LDS window ring): SpMV, residual and two Jacobi sweeps bit-exact with the oracle,
+    with chunk boundaries inside the grid (3, 8) and one chunk per column (1)."""
+    from parallel_amg_amd._lib import layout_of
+    M = O.generate(kind, *shape)
+    Ad, _h = upload(ctx, M)
+    lay = layout_of(Ad)
+    assert lay["sym"] and lay["sym_vd"] and lay["jr_fused"], lay
+    rng = np.random.default_rng(shape[2] + zch)
+    xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
+    x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
+    with _with_option("sym_stream", zch):
+        mul(y, Ad, x)
+        assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
+        residual(y, Ad, x, b)
+        assert np.array_equal(bits(y.own_values()), bits(O.residual(M, xh, bh)))
+        t = PVector(ctx, M.nrows)
+        jacobi(x, Ad, b, t, 0.57, 2)
+    assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.57), bh, 0.57)))
+
+
 @pytest.mark.parametrize("breaker", ["asym_value", "signed_zero", "unsorted_row", "diagonal_only"])
 def test_sym_dia_declines_what_it_cannot_reproduce(ctx, breaker):
     """A mirror that differs in one bit (or +0.0 against -0.0), a row whose storage order is
