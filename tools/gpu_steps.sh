@@ -29,6 +29,9 @@ for step in "$@"; do
     timed)
         timeout -k 10 800 $PYT tests/test_gpu_timed_path.py tests/test_gpu_parity.py tests/test_gpu_local_world.py -m gpu > "$OUT/timed.log" 2>&1
         ;;
+    stream)
+        timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "sym_stream or symd_units" -m gpu > "$OUT/stream.log" 2>&1
+        ;;
     world)
         timeout -k 10 600 $PYT tests/test_gpu_local_world.py -m gpu > "$OUT/world.log" 2>&1
         ;;
@@ -59,7 +62,7 @@ for step in "$@"; do
         python3 tools/pmc_anatomy.py "$OUT/an1" "$OUT/an2" "$OUT/an3" "$OUT/an4" > "$OUT/anatomy.json"
         ;;
     part)
-        timeout -k 10 600 python3 -u tools/part_bench.py --n 512 --parts 8 --part 3 > "$OUT/part.json" 2> "$OUT/part.err"
+        timeout -k 10 600 python3 -u tools/part_bench.py ${PART_ARGS:---n 512 --parts 8 --part 3} > "$OUT/part.json" 2> "$OUT/part.err"
         ;;
     kbench)
         timeout -k 10 400 python3 -u tools/kbench.py $KBA > "$OUT/kbench.jsonl" 2> "$OUT/kbench.err"

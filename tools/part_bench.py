@@ -34,6 +34,7 @@ OPNAME = {0: "spmv", 1: "residual", 2: "jacobi", 3: "prolong", 4: "jacobi_residu
 
 
 def time_op(ctx, M, op, reps):
+    print(f"#   op {OPNAME[op]} ({M.nrows} rows)", file=sys.stderr, flush=True)
     x = PVector(ctx, M.n_own_cols, M.n_ghost, np.random.default_rng(1).standard_normal(M.n_own_cols))
     b = PVector(ctx, M.nrows, 0, np.ones(M.nrows))
     y = PVector(ctx, M.nrows)
