@@ -289,7 +289,11 @@ def main():
     # the instance name as rocprofv3 demangles it (every template argument, defaults included)
     tf = lambda v: "true" if v else "false"  # noqa: E731
     if pipelined:
-        kname = f"k_sym_tbd<3, {_tb_pd()}>" if lay.get("sym_vd") else "k_sym_tb<3>"
+        if lay.get("sym_vd"):  # k_sym_tbd<S, PD, TY> (8-line tiles run one plane ahead)
+            ty = _option("tb_ty")
+            kname = f"k_sym_tbd<3, {1 if ty == 8 else _tb_pd()}, {ty}>"
+        else:
+            kname = "k_sym_tb<3>"
         post_ms = float(fused["chain3_ms"])
         post_bytes = float(S.csr_bytes(A0, 3))       # matrix once + in0 + b + 3 outputs
         post_fbytes = float(S.rowsum_bytes(A0, 3))

@@ -1103,10 +1103,10 @@ __global__ __launch_bounds__(kBlock) void k_rows_symd(
 constexpr int kTbPX = (kTbX + 4) / 2;  // row pairs per line: x0-2 .. x0+kTbX+1
 constexpr int kTbLW = kTbX + 8;        // LDS line: column x - x0 + 4 (even for even x; pads 0-1, kTbX+6-7)
 
-template <int S>
-struct TbShape {
+template <int S, int TY = kTbY>
+struct TbShape {                                 // TY: tile height (Options::tb_ty; kTbY by default)
     static constexpr int H = S - 1;              // stage-0 halo in y and z
-    static constexpr int RY = kTbY + 2 * H;      // grid lines of stage 0
+    static constexpr int RY = TY + 2 * H;        // grid lines of stage 0
     static constexpr int NT = kTbPX * RY;        // threads with a row pair
     static constexpr int threads = (NT + 63) / 64 * 64;
     static constexpr int XL = RY + 2;            // lines of the in0 window (stage 0's region + 1)
@@ -1194,16 +1194,16 @@ struct TbCtx {
 // whole workgroup returns before any barrier). Tiles: consecutive tiles on one XCD (block b runs
 // on XCD b % 8; speed only), ordered y-fastest so that the tiles sharing the wide y halos
 // (kTbX + 4 points x S-1 lines) sit on one XCD.
-template <int S>
+template <int S, int TY = kTbY>
 __device__ __forceinline__ bool tb_ctx_init(TbCtx<S>& t, const TbGeom& g, int nrows) {
-    using Sh = TbShape<S>;
+    using Sh = TbShape<S, TY>;
     const int ntiles = g.tiles_x * g.tiles_y * g.zchunks;
     const int per = (ntiles + 7) / 8;
     const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
     if (lin >= ntiles) return false;
     const int ty = lin % g.tiles_y, tx = (lin / g.tiles_y) % g.tiles_x, zc = lin / (g.tiles_x * g.tiles_y);
     if (g.zlo + zc * g.zlen >= g.zhi) return false;  // (a chunk past the output range: uniform)
-    const int x0 = tx * kTbX, y0 = ty * kTbY;
+    const int x0 = tx * kTbX, y0 = ty * TY;
     t.x0 = x0;
     t.y0 = y0;
     t.nx = g.nx;
@@ -1222,7 +1222,7 @@ __device__ __forceinline__ bool tb_ctx_init(TbCtx<S>& t, const TbGeom& g, int nr
     t.col = 2 * px + 2;
     t.ixy = (int64_t)y * g.nx + x;
     t.pos_ok = has && x >= 0 && x < g.nx && y >= 0 && y < g.ny;
-    t.own_xy = t.pos_ok && px >= 1 && px <= kTbX / 2 && y >= y0 && y < y0 + kTbY;
+    t.own_xy = t.pos_ok && px >= 1 && px <= kTbX / 2 && y >= y0 && y < y0 + TY;
     return true;
 }
 
@@ -1234,9 +1234,9 @@ struct TbWin {
     double2 v[2];
     bool ok[2];
 };
-template <int S>
+template <int S, int TY = kTbY>
 __device__ __forceinline__ void tb_win_load(TbWin<S>& w, const TbCtx<S>& t, const double* __restrict__ in0, int q) {
-    using Sh = TbShape<S>;
+    using Sh = TbShape<S, TY>;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int p = threadIdx.x + h * Sh::threads;
@@ -1246,9 +1246,9 @@ __device__ __forceinline__ void tb_win_load(TbWin<S>& w, const TbCtx<S>& t, cons
         w.v[h] = tb_pair(in0, (int64_t)q * t.M + (int64_t)y * t.nx + x, t.n);
     }
 }
-template <int S>
-__device__ __forceinline__ void tb_win_store(const TbWin<S>& w, double (*xin)[TbShape<S>::XL][kTbLW], int slot) {
-    using Sh = TbShape<S>;
+template <int S, int TY = kTbY>
+__device__ __forceinline__ void tb_win_store(const TbWin<S>& w, double (*xin)[TbShape<S, TY>::XL][kTbLW], int slot) {
+    using Sh = TbShape<S, TY>;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int p = threadIdx.x + h * Sh::threads;
@@ -1452,16 +1452,17 @@ __device__ __forceinline__ void tbd_rows(const SymTab<3>& tab, const TbdRow& c, 
 // one step k: En <- plane k+PD (loads issued), E0 = plane k (stage 0), E1 = k-1 (stage 1),
 // E2 = k-2 (stage 2, S = 3), E3 = k-3 (the -M ids of stage 2; of stage 1 when S = 2 it is E2);
 // win holds plane k+1's window on entry (loaded PD steps earlier), plane k+1+PD's on exit
-template <int S, int PD>
+template <int S, int PD, int TY>
 __device__ __forceinline__ void tbd_step(int k, TbdRow& En, const TbdRow& E0, const TbdRow& E1, const TbdRow& E2,
                                          const TbdRow& E3, TbWin<S>& win, const TbCtx<S>& t,
                                          const uint8_t* __restrict__ tid, const SymDia& sd, const TbArgs& ta,
-                                         const SymTab<3>& tab, double (*l0)[TbShape<S>::RY][kTbLW],
-                                         double (*l1)[TbShape<S>::RY][kTbLW], double (*xin)[TbShape<S>::XL][kTbLW]) {
-    using Sh = TbShape<S>;
+                                         const SymTab<3>& tab, double (*l0)[TbShape<S, TY>::RY][kTbLW],
+                                         double (*l1)[TbShape<S, TY>::RY][kTbLW],
+                                         double (*xin)[TbShape<S, TY>::XL][kTbLW]) {
+    using Sh = TbShape<S, TY>;
     if (k >= t.kend) return;  // uniform: the whole workgroup
-    tb_win_store<S>(win, xin, tb_mod3(k + 1));  // loaded PD steps ago
-    tb_win_load<S>(win, t, ta.in0, k + 1 + PD);
+    tb_win_store<S, TY>(win, xin, tb_mod3(k + 1));  // loaded PD steps ago
+    tb_win_load<S, TY>(win, t, ta.in0, k + 1 + PD);
     {
         const int p = k + PD;
         const bool ok = t.pos_ok && p >= 0 && p < t.nz;
@@ -1515,30 +1516,30 @@ __device__ __forceinline__ void tbd_step(int k, TbdRow& En, const TbdRow& E0, co
 
 // PD (Options::tb_pd): how many planes ahead the loads run — 1: a ring of S + 2 planes and one
 // window register set; 2: S + 3 planes and two window sets used in alternation
-template <int S, int PD>
-__global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tbd(int nrows, const uint8_t* __restrict__ tid,
+template <int S, int PD, int TY = kTbY>
+__global__ __launch_bounds__((TbShape<S, TY>::threads)) void k_sym_tbd(int nrows, const uint8_t* __restrict__ tid,
                                                                   const double* __restrict__ vtab,
                                                                   const uint32_t* __restrict__ mtab, int nv,
                                                                   const SymDia sd, const TbArgs ta) {
-    using Sh = TbShape<S>;
+    using Sh = TbShape<S, TY>;
     static_assert(PD == 1 || PD == 2, "one or two planes ahead");
     __shared__ __attribute__((aligned(16))) double l0[3][Sh::RY][kTbLW];
     __shared__ __attribute__((aligned(16))) double l1[S == 3 ? 3 : 1][Sh::RY][kTbLW];
     __shared__ __attribute__((aligned(16))) double xin[3][Sh::XL][kTbLW];
     __shared__ __attribute__((aligned(16))) SymTab<3> tab;
     TbCtx<S> t;
-    if (!tb_ctx_init<S>(t, sd.tb, nrows)) return;  // the whole workgroup, before any barrier
+    if (!tb_ctx_init<S, TY>(t, sd.tb, nrows)) return;  // the whole workgroup, before any barrier
     symtab_fill<3>(tab, vtab, mtab, nv);           // (read after the first step's barrier)
     const int k0 = t.zs - Sh::H;
     TbWin<S> wa, wb;
     {  // the in0 windows of planes k0-1 and k0; planes k0+1 (.. k0+PD) stay in registers
 #pragma unroll
         for (int q = -1; q <= 0; ++q) {
-            tb_win_load<S>(wa, t, ta.in0, k0 + q);
-            tb_win_store<S>(wa, xin, tb_mod3(k0 + q));
+            tb_win_load<S, TY>(wa, t, ta.in0, k0 + q);
+            tb_win_store<S, TY>(wa, xin, tb_mod3(k0 + q));
         }
-        tb_win_load<S>(wa, t, ta.in0, k0 + 1);
-        if constexpr (PD == 2) tb_win_load<S>(wb, t, ta.in0, k0 + 2);
+        tb_win_load<S, TY>(wa, t, ta.in0, k0 + 1);
+        if constexpr (PD == 2) tb_win_load<S, TY>(wb, t, ta.in0, k0 + 2);
     }
     // the plane ring (planes k+PD .. k-S), rotated by the unrolled loop; planes k0-1 .. k0+PD-1 first
     TbdRow e0{}, e1{}, e2{}, e3{}, e4{}, e5{};
@@ -1552,40 +1553,40 @@ __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tbd(int nrows, cons
     if constexpr (PD == 2) load(e1, k0 + 1);
     if constexpr (S == 2 && PD == 1) {  // planes k+1, k, k-1, k-2
         for (int k = k0; k < t.kend; k += 4) {
-            tbd_step<S, PD>(k, e1, e0, e3, e2, e2, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 1, e2, e1, e0, e3, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 2, e3, e2, e1, e0, e0, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 3, e0, e3, e2, e1, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k, e1, e0, e3, e2, e2, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 1, e2, e1, e0, e3, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 2, e3, e2, e1, e0, e0, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 3, e0, e3, e2, e1, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
         }
     } else if constexpr (S == 3 && PD == 1) {  // planes k+1, k, k-1, k-2, k-3
         for (int k = k0; k < t.kend; k += 5) {
-            tbd_step<S, PD>(k, e1, e0, e4, e3, e2, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 1, e2, e1, e0, e4, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 2, e3, e2, e1, e0, e4, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 3, e4, e3, e2, e1, e0, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 4, e0, e4, e3, e2, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k, e1, e0, e4, e3, e2, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 1, e2, e1, e0, e4, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 2, e3, e2, e1, e0, e4, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 3, e4, e3, e2, e1, e0, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 4, e0, e4, e3, e2, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
         }
     } else if constexpr (S == 2) {  // PD 2: planes k+2, k+1, k, k-1, k-2; windows wa / wb alternate
         for (int k = k0; k < t.kend; k += 10) {
-            tbd_step<S, PD>(k, e2, e0, e4, e3, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 1, e3, e1, e0, e4, e4, wb, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 2, e4, e2, e1, e0, e0, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 3, e0, e3, e2, e1, e1, wb, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 4, e1, e4, e3, e2, e2, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 5, e2, e0, e4, e3, e3, wb, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 6, e3, e1, e0, e4, e4, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 7, e4, e2, e1, e0, e0, wb, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 8, e0, e3, e2, e1, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 9, e1, e4, e3, e2, e2, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k, e2, e0, e4, e3, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 1, e3, e1, e0, e4, e4, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 2, e4, e2, e1, e0, e0, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 3, e0, e3, e2, e1, e1, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 4, e1, e4, e3, e2, e2, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 5, e2, e0, e4, e3, e3, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 6, e3, e1, e0, e4, e4, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 7, e4, e2, e1, e0, e0, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 8, e0, e3, e2, e1, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 9, e1, e4, e3, e2, e2, wb, t, tid, sd, ta, tab, l0, l1, xin);
         }
     } else {  // S 3, PD 2: planes k+2, k+1, k, k-1, k-2, k-3; windows wa / wb alternate
         for (int k = k0; k < t.kend; k += 6) {
-            tbd_step<S, PD>(k, e2, e0, e5, e4, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 1, e3, e1, e0, e5, e4, wb, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 2, e4, e2, e1, e0, e5, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 3, e5, e3, e2, e1, e0, wb, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 4, e0, e4, e3, e2, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD>(k + 5, e1, e5, e4, e3, e2, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k, e2, e0, e5, e4, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 1, e3, e1, e0, e5, e4, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 2, e4, e2, e1, e0, e5, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 3, e5, e3, e2, e1, e0, wb, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 4, e0, e4, e3, e2, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
+            tbd_step<S, PD, TY>(k + 5, e1, e5, e4, e3, e2, wb, t, tid, sd, ta, tab, l0, l1, xin);
         }
     }
 }
@@ -2123,6 +2124,22 @@ void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s) {
     g.zchunks = (span + g.zlen - 1) / g.zlen;
     const int ntiles = g.tiles_x * g.tiles_y * g.zchunks;
     const int grid = (ntiles + 7) / 8 * 8;
+    if (sd.vd_n && options().tb_ty == 8) {
+        // 8-line tiles (Options::tb_ty): twice the tiles per plane, half the LDS per workgroup
+        // (two workgroups per CU); the z split recomputed for the tile count
+        g.tiles_y = g.ny / 8;
+        g.zchunks = std::max(1, std::min((g.zchunks + 1) / 2, span / 2 > 0 ? span / 2 : 1));
+        g.zlen = (span + g.zchunks - 1) / g.zchunks;
+        g.zchunks = (span + g.zlen - 1) / g.zlen;
+        const int gr = (g.tiles_x * g.tiles_y * g.zchunks + 7) / 8 * 8;
+        if (ta.nstages == 2)
+            k_sym_tbd<2, 1, 8><<<gr, TbShape<2, 8>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab,
+                                                                    sd.vd_n, sd, ta);
+        else
+            k_sym_tbd<3, 1, 8><<<gr, TbShape<3, 8>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab,
+                                                                    sd.vd_n, sd, ta);
+        return;
+    }
     if (sd.vd_n) {
         const bool pd2 = options().tb_pd == 2;
         if (ta.nstages == 2 && pd2)

@@ -143,6 +143,8 @@ struct Options {
     int x_stage_tiles = 0;     // 1: per-tile x staging with row lanes for per-tile dictionary sets (k_rows_xsr)
     int symd_chunks = 2;       // 512-row units per block of k_rows_symd (1, 2 or 4; 2: SpMV -2 %, residual and
                                // Jacobi -4..-5 %, 4: -1..-2 %; same-box A/B profiles/r04_g_c2/, r04_g_c4/)
+    int tb_ty = 16;            // tile height of the row-class chain (k_sym_tbd): 16, or 8 (half the LDS: two
+                               // workgroups per CU)
     int sym_stream = 0;        // > 0: one-sweep row-class operators on a whole grid stream planes (k_sym_tbs)
                                // in this many z-chunks per 64 x 16 tile column; 0: k_rows_symd
     int xsr_kernel = 0;        // staged sets: 0 row lanes (k_rows_xsr), 1 nonzero lanes (k_rows_tm, 2048-nonzero tiles)

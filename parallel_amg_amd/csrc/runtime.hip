@@ -3285,6 +3285,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "xsr_kernel" && (value == 0 || value == 1)) o.xsr_kernel = (int)value;
     else if (k == "symd_chunks" && (value == 1 || value == 2 || value == 4)) o.symd_chunks = (int)value;
     else if (k == "sym_stream" && value >= 0 && value <= 4096) o.sym_stream = (int)value;
+    else if (k == "tb_ty" && (value == 8 || value == 16)) o.tb_ty = (int)value;
     else if (k == "tb_pd" && (value == 1 || value == 2)) o.tb_pd = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
@@ -3318,6 +3319,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "xsr_kernel") *value = o.xsr_kernel;
     else if (k == "symd_chunks") *value = o.symd_chunks;
     else if (k == "sym_stream") *value = o.sym_stream;
+    else if (k == "tb_ty") *value = o.tb_ty;
     else if (k == "tb_pd") *value = o.tb_pd;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;

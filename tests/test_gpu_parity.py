@@ -1329,9 +1329,11 @@ def test_row_lane_x_staging_bit_exact(ctx, level1_128, tnnz, xk):
 
 
 @pytest.mark.parametrize("kind", ["poisson3d", "aniso3d"])
-def test_chain_two_planes_ahead_bit_exact(ctx, kind):
-    """tb_pd = 2 (k_sym_tbd<S, 2>: the chain's loads two planes ahead, two window register sets in
-    alternation): the fused pre-smoothing pass and pipelined cycles keep the oracle's bits."""
+@pytest.mark.parametrize("key,val", [("tb_pd", 2), ("tb_pd", 1), ("tb_ty", 8)])
+def test_chain_two_planes_ahead_bit_exact(ctx, kind, key, val):
+    """The chain's variants — tb_pd = 2 / 1 (k_sym_tbd<S, PD>: loads two planes ahead with two
+    window register sets in alternation, or one) and tb_ty = 8 (8-line tiles, two workgroups per
+    CU): the fused pre-smoothing pass and pipelined cycles keep the oracle's bits."""
     from parallel_amg_amd._lib import layout_of
     from parallel_amg_amd.partitioned import jacobi_residual
     be = pa.SequentialBackend(1)
@@ -1345,7 +1347,7 @@ def test_chain_two_planes_ahead_bit_exact(ctx, kind):
     Ao = O.generate(kind, n, n, n)
     rng = np.random.default_rng(2)
     xh, bh = rng.standard_normal(Ao.nrows), rng.standard_normal(Ao.nrows)
-    with _with_option("tb_pd", 2):
+    with _with_option(key, val):
         t, r = PVector(ctx, Ao.nrows), PVector(ctx, Ao.nrows)
         assert jacobi_residual(t, r, S.A[0], PVector(ctx, Ao.nrows, 0, xh), PVector(ctx, Ao.nrows, 0, bh), 0.66)
         S.set_graph(False)

@@ -32,6 +32,9 @@ for step in "$@"; do
     stream)
         timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "sym_stream or symd_units" -m gpu > "$OUT/stream.log" 2>&1
         ;;
+    chain)
+        timeout -k 10 400 $PYT tests/test_gpu_parity.py -k "chain_two_planes or jacobi_residual_op or pipelined_cycles" -m gpu > "$OUT/chain.log" 2>&1
+        ;;
     world)
         timeout -k 10 600 $PYT tests/test_gpu_local_world.py -m gpu > "$OUT/world.log" 2>&1
         ;;
