@@ -3364,14 +3364,21 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
         return fail(PAMG_E_STATE, "bench_rowop: op %d needs the temporally blocked layout (pamg_mat_layout bit 5)", op);
     if (x == y) return fail(PAMG_E_ARG, "bench_rowop: x and y must differ");
     CHECK(check_vec_for(A, x, "bench_rowop"));
+    // a part's blocked passes (sweeps_part) feed each stage's output to the next stage's boundary
+    // rows, which read its ghost slots: y and the scratch stages need the column length
+    const bool part_tb = op >= 4 && A->sym.tb_part;
+    if (part_tb) CHECK(check_vec_for(A, y, "bench_rowop (y: input of the next stage)"));
     CHECK(set_device(ctx));
     // ops 4 / 5: the temporally blocked passes k_sym_tb<2> (Jacobi -> residual) and <3>
     // (Jacobi -> Jacobi -> residual), the first output into y, the others into scratch
     double* scratch[2] = {nullptr, nullptr};
-    if (op >= 4)
+    if (op >= 4) {
+        const int64_t len = part_tb ? (A->plan ? A->plan->n_own + A->plan->n_ghost : A->ncols) : A->nrows;
         for (double*& p : scratch) {
-            CHECK(dalloc(&p, A->nrows + kVecPad));
+            CHECK(dalloc(&p, std::max<int64_t>(len, A->nrows) + kVecPad));
+            HIPC(hipMemset(p, 0, sizeof(double) * (size_t)(std::max<int64_t>(len, A->nrows) + kVecPad)));
         }
+    }
     pamg::TbArgs ta;
     ta.nstages = op - 2;
     ta.last_resid = true;

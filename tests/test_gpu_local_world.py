@@ -177,3 +177,34 @@ def test_ranks_disagreeing_on_the_pipeline_bit_exact(built):
     assert np.array_equal(bits(got_xp), bits(xo))
     for p in range(nparts):
         np.testing.assert_allclose(hist[p], ho, rtol=1e-12)
+
+
+def test_part_bench_rowop_stage_vectors_need_ghost_slots(built):
+    """pamg_bench_rowop's blocked passes on one part (ops 4 / 5: sweeps_part without exchanges)
+    feed each stage's output to the next stage's boundary rows, which read ghost slots: an output
+    vector without them is refused (it once faulted the GPU at 512 x 512 x 64), one with them runs."""
+    from parallel_amg_amd._lib import PamgError
+    from parallel_amg_amd.partitioned import PSparseMatrix
+    nparts = 4
+    W = LocalWorld(nparts)
+    try:
+        be = pa.SequentialBackend(nparts)
+        A, offs, xs = pa.generate_problem(be, "poisson3d", 64)
+        H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=W.ctxs[0])
+        ctx = W.ctxs[1]
+        lp = H.levels[0][1]
+        Ad = PSparseMatrix(ctx, lp.A, lp.planA)
+        assert layout_of(Ad)["jr_fused"], layout_of(Ad)
+        x = PVector(ctx, Ad.n_own_cols, Ad.n_ghost, xs[1])
+        b = PVector(ctx, Ad.nrows, 0, np.ones(Ad.nrows))
+        ms = ctypes.c_double()
+        with pytest.raises(PamgError):
+            call("pamg_bench_rowop", ctx.handle, Ad.handle, 4, x.handle, b.handle, PVector(ctx, Ad.nrows).handle,
+                 0.6, 1, ctypes.byref(ms))
+        y = PVector(ctx, Ad.n_own_cols, Ad.n_ghost)
+        for op in (4, 5):
+            call("pamg_bench_rowop", ctx.handle, Ad.handle, op, x.handle, b.handle, y.handle, 0.6, 2, ctypes.byref(ms))
+            assert ms.value > 0
+        del Ad
+    finally:
+        W.close()

@@ -37,7 +37,8 @@ def time_op(ctx, M, op, reps):
     print(f"#   op {OPNAME[op]} ({M.nrows} rows)", file=sys.stderr, flush=True)
     x = PVector(ctx, M.n_own_cols, M.n_ghost, np.random.default_rng(1).standard_normal(M.n_own_cols))
     b = PVector(ctx, M.nrows, 0, np.ones(M.nrows))
-    y = PVector(ctx, M.nrows)
+    # (the blocked passes of a part feed y to the next stage's boundary rows: ghost slots too)
+    y = PVector(ctx, M.n_own_cols, M.n_ghost) if op >= 4 else PVector(ctx, M.nrows)
     ms = C.c_double()
     call("pamg_bench_rowop", ctx.handle, M.handle, op, x.handle, b.handle, y.handle, 0.6, reps, C.byref(ms))
     return ms.value
