@@ -295,8 +295,11 @@ def main():
         else:
             kname = "k_sym_tb<3>"
         post_ms = float(fused["chain3_ms"])
-        post_bytes = float(S.csr_bytes(A0, 3))       # matrix once + in0 + b + 3 outputs
-        post_fbytes = float(S.rowsum_bytes(A0, 3))
+        # matrix once + in0 + b + the outputs the pipelined chain stores: the pre-smoothed iterate
+        # and the residual (+ the post-smoothed iterate only with chain_store_x)
+        nvec = 2 + _option("chain_store_x")
+        post_bytes = float(S.csr_bytes(A0, nvec))
+        post_fbytes = float(S.rowsum_bytes(A0, nvec))
         achieved = post_bytes / (post_ms * 1e-3) / 1e9
     elif lay.get("sym"):
         kname = _sym_kname(2, lay)
@@ -377,7 +380,8 @@ def main():
                                    "Jacobi -> next pre-smoothing Jacobi -> residual, temporally blocked over the "
                                    "symmetric diagonal-class layout" + (" with its row-class dictionary" if lay.get("sym_vd")
                                                                         else "") +
-                                   ", the matrix streamed once)" if pipelined else
+                                   ", the matrix streamed once; stores the pre-smoothed iterate and the residual)"
+                                   if pipelined else
                                    " (level-0 post-smoothing Jacobi, symmetric diagonal-class layout: "
                                    "diagonal + upper values per row, lower values from their mirrors)"
                                    if lay.get("sym") else " (level-0 post-smoothing Jacobi"

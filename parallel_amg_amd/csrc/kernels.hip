@@ -1306,7 +1306,8 @@ __device__ __forceinline__ void tb_step(int k, TbCoef& cA, TbCoef& cB, TbCoef& c
             double xv[2][7];
             tb_gather_lds<Sh::XL>(xin, tb_mod3(k - 1), tb_mod3(k), tb_mod3(k + 1), t.ry + 1, t.col, xv);
             tb_rows(cA, xv, S == 1 && ta.last_resid, ta.omega, o);
-            if (t.own_xy && k >= t.zs && k < t.ze) *reinterpret_cast<double2*>(ta.out[0] + i) = make_double2(o[0], o[1]);
+            if (ta.out[0] && t.own_xy && k >= t.zs && k < t.ze)
+                *reinterpret_cast<double2*>(ta.out[0] + i) = make_double2(o[0], o[1]);
         }
         if (t.ry >= 0) *reinterpret_cast<double2*>(&l0[tb_mod3(k)][t.ry][t.col]) = make_double2(o[0], o[1]);
     }
@@ -1476,7 +1477,9 @@ __device__ __forceinline__ void tbd_step(int k, TbdRow& En, const TbdRow& E0, co
             double xv[2][7];
             tb_gather_lds<Sh::XL>(xin, tb_mod3(k - 1), tb_mod3(k), tb_mod3(k + 1), t.ry + 1, t.col, xv);
             tbd_rows(tab, E0, E1.own, xv, S == 1 && ta.last_resid, ta.omega, o);
-            if (t.own_xy && k >= t.zs && k < t.ze)
+            // (out[0] NULL: the stage-0 result only feeds stage 1 — the pipeline's post-smoothed
+            // iterate, which no later launch reads; uniform branch)
+            if (ta.out[0] && t.own_xy && k >= t.zs && k < t.ze)
                 *reinterpret_cast<double2*>(ta.out[0] + (int64_t)k * t.M + t.ixy) = make_double2(o[0], o[1]);
         }
         if (t.ry >= 0) *reinterpret_cast<double2*>(&l0[tb_mod3(k)][t.ry][t.col]) = make_double2(o[0], o[1]);

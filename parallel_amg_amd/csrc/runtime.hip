@@ -2976,7 +2976,10 @@ static int launch_chain3(pamg_hier* H, double* x, const double* b, const double*
     ta.nstages = 3;
     ta.last_resid = true;
     ta.in0 = t_prev;
-    ta.out[0] = x;
+    // the post-smoothed iterate of cycle k is read only by this launch's next stage (from LDS):
+    // the V-cycle's x is written by the tail's post-smoothing, so a steady chain stores it only
+    // when asked (Options::chain_store_x; same bits either way)
+    ta.out[0] = pamg::options().chain_store_x ? x : nullptr;
     ta.out[1] = t_next;
     ta.out[2] = H->r[0];
     ta.b = b;
@@ -3286,6 +3289,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "symd_chunks" && (value == 1 || value == 2 || value == 4)) o.symd_chunks = (int)value;
     else if (k == "sym_stream" && value >= 0 && value <= 4096) o.sym_stream = (int)value;
     else if (k == "tb_ty" && (value == 8 || value == 16)) o.tb_ty = (int)value;
+    else if (k == "chain_store_x" && (value == 0 || value == 1)) o.chain_store_x = (int)value;
     else if (k == "tb_pd" && (value == 1 || value == 2)) o.tb_pd = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
@@ -3320,6 +3324,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "symd_chunks") *value = o.symd_chunks;
     else if (k == "sym_stream") *value = o.sym_stream;
     else if (k == "tb_ty") *value = o.tb_ty;
+    else if (k == "chain_store_x") *value = o.chain_store_x;
     else if (k == "tb_pd") *value = o.tb_pd;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;

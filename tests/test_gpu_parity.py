@@ -1329,7 +1329,7 @@ def test_row_lane_x_staging_bit_exact(ctx, level1_128, tnnz, xk):
 
 
 @pytest.mark.parametrize("kind", ["poisson3d", "aniso3d"])
-@pytest.mark.parametrize("key,val", [("tb_pd", 2), ("tb_pd", 1), ("tb_ty", 8)])
+@pytest.mark.parametrize("key,val", [("tb_pd", 2), ("tb_pd", 1), ("tb_ty", 8), ("chain_store_x", 1)])
 def test_chain_two_planes_ahead_bit_exact(ctx, kind, key, val):
     """The chain's variants — tb_pd = 2 / 1 (k_sym_tbd<S, PD>: loads two planes ahead with two
     window register sets in alternation, or one) and tb_ty = 8 (8-line tiles, two workgroups per
