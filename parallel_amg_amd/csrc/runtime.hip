@@ -3388,7 +3388,9 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
     ta.nstages = op - 2;
     ta.last_resid = true;
     ta.in0 = x->d;
-    ta.out[0] = y->d;
+    // op 5 on one part mirrors the pipeline's chain (launch_chain3): its stage-0 output is stored
+    // only with chain_store_x (a part's passes feed it to the edge planes: always stored there)
+    ta.out[0] = op == 5 && !part_tb && !pamg::options().chain_store_x ? nullptr : y->d;
     ta.out[1] = scratch[0];
     ta.out[2] = scratch[1];
     ta.b = b ? b->d : nullptr;
