@@ -158,7 +158,9 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     // CD (column dictionary, 4 or 8 bits per nonzero): column = row + ctab[index], with the
     // tile set's <= 16 / <= 256 distinct offsets (a stencil's 7 for A0) in LDS; every
     // position's row (lrow, tile-local) is marked by the lane that owns the row (RL8 scan)
-    static_assert(CD == 0 || (RL8 && !C24 && !VD), "column dictionary: 8-bit rows, plain values");
+    // (with VD: per-tile dictionaries of a prolongator whose values are 4-bit indices too,
+    // Options::vd_col_dict)
+    static_assert(CD == 0 || (RL8 && !C24), "column dictionary: 8-bit rows");
     __shared__ int ltab[CD != 0 ? BS : 1];
     __shared__ __attribute__((aligned(4))) uint8_t lrow[CD ? TNNZ + 8 : 4];
     __shared__ int lanc[ANC ? BS : 1];
@@ -1915,6 +1917,25 @@ template <int OP, int TNNZ, bool PT>
 void launch_tile2_cd(const pamg_mat& A, const TileSet& ts, const double* x, const double* b, double* y,
                      double omega, hipStream_t s) {
     const int n = ts.n_short;
+    if (PT && ts.vd) {  // per-tile column dictionaries + 4-bit value dictionaries (Options::vd_col_dict)
+        if (ts.anc && ts.cd == 4)
+            k_rows_tile2<OP, TNNZ, false, true, true, 4, true, true><<<n, kBlock, 0, s>>>(
+                ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, A.d_vidx,
+                ts.d_vtab, A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n, A.d_anc16, ts.d_abase);
+        else if (ts.anc)
+            k_rows_tile2<OP, TNNZ, false, true, true, 8, true, true><<<n, kBlock, 0, s>>>(
+                ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, A.d_vidx,
+                ts.d_vtab, A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n, A.d_anc16, ts.d_abase);
+        else if (ts.cd == 4)
+            k_rows_tile2<OP, TNNZ, false, true, true, 4, true><<<n, kBlock, 0, s>>>(
+                ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, A.d_vidx,
+                ts.d_vtab, A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n);
+        else
+            k_rows_tile2<OP, TNNZ, false, true, true, 8, true><<<n, kBlock, 0, s>>>(
+                ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, A.d_vidx,
+                ts.d_vtab, A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n);
+        return;
+    }
     if (PT && ts.anc) {
         if (ts.cd == 4)
             k_rows_tile2<OP, TNNZ, false, false, true, 4, true, true><<<n, kBlock, 0, s>>>(

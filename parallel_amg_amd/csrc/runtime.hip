@@ -570,10 +570,20 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
     std::vector<uint16_t> anc16;  // per-tile anchored sets: each row's first column - tile base
     for (int q = 0; q < 2; ++q) {
         pamg::TileSet* ts = sets[q];
-        if (!opt.col_dict || ts->vd || ts->n_short == 0 || ts->max_short_len > 255)
+        if (!opt.col_dict || ts->n_short == 0 || ts->max_short_len > 255)
             continue;
+        // a set with 4-bit value dictionaries (the prolongators) takes per-tile column
+        // dictionaries in the descriptor kernel only (Options::vd_col_dict), its values staying
+        // 4-bit indices
+        if (ts->vd && !(opt.vd_col_dict && opt.col_dict_tile)) continue;
         if (idx.empty()) idx.assign((size_t)A->nnz + kVecPad, 0);
         const std::vector<int4>& tiles = *tl[q];
+        if (ts->vd) {
+            ts->anc = false;
+            ts->pt = false;
+            CHECK(build_tile_dicts(A, rp, ci, tiles, ts, &idx, &tab[q], &anc16));
+            continue;
+        }
         const int64_t nt = (int64_t)tiles.size();
         // Offset of a nonzero: col - row (row-relative: stencils), or col - the row's first
         // column (anchored: rows of a repeated shape whose columns do not follow the row
@@ -3290,6 +3300,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "sym_stream" && value >= 0 && value <= 4096) o.sym_stream = (int)value;
     else if (k == "tb_ty" && (value == 8 || value == 16)) o.tb_ty = (int)value;
     else if (k == "chain_store_x" && (value == 0 || value == 1)) o.chain_store_x = (int)value;
+    else if (k == "vd_col_dict" && (value == 0 || value == 1)) o.vd_col_dict = (int)value;
     else if (k == "tb_pd" && (value == 1 || value == 2)) o.tb_pd = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
@@ -3325,6 +3336,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "sym_stream") *value = o.sym_stream;
     else if (k == "tb_ty") *value = o.tb_ty;
     else if (k == "chain_store_x") *value = o.chain_store_x;
+    else if (k == "vd_col_dict") *value = o.vd_col_dict;
     else if (k == "tb_pd") *value = o.tb_pd;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;

@@ -1155,6 +1155,31 @@ def test_prolongator_value_dictionary_row_lengths_bit_exact(ctx, rl8, lengths):
     assert lay["vd"] and lay["c24"] and lay["rl8"] == bool(rl8 and short), lay
 
 
+@pytest.mark.parametrize("kind,n", [("poisson3d", 64), ("aniso3d", 48), ("poisson2d", 300), ("poisson3d", 40)])
+def test_prolongator_column_and_value_dictionaries_bit_exact(ctx, kind, n):
+    """vd_col_dict: an AMG prolongator's tiles keep their 4-bit value dictionaries and take
+    per-tile column dictionaries (anchored or row-relative) in the descriptor kernel instead of
+    24-bit columns: SpMV, residual and prolongate-add bit-exact with the oracle, and the
+    operator streams fewer bytes than without."""
+    from parallel_amg_amd._lib import layout_of
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, kind, n)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=200))
+    P = H.levels[0][0].P
+    M = O.CSR(P.rowptr.copy(), P.col.astype(np.int64), P.val.copy(), P.ncols)
+    rng = np.random.default_rng(n)
+    with _with_option("vd_col_dict", 0):
+        A0 = _layout_ops_match_oracle(ctx, M, rng)
+    lay0, sb0 = layout_of(A0), A0.stream_bytes
+    del A0
+    with _with_option("vd_col_dict", 1):
+        A1 = _layout_ops_match_oracle(ctx, M, rng)
+    lay1 = layout_of(A1)
+    assert lay0["vd"] and lay0["cd"] == 0, lay0
+    assert lay1["vd"] and lay1["cd"] in (4, 8) and lay1["per_tile"], lay1
+    assert A1.stream_bytes < sb0
+
+
 @pytest.mark.parametrize("kind,shape", [("poisson3d", (128, 128, 128)), ("aniso3d", (128, 128, 128)),
                                         ("poisson3d", (256, 256, 256)), ("poisson3d", (64, 32, 40)),
                                         ("aniso3d", (192, 48, 7))])

@@ -38,6 +38,9 @@ for step in "$@"; do
     cab)
         timeout -k 10 500 python3 -u tools/cycle_ab.py ${CAB_ARGS:---ab chain_store_x=1,0} > "$OUT/cycle_ab.jsonl" 2> "$OUT/cycle_ab.err"
         ;;
+    sub)
+        timeout -k 10 400 $PYT tests/test_gpu_parity.py -k "${SUB_K:-prolongator}" -m gpu > "$OUT/sub.log" 2>&1
+        ;;
     world)
         timeout -k 10 600 $PYT tests/test_gpu_local_world.py -m gpu > "$OUT/world.log" 2>&1
         ;;
