@@ -979,6 +979,11 @@ __device__ __forceinline__ void symtab_fill(SymTab<NU>& t, const double* __restr
     for (int e = threadIdx.x; e < nv; e += blockDim.x) t.m[e] = mtab[e];
 }
 
+__device__ __forceinline__ uint16_t tbd_pair_ids(const uint8_t* __restrict__ tid, int64_t j, int64_t n) {
+    j = j < 0 ? 0 : (j > n - 2 ? n - 2 : j);  // (even j; clamped ones meet clear mask bits only)
+    return *reinterpret_cast<const uint16_t*>(tid + j);
+}
+
 __device__ __forceinline__ uint32_t tid_at(const uint8_t* __restrict__ tid, int64_t j, int64_t n) {
     return tid[j >= 0 && j < n ? j : 0];
 }
@@ -990,7 +995,7 @@ template <int OP, int NU, int CH = 1>
 __global__ __launch_bounds__(kBlock) void k_rows_symd(
     int nrows, int ncols, const uint8_t* __restrict__ tid, const double* __restrict__ vtab,
     const uint32_t* __restrict__ mtab, int nv, const SymDia sd, const double* __restrict__ x,
-    const double* __restrict__ b, double* __restrict__ y, double omega) {
+    const double* __restrict__ b, double* __restrict__ y, double omega, bool pair_ids = true) {
     constexpr int RB = 2 * kBlock;  // rows per unit
     constexpr int P = CH < 2 ? CH : 2;
     static_assert(CH % P == 0, "units in pairs");
@@ -1021,8 +1026,19 @@ __global__ __launch_bounds__(kBlock) void k_rows_symd(
 #pragma unroll
             for (int c = 0; c < NU; ++c) {
                 const int o = sd.off[NU - 1 - c];
-                tl[q][0][c] = tid_at(tid, ib[q] - o, n);
-                tl[q][1][c] = tid_at(tid, ib[q] + 1 - o, n);
+                // the mirror rows' ids as one 2-byte load where the pair is aligned (even o), and
+                // for o = 1 the byte below the own pair (the other one is row ib's own id)
+                if (pair_ids && o == 1) {
+                    tl[q][0][c] = (uint32_t)tbd_pair_ids(tid, ib[q] - 2, n) >> 8;
+                    tl[q][1][c] = tw[q] & 0xffu;
+                } else if (pair_ids && (o & 1) == 0) {
+                    const uint32_t w = tbd_pair_ids(tid, ib[q] - o, n);
+                    tl[q][0][c] = w & 0xffu;
+                    tl[q][1][c] = w >> 8;
+                } else {
+                    tl[q][0][c] = tid_at(tid, ib[q] - o, n);
+                    tl[q][1][c] = tid_at(tid, ib[q] + 1 - o, n);
+                }
                 const double2 xx = ld_pair(x, ib[q] - o, ncols, (o & 1) == 0);
                 xv[q][0][c] = xx.x;
                 xv[q][1][c] = xx.y;
@@ -1399,10 +1415,6 @@ struct TbdRow {    // one row pair on one plane, as loaded (narrow types: widene
     double b[2];
 };
 
-__device__ __forceinline__ uint16_t tbd_pair_ids(const uint8_t* __restrict__ tid, int64_t j, int64_t n) {
-    j = j < 0 ? 0 : (j > n - 2 ? n - 2 : j);  // (even j; clamped ones meet clear mask bits only)
-    return *reinterpret_cast<const uint16_t*>(tid + j);
-}
 
 // plane p's entry of the pair at i (even; 0 when the pair or plane is inactive)
 __device__ __forceinline__ void tbd_load(TbdRow& c, const uint8_t* __restrict__ tid, const double* __restrict__ b,
@@ -2078,17 +2090,19 @@ void launch_sym_nu(const pamg_mat& A, const double* x, const double* b, double* 
         if constexpr (NU <= 3) {
             if (ch == 2) {
                 k_rows_symd<OP, NU, 2><<<g, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab,
-                                                            sd.d_mtab, sd.vd_n, sd, x, b, y, omega);
+                                                            sd.d_mtab, sd.vd_n, sd, x, b, y, omega,
+                                                            options().symd_pair_ids != 0);
                 return;
             }
             if (ch == 4) {
                 k_rows_symd<OP, NU, 4><<<g, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab,
-                                                            sd.d_mtab, sd.vd_n, sd, x, b, y, omega);
+                                                            sd.d_mtab, sd.vd_n, sd, x, b, y, omega,
+                                                            options().symd_pair_ids != 0);
                 return;
             }
         }
         k_rows_symd<OP, NU><<<grid, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab,
-                                                  sd.vd_n, sd, x, b, y, omega);
+                                                  sd.vd_n, sd, x, b, y, omega, options().symd_pair_ids != 0);
         return;
     }
     if (sd.rpl == 2) {

@@ -3301,6 +3301,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "tb_ty" && (value == 8 || value == 16)) o.tb_ty = (int)value;
     else if (k == "chain_store_x" && (value == 0 || value == 1)) o.chain_store_x = (int)value;
     else if (k == "vd_col_dict" && (value == 0 || value == 1)) o.vd_col_dict = (int)value;
+    else if (k == "symd_pair_ids" && (value == 0 || value == 1)) o.symd_pair_ids = (int)value;
     else if (k == "tb_pd" && (value == 1 || value == 2)) o.tb_pd = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
@@ -3337,6 +3338,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "tb_ty") *value = o.tb_ty;
     else if (k == "chain_store_x") *value = o.chain_store_x;
     else if (k == "vd_col_dict") *value = o.vd_col_dict;
+    else if (k == "symd_pair_ids") *value = o.symd_pair_ids;
     else if (k == "tb_pd") *value = o.tb_pd;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;

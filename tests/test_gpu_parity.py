@@ -958,7 +958,8 @@ def test_sym_dia_bit_exact(ctx, kind, n, seed, order, rows, vd):
                                     ("poisson3d", 33)])
 @pytest.mark.parametrize("order", [0, 1])
 @pytest.mark.parametrize("ch", [2, 4])
-def test_symd_units_per_block_bit_exact(ctx, kind, n, order, ch):
+@pytest.mark.parametrize("pid", [1, 0])
+def test_symd_units_per_block_bit_exact(ctx, kind, n, order, ch, pid):
     """k_rows_symd with CH 512-row units per block (symd_chunks; a unit count that CH does not
     divide leaves the last block's tail units idle): SpMV, residual, Jacobi bit-exact with the
     oracle."""
@@ -970,7 +971,7 @@ def test_symd_units_per_block_bit_exact(ctx, kind, n, order, ch):
     rng = np.random.default_rng(n + ch)
     xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
     x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
-    with _with_option("symd_chunks", ch):
+    with _with_option("symd_chunks", ch), _with_option("symd_pair_ids", pid):
         mul(y, A, x)
         assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
         residual(y, A, x, b)
