@@ -995,7 +995,7 @@ template <int OP, int NU, int CH = 1>
 __global__ __launch_bounds__(kBlock) void k_rows_symd(
     int nrows, int ncols, const uint8_t* __restrict__ tid, const double* __restrict__ vtab,
     const uint32_t* __restrict__ mtab, int nv, const SymDia sd, const double* __restrict__ x,
-    const double* __restrict__ b, double* __restrict__ y, double omega, bool pair_ids = true) {
+    const double* __restrict__ b, double* __restrict__ y, double omega, bool pair_ids = true, int main = -1) {
     constexpr int RB = 2 * kBlock;  // rows per unit
     constexpr int P = CH < 2 ? CH : 2;
     static_assert(CH % P == 0, "units in pairs");
@@ -1004,6 +1004,8 @@ __global__ __launch_bounds__(kBlock) void k_rows_symd(
     const int xcd = bid & 7, u0 = (bid >> 3) * CH;
     const int nunits = sd.nbands * sd.eighth;
     const int64_t n = nrows;
+    double vmain[NU + 1] = {};  // the main class's values and mask (fast path; main >= 0)
+    uint32_t mmain = 0;
 #pragma unroll 1
     for (int k0 = 0; k0 < CH; k0 += P) {
         int64_t ib[P];
@@ -1063,19 +1065,39 @@ __global__ __launch_bounds__(kBlock) void k_rows_symd(
         if (k0 == 0) {  // (uniform)
             symtab_fill<NU>(tab, vtab, mtab, nv);
             __syncthreads();
+            if (main >= 0) {
+#pragma unroll
+                for (int c = 0; c <= NU; ++c) vmain[c] = tab.v[main][c];
+                mmain = tab.m[main];
+            }
         }
 #pragma unroll
         for (int q = 0; q < P; ++q) {
+            // fast path (main >= 0): every row of the wave and every mirror row is of the main
+            // class — its values are the same table entry for all of them, read once (broadcast)
+            bool mine = main >= 0 && (tw[q] & 0xffu) == (uint32_t)main && (tw[q] >> 8) == (uint32_t)main;
+#pragma unroll
+            for (int c = 0; c < NU; ++c) mine = mine && tl[q][0][c] == (uint32_t)main && tl[q][1][c] == (uint32_t)main;
+            const bool fast = __all(mine);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const uint32_t t = r == 0 ? (tw[q] & 0xffu) : (tw[q] >> 8);
-                const uint32_t m = tab.m[t];
+                uint32_t m;
                 double v[2 * NU + 1];
+                if (fast) {
+                    m = mmain;
 #pragma unroll
-                for (int c = 0; c < NU; ++c) v[c] = tab.v[tl[q][r][c]][1 + (NU - 1 - c)];
-                v[NU] = tab.v[t][0];
+                    for (int c = 0; c <= NU; ++c) v[NU + c] = vmain[c];
 #pragma unroll
-                for (int c = 0; c < NU; ++c) v[NU + 1 + c] = tab.v[t][1 + c];
+                    for (int c = 0; c < NU; ++c) v[c] = v[NU + NU - c];  // U_c of the same class
+                } else {
+                    m = tab.m[t];
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) v[c] = tab.v[tl[q][r][c]][1 + (NU - 1 - c)];
+                    v[NU] = tab.v[t][0];
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) v[NU + 1 + c] = tab.v[t][1 + c];
+                }
                 double s = 0.0;
 #pragma unroll
                 for (int k = 0; k < 2 * NU + 1; ++k) {
@@ -2091,18 +2113,21 @@ void launch_sym_nu(const pamg_mat& A, const double* x, const double* b, double* 
             if (ch == 2) {
                 k_rows_symd<OP, NU, 2><<<g, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab,
                                                             sd.d_mtab, sd.vd_n, sd, x, b, y, omega,
-                                                            options().symd_pair_ids != 0);
+                                                            options().symd_pair_ids != 0,
+                                                            options().symd_fast ? sd.vd_main : -1);
                 return;
             }
             if (ch == 4) {
                 k_rows_symd<OP, NU, 4><<<g, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab,
                                                             sd.d_mtab, sd.vd_n, sd, x, b, y, omega,
-                                                            options().symd_pair_ids != 0);
+                                                            options().symd_pair_ids != 0,
+                                                            options().symd_fast ? sd.vd_main : -1);
                 return;
             }
         }
         k_rows_symd<OP, NU><<<grid, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab,
-                                                  sd.vd_n, sd, x, b, y, omega, options().symd_pair_ids != 0);
+                                                  sd.vd_n, sd, x, b, y, omega, options().symd_pair_ids != 0,
+                                                  options().symd_fast ? sd.vd_main : -1);
         return;
     }
     if (sd.rpl == 2) {

@@ -145,6 +145,8 @@ struct Options {
                                // Jacobi -4..-5 %, 4: -1..-2 %; same-box A/B profiles/r04_g_c2/, r04_g_c4/)
     int tb_ty = 16;            // tile height of the row-class chain (k_sym_tbd): 16, or 8 (half the LDS: two
                                // workgroups per CU)
+    int symd_fast = 1;         // launch-time: waves whose rows and mirrors are all of the main class take its
+                               // values from registers (no per-row table reads)
     int symd_pair_ids = 1;     // launch-time: k_rows_symd loads mirror-row class ids as aligned pairs
     int vd_col_dict = 0;       // upload: per-tile column dictionaries also for 4-bit value-dictionary sets
     int chain_store_x = 0;     // 1: the pipelined chain also stores its post-smoothed iterate (never read)
@@ -203,6 +205,7 @@ struct SymDia {
     // class d_tid[i]; class e's values d_vtab[e * (nu + 1) + {0: D, 1 + c: U_c}], mask d_mtab[e]
     // (the in-set flag included); the lower value a(i, i - o_c) is U_c of class d_tid[i - o_c]
     int vd_n = 0;
+    int vd_main = 0;                // the most frequent class (k_rows_symd's register fast path)
     uint8_t* d_tid = nullptr;       // nrows (+ pad)
     double* d_vtab = nullptr;
     uint32_t* d_mtab = nullptr;

@@ -1220,6 +1220,18 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
                 for (int c = 0; c <= nu; ++c) std::memcpy(&vtab[(size_t)e * (nu + 1) + c], &tab[e][1 + c], 8);
             }
             sd.vd_n = nv;
+            // the most frequent class (a grid's interior rows): k_rows_symd's register fast path
+            std::vector<int64_t> cnt(nv, 0);
+            {
+                std::mutex mu;
+                par_for(n, [&](int64_t a, int64_t b) {
+                    std::vector<int64_t> c(nv, 0);
+                    for (int64_t i = a; i < b; ++i) ++c[tid[i]];
+                    std::lock_guard<std::mutex> lk(mu);
+                    for (int e = 0; e < nv; ++e) cnt[e] += c[e];
+                });
+            }
+            sd.vd_main = (int)(std::max_element(cnt.begin(), cnt.end()) - cnt.begin());
         }
     }
     if (sd.vd_n) {
@@ -3302,6 +3314,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "chain_store_x" && (value == 0 || value == 1)) o.chain_store_x = (int)value;
     else if (k == "vd_col_dict" && (value == 0 || value == 1)) o.vd_col_dict = (int)value;
     else if (k == "symd_pair_ids" && (value == 0 || value == 1)) o.symd_pair_ids = (int)value;
+    else if (k == "symd_fast" && (value == 0 || value == 1)) o.symd_fast = (int)value;
     else if (k == "tb_pd" && (value == 1 || value == 2)) o.tb_pd = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
@@ -3339,6 +3352,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "chain_store_x") *value = o.chain_store_x;
     else if (k == "vd_col_dict") *value = o.vd_col_dict;
     else if (k == "symd_pair_ids") *value = o.symd_pair_ids;
+    else if (k == "symd_fast") *value = o.symd_fast;
     else if (k == "tb_pd") *value = o.tb_pd;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;

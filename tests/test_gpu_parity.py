@@ -961,8 +961,9 @@ def test_sym_dia_bit_exact(ctx, kind, n, seed, order, rows, vd):
 @pytest.mark.parametrize("pid", [1, 0])
 def test_symd_units_per_block_bit_exact(ctx, kind, n, order, ch, pid):
     """k_rows_symd with CH 512-row units per block (symd_chunks; a unit count that CH does not
-    divide leaves the last block's tail units idle): SpMV, residual, Jacobi bit-exact with the
-    oracle."""
+    divide leaves the last block's tail units idle), with (pid 1) or without (0) the mirror ids
+    as pair loads and the main-class register fast path: SpMV, residual, Jacobi bit-exact with
+    the oracle."""
     from parallel_amg_amd._lib import layout_of
     M = _sym_grid(kind, n)
     with _with_option("tile_order", order), _with_option("sym_rows", 2), _with_option("sym_vd", 1):
@@ -971,7 +972,7 @@ def test_symd_units_per_block_bit_exact(ctx, kind, n, order, ch, pid):
     rng = np.random.default_rng(n + ch)
     xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
     x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
-    with _with_option("symd_chunks", ch), _with_option("symd_pair_ids", pid):
+    with _with_option("symd_chunks", ch), _with_option("symd_pair_ids", pid), _with_option("symd_fast", pid):
         mul(y, A, x)
         assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
         residual(y, A, x, b)
