@@ -1157,18 +1157,44 @@ def test_prolongator_value_dictionary_row_lengths_bit_exact(ctx, rl8, lengths):
     assert lay["vd"] and lay["c24"] and lay["rl8"] == bool(rl8 and short), lay
 
 
-@pytest.mark.parametrize("kind,n", [("poisson3d", 64), ("aniso3d", 48), ("poisson2d", 300), ("poisson3d", 40)])
-def test_prolongator_column_and_value_dictionaries_bit_exact(ctx, kind, n):
-    """vd_col_dict: an AMG prolongator's tiles keep their 4-bit value dictionaries and take
-    per-tile column dictionaries (anchored or row-relative) in the descriptor kernel instead of
-    24-bit columns: SpMV, residual and prolongate-add bit-exact with the oracle, and the
-    operator streams fewer bytes than without."""
+def _grid_prolongator(n, nvals, seed):
+    """A prolongator of the 512^3 P0's shape on an n^3 grid: 2 x 2 x 2 aggregates in
+    lexicographic order, each fine row reading its own aggregate and, per direction, the
+    neighbour aggregate on its side (ascending columns, clipped at the boundary), values from a
+    palette of nvals — <= 16 distinct values per tile (4-bit value dictionaries) and a few
+    anchored column offsets per tile."""
+    rng = np.random.default_rng(seed)
+    m = n // 2
+    z, y, x = np.meshgrid(np.arange(n), np.arange(n), np.arange(n), indexing="ij")
+    X, Y, Z = x.ravel() // 2, y.ravel() // 2, z.ravel() // 2
+    sx = np.where(x.ravel() % 2 == 0, -1, 1)
+    sy = np.where(y.ravel() % 2 == 0, -1, 1)
+    sz = np.where(z.ravel() % 2 == 0, -1, 1)
+    cols = [Z * m * m + Y * m + X]
+    for (ax, s_) in ((X, sx), (Y, sy), (Z, sz)):
+        nb = ax + s_
+        ok = (nb >= 0) & (nb < m)
+        c = cols[0] + np.where(ax is X, s_, np.where(ax is Y, s_ * m, s_ * m * m))
+        cols.append(np.where(ok, c, -1))
+    C = np.stack(cols, axis=1)
+    C.sort(axis=1)
+    rowptr = np.zeros(n ** 3 + 1, np.int64)
+    valid = C >= 0
+    rowptr[1:] = np.cumsum(valid.sum(axis=1))
+    col = C[valid].astype(np.int64)
+    pal = 0.03125 * (1 + np.arange(nvals))
+    val = pal[rng.integers(0, nvals, col.size)]
+    return O.CSR(rowptr, col, val, m ** 3)
+
+
+@pytest.mark.parametrize("n,nvals", [(64, 6), (48, 16), (32, 3)])
+def test_prolongator_column_and_value_dictionaries_bit_exact(ctx, n, nvals):
+    """vd_col_dict: a prolongator whose tiles hold <= 16 values (4-bit value dictionaries, the
+    512^3 P0's layout) also takes per-tile column dictionaries (anchored or row-relative) in the
+    descriptor kernel instead of 24-bit columns: SpMV, residual and prolongate-add bit-exact with
+    the oracle, and fewer streamed bytes than without."""
     from parallel_amg_amd._lib import layout_of
-    be = pa.SequentialBackend(1)
-    A, offs, xs = pa.generate_problem(be, kind, n)
-    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=200))
-    P = H.levels[0][0].P
-    M = O.CSR(P.rowptr.copy(), P.col.astype(np.int64), P.val.copy(), P.ncols)
+    M = _grid_prolongator(n, nvals, n)
     rng = np.random.default_rng(n)
     with _with_option("vd_col_dict", 0):
         A0 = _layout_ops_match_oracle(ctx, M, rng)
