@@ -145,9 +145,11 @@ struct Options {
                                // Jacobi -4..-5 %, 4: -1..-2 %; same-box A/B profiles/r04_g_c2/, r04_g_c4/)
     int tb_ty = 16;            // tile height of the row-class chain (k_sym_tbd): 16, or 8 (half the LDS: two
                                // workgroups per CU)
-    int symd_fast = 1;         // launch-time: waves whose rows and mirrors are all of the main class take its
-                               // values from registers (no per-row table reads)
-    int symd_pair_ids = 1;     // launch-time: k_rows_symd loads mirror-row class ids as aligned pairs
+    int symd_fast = 0;         // launch-time: waves whose rows and mirrors are all of the main class take its
+                               // values from registers (no per-row table reads; +0.3 %, more VGPRs:
+                               // profiles/r04_m_fast/)
+    int symd_pair_ids = 0;     // launch-time: k_rows_symd loads mirror-row class ids as aligned pairs
+                               // (+0.3…1 %: profiles/r04_m_pid/)
     int vd_col_dict = 0;       // upload: per-tile column dictionaries also for 4-bit value-dictionary sets
     int chain_store_x = 0;     // 1: the pipelined chain also stores its post-smoothed iterate (never read)
     int sym_stream = 0;        // > 0: one-sweep row-class operators on a whole grid stream planes (k_sym_tbs)
