@@ -44,3 +44,15 @@ def test_per_part_bytes_scale_with_the_slab():
                                               n_own_cols=rows, n_ghost=2 * plane), 0)
     assert parts * mid > full  # ghosts are re-read by both neighbours
     assert abs(parts * mid - full) / full < 0.01
+
+
+def test_chain_bytes_per_launch_512():
+    """The pipelined chain's algorithmic bytes (bench.py roofline for k_sym_tbd<3>): the matrix
+    once, in0 and b, and the outputs it stores — the pre-smoothed iterate and the residual
+    (chain_store_x 0, the default), plus the post-smoothed iterate with chain_store_x 1."""
+    n = 512 ** 3
+    A0 = SimpleNamespace(nnz=_nnz_grid(512, 3), nrows=n, n_own_cols=n, n_ghost=0)
+    two = AMGSolver.csr_bytes(A0, 2)
+    three = AMGSolver.csr_bytes(A0, 3)
+    assert two == 12 * A0.nnz + 36 * n + 4 == 16_087_252_996
+    assert three - two == 8 * n
