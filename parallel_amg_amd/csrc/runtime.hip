@@ -347,6 +347,16 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows, bo
             tnnz = 4096;
         else if (nz >= (int64_t)opt.long_tiles_min * nr && nz >= int64_t(32) * 4096 * device_cus())
             tnnz = 2048;
+    } else if (opt.long_tiles && !square && !tall && tnnz == 1024 && !rows.empty()) {
+        // Round 4: a restriction with 24 .. 47 nonzeros per row on a set large enough for the
+        // rule above (512^3 R0: 32 per row, anchored dictionary in tile-major slots) takes
+        // 2048-nonzero tiles: 1.09-1.10 -> 1.03 ms (4096: 1.03), profiles/r04_p/kbench_tn.jsonl;
+        // the long-row R1 (~150 per row) stays at 1024 (2048 / 4096: +14-16 %, r03)
+        int64_t nz = 0;
+        for (int r : rows) nz += rp[r + 1] - rp[r];
+        const int64_t nr = (int64_t)rows.size();
+        if (nz >= (int64_t)opt.long_tiles_min * nr && nz < 48 * nr && nz >= int64_t(32) * 4096 * device_cus())
+            tnnz = 2048;
     }
     ts->tile_nnz = tnnz;
     std::vector<int4> tiles;

@@ -721,6 +721,23 @@ def test_restriction_takes_anchored_dictionary(ctx, novd):
     assert lay["anchored"] and lay["tm"] and lay["cd"] == 8 and lay["cd_offsets"] <= 256, lay
 
 
+@pytest.mark.parametrize("tnnz", [1024, 2048, 4096])
+def test_restriction_anchored_tiles_bit_exact(ctx, tnnz):
+    """The level-0 restriction (anchored 8-bit dictionary, 8-bit value dictionary, tile-major
+    slots) on 1024-, 2048- (the 512^3 R0's budget since round 4) and 4096-nonzero tiles: SpMV,
+    residual and prolongate-add bit-exact with the oracle."""
+    from parallel_amg_amd._lib import layout_of
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 40)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=100))
+    R = H.levels[0][0].R
+    M = O.CSR(R.rowptr.copy(), R.col.astype(np.int64), R.val.copy(), R.ncols)
+    with _with_option("tile_nnz", tnnz):
+        D = _layout_ops_match_oracle(ctx, M, np.random.default_rng(tnnz))
+    lay = layout_of(D)
+    assert lay["anchored"] and lay["tm"] and lay["tile_nnz"] == tnnz, lay
+
+
 @pytest.mark.parametrize("seed,n,density,weak,iso", [(1, 3000, 0.003, 0.3, 0.02), (2, 5000, 0.001, 0.0, 0.0),
                                                      (3, 2500, 0.01, 0.6, 0.05), (4, 4000, 0.002, 0.2, 0.1)])
 def test_vcycle_random_spd_bit_exact(ctx, seed, n, density, weak, iso):
