@@ -12,6 +12,10 @@
 #              three --pmc passes (requests by size; DRAM / L2 hits / writes; SQ wave-cycle split)
 #   part       tools/part_bench.py: one part (3 of 8 z-slabs of 512^3) timed alone (the T_8 model)
 #   kbench     tools/kbench.py --n 512 --levels 2 timings (KB_ARGS overrides)
+#   world      the in-process device-world tests (tests/test_gpu_local_world.py)
+#   stream / chain / sub   parity subsets: streamed sweeps; chain variants; -k "$SUB_K"
+#   cab        tools/cycle_ab.py: same-box A/B of a cycle-level option (CAB_ARGS overrides)
+#   census     tools/xsr_census.py 512 (per-tile x-run census of the level-1 operator)
 # Output: gpurun_out/TAG/.
 set -euo pipefail
 export TMPDIR=/tmp
