@@ -86,11 +86,20 @@ int pamg_comm_init_host(pamg_ctx* ctx, int nranks, int rank, pamg_host_comm_fn f
  * rendezvous in the world and move data by device-to-device copies along the plans' send/recv
  * lists — straight from the sibling's vector into the ghost slots (hipMemcpyAsync with peer
  * access across GPUs; siblings may share one GPU). Synchronous like the host transport: no
- * overlap, no graph capture. A rank that does not arrive within 300 s fails the collective
- * (PAMG_E_STATE) on every rank. The world lives until it and all its contexts are destroyed. */
+ * overlap, no graph capture. Ghost exchanges meet pairwise: a part waits only for the
+ * neighbours its plan lists with a non-zero count, and each pair's exchanges are matched by
+ * sequence number and plan tag (pamg_plan_set_tag) — parts whose schedules diverge fail with
+ * PAMG_E_STATE instead of exchanging the wrong vectors. All-reduce / all-gather meet every rank.
+ * A rank that does not arrive within 300 s, a failed collective, a failed part of a
+ * pamg_world_* call or pamg_world_abort marks the world broken: every waiting and later
+ * collective fails (PAMG_E_STATE) at once. pamg_world_reset clears that — call it only when no
+ * rank is inside a library call. The world lives until it and all its contexts are destroyed. */
 typedef struct pamg_world pamg_world;
 int pamg_world_create(int nparts, pamg_world** out);
 int pamg_world_destroy(pamg_world* w);
+int pamg_world_abort(pamg_world* w);
+int pamg_world_reset(pamg_world* w);
+int pamg_world_state(pamg_world* w, int* broken);
 int pamg_comm_init_local(pamg_ctx* ctx, pamg_world* w, int rank);
 /* All parts of a world at once (one host thread per part inside, each on its own context; for
  * callers with one host thread, e.g. PartitionedArrays with_debug's map over the parts): the
@@ -112,6 +121,10 @@ int pamg_world_pcg(pamg_world* w, pamg_hier* const* H, pamg_vec* const* x, pamg_
 int pamg_plan_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, int n_nbr,
                      const int32_t* nbr_rank, const int64_t* recv_counts,
                      const int64_t* send_counts, const int64_t* send_idx, pamg_plan** out);
+/* Identity of the index space a plan describes (e.g. "level 2, the columns of R"), the same
+ * number on every part; default 0. The in-process world refuses to pair two parts' exchanges
+ * whose plans carry different tags (RCCL and the host transport ignore it). */
+int pamg_plan_set_tag(pamg_plan* plan, int64_t tag);
 int pamg_plan_destroy(pamg_plan* plan);
 
 /* ------------------------------------------------------------------ vectors (PVector) */

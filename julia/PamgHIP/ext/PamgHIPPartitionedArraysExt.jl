@@ -337,14 +337,21 @@ function _localize(M::HostCSR, pl::Union{Nothing,HostPlan})
     (copy(rp), lc, copy(v), pl.n_own + length(pl.ghost_ids))
 end
 
-_device_plan(ctx, pl::HostPlan) = isempty(pl.nbrs) ? nothing :
-    ExchangePlan(ctx, pl.n_own, length(pl.ghost_ids), Int32.(pl.nbrs .- 1), pl.recv_counts,
-                 pl.send_counts, pl.send_idx .+ 1)
-
-function _upload(ctx, M::HostCSR, pl::Union{Nothing,HostPlan})
-    rp, c, v, nc = _localize(M, pl)
-    DeviceMatrix(ctx, rp, c, v, nc; plan = pl === nothing ? nothing : _device_plan(ctx, pl), index_base = 0)
+# tag = the plan's index-space identity, the same on every part (pamg_plan_set_tag; the
+# hierarchy's plans: 1 + 3 (level - 1) + (A 0, P 1, R 2), as parallel_amg_amd/solver.py plan_tag)
+function _device_plan(ctx, pl::HostPlan, tag::Integer = 0)
+    isempty(pl.nbrs) && return nothing
+    p = ExchangePlan(ctx, pl.n_own, length(pl.ghost_ids), Int32.(pl.nbrs .- 1), pl.recv_counts,
+                     pl.send_counts, pl.send_idx .+ 1)
+    tag != 0 && PamgHIP.set_tag!(p, tag)
+    p
 end
+
+function _upload(ctx, M::HostCSR, pl::Union{Nothing,HostPlan}, tag::Integer = 0)
+    rp, c, v, nc = _localize(M, pl)
+    DeviceMatrix(ctx, rp, c, v, nc; plan = pl === nothing ? nothing : _device_plan(ctx, pl, tag), index_base = 0)
+end
+_plan_tag(l, op) = 1 + 3 * (l - 1) + (op === :A ? 0 : op === :P ? 1 : 2)
 
 function _gather_full(mats, offs)
     rp_all = _allgather(map(M -> PamgHIP.arrays(M)[1], mats))
@@ -445,10 +452,11 @@ function HIPPVCycle(ctxs, A::PSparseMatrix; theta::Real = 0.02, max_coarse::Inte
     # goes through map, so the same code runs under with_debug and with_mpi)
     L = length(levels)
     none = map(_ -> nothing, ctxs)
-    dA = [map(_upload, ctxs, lev[:A], lev[:planA]) for lev in levels]
+    dA = [map((c, M, pl) -> _upload(c, M, pl, _plan_tag(l, :A)), ctxs, levels[l][:A], levels[l][:planA]) for l in 1:L]
     withP = [l for l in 1:L if haskey(levels[l], :P)]
-    dP = [map(_upload, ctxs, levels[l][:P], (tail !== nothing && l == L) ? none : levels[l][:planP]) for l in withP]
-    dR = [map(_upload, ctxs, levels[l][:R], levels[l][:planR]) for l in withP]
+    dP = [map((c, M, pl) -> _upload(c, M, pl, _plan_tag(l, :P)), ctxs, levels[l][:P],
+              (tail !== nothing && l == L) ? none : levels[l][:planP]) for l in withP]
+    dR = [map((c, M, pl) -> _upload(c, M, pl, _plan_tag(l, :R)), ctxs, levels[l][:R], levels[l][:planR]) for l in withP]
     om = [lev[:omega] for lev in levels]
     if tail === nothing
         # coarsest level: every part assembles the whole matrix and the same inverse
@@ -485,7 +493,8 @@ function LinearAlgebra.ldiv!(x::HIPPVector, M::HIPPVCycle, b::HIPPVector)
     else  # one V-cycle from zero per ldiv! (the preconditioner), all parts in one call
         xs = collect(x.parts)
         foreach(v -> fill!(v, 0.0), xs)
-        PamgHIP.world_vcycle!(w, xs, collect(M.parts), collect(b.parts); ncycles = first(collect(M.parts)).ncycles)
+        PamgHIP.world_vcycle!(w, xs, collect(M.parts), collect(b.parts); ncycles = first(collect(M.parts)).ncycles,
+                               hist = false)
     end
     x
 end

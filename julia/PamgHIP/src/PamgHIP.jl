@@ -26,7 +26,7 @@ export Context, ExchangePlan, DeviceVector, DeviceMatrix, HostCSR, VCycle, Excha
        download_own, download_ghosts, exchange_begin, residual!, jacobi!, jacobi_residual!, vcycle!, pcg!, set_sweeps!,
        set_perm!, setup_hierarchy, gen_grid, gen_xstar, read_mtx, rcm_order, locality_order, unique_id,
        comm_init!, runtime_versions, hip, World, world_spmv!, world_exchange!, world_dot, world_vcycle!,
-       world_pcg!
+       world_pcg!, world_abort!, world_reset!, world_broken, set_tag!
 
 """
     hip(ctxs, A::PSparseMatrix) / hip(ctxs, x::PVector)
@@ -162,14 +162,30 @@ function world_dot(w::World, xs, ys)
                 w.h, _handles(xs), _handles(ys), out))
     out[]
 end
-"ncycles V-cycles on every part's hierarchy; returns the residual history (part 1's = all parts')."
-function world_vcycle!(w::World, xs, Ms, bs; ncycles::Integer = 1)
-    hist = zeros(Float64, ncycles)
+"""
+    world_vcycle!(w, xs, Ms, bs; ncycles = 1, hist = true)
+
+ncycles V-cycles on every part's hierarchy; returns the residual history (part 1's = all
+parts'), or `nothing` with `hist = false` — then no residual norm (and no all-reduce) is
+computed per cycle and stationary runs take the pipelined cycles (the preconditioner's case).
+"""
+function world_vcycle!(w::World, xs, Ms, bs; ncycles::Integer = 1, hist::Bool = true)
+    h = hist ? zeros(Float64, ncycles) : nothing
     check(ccall((:pamg_world_vcycle, libpamg), Cint,
                 (Ptr{Cvoid}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Cint, Ptr{Float64}),
-                w.h, _handles(Ms), _handles(xs), _handles(bs), ncycles, hist))
-    hist
+                w.h, _handles(Ms), _handles(xs), _handles(bs), ncycles, hist ? h : C_NULL))
+    h
 end
+"Mark the world broken (pamg_world_abort): parts waiting in an exchange fail instead of waiting 300 s."
+world_abort!(w::World) = check(ccall((:pamg_world_abort, libpamg), Cint, (Ptr{Cvoid},), w.h))
+"Whether the world is broken (a collective failed or was abandoned; pamg_world_state)."
+function world_broken(w::World)
+    b = Ref{Cint}(0)
+    check(ccall((:pamg_world_state, libpamg), Cint, (Ptr{Cvoid}, Ptr{Cint}), w.h, b))
+    b[] != 0
+end
+"Clear a broken world (pamg_world_reset); only when no part is inside a libpamg call."
+world_reset!(w::World) = check(ccall((:pamg_world_reset, libpamg), Cint, (Ptr{Cvoid},), w.h))
 "PCG with the V-cycle preconditioner on every part; returns (iterations, residual history)."
 function world_pcg!(w::World, xs, Ms, bs; rtol::Real = 1e-8, maxit::Integer = 100)
     it = Ref{Cint}(0)
@@ -207,6 +223,9 @@ function ExchangePlan(ctx::Context, n_own::Integer, n_ghost::Integer, nbr_ranks:
     p = ExchangePlan(h[], ctx, n_own, n_ghost)
     finalizer(close, p)
 end
+"The plan's index-space identity (pamg_plan_set_tag), the same on every part."
+set_tag!(p::ExchangePlan, tag::Integer) =
+    check(ccall((:pamg_plan_set_tag, libpamg), Cint, (Ptr{Cvoid}, Int64), p.h, tag))
 function Base.close(p::ExchangePlan)
     p.h == C_NULL && return nothing
     ccall((:pamg_plan_destroy, libpamg), Cint, (Ptr{Cvoid},), p.h)

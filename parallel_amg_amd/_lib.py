@@ -47,6 +47,9 @@ SIGNATURES = {
     "pamg_comm_init_host": [vp, i32, i32, vp, vp],
     "pamg_world_create": [i32, pvp],
     "pamg_world_destroy": [vp],
+    "pamg_world_abort": [vp],
+    "pamg_world_reset": [vp],
+    "pamg_world_state": [vp, vp],
     "pamg_comm_init_local": [vp, vp, i32],
     "pamg_world_spmv": [vp, vp, vp, vp],
     "pamg_world_exchange": [vp, vp, vp],
@@ -54,6 +57,7 @@ SIGNATURES = {
     "pamg_world_vcycle": [vp, vp, vp, vp, i32, vp],
     "pamg_world_pcg": [vp, vp, vp, vp, dbl, i32, C.POINTER(C.c_int), vp],
     "pamg_plan_create": [vp, i64, i64, i32, vp, vp, vp, vp, pvp],
+    "pamg_plan_set_tag": [vp, i64],
     "pamg_plan_destroy": [vp],
     "pamg_vec_create": [vp, i64, i64, pvp],
     "pamg_vec_destroy": [vp],

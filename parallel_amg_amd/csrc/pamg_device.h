@@ -251,6 +251,9 @@ struct pamg_plan {
     // split exchange (pamg_exchange_begin / _end): completion event on the comm stream
     hipEvent_t ev_done = nullptr;
     const void* in_flight = nullptr;  // the vector of the exchange begun and not yet ended
+    // identity of the index space the plan describes, the same on every part (pamg_plan_set_tag;
+    // 0 = untagged): the in-process world refuses to pair two parts' exchanges whose tags differ
+    int64_t tag = 0;
 };
 
 struct pamg_vec {

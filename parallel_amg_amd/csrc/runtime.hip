@@ -1343,10 +1343,15 @@ void free_tiles(pamg::TileSet& ts) {
 
 }  // namespace
 
-// In-process world of sibling contexts (pamg_comm_init_local): a generation barrier over the
-// rank threads and one posting slot per rank. Collectives post, meet, read the siblings' posts
-// (device-to-device copies on the reader's stream, after the poster's ready event), sync their
-// stream and meet again, so no post is overwritten while a sibling still reads it.
+// In-process world of sibling contexts (pamg_comm_init_local).
+// Ghost exchanges rendezvous PAIRWISE: a part meets only the neighbours its plan lists with a
+// non-zero count (so a part with no neighbours, or a decoupled pair of parts, never waits for
+// the others — ADVICE r4), and each directed pair carries a sequence number and the plan's tag,
+// so two parts whose schedules diverge fail with PAMG_E_STATE instead of exchanging the wrong
+// vectors. All-reduce and all-gather are world-wide collectives: every rank
+// calls them, they meet at a generation barrier. A failed or abandoned collective marks the
+// world broken (every waiting rank fails at once); pamg_world_reset clears that once every rank
+// has returned.
 struct pamg_world {
     int n = 0;
     std::mutex mu;
@@ -1354,17 +1359,47 @@ struct pamg_world {
     int arrived = 0;
     uint64_t gen = 0;
     bool broken = false;
+    std::string why;  // first reason the world broke
     int refs = 1;  // the creator's + one per registered context
     struct Slot {
         const double* x = nullptr;        // the posted vector / buffer
-        const pamg_plan* plan = nullptr;  // exchanges: the poster's plan
         hipEvent_t ready = nullptr;       // recorded after the work that wrote x
         double scalar = 0.0;              // all-reduce operand
     };
     std::vector<Slot> slot;
+    // directed pair (q -> p) at index q * n + p: q's post for its exchanges with p
+    struct Post {
+        uint64_t seq = 0;                 // exchanges q has posted for p so far
+        uint64_t read = 0;                // of those, the ones p has finished reading
+        const double* x = nullptr;
+        const pamg_plan* plan = nullptr;
+        hipEvent_t ready = nullptr;
+        int64_t tag = 0;
+    };
+    std::vector<Post> post;
     std::vector<pamg_ctx*> ctx;
-    // false when a rank does not come within 300 s (or an earlier meeting failed): every
-    // waiting rank then fails instead of hanging
+    static constexpr int kTimeoutS = 300;
+    void abort_locked(const char* reason) {
+        if (!broken) why = reason;
+        broken = true;
+        cv.notify_all();
+    }
+    void abort(const char* reason) {
+        std::lock_guard<std::mutex> lk(mu);
+        abort_locked(reason);
+    }
+    // wait (lock held) until pred() or the world breaks; false on a break or timeout
+    template <class P>
+    bool wait_locked(std::unique_lock<std::mutex>& lk, P pred, const char* what) {
+        if (broken) return false;
+        if (!cv.wait_for(lk, std::chrono::seconds(kTimeoutS), [&] { return pred() || broken; })) {
+            abort_locked(what);
+            return false;
+        }
+        return !broken;
+    }
+    // false when a rank does not come within 300 s (or the world broke): every waiting rank
+    // then fails instead of hanging
     bool barrier() {
         std::unique_lock<std::mutex> lk(mu);
         if (broken) return false;
@@ -1375,12 +1410,7 @@ struct pamg_world {
             cv.notify_all();
             return true;
         }
-        if (!cv.wait_for(lk, std::chrono::seconds(300), [&] { return gen != g || broken; }) || broken) {
-            broken = true;
-            cv.notify_all();
-            return false;
-        }
-        return true;
+        return wait_locked(lk, [&] { return gen != g; }, "a rank did not arrive at a collective within 300 s");
     }
     void release() {
         bool last;
@@ -1398,34 +1428,67 @@ namespace {
 // the call, so nothing overlaps them and nothing can be graph-captured
 bool sync_transport(const pamg_ctx* ctx) { return ctx->host_fn != nullptr || ctx->world != nullptr; }
 
-// The in-process exchange: every rank posts (x, plan, ready event), the ranks meet, each copies
-// the segments its neighbours' send lists hold for it straight from their vectors into its
-// ghost slots — a contiguous run by one copy, any other list by a gather kernel reading the
-// sibling's vector — waits for its copies, and the ranks meet again.
+// The in-process exchange. For every neighbour q with a non-zero count, part me posts (x, plan,
+// tag, ready event) on the pair (me -> q) under the next sequence number, waits for q's post of
+// the same number on (q -> me), checks that both posts carry the same tag and matching counts,
+// copies the segment q's send list holds for it straight from q's vector into its ghost slots —
+// a contiguous run by one copy, any other list by a gather kernel reading the sibling's vector —
+// waits for its copies, marks q's post read, and before returning waits until each neighbour has
+// read its own post (so x is not written while a sibling still reads it).
 int exchange_local(const pamg_plan* plan, double* x, hipStream_t s) {
     pamg_ctx* ctx = plan->ctx;
     pamg_world* w = ctx->world;
-    const int me = ctx->rank, nn = (int)plan->nbr.size();
-    w->slot[me].x = x;
-    w->slot[me].plan = plan;
-    w->slot[me].ready = ctx->ev_ready;
+    const int me = ctx->rank, nn = (int)plan->nbr.size(), n = w->n;
+    std::vector<int> ks;  // neighbours this exchange pairs with
+    for (int k = 0; k < nn; ++k)
+        if (plan->recv_off[k + 1] > plan->recv_off[k] || plan->send_off[k + 1] > plan->send_off[k]) ks.push_back(k);
+    if (ks.empty()) return PAMG_OK;
     HIPC(hipEventRecord(ctx->ev_ready, s));
-    if (!w->barrier()) return fail(PAMG_E_STATE, "local exchange: a sibling part did not arrive");
+    std::vector<uint64_t> seq(ks.size());
+    {
+        std::lock_guard<std::mutex> lk(w->mu);
+        if (w->broken) return fail(PAMG_E_STATE, "local exchange: the world is broken (%s)", w->why.c_str());
+        for (size_t i = 0; i < ks.size(); ++i) {
+            pamg_world::Post& p = w->post[(size_t)me * n + plan->nbr[ks[i]]];
+            p.x = x;
+            p.plan = plan;
+            p.ready = ctx->ev_ready;
+            p.tag = plan->tag;
+            seq[i] = ++p.seq;
+        }
+        w->cv.notify_all();
+    }
     int rc = PAMG_OK;
-    for (int k = 0; k < nn && rc == PAMG_OK; ++k) {
-        const int64_t cnt = plan->recv_off[k + 1] - plan->recv_off[k];
-        if (cnt == 0) continue;
-        const int q = plan->nbr[k];
-        const pamg_world::Slot& sq = w->slot[q];
+    for (size_t i = 0; i < ks.size() && rc == PAMG_OK; ++i) {
+        const int k = ks[i], q = plan->nbr[k];
+        pamg_world::Post sq;
+        {
+            std::unique_lock<std::mutex> lk(w->mu);
+            const pamg_world::Post& pq = w->post[(size_t)q * n + me];
+            if (!w->wait_locked(lk, [&] { return pq.seq >= seq[i]; }, "a neighbour part did not post its exchange within 300 s"))
+                return fail(PAMG_E_STATE, "local exchange: part %d waited for part %d: the world is broken (%s)", me, q,
+                            w->why.c_str());
+            sq = pq;
+            if (sq.seq != seq[i] || sq.tag != plan->tag) {
+                w->abort_locked("exchange pairing mismatch");
+                return fail(PAMG_E_STATE,
+                            "local exchange: part %d's exchange #%llu with part %d (plan tag %lld) met part %d's exchange "
+                            "#%llu (plan tag %lld): the parts' schedules diverged", me, (unsigned long long)seq[i], q,
+                            (long long)plan->tag, q, (unsigned long long)sq.seq, (long long)sq.tag);
+            }
+        }
         const pamg_plan* pq = sq.plan;
         int kq = -1;
         for (int j = 0; pq && j < (int)pq->nbr.size(); ++j)
             if (pq->nbr[j] == me) kq = j;
-        if (kq < 0 || pq->send_off[kq + 1] - pq->send_off[kq] != cnt) {
-            rc = fail(PAMG_E_ARG, "local exchange: part %d expects %lld ghosts from part %d, which sends %lld", me,
-                      (long long)cnt, q, kq < 0 ? 0LL : (long long)(pq->send_off[kq + 1] - pq->send_off[kq]));
-            break;
+        const int64_t cnt = plan->recv_off[k + 1] - plan->recv_off[k];
+        const int64_t scnt = plan->send_off[k + 1] - plan->send_off[k];
+        if (kq < 0 || pq->send_off[kq + 1] - pq->send_off[kq] != cnt || pq->recv_off[kq + 1] - pq->recv_off[kq] != scnt) {
+            w->abort("exchange count mismatch");
+            return fail(PAMG_E_STATE, "local exchange: part %d expects %lld ghosts from part %d, which sends %lld", me,
+                        (long long)cnt, q, kq < 0 ? 0LL : (long long)(pq->send_off[kq + 1] - pq->send_off[kq]));
         }
+        if (cnt == 0) continue;
         double* dst = x + plan->n_own + plan->recv_off[k];
         if (hipStreamWaitEvent(s, sq.ready, 0) != hipSuccess) {
             rc = fail(PAMG_E_HIP, "local exchange: stream wait failed");
@@ -1439,8 +1502,21 @@ int exchange_local(const pamg_plan* plan, double* x, hipStream_t s) {
         }
     }
     if (rc == PAMG_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PAMG_E_HIP, "local exchange: sync failed");
-    if (!w->barrier() && rc == PAMG_OK) rc = fail(PAMG_E_STATE, "local exchange: a sibling part did not arrive");
-    return rc;
+    std::unique_lock<std::mutex> lk(w->mu);
+    if (rc != PAMG_OK) {
+        w->abort_locked("a part's exchange failed");
+        return rc;
+    }
+    for (size_t i = 0; i < ks.size(); ++i) w->post[(size_t)plan->nbr[ks[i]] * n + me].read = seq[i];
+    w->cv.notify_all();
+    for (size_t i = 0; i < ks.size(); ++i) {
+        const int q = plan->nbr[ks[i]];
+        const pamg_world::Post& mine = w->post[(size_t)me * n + q];
+        if (!w->wait_locked(lk, [&] { return mine.read >= seq[i]; }, "a neighbour part did not read its exchange within 300 s"))
+            return fail(PAMG_E_STATE, "local exchange: part %d waited for part %d to read: the world is broken (%s)", me,
+                        q, w->why.c_str());
+    }
+    return PAMG_OK;
 }
 
 // sum of the ranks' *v in rank order, on every rank
@@ -2009,6 +2085,7 @@ int pamg_world_create(int nparts, pamg_world** out) {
     auto w = new pamg_world();
     w->n = nparts;
     w->slot.resize(nparts);
+    w->post.resize((size_t)nparts * nparts);
     w->ctx.assign(nparts, nullptr);
     *out = w;
     return PAMG_OK;
@@ -2016,6 +2093,29 @@ int pamg_world_create(int nparts, pamg_world** out) {
 
 int pamg_world_destroy(pamg_world* w) {
     if (w) w->release();
+    return PAMG_OK;
+}
+
+int pamg_world_abort(pamg_world* w) {
+    if (!w) return fail(PAMG_E_ARG, "world_abort: NULL");
+    w->abort("pamg_world_abort");
+    return PAMG_OK;
+}
+
+int pamg_world_reset(pamg_world* w) {
+    if (!w) return fail(PAMG_E_ARG, "world_reset: NULL");
+    std::lock_guard<std::mutex> lk(w->mu);
+    w->broken = false;
+    w->why.clear();
+    w->arrived = 0;
+    for (auto& p : w->post) p = pamg_world::Post();
+    return PAMG_OK;
+}
+
+int pamg_world_state(pamg_world* w, int* broken) {
+    if (!w || !broken) return fail(PAMG_E_ARG, "world_state: bad args");
+    std::lock_guard<std::mutex> lk(w->mu);
+    *broken = w->broken ? 1 : 0;
     return PAMG_OK;
 }
 
@@ -2071,7 +2171,10 @@ int world_each(pamg_world* w, F&& f) {
     for (int r = 0; r < w->n; ++r)
         th.emplace_back([&, r] {
             rc[r] = f(r);
-            if (rc[r] != PAMG_OK) msg[r] = pamg::last_error();
+            if (rc[r] != PAMG_OK) {
+                msg[r] = pamg::last_error();
+                w->abort("a part's call failed");  // its siblings stop waiting for it now
+            }
         });
     for (auto& t : th) t.join();
     for (int r = 0; r < w->n; ++r)
@@ -2183,6 +2286,12 @@ int pamg_plan_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, int n_nbr,
     CHECK(dalloc(&p->d_sendbuf, ns));
     if (ns) HIPC(hipMemcpy(p->d_send_idx, idx.data(), sizeof(int) * ns, hipMemcpyHostToDevice));
     *out = p.release();
+    return PAMG_OK;
+}
+
+int pamg_plan_set_tag(pamg_plan* p, int64_t tag) {
+    if (!p) return fail(PAMG_E_ARG, "plan_set_tag: NULL");
+    p->tag = tag;
     return PAMG_OK;
 }
 

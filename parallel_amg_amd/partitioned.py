@@ -204,7 +204,14 @@ class LocalWorld:
             except BaseException as e:  # noqa: BLE001 - re-raised below
                 err[p] = e
 
-        th = [threading.Thread(target=body, args=(p,), daemon=True) for p in parts]
+        def guarded(p):
+            body(p)
+            if p in err and self._h:
+                # a part that fails outside a collective would leave its siblings
+                # waiting 300 s for it; mark the world broken so they fail now
+                call("pamg_world_abort", self._h)
+
+        th = [threading.Thread(target=guarded, args=(p,), daemon=True) for p in parts]
         for t in th:
             t.start()
         for t in th:
@@ -213,6 +220,16 @@ class LocalWorld:
             p = min(err)
             raise RuntimeError(f"part {p}: {err[p]!r}") from err[p]
         return [out[p] for p in parts]
+
+    @property
+    def broken(self) -> bool:
+        v = C.c_int()
+        call("pamg_world_state", self._h, C.byref(v))
+        return bool(v.value)
+
+    def reset(self):
+        """Clear a broken world (pamg_world_reset) once every part has returned."""
+        call("pamg_world_reset", self._h)
 
     def close(self):
         # drop this object's references only: a context is destroyed when its last user (a
@@ -227,7 +244,9 @@ class LocalWorld:
 class DevicePlan:
     """Device exchange plan built from a ``HostPlan`` (``pamg_plan``)."""
 
-    def __init__(self, ctx: Context, plan: HostPlan):
+    def __init__(self, ctx: Context, plan: HostPlan, tag: int = 0):
+        """``tag``: the identity of the index space (pamg_plan_set_tag), the same on every part —
+        the in-process world refuses to pair exchanges of plans with different tags."""
         self.ctx, self.host = ctx, plan
         nb = np.asarray(plan.nbrs, np.int32)
         rc = np.asarray(plan.recv_counts, np.int64)
@@ -237,7 +256,9 @@ class DevicePlan:
         call("pamg_plan_create", ctx.handle, plan.n_own, plan.n_ghost, len(nb), ptr(nb), ptr(rc),
              ptr(sc), ptr(si), C.byref(h))
         self._h = h
-        self.n_own, self.n_ghost = plan.n_own, plan.n_ghost
+        if tag:
+            call("pamg_plan_set_tag", h, int(tag))
+        self.n_own, self.n_ghost, self.tag = plan.n_own, plan.n_ghost, int(tag)
 
     @property
     def handle(self):
@@ -294,13 +315,14 @@ class PSparseMatrix:
     """Device CSR of one part: own rows, columns local to ``plan`` (own, then ghosts)."""
 
     def __init__(self, ctx: Context, M: HCSR, plan: HostPlan | None = None,
-                 dplan: DevicePlan | None = None, row_perm=None, col_perm=None):
+                 dplan: DevicePlan | None = None, row_perm=None, col_perm=None, tag: int = 0):
         """``row_perm`` / ``col_perm`` (pamg_mat_upload_perm): device row i is row
         ``row_perm[i]`` of M, device own column k is own column ``col_perm[k]`` (None: the
-        identity); rows keep their storage order, so row sums keep their bits."""
+        identity); rows keep their storage order, so row sums keep their bits. ``tag``: the
+        column plan's identity (DevicePlan)."""
         self.ctx = ctx
         if plan is not None and dplan is None and plan.nbrs:
-            dplan = DevicePlan(ctx, plan)
+            dplan = DevicePlan(ctx, plan, tag)
         self.plan = dplan
         if plan is not None:
             col = plan.localize(M.col) if (plan.n_ghost or plan.col0) else M.col

@@ -20,6 +20,31 @@ OPS = ("jacobi_pre", "residual", "restrict", "prolong", "jacobi_post", "coarse")
 REORDER = {"off": 0, "auto": 1, "on": 2}
 
 
+def plan_tag(level: int, op: str) -> int:
+    """Tag of a hierarchy's column plan (pamg_plan_set_tag): 1 + 3 level + (A 0, P 1, R 2)."""
+    return 1 + 3 * int(level) + "APR".index(op)
+
+
+class _LevelOps:
+    """Read-only sequence view of an AMGSolver's level operators: index 0 resolves through
+    ``fine_operator()`` (the caller's numbering), every other index is ``A_dev[l]``."""
+
+    def __init__(self, solver):
+        self._s = solver
+
+    def __len__(self):
+        return len(self._s.A_dev)
+
+    def __getitem__(self, l):
+        if isinstance(l, slice):
+            return [self[i] for i in range(*l.indices(len(self)))]
+        l = range(len(self))[l]
+        return self._s.fine_operator() if l == 0 else self._s.A_dev[l]
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+
 class AMGSolver:
     def __init__(self, ctx: Context, H: HostHierarchy, part: int = 0, graph: bool | None = None,
                  reorder: str = "auto"):
@@ -57,12 +82,13 @@ class AMGSolver:
             lp = H.levels[l][part]
             pl = self.perm[l]
             pn = self.perm[l + 1] if l + 1 < H.nlevels else None
-            self.A_dev.append(PSparseMatrix(ctx, lp.A, lp.planA, row_perm=pl, col_perm=pl))
+            # plan tags (pamg_plan_set_tag): level and operator, the same on every part
+            self.A_dev.append(PSparseMatrix(ctx, lp.A, lp.planA, row_perm=pl, col_perm=pl, tag=plan_tag(l, "A")))
             self.omega.append(lp.omega)
             if l < H.nlevels - 1:
                 self.P.append(PSparseMatrix(ctx, lp.P, None if l + 1 >= rep else lp.planP,
-                                            row_perm=pl, col_perm=pn))
-                self.R.append(PSparseMatrix(ctx, lp.R, lp.planR, row_perm=pn, col_perm=pl))
+                                            row_perm=pl, col_perm=pn, tag=plan_tag(l, "P")))
+                self.R.append(PSparseMatrix(ctx, lp.R, lp.planR, row_perm=pn, col_perm=pl, tag=plan_tag(l, "R")))
         self.level_rows = [int(H.levels[l][part].A.nrows) for l in range(H.nlevels)]
         self.n_coarse = H.n_coarse
         L = self.L
@@ -84,12 +110,13 @@ class AMGSolver:
             self.set_graph(graph)
 
     @property
-    def A(self) -> list:
+    def A(self) -> "_LevelOps":
         """The level operators, level 0 in the CALLER's numbering (b = A[0] x, residuals of the
         caller's vectors): the hierarchy's own A_0 when level 0 is not permuted, else an
-        unpermuted upload made on first use (``fine_operator``). Levels >= 1 are internal to the
-        cycle and listed as the hierarchy holds them (``A_dev``)."""
-        return [self.fine_operator()] + self.A_dev[1:]
+        unpermuted upload made on first use of index 0 (``fine_operator``; ADVICE r4: ``A[l]``
+        for l >= 1 never triggers it). Levels >= 1 are internal to the cycle and listed as the
+        hierarchy holds them (``A_dev``)."""
+        return _LevelOps(self)
 
     @property
     def reordered(self) -> list:

@@ -40,6 +40,7 @@ def option(key, value):
     (3, "poisson2d", 60, 200, 0),
     (4, "poisson3d", 24, 60, 0),          # interior parts with two neighbours
     (2, "poisson2d", 20, 1000, 0),        # one level: the distributed coarsest solve
+    (2, "poisson2d", 256, 1000, 0),       # BASELINE.json configs[0] at its size (golden test below)
     (8, "poisson3d", 64, 1000, 0),        # BASELINE.json configs[2]'s part count; z-slabs: the
     (8, "aniso3d", 64, 1000, 32768),      # blocked level-0 passes run on every part (tb_part)
 ])
@@ -110,6 +111,46 @@ def test_local_world_vcycle_bit_exact(built, nparts, kind, n, max_coarse, agglom
         gid, gv = ghosts[p]
         if A0[0].plan is not None and len(gid):
             assert np.array_equal(bits(gv), bits(got_x[gid]))
+
+
+def test_baseline_config0_golden(built):
+    """BASELINE.json configs[0] — 2D 5-pt Poisson 256 x 256, 2 parts, the PartitionedArrays
+    sequential-backend shape — on the HIP path (both parts in one process, the device world) against
+    the committed fixture tests/golden/poisson2d_256_p2.npz (tests/golden/make_golden.py: 10 V-cycles
+    of the oracle's 2-part, decoupled hierarchy): b, x after 10 cycles by sha256, bit for bit, the
+    leading 64 entries of x, and the residual history to 1e-12."""
+    import hashlib
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "poisson2d_256_p2.npz"))
+    kind, n, nparts = str(g["kind"]), int(g["n"]), int(g["nparts"])
+    ncycles, max_coarse = int(g["ncycles"]), int(g["max_coarse"])
+    assert (kind, n, nparts) == ("poisson2d", 256, 2)
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
+    with option("poison_ghosts", 1):
+        W = LocalWorld(nparts)
+        try:
+            be = pa.SequentialBackend(nparts)
+            A, offs, xs = pa.generate_problem(be, kind, n)
+            H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=max_coarse, agglomerate=0),
+                                   device=W.ctxs[0])
+            assert H.nlevels == int(g["nlevels"])
+            S = [AMGSolver(W.ctxs[p], H, part=p) for p in range(nparts)]
+            A0 = [s.A[0] for s in S]
+            xst = [PVector(W.ctxs[p], A0[p].n_own_cols, A0[p].n_ghost, xs[p]) for p in range(nparts)]
+            b = [PVector(W.ctxs[p], A0[p].nrows) for p in range(nparts)]
+            W.run(lambda p: mul(b[p], A0[p], xst[p]))
+            x = [s.new_vector() for s in S]
+            hist = W.run(lambda p: S[p].vcycle(x[p], b[p], ncycles, res_hist=True))
+            got_b = np.concatenate([v.own_values() for v in b])
+            got_x = np.concatenate([v.own_values() for v in x])
+        finally:
+            del S
+            W.close()
+    assert sha(got_b) == str(g["b_sha"])
+    assert np.array_equal(bits(got_x[:64]), bits(g["x"]))
+    assert sha(got_x) == str(g["x_sha"])
+    for p in range(nparts):
+        np.testing.assert_allclose(hist[p], g["res_hist"], rtol=1e-12)
 
 
 def test_local_world_rejects_a_second_transport(built):
@@ -208,3 +249,122 @@ def test_part_bench_rowop_stage_vectors_need_ghost_slots(built):
         del Ad
     finally:
         W.close()
+
+
+def _two_plans(nparts=2, n_own=10):
+    """Two exchange plans over the same 2-part index space with EQUAL counts between the parts
+    (3 ghosts each way) but different ghost ids: tags 1 and 2."""
+    from parallel_amg_amd.hierarchy import build_plans
+    be = pa.SequentialBackend(nparts)
+    offs = np.array([0, n_own, 2 * n_own], np.int64)
+    pa_ = build_plans(be, {0: np.array([10, 11, 12]), 1: np.array([7, 8, 9])}, offs)
+    pb_ = build_plans(be, {0: np.array([15, 16, 17]), 1: np.array([0, 1, 2])}, offs)
+    return pa_, pb_
+
+
+def test_local_world_mismatched_pairing_fails(built):
+    """part 0 exchanging plan A while part 1 exchanges plan B (same counts
+    between the two parts) must fail on both parts (PAMG_E_STATE, tags differ) instead of moving
+    B's rows into A's ghost slots; after pamg_world_reset the correctly paired exchange runs and
+    lands the owners' values."""
+    from parallel_amg_amd.partitioned import DevicePlan
+    hA, hB = _two_plans()
+    W = LocalWorld(2)
+    try:
+        pA = [DevicePlan(W.ctxs[p], hA[p], tag=1) for p in range(2)]
+        pB = [DevicePlan(W.ctxs[p], hB[p], tag=2) for p in range(2)]
+        v = [PVector(W.ctxs[p], 10, 3, np.arange(10.0) + 10 * p) for p in range(2)]
+        with pytest.raises(RuntimeError, match="schedules diverged|broken"):
+            W.run(lambda p: consistent(v[p], pA[p] if p == 0 else pB[p]))
+        assert W.broken
+        W.reset()
+        assert not W.broken
+        W.run(lambda p: consistent(v[p], pA[p]))
+        assert np.array_equal(v[0].ghost_values(), [10.0, 11.0, 12.0])
+        assert np.array_equal(v[1].ghost_values(), [7.0, 8.0, 9.0])
+        W.run(lambda p: consistent(v[p], pB[p]))
+        assert np.array_equal(v[0].ghost_values(), [15.0, 16.0, 17.0])
+        assert np.array_equal(v[1].ghost_values(), [0.0, 1.0, 2.0])
+        del pA, pB, v
+    finally:
+        W.close()
+
+
+def test_local_world_failed_part_releases_siblings(built):
+    """a part that fails before an exchange (here a Python exception) breaks the
+    world at once, so its sibling's exchange fails within seconds instead of waiting 300 s."""
+    import time
+    from parallel_amg_amd.partitioned import DevicePlan
+    hA, _hB = _two_plans()
+    W = LocalWorld(2)
+    try:
+        pA = [DevicePlan(W.ctxs[p], hA[p], tag=1) for p in range(2)]
+        v = [PVector(W.ctxs[p], 10, 3, np.arange(10.0)) for p in range(2)]
+
+        def body(p):
+            if p == 0:
+                raise ValueError("part 0 gives up")
+            consistent(v[p], pA[p])
+
+        t = time.time()
+        with pytest.raises(RuntimeError, match="part 0"):
+            W.run(body)
+        assert time.time() - t < 60
+        assert W.broken
+        W.reset()
+        W.run(lambda p: consistent(v[p], pA[p]))
+        del pA, v
+    finally:
+        W.close()
+
+
+def test_local_world_part_without_neighbours(built):
+    """a part whose operator has no neighbour (a decoupled block) never meets
+    the others at an exchange; the coupled parts still exchange, pairwise. Two decoupled 2D Poisson
+    blocks, the first split over parts 0 and 1, the second all on part 2: b = A x* and x after 4
+    V-cycles equal the oracle's 3-part setup bit for bit."""
+    import scipy.sparse as sp
+    from parallel_amg_amd.hcsr import HCSR
+    nb = 20
+    whole, _o, _x = pa.generate_problem(pa.SequentialBackend(1), "poisson2d", nb)
+    M1 = whole[0]
+    B = sp.csr_matrix((M1.val, M1.col, M1.rowptr), shape=(M1.nrows, M1.nrows))
+    Mbd = sp.block_diag([B, B], format="csr")
+    Mbd.sort_indices()
+    n = Mbd.shape[0]
+    rng = np.random.default_rng(3)
+    xstar = rng.uniform(-1, 1, n)
+    offs = np.array([0, n // 4, n // 2, n], np.int64)
+    rp, col, val = Mbd.indptr.astype(np.int64), Mbd.indices.astype(np.int64), Mbd.data.copy()
+    A, xs = {}, {}
+    for p in range(3):
+        a, c = int(offs[p]), int(offs[p + 1])
+        lo, hi = int(rp[a]), int(rp[c])
+        A[p] = HCSR.from_arrays(rp[a:c + 1] - lo, col[lo:hi].copy(), val[lo:hi].copy(), n)
+        xs[p] = np.ascontiguousarray(xstar[a:c])
+    ncycles = 4
+    with option("poison_ghosts", 1):
+        W = LocalWorld(3)
+        try:
+            be = pa.SequentialBackend(3)
+            H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=40, agglomerate=0), device=W.ctxs[0])
+            assert not H.levels[0][2].planA.nbrs and H.levels[0][0].planA.nbrs
+            S = [AMGSolver(W.ctxs[p], H, part=p) for p in range(3)]
+            A0 = [s.A[0] for s in S]
+            assert A0[2].plan is None and A0[0].plan is not None
+            xst = [PVector(W.ctxs[p], A0[p].n_own_cols, A0[p].n_ghost, xs[p]) for p in range(3)]
+            b = [PVector(W.ctxs[p], A0[p].nrows) for p in range(3)]
+            W.run(lambda p: mul(b[p], A0[p], xst[p]))
+            x = [s.new_vector() for s in S]
+            W.run(lambda p: S[p].vcycle(x[p], b[p], ncycles))
+            got_b = np.concatenate([v.own_values() for v in b])
+            got_x = np.concatenate([v.own_values() for v in x])
+        finally:
+            del S
+            W.close()
+    Ao = O.CSR(rp, col, val, n)
+    bo = O.spmv(Ao, xstar)
+    Ho = O.setup(Ao, offsets=offs, max_coarse=40, agglomerate=0)
+    xo = Ho.solve(bo, ncycles)
+    assert np.array_equal(bits(got_b), bits(bo))
+    assert np.array_equal(bits(got_x), bits(xo))

@@ -12,8 +12,10 @@ workgroup, 256 workgroups), so these tests pin it against separate, unfused cycl
   bit, from x = 0 and continued from a non-zero iterate (the bench's warm-up then timed runs);
 * the temporally blocked pre-smoothing pass ``k_sym_tb<2>`` == Jacobi then residual, bit for bit.
 
-The separate cycles are themselves oracle-bit-exact at 128^3 (test_gpu_parity.py); no oracle
-run is possible at 134M rows in a test's time budget.
+* the oracle (oracle/pamg_oracle.c, OpenMP) run on the same 512^3 hierarchy (its level operators
+  handed over by ``O.hierarchy_from_levels``, as bench.py's cpu_baseline does) for 3 V-cycles from
+  x = 0 on the same b == the pipelined, graph-replayed cycles bench.py times, bit for bit
+  (~4 s of oracle work on the box's 16 host threads).
 """
 import contextlib
 import ctypes
@@ -93,6 +95,30 @@ def test_pipelined_cycles_512_bit_exact(ctx, h512):
     assert d3.size == 0, (d3.size, d3[:8], n)
     d5 = np.flatnonzero(bits(got5) != bits(ref[5]))
     assert d5.size == 0, (d5.size, d5[:8], n)
+
+
+def test_timed_path_512_matches_oracle(ctx, h512):
+    """The bench's timed call (vcycle_async: graph replay of the cross-cycle pipeline) against the
+    CPU oracle's V-cycle on the same 512^3 hierarchy, 3 cycles from x = 0, bit for bit."""
+    from oracle import oracle as O
+    S, b = h512
+    H = S._H
+    lv = [H.levels[l][0] for l in range(H.nlevels)]
+    Ho = O.hierarchy_from_levels([p.A for p in lv], [p.P for p in lv[:-1]], [p.R for p in lv[:-1]],
+                                 [p.omega for p in lv], H.ainv)
+    bh = b.own_values()
+    xo = Ho.solve(bh, 3)
+    del Ho
+    S.set_graph(False)
+    S.set_graph(True)
+    with option("jr_fuse", 1):
+        x = S.new_vector()
+        S.vcycle_async(x, b, 3)
+        ctx.sync()
+        assert S.graph_state()["captured"]
+        got = x.own_values()
+    d = np.flatnonzero(bits(got) != bits(xo))
+    assert d.size == 0, (d.size, d[:8], np.abs(got - xo).max())
 
 
 def test_blocked_pre_smoothing_512_bit_exact(ctx, h512):

@@ -6,6 +6,7 @@
 # steps (each GPU step under its own time limit; the first failure ends the script):
 #   tests      the whole -m gpu suite (one process)
 #   timed      the 512^3 timed-path tests + the parity file (faster than `tests`)
+#   tp         the 512^3 timed-path tests alone (oracle parity at the benchmarked size)
 #   bench      the default bench line (live PMC passes included) -> TAG/bench.json, bench.log
 #   trace      rocprofv3 --kernel-trace --stats of bench.py (5 steps, no CPU leg, no PMC)
 #   anatomy    counter anatomy of the level-0/1 row operators (A0 chain/SpMV, R0, P0, A1, R1, P1):
@@ -32,6 +33,9 @@ for step in "$@"; do
         ;;
     timed)
         timeout -k 10 800 $PYT tests/test_gpu_timed_path.py tests/test_gpu_parity.py tests/test_gpu_local_world.py -m gpu > "$OUT/timed.log" 2>&1
+        ;;
+    tp)
+        timeout -k 10 500 $PYT tests/test_gpu_timed_path.py -m gpu > "$OUT/tp.log" 2>&1
         ;;
     stream)
         timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "sym_stream or symd_units" -m gpu > "$OUT/stream.log" 2>&1
