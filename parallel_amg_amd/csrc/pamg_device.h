@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cstdint>
 #include <vector>
 
@@ -218,6 +219,9 @@ Options& options();
 
 struct pamg_ctx {
     int device = 0;
+    // references: the caller's handle + one per plan / vector / matrix / hierarchy on it
+    // (runtime.hip ctx_ref / ctx_unref); the context is torn down when the last one is dropped
+    std::atomic<int> refs{1};
     hipStream_t s_comp = nullptr;  // compute stream
     hipStream_t s_comm = nullptr;  // ghost exchange stream
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -236,6 +240,9 @@ struct pamg_ctx {
     char* stage[2] = {nullptr, nullptr};
     hipEvent_t stage_done[2] = {nullptr, nullptr};
 };
+
+void ctx_ref(pamg_ctx* ctx);
+void ctx_unref(pamg_ctx* ctx);
 
 struct pamg_plan {
     pamg_ctx* ctx = nullptr;

@@ -1975,6 +1975,18 @@ int pamg_ctx_create(int device, pamg_ctx** out) {
 
 int pamg_ctx_destroy(pamg_ctx* ctx) {
     if (!ctx) return PAMG_OK;
+    ctx_unref(ctx);
+    return PAMG_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// The context's teardown, when its last reference is dropped: the caller's handle
+// (pamg_ctx_destroy) and one per plan / vector / matrix / hierarchy made on it. So the handles
+// may be destroyed in any order — e.g. by a garbage collector that finalises a context before
+// the vectors that referenced it.
+void ctx_teardown(pamg_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->s_comp);
     (void)hipStreamSynchronize(ctx->s_comm);
@@ -1998,8 +2010,15 @@ int pamg_ctx_destroy(pamg_ctx* ctx) {
     (void)hipStreamDestroy(ctx->s_comp);
     (void)hipStreamDestroy(ctx->s_comm);
     delete ctx;
-    return PAMG_OK;
 }
+}  // namespace
+
+void ctx_ref(pamg_ctx* ctx) { ctx->refs.fetch_add(1); }
+void ctx_unref(pamg_ctx* ctx) {
+    if (ctx->refs.fetch_sub(1) == 1) ctx_teardown(ctx);
+}
+
+extern "C" {
 
 int pamg_device_count(int* n) {
     if (!n) return fail(PAMG_E_ARG, "device_count: NULL");
@@ -2285,6 +2304,7 @@ int pamg_plan_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, int n_nbr,
     CHECK(dalloc(&p->d_send_idx, ns));
     CHECK(dalloc(&p->d_sendbuf, ns));
     if (ns) HIPC(hipMemcpy(p->d_send_idx, idx.data(), sizeof(int) * ns, hipMemcpyHostToDevice));
+    ctx_ref(ctx);
     *out = p.release();
     return PAMG_OK;
 }
@@ -2302,7 +2322,9 @@ int pamg_plan_destroy(pamg_plan* p) {
     if (p->ev_done) (void)hipEventDestroy(p->ev_done);
     dfree(p->d_send_idx);
     dfree(p->d_sendbuf);
+    pamg_ctx* owner = p->ctx;
     delete p;
+    ctx_unref(owner);
     return PAMG_OK;
 }
 
@@ -2316,6 +2338,7 @@ int pamg_vec_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, pamg_vec** ou
     CHECK(dalloc(&v->d, n_own + n_ghost + kVecPad));
     HIPC(hipMemsetAsync(v->d, 0, sizeof(double) * (n_own + n_ghost + kVecPad), ctx->s_comp));
     HIPC(hipStreamSynchronize(ctx->s_comp));
+    ctx_ref(ctx);
     *out = v.release();
     return PAMG_OK;
 }
@@ -2325,7 +2348,9 @@ int pamg_vec_destroy(pamg_vec* v) {
     (void)hipSetDevice(v->ctx->device);
     (void)hipStreamSynchronize(v->ctx->s_comp);
     dfree(v->d);
+    pamg_ctx* owner = v->ctx;
     delete v;
+    ctx_unref(owner);
     return PAMG_OK;
 }
 
@@ -2645,6 +2670,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         CHECK(h2d(ctx, A->d_chi, hi.data(), sizeof(uint8_t) * hi.size()));
     }
     tr.mark("rest");
+    ctx_ref(ctx);
     *out = A.release();
     return PAMG_OK;
 }
@@ -2735,7 +2761,9 @@ int pamg_mat_destroy(pamg_mat* A) {
     dfree(A->sym.d_mtab);
     free_tiles(A->interior);
     free_tiles(A->boundary);
+    pamg_ctx* owner = A->ctx;
     delete A;
+    ctx_unref(owner);
     return PAMG_OK;
 }
 
@@ -2969,6 +2997,7 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
         HIPC(hipMemset(H->d_bsend, 0, sizeof(double) * (H->cmax + kVecPad)));
     }
     H->prof_ms.assign((size_t)L * 6, 0.0);
+    ctx_ref(ctx);
     *out = H.release();
     return PAMG_OK;
 }
@@ -3017,7 +3046,9 @@ int pamg_hier_destroy(pamg_hier* H) {
     dfree(H->px);
     dfree(H->pb);
     for (auto e : H->ev) (void)hipEventDestroy(e);
+    pamg_ctx* owner = H->ctx;
     delete H;
+    ctx_unref(owner);
     return PAMG_OK;
 }
 

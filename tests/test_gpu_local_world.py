@@ -368,3 +368,19 @@ def test_local_world_part_without_neighbours(built):
     xo = Ho.solve(bo, ncycles)
     assert np.array_equal(bits(got_b), bits(bo))
     assert np.array_equal(bits(got_x), bits(xo))
+
+
+def test_context_outlives_its_handle(built):
+    """Handles may be destroyed in any order (a garbage collector finalises the objects of a
+    reference cycle in no particular order): a context whose handle is destroyed stays alive
+    while a vector made on it exists, and is torn down with the last one."""
+    from parallel_amg_amd.partitioned import Context
+    c = Context(0)
+    v = PVector(c, 16, 0, np.arange(16.0))
+    raw = c._h
+    call("pamg_ctx_destroy", raw)
+    c._h = None
+    out = np.empty(16)
+    call("pamg_vec_download", raw, v.handle, out.ctypes.data_as(ctypes.c_void_p))
+    assert np.array_equal(out, np.arange(16.0))
+    del v
