@@ -507,6 +507,8 @@ def _sym_kname(op: int, lay: dict) -> str:
     """The symmetric-layout row kernel's instance name as rocprofv3 demangles it: k_rows_symd<OP,
     NU, CH> (row-class dictionary; CH = symd_chunks for NU <= 3), k_rows_sym2 / k_rows_sym<OP, NU>."""
     nu = lay["cd_offsets"]
+    if lay.get("sym_vd") and lay.get("jr_fused") and nu == 3 and _option("sym_zm"):
+        return f"k_sym_zm<{op}>"  # the whole one-part grid operator's z-marching sweep
     if lay.get("sym_vd"):
         return f"k_rows_symd<{op}, {nu}, {_option('symd_chunks') if nu <= 3 else 1}>"
     return f"k_rows_sym{'2' if lay['sym_rows'] == 2 else ''}<{op}, {nu}>"

@@ -1630,139 +1630,188 @@ __global__ __launch_bounds__((TbShape<S, TY>::threads)) void k_sym_tbd(int nrows
     }
 }
 
-// ---- k_sym_tbs<OP,PD>: ONE sweep (SpMV, residual or Jacobi) of the row-class dictionary operator
-// streamed plane by plane like k_sym_tbd (Options::sym_stream; one part, tb_ok): a 576-thread
-// workgroup owns a 64 x 16 column of the grid over a z-chunk, keeps the x window of planes
-// k-1 .. k+1 (tile + 1 line / 2 points around it) in a 4-slot LDS ring — so one barrier per plane —
-// and reads the 7 neighbour values of a row pair from LDS instead of 7 global loads. The loads of
-// plane k+PD's class ids and b and of plane k+1+PD's window are issued before the barrier of plane
-// k and consumed PD steps later. Every value is k_rows_symd's expression (same classes, same
-// order: SPEC §S3 bits). No halo recompute: the window's extra lines are L2 hits of the
-// neighbour tiles' lines.
-struct TbsRow {
-    uint16_t own;  // as TbdRow (narrow until use)
-    uint8_t m0;
-    uint16_t m1;
-    double b[2];
+// ---- k_sym_zm<OP>: ONE sweep (SpMV, residual or Jacobi) of a whole one-part 7-point grid operator
+// in the row-class dictionary (SymDia::vd_n, tb_ok), marching along z (Options::sym_zm; round 5,
+// VERDICT r4 next-3). The shape is the one tools/stencil_ceiling.hip measured closest to the copy
+// rate for a 7-point sweep at 512^3 (constant coefficients: 0.39 ms against 0.35 for y = x and
+// 0.66-0.81 ms for 7 global loads per row pair, profiles/r05_c/): a 256-thread workgroup owns a
+// kTbX x kTbY xy tile over a chunk of planes; each thread holds two row pairs (lines ly, ly + 8)
+// and keeps their x of planes k-1, k, k+1 (+ k+2 in flight) and their class ids of planes k-1, k
+// in registers, so the z neighbours and the -M mirror class never touch LDS; only plane k's x and
+// ids (tile + a one-point / one-line halo) go through a double-buffered LDS plane, one barrier per
+// plane. Every load a step issues is consumed one step later. The products, their order (ascending
+// class: -M, -nx, -1, 0, +1, +nx, +M), the mask selects and the epilogue are k_rows_symd's, so
+// are the bits (SPEC §S3). Preconditions (tb_ok): nx % kTbX == 0, ny % kTbY == 0, every row in
+// the set, no row reaching across a grid face (points outside the grid meet clear mask bits).
+constexpr int kZmThreads = 256;
+constexpr int kZmPX = kTbX / 2;            // row pairs per tile line
+constexpr int kZmW = kZmPX + 2;            // LDS line: the left halo pair, 32 pairs, the right halo pair
+constexpr int kZmHalo = 2 * kZmPX + 2 * kTbY;  // halo pairs of a plane: lines y0-1, y0+16; pairs x0-2, x0+64
+
+struct ZmHalo {      // one halo item of the next plane, as loaded
+    double2 x;
+    uint16_t id;
 };
 
-template <bool NEEDB>
-__device__ __forceinline__ void tbs_load(TbsRow& c, const uint8_t* __restrict__ tid, const double* __restrict__ b,
-                                         const SymDia& sd, int64_t i, int64_t n) {
-    c.own = *reinterpret_cast<const uint16_t*>(tid + i);
-    c.m0 = tid[i >= 1 ? i - 1 : 0];
-    c.m1 = tbd_pair_ids(tid, i - sd.off[1], n);
-    if constexpr (NEEDB) {
-        const double2 bb = *reinterpret_cast<const double2*>(b + i);
-        c.b[0] = bb.x;
-        c.b[1] = bb.y;
+__device__ __forceinline__ void zm_halo_load(ZmHalo& h, const double* __restrict__ x, const uint8_t* __restrict__ tid,
+                                             int x0, int y0, int nx, int ny, int nz, int64_t M, int q) {
+    const int t = threadIdx.x;
+    int xh = 0, yh = 0;
+    bool ok = false;
+    if (t < 2 * kZmPX) {  // lines below / above the tile
+        const int top = t / kZmPX;
+        xh = x0 + 2 * (t % kZmPX);
+        yh = top ? y0 + kTbY : y0 - 1;
+        ok = yh >= 0 && yh < ny;
+    } else if (t < kZmHalo) {  // the pairs left / right of the tile's lines
+        const int u = t - 2 * kZmPX, right = u / kTbY;
+        xh = right ? x0 + kTbX : x0 - 2;
+        yh = y0 + u % kTbY;
+        ok = xh >= 0 && xh < nx;
     }
+    ok = ok && q >= 0 && q < nz;
+    const int64_t i = ok ? (int64_t)q * M + (int64_t)yh * nx + xh : 0;
+    h.x = ok ? *reinterpret_cast<const double2*>(x + i) : make_double2(0.0, 0.0);
+    h.id = *reinterpret_cast<const uint16_t*>(tid + i);  // (outside: row 0's ids; they meet clear mask bits)
 }
 
-template <int OP, int PD>
-__device__ __forceinline__ void tbs_step(int k, TbsRow& En, const TbsRow& E0, const TbsRow& E1, TbWin<1>& win,
-                                         const TbCtx<1>& t, const uint8_t* __restrict__ tid, const SymDia& sd,
-                                         const SymTab<3>& tab, const double* __restrict__ x,
-                                         const double* __restrict__ b, double* __restrict__ y, double omega,
-                                         double (*xin)[TbShape<1>::XL][kTbLW]) {
-    using Sh = TbShape<1>;
-    if (k >= t.ze) return;  // uniform: the whole workgroup
-    tb_win_store<1>(win, xin, (k + 1) & 3);  // loaded PD steps ago
-    tb_win_load<1>(win, t, x, k + 1 + PD);
-    {
-        const int p = k + PD;
-        const bool ok = t.pos_ok && p < t.nz;
-        tbs_load<OP != OP_SPMV>(En, tid, b, sd, ok ? (int64_t)p * t.M + t.ixy : 0, t.n);
+__device__ __forceinline__ void zm_halo_store(const ZmHalo& h, double2 (*sx)[kZmW], uint16_t (*sid)[kZmW]) {
+    const int t = threadIdx.x;
+    int line = 0, col = 0;
+    if (t < 2 * kZmPX) {
+        line = t / kZmPX ? kTbY + 1 : 0;
+        col = 1 + t % kZmPX;
+    } else if (t < kZmHalo) {
+        const int u = t - 2 * kZmPX;
+        line = 1 + u % kTbY;
+        col = u / kTbY ? kZmPX + 1 : 0;
+    } else {
+        return;
     }
-    __syncthreads();  // xin (planes k-1 .. k+1); the slot stored next step was last read a step ago
-    if (t.own_xy) {
-        double xv[2][7];
-        tb_gather_lds<Sh::XL>(xin, (k - 1) & 3, k & 3, (k + 1) & 3, t.ry + 1, t.col, xv);
-        const uint32_t m2 = E1.own;  // the pair's ids one plane down: their U_2 are the -M values
-        const uint32_t t0 = E0.own & 0xffu, t1 = (E0.own >> 8) & 0xffu;
-        const uint32_t tr[2] = {t0, t1}, l0[2] = {E0.m0 & 0xffu, t0};
-        const uint32_t l1[2] = {E0.m1 & 0xffu, (E0.m1 >> 8) & 0xffu}, l2[2] = {m2 & 0xffu, (m2 >> 8) & 0xffu};
-        double o[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const uint32_t tc = tr[r];
-            const uint32_t m = tab.m[tc];
-            double v[7];
-            v[0] = tab.v[l2[r]][3];
-            v[1] = tab.v[l1[r]][2];
-            v[2] = tab.v[l0[r]][1];
-            v[3] = tab.v[tc][0];
-            v[4] = tab.v[tc][1];
-            v[5] = tab.v[tc][2];
-            v[6] = tab.v[tc][3];
-            double s = 0.0;
-#pragma unroll
-            for (int q = 0; q < 7; ++q) {
-                const double pr = v[q] * xv[r][q];
-                const double u = s + pr;
-                s = ((m >> q) & 1u) ? u : s;
-            }
-            if constexpr (OP == OP_SPMV) {
-                o[r] = s;
-            } else if constexpr (OP == OP_RESID) {
-                o[r] = E0.b[r] - s;
-            } else {
-                const double u = E0.b[r] - s;
-                const double w = omega * u;
-                const double q = w / v[3];
-                o[r] = xv[r][3] + q;
-            }
-        }
-        *reinterpret_cast<double2*>(y + (int64_t)k * t.M + t.ixy) = make_double2(o[0], o[1]);
-    }
+    sx[line][col] = h.x;
+    sid[line][col] = h.id;
 }
 
-template <int OP, int PD>
-__global__ __launch_bounds__(TbShape<1>::threads) void k_sym_tbs(int nrows, const uint8_t* __restrict__ tid,
-                                                                 const double* __restrict__ vtab,
-                                                                 const uint32_t* __restrict__ mtab, int nv,
-                                                                 const SymDia sd, const TbGeom g,
-                                                                 const double* __restrict__ x,
-                                                                 const double* __restrict__ b, double* __restrict__ y,
-                                                                 double omega) {
-    static_assert(PD == 1 || PD == 2, "one or two planes ahead");
-    __shared__ __attribute__((aligned(16))) double xin[4][TbShape<1>::XL][kTbLW];
+template <int OP>
+__global__ __launch_bounds__(kZmThreads) void k_sym_zm(int nrows, const uint8_t* __restrict__ tid,
+                                                       const double* __restrict__ vtab, const uint32_t* __restrict__ mtab,
+                                                       int nv, const TbGeom g, const double* __restrict__ x,
+                                                       const double* __restrict__ b, double* __restrict__ y,
+                                                       double omega) {
+    __shared__ __attribute__((aligned(16))) double2 sx[2][kTbY + 2][kZmW];
+    __shared__ __attribute__((aligned(16))) uint16_t sid[2][kTbY + 2][kZmW];
     __shared__ __attribute__((aligned(16))) SymTab<3> tab;
-    TbCtx<1> t;
-    if (!tb_ctx_init<1>(t, g, nrows)) return;  // the whole workgroup, before any barrier
-    symtab_fill<3>(tab, vtab, mtab, nv);       // (read after the first step's barrier)
-    const int k0 = t.zs;
-    TbWin<1> wa, wb;
+    const int ntiles = g.tiles_x * g.tiles_y * g.zchunks;
+    const int per = (ntiles + 7) / 8;
+    const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);  // consecutive tiles on one XCD
+    if (lin >= ntiles) return;  // the whole workgroup, before any barrier
+    const int ty = lin % g.tiles_y, tx = (lin / g.tiles_y) % g.tiles_x, zc = lin / (g.tiles_x * g.tiles_y);
+    const int z0 = zc * g.zlen, z1 = min(g.nz, z0 + g.zlen);
+    if (z0 >= z1) return;
+    const int x0 = tx * kTbX, y0 = ty * kTbY;
+    const int64_t M = (int64_t)g.nx * g.ny;
+    const int px = threadIdx.x % kZmPX, ly = threadIdx.x / kZmPX;  // ly 0..7: lines ly, ly + 8
+    int64_t ixy[2];
 #pragma unroll
-    for (int q = -1; q <= 0; ++q) {
-        tb_win_load<1>(wa, t, x, k0 + q);
-        tb_win_store<1>(wa, xin, (k0 + q) & 3);
-    }
-    tb_win_load<1>(wa, t, x, k0 + 1);
-    if constexpr (PD == 2) tb_win_load<1>(wb, t, x, k0 + 2);
-    // the id ring: planes k+PD .. k-1
-    TbsRow e0{}, e1{}, e2{}, e3{};
-    auto load = [&](TbsRow& e, int p) {
-        const bool ok = t.pos_ok && p >= 0 && p < t.nz;
-        tbs_load<OP != OP_SPMV>(e, tid, b, sd, ok ? (int64_t)p * t.M + t.ixy : 0, t.n);
+    for (int h = 0; h < 2; ++h) ixy[h] = (int64_t)(y0 + ly + 8 * h) * g.nx + x0 + 2 * px;
+    symtab_fill<3>(tab, vtab, mtab, nv);  // (read after the first barrier)
+    auto ldx = [&](int q, int h) {
+        return q >= 0 && q < g.nz ? *reinterpret_cast<const double2*>(x + (int64_t)q * M + ixy[h]) : make_double2(0.0, 0.0);
     };
-    load(PD == 1 ? e2 : e3, k0 - 1);
-    load(e0, k0);
-    if constexpr (PD == 2) load(e1, k0 + 1);
-    if constexpr (PD == 1) {  // planes k+1, k, k-1
-        for (int k = k0; k < t.ze; k += 3) {
-            tbs_step<OP, PD>(k, e1, e0, e2, wa, t, tid, sd, tab, x, b, y, omega, xin);
-            tbs_step<OP, PD>(k + 1, e2, e1, e0, wa, t, tid, sd, tab, x, b, y, omega, xin);
-            tbs_step<OP, PD>(k + 2, e0, e2, e1, wa, t, tid, sd, tab, x, b, y, omega, xin);
-        }
-    } else {  // planes k+2, k+1, k, k-1; windows wa / wb alternate
-        for (int k = k0; k < t.ze; k += 4) {
-            tbs_step<OP, PD>(k, e2, e0, e3, wa, t, tid, sd, tab, x, b, y, omega, xin);
-            tbs_step<OP, PD>(k + 1, e3, e1, e0, wb, t, tid, sd, tab, x, b, y, omega, xin);
-            tbs_step<OP, PD>(k + 2, e0, e2, e1, wa, t, tid, sd, tab, x, b, y, omega, xin);
-            tbs_step<OP, PD>(k + 3, e1, e3, e2, wb, t, tid, sd, tab, x, b, y, omega, xin);
-        }
+    auto ldid = [&](int q, int h) -> uint32_t {
+        return q >= 0 && q < g.nz ? *reinterpret_cast<const uint16_t*>(tid + (int64_t)q * M + ixy[h]) : 0u;
+    };
+    auto ldb = [&](int q, int h) {
+        if constexpr (OP == OP_SPMV) return make_double2(0.0, 0.0);
+        return q < g.nz ? *reinterpret_cast<const double2*>(b + (int64_t)q * M + ixy[h]) : make_double2(0.0, 0.0);
+    };
+    double2 xm[2], xc[2], xp[2], xn[2], bc[2], bn[2];
+    uint32_t idm[2], idc[2], idn[2];
+    ZmHalo hc, hn;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        xm[h] = ldx(z0 - 1, h);
+        xc[h] = ldx(z0, h);
+        xp[h] = ldx(z0 + 1, h);
+        idm[h] = ldid(z0 - 1, h);
+        idc[h] = ldid(z0, h);
+        bc[h] = ldb(z0, h);
     }
+    zm_halo_load(hc, x, tid, x0, y0, g.nx, g.ny, g.nz, M, z0);
+    for (int k = z0; k < z1; ++k) {
+        const int sl = k & 1;
+        // plane k into LDS (own pairs and halo), then the loads the next step consumes
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            sx[sl][1 + ly + 8 * h][1 + px] = xc[h];
+            sid[sl][1 + ly + 8 * h][1 + px] = (uint16_t)idc[h];
+        }
+        zm_halo_store(hc, sx[sl], sid[sl]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            xn[h] = ldx(k + 2, h);
+            idn[h] = ldid(k + 1, h);
+            bn[h] = ldb(k + 1, h);
+        }
+        zm_halo_load(hn, x, tid, x0, y0, g.nx, g.ny, g.nz, M, k + 1);
+        __syncthreads();  // plane k's slot; the slot stored next step was last read a step ago
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int ry = 1 + ly + 8 * h, col = 1 + px;
+            const double2 lft = sx[sl][ry][col - 1], rgt = sx[sl][ry][col + 1];
+            const double2 dn = sx[sl][ry - 1][col], up = sx[sl][ry + 1][col];
+            const uint32_t idl = sid[sl][ry][col - 1], idd = sid[sl][ry - 1][col];
+            const double xv[2][7] = {{xm[h].x, dn.x, lft.y, xc[h].x, xc[h].y, up.x, xp[h].x},
+                                     {xm[h].y, dn.y, xc[h].x, xc[h].y, rgt.x, up.y, xp[h].y}};
+            const uint32_t t0 = idc[h] & 0xffu, t1 = idc[h] >> 8;
+            const uint32_t tr[2] = {t0, t1}, l0[2] = {idl >> 8, t0};
+            const uint32_t l1[2] = {idd & 0xffu, idd >> 8}, l2[2] = {idm[h] & 0xffu, idm[h] >> 8};
+            const double bv[2] = {bc[h].x, bc[h].y};
+            double o[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const uint32_t tc = tr[r];
+                const uint32_t m = tab.m[tc];
+                double v[7];
+                v[0] = tab.v[l2[r]][3];  // a(i, i-M)  = U_2 of row i-M
+                v[1] = tab.v[l1[r]][2];  // a(i, i-nx) = U_1 of row i-nx
+                v[2] = tab.v[l0[r]][1];  // a(i, i-1)  = U_0 of row i-1
+                v[3] = tab.v[tc][0];
+                v[4] = tab.v[tc][1];
+                v[5] = tab.v[tc][2];
+                v[6] = tab.v[tc][3];
+                double sacc = 0.0;
+#pragma unroll
+                for (int q = 0; q < 7; ++q) {
+                    const double p = v[q] * xv[r][q];
+                    const double u = sacc + p;
+                    sacc = ((m >> q) & 1u) ? u : sacc;
+                }
+                if constexpr (OP == OP_SPMV) {
+                    o[r] = sacc;
+                } else if constexpr (OP == OP_RESID) {
+                    o[r] = bv[r] - sacc;
+                } else {
+                    const double u = bv[r] - sacc;
+                    const double w = omega * u;
+                    const double q = w / v[3];
+                    o[r] = xv[r][3] + q;
+                }
+            }
+            *reinterpret_cast<double2*>(y + (int64_t)k * M + ixy[h]) = make_double2(o[0], o[1]);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            xm[h] = xc[h];
+            xc[h] = xp[h];
+            xp[h] = xn[h];
+            idm[h] = idc[h];
+            idc[h] = idn[h];
+            bc[h] = bn[h];
+        }
+        hc = hn;
+    }
+    (void)nrows;
 }
 
 template <int OP>
@@ -2091,18 +2140,19 @@ void launch_sym_nu(const pamg_mat& A, const double* x, const double* b, double* 
     const SymDia& sd = A.sym;
     const int grid = sd.nbands * 8 * sd.eighth;
     if constexpr (NU == 3) {
-        // streamed one-sweep kernel (Options::sym_stream): the whole one-part grid operator
-        if (sd.vd_n && sd.tb_ok && !sd.tb_part && options().sym_stream > 0 && sd.plane0 == 0 &&
-            sd.nbands == sd.tb.nz && (int64_t)sd.band == (int64_t)sd.tb.nx * sd.tb.ny && A.nrows % 2 == 0) {
+        // the whole one-part grid operator: the z-marching sweep (Options::sym_zm)
+        if (sd.vd_n && sd.tb_ok && !sd.tb_part && options().sym_zm && sd.plane0 == 0 && sd.nbands == sd.tb.nz &&
+            (int64_t)sd.band == (int64_t)sd.tb.nx * sd.tb.ny && A.nrows % 2 == 0) {
             TbGeom g = sd.tb;
-            g.zlo = 0;
-            g.zhi = g.nz;
-            g.zchunks = std::max(1, std::min(options().sym_stream, g.nz));
-            g.zlen = (g.nz + g.zchunks - 1) / g.zchunks;
+            const int tiles = g.tiles_x * g.tiles_y;
+            // z chunks: ~4 workgroups per CU (1024), chunks of >= 16 planes; zm_chunks overrides
+            int zc = options().zm_chunks > 0 ? options().zm_chunks : std::min((1024 + tiles - 1) / tiles, g.nz / 16);
+            zc = std::max(1, std::min(zc, g.nz));
+            g.zlen = (g.nz + zc - 1) / zc;
             g.zchunks = (g.nz + g.zlen - 1) / g.zlen;
-            const int gr = (g.tiles_x * g.tiles_y * g.zchunks + 7) / 8 * 8;
-            k_sym_tbs<OP, 1><<<gr, TbShape<1>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab,
-                                                                sd.vd_n, sd, g, x, b, y, omega);
+            const int gr = (tiles * g.zchunks + 7) / 8 * 8;
+            k_sym_zm<OP><<<gr, kZmThreads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n, g, x, b, y,
+                                                   omega);
             return;
         }
     }

@@ -153,8 +153,9 @@ struct Options {
                                // (+0.3…1 %: profiles/r04_m_pid/)
     int vd_col_dict = 0;       // upload: per-tile column dictionaries also for 4-bit value-dictionary sets
     int chain_store_x = 0;     // 1: the pipelined chain also stores its post-smoothed iterate (never read)
-    int sym_stream = 0;        // > 0: one-sweep row-class operators on a whole grid stream planes (k_sym_tbs)
-                               // in this many z-chunks per 64 x 16 tile column; 0: k_rows_symd
+    int sym_zm = 1;            // 1: one-sweep ops of a whole one-part row-class grid operator march along z
+                               //    (k_sym_zm); 0: k_rows_symd
+    int zm_chunks = 0;         // z chunks per tile column of k_sym_zm (0: ~4 workgroups per CU)
     int xsr_kernel = 0;        // staged sets: 0 row lanes (k_rows_xsr), 1 nonzero lanes (k_rows_tm, 2048-nonzero tiles)
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)

@@ -1002,11 +1002,13 @@ def test_symd_units_per_block_bit_exact(ctx, kind, n, order, ch, pid):
 @pytest.mark.parametrize("kind,shape", [("poisson3d", (64, 64, 64)), ("aniso3d", (64, 64, 64)),
                                         ("poisson3d", (128, 128, 128)), ("poisson3d", (64, 32, 40)),
                                         ("aniso3d", (192, 48, 7))])
-@pytest.mark.parametrize("zch", [1, 3, 8])
-def test_sym_stream_bit_exact(ctx, kind, shape, zch):
-    """k_sym_tbs (sym_stream = z-chunks per tile column: one sweep streamed plane by plane, x from
-    a 4-slot LDS window ring): SpMV, residual and two Jacobi sweeps bit-exact with the oracle,
-    with chunk boundaries inside the grid (3, 8) and one chunk per column (1)."""
+@pytest.mark.parametrize("zch", [0, 1, 3, 8])
+def test_sym_zm_bit_exact(ctx, kind, shape, zch):
+    """k_sym_zm (the default one-sweep kernel of a whole one-part grid operator: marches along z,
+    x and ids of planes k-1..k+1 in registers, plane k's in-plane neighbours through a
+    double-buffered LDS plane; zm_chunks = z chunks per tile column, 0 = auto): SpMV, residual
+    and two Jacobi sweeps bit-exact with the oracle, with chunk boundaries inside the grid (3, 8),
+    one chunk per column (1) and the automatic split (0)."""
     from parallel_amg_amd._lib import layout_of
     M = O.generate(kind, *shape)
     Ad, _h = upload(ctx, M)
@@ -1015,7 +1017,7 @@ def test_sym_stream_bit_exact(ctx, kind, shape, zch):
     rng = np.random.default_rng(shape[2] + zch)
     xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
     x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
-    with _with_option("sym_stream", zch):
+    with _with_option("zm_chunks", zch):
         mul(y, Ad, x)
         assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
         residual(y, Ad, x, b)

@@ -38,7 +38,7 @@ for step in "$@"; do
         timeout -k 10 500 $PYT tests/test_gpu_timed_path.py -m gpu > "$OUT/tp.log" 2>&1
         ;;
     stream)
-        timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "sym_stream or symd_units" -m gpu > "$OUT/stream.log" 2>&1
+        timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "sym_zm or symd_units" -m gpu > "$OUT/stream.log" 2>&1
         ;;
     chain)
         timeout -k 10 400 $PYT tests/test_gpu_parity.py -k "chain_two_planes or jacobi_residual_op or pipelined_cycles" -m gpu > "$OUT/chain.log" 2>&1
