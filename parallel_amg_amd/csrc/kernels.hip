@@ -2141,8 +2141,10 @@ void launch_sym_nu(const pamg_mat& A, const double* x, const double* b, double* 
     const int grid = sd.nbands * 8 * sd.eighth;
     if constexpr (NU == 3) {
         // the whole one-part grid operator: the z-marching sweep (Options::sym_zm)
-        if (sd.vd_n && sd.tb_ok && !sd.tb_part && options().sym_zm && sd.plane0 == 0 && sd.nbands == sd.tb.nz &&
-            (int64_t)sd.band == (int64_t)sd.tb.nx * sd.tb.ny && A.nrows % 2 == 0) {
+        // (plane0 == 0 and the bands covering every row: not a plane window of launch_sym_planes)
+        if (sd.vd_n && sd.tb_ok && !sd.tb_part && options().sym_zm && sd.plane0 == 0 &&
+            (int64_t)sd.nbands * sd.band >= A.nrows && A.nrows == (int64_t)sd.tb.nx * sd.tb.ny * sd.tb.nz &&
+            A.nrows % 2 == 0) {
             TbGeom g = sd.tb;
             const int tiles = g.tiles_x * g.tiles_y;
             // z chunks: ~4 workgroups per CU (1024), chunks of >= 16 planes; zm_chunks overrides
