@@ -1630,6 +1630,184 @@ __global__ __launch_bounds__((TbShape<S, TY>::threads)) void k_sym_tbd(int nrows
     }
 }
 
+// ---- k_sym_zc<S>: the S dependent sweeps of k_sym_tbd (same tiles, halos, activity ranges,
+// row expressions — so the same bits) restructured the way k_sym_zm marches (round 5): every
+// thread owns one row pair of stage 0's region for the whole z range, so the z neighbours of
+// every stage (in0 of planes k-1, k+1; stage 0 of k-2, k; stage 1 of k-3, k-1) sit in its own
+// registers, and only in-plane neighbours go through LDS — one double-buffered plane per stage.
+// A stage's LDS plane is stored at the start of the step AFTER the one that computed it, so the
+// three stages of a step (stage 0 on plane k, stage 1 on k-1, stage 2 on k-2) read only data
+// stored before the step's single barrier: one barrier per plane instead of three, and the
+// stages' loads and arithmetic interleave within a thread. Every global load a step issues
+// (in0 of plane k+2, the class ids and b of plane k+1, the in0 halo of plane k+1) is consumed
+// one step later.
+template <int S>
+struct ZcShape {
+    static constexpr int H = S - 1;               // stage-0 halo in y (lines) and z (planes)
+    static constexpr int RY = kTbY + 2 * H;       // stage-0 lines
+    static constexpr int NT = kTbPX * RY;         // stage-0 row pairs (positions), one per thread
+    static constexpr int threads = (NT + 63) / 64 * 64;
+    static constexpr int XL = RY + 2;             // in0 plane: stage 0's region + one line / pair around
+    static constexpr int XW = kTbPX + 2;
+    static constexpr int NHALO = 2 * XW + 2 * RY; // in0 halo pairs: lines 0, XL-1; pairs 0, XW-1 of the others
+    static_assert(NHALO <= threads, "one halo pair per thread at most");
+};
+
+template <int S>
+__device__ __forceinline__ void zc_halo_load(double2& v, const TbCtx<S>& t, const double* __restrict__ in0, int q) {
+    using Sh = ZcShape<S>;
+    const int h = threadIdx.x;
+    int line = 0, col = 0;
+    if (h < 2 * Sh::XW) {
+        line = h < Sh::XW ? 0 : Sh::XL - 1;
+        col = h % Sh::XW;
+    } else {
+        const int u = h - 2 * Sh::XW;
+        line = 1 + u % Sh::RY;
+        col = u / Sh::RY ? Sh::XW - 1 : 0;
+    }
+    const int x = t.x0 - 4 + 2 * col, y = t.y0 - Sh::H - 1 + line;
+    const bool ok = h < Sh::NHALO && x >= 0 && x < t.nx && y >= 0 && y < t.ny && q >= 0 && q < t.nz;
+    v = ok ? *reinterpret_cast<const double2*>(in0 + (int64_t)q * t.M + (int64_t)y * t.nx + x) : make_double2(0.0, 0.0);
+}
+
+template <int S>
+__device__ __forceinline__ void zc_halo_store(const double2& v, double2 (*sin)[ZcShape<S>::XW]) {
+    using Sh = ZcShape<S>;
+    const int h = threadIdx.x;
+    if (h >= Sh::NHALO) return;
+    if (h < 2 * Sh::XW) {
+        sin[h < Sh::XW ? 0 : Sh::XL - 1][h % Sh::XW] = v;
+    } else {
+        const int u = h - 2 * Sh::XW;
+        sin[1 + u % Sh::RY][u / Sh::RY ? Sh::XW - 1 : 0] = v;
+    }
+}
+
+// the 7 neighbour values of the pair at (line, column) of an LDS plane, z from registers
+__device__ __forceinline__ void zc_gather(const double2* __restrict__ dn_line, const double2* __restrict__ line,
+                                          const double2* __restrict__ up_line, int col, const double2& own,
+                                          const double2& zm, const double2& zp, double (&xv)[2][7]) {
+    const double2 lft = line[col - 1], rgt = line[col + 1], dn = dn_line[col], up = up_line[col];
+    xv[0][0] = zm.x;  xv[1][0] = zm.y;
+    xv[0][1] = dn.x;  xv[1][1] = dn.y;
+    xv[0][2] = lft.y; xv[1][2] = own.x;
+    xv[0][3] = own.x; xv[1][3] = own.y;
+    xv[0][4] = own.y; xv[1][4] = rgt.x;
+    xv[0][5] = up.x;  xv[1][5] = up.y;
+    xv[0][6] = zp.x;  xv[1][6] = zp.y;
+}
+
+template <int S>
+__global__ __launch_bounds__(ZcShape<S>::threads) void k_sym_zc(int nrows, const uint8_t* __restrict__ tid,
+                                                                 const double* __restrict__ vtab,
+                                                                 const uint32_t* __restrict__ mtab, int nv,
+                                                                 const SymDia sd, const TbArgs ta) {
+    using Sh = ZcShape<S>;
+    static_assert(S == 2 || S == 3, "two or three sweeps");
+    __shared__ __attribute__((aligned(16))) double2 sin[2][Sh::XL][Sh::XW];
+    __shared__ __attribute__((aligned(16))) double2 s0l[2][Sh::RY][Sh::XW];
+    __shared__ __attribute__((aligned(16))) double2 s1l[S == 3 ? 2 : 1][S == 3 ? Sh::RY : 1][Sh::XW];
+    __shared__ __attribute__((aligned(16))) SymTab<3> tab;
+    TbCtx<S> t;
+    if (!tb_ctx_init<S>(t, sd.tb, nrows)) return;  // the whole workgroup, before any barrier
+    symtab_fill<3>(tab, vtab, mtab, nv);            // (read after the first barrier)
+    const int T = threadIdx.x;
+    const bool has = t.ry >= 0;                     // a stage-0 position
+    const int ry = has ? t.ry : 0, col = has ? (T % kTbPX) + 1 : 1;  // LDS column of the pair
+    // the stage planes' pad columns (0, XW-1) are read only by pairs whose affected element is
+    // discarded; zero them once so no stale LDS enters even a discarded value
+    if (T < 2 * Sh::RY) {
+        const int l = T % Sh::RY, c = T < Sh::RY ? 0 : Sh::XW - 1;
+        for (int q = 0; q < 2; ++q) {
+            s0l[q][l][c] = make_double2(0.0, 0.0);
+            if constexpr (S == 3) s1l[q][l][c] = make_double2(0.0, 0.0);
+        }
+    }
+    const int k0 = t.zs - Sh::H;
+    auto ldx = [&](int q) {
+        return t.pos_ok && q >= 0 && q < t.nz ? *reinterpret_cast<const double2*>(ta.in0 + (int64_t)q * t.M + t.ixy)
+                                              : make_double2(0.0, 0.0);
+    };
+    auto ldrow = [&](TbdRow& e, int q) {
+        const bool ok = t.pos_ok && q >= 0 && q < t.nz;
+        tbd_load(e, tid, ta.b, sd, ok ? (int64_t)q * t.M + t.ixy : 0, t.n);
+    };
+    const double2 zero = make_double2(0.0, 0.0);
+    double2 xm = ldx(k0 - 1), xc = ldx(k0), xp = ldx(k0 + 1), xn = zero;
+    double2 hc, hn;
+    zc_halo_load<S>(hc, t, ta.in0, k0);
+    TbdRow En{}, E0{}, E1{}, E2{}, E3{};
+    ldrow(E0, k0);
+    ldrow(E1, k0 - 1);
+    double2 s0m1 = zero, s0m2 = zero;  // stage 0 of planes k-1, k-2
+    double2 s1m2 = zero, s1m3 = zero;  // stage 1 of planes k-2, k-3
+    constexpr int hz = Sh::H - 1;
+    for (int k = k0; k < t.kend; ++k) {
+        const int a = k & 1, a1 = (k - 1) & 1, a2 = (k - 2) & 1;
+        // this step's LDS planes: in0 of plane k (own pair + halo), stage 0 of k-1, stage 1 of k-2
+        if (has) {
+            sin[a][ry + 1][col] = xc;
+            s0l[a1][ry][col] = s0m1;
+            if constexpr (S == 3) s1l[a2][ry][col] = s1m2;
+        }
+        zc_halo_store<S>(hc, sin[a]);
+        // next step's loads
+        xn = ldx(k + 2);
+        zc_halo_load<S>(hn, t, ta.in0, k + 1);
+        ldrow(En, k + 1);
+        __syncthreads();
+        // ---- stage 0 on plane k: a Jacobi sweep from in0
+        double2 s0k = zero;
+        if (t.pos_ok && k >= 0 && k < t.nz) {
+            double xv[2][7], o[2];
+            zc_gather(&sin[a][ry][0], &sin[a][ry + 1][0], &sin[a][ry + 2][0], col, xc, xm, xp, xv);
+            tbd_rows(tab, E0, E1.own, xv, S == 1 && ta.last_resid, ta.omega, o);
+            s0k = make_double2(o[0], o[1]);
+            if (ta.out[0] && t.own_xy && k >= t.zs && k < t.ze)
+                *reinterpret_cast<double2*>(ta.out[0] + (int64_t)k * t.M + t.ixy) = s0k;
+        }
+        // ---- stage 1 on plane k-1 from stage 0 (in-plane: the LDS plane stored this step)
+        double2 s1k = zero;
+        {
+            const int p = k - 1;
+            constexpr bool last = S == 2;
+            if (t.pos_ok && ry >= 1 && ry < Sh::RY - 1 && p >= 0 && p < t.nz && p >= t.zs - hz && p < t.ze + hz &&
+                (!last || t.own_xy)) {
+                double xv[2][7], o[2];
+                zc_gather(&s0l[a1][ry - 1][0], &s0l[a1][ry][0], &s0l[a1][ry + 1][0], col, s0m1, s0m2, s0k, xv);
+                tbd_rows(tab, E1, E2.own, xv, last && ta.last_resid, ta.omega, o);
+                s1k = make_double2(o[0], o[1]);
+                if (t.own_xy && p >= t.zs && p < t.ze)
+                    *reinterpret_cast<double2*>(ta.out[1] + (int64_t)p * t.M + t.ixy) = s1k;
+            }
+        }
+        // ---- stage 2 on plane k-2 from stage 1 (S = 3)
+        if constexpr (S == 3) {
+            const int p = k - 2;
+            if (t.own_xy && ry >= 2 && ry < Sh::RY - 2 && p >= t.zs && p < t.ze) {
+                double xv[2][7], o[2];
+                zc_gather(&s1l[a2][ry - 1][0], &s1l[a2][ry][0], &s1l[a2][ry + 1][0], col, s1m2, s1m3, s1k, xv);
+                tbd_rows(tab, E2, E3.own, xv, ta.last_resid, ta.omega, o);
+                *reinterpret_cast<double2*>(ta.out[2] + (int64_t)p * t.M + t.ixy) = make_double2(o[0], o[1]);
+            }
+        }
+        // rotate the plane rings
+        xm = xc;
+        xc = xp;
+        xp = xn;
+        hc = hn;
+        s0m2 = s0m1;
+        s0m1 = s0k;
+        s1m3 = s1m2;
+        s1m2 = s1k;
+        E3 = E2;
+        E2 = E1;
+        E1 = E0;
+        E0 = En;
+    }
+}
+
 // ---- k_sym_zm<OP>: ONE sweep (SpMV, residual or Jacobi) of a whole one-part 7-point grid operator
 // in the row-class dictionary (SymDia::vd_n, tb_ok), marching along z (Options::sym_zm; round 5,
 // VERDICT r4 next-3). The shape is the one tools/stencil_ceiling.hip measured closest to the copy
@@ -2253,6 +2431,15 @@ void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s) {
         else
             k_sym_tbd<3, 1, 8><<<gr, TbShape<3, 8>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab,
                                                                     sd.vd_n, sd, ta);
+        return;
+    }
+    if (sd.vd_n && options().tb_zc) {
+        if (ta.nstages == 2)
+            k_sym_zc<2><<<grid, ZcShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n, sd,
+                                                             ta);
+        else
+            k_sym_zc<3><<<grid, ZcShape<3>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n, sd,
+                                                             ta);
         return;
     }
     if (sd.vd_n) {

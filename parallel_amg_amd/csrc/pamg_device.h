@@ -153,6 +153,8 @@ struct Options {
                                // (+0.3…1 %: profiles/r04_m_pid/)
     int vd_col_dict = 0;       // upload: per-tile column dictionaries also for 4-bit value-dictionary sets
     int chain_store_x = 0;     // 1: the pipelined chain also stores its post-smoothed iterate (never read)
+    int tb_zc = 1;             // 1: the level-0 blocked passes (row-class dictionary) march along z with one barrier
+                               //    per plane (k_sym_zc); 0: k_sym_tbd
     int sym_zm = 1;            // 1: one-sweep ops of a whole one-part row-class grid operator march along z
                                //    (k_sym_zm); 0: k_rows_symd
     int zm_chunks = 0;         // z chunks per tile column of k_sym_zm (0: ~4 workgroups per CU)
