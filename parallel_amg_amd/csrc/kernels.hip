@@ -967,16 +967,39 @@ __global__ __launch_bounds__(kBlock) void k_rows_sym2(
 // ids are the same bytes a block o_c rows earlier read, cache hits) instead of 33. The products
 // and their order are k_rows_sym2's, so are the bits.
 template <int NU>
-struct SymTab {  // the class table in LDS: values (D, U_0 .. U_{NU-1}) per class, and masks
+struct SymTab {  // the class table in LDS: values (D, U_0 .. U_{NU-1}) per class, masks, 1 / D
     double v[kSymVdMax][NU + 1];
     uint32_t m[kSymVdMax];
+    double r[kSymVdMax];  // RN(1 / D) (div_rn)
 };
 
 template <int NU>
 __device__ __forceinline__ void symtab_fill(SymTab<NU>& t, const double* __restrict__ vtab,
                                             const uint32_t* __restrict__ mtab, int nv) {
     for (int e = threadIdx.x; e < nv * (NU + 1); e += blockDim.x) (&t.v[0][0])[e] = vtab[e];
-    for (int e = threadIdx.x; e < nv; e += blockDim.x) t.m[e] = mtab[e];
+    for (int e = threadIdx.x; e < nv; e += blockDim.x) {
+        t.m[e] = mtab[e];
+        t.r[e] = 1.0 / vtab[e * (NU + 1)];
+    }
+}
+
+// RN(w / d) given r = RN(1 / d): q0 = RN(w r) and two residual corrections through exact FMA
+// residuals (Markstein: q1 is within one ulp of w / d, so q2 = RN(q1 + (w - q1 d) r) is the
+// correctly rounded quotient) — 5 f64 operations instead of the ~11 of the IEEE division
+// sequence. Outside |w| in [2^-900, 2^900] (zeros — whose sign the sequence could lose —,
+// subnormals, huge values, inf, NaN) and for a d whose reciprocal is not a normal number, the
+// division itself. Bitwise the same as w / d (checked on 3e8 random and near-midpoint cases,
+// tools/div_check.c, and by every oracle test of the kernels that use it).
+__device__ __forceinline__ double div_rn(double w, double d, double r) {
+    const double aw = fabs(w), ar = fabs(r);
+    if (aw >= 0x1p-900 && aw <= 0x1p900 && ar >= 0x1p-900 && ar <= 0x1p900) {
+        const double q0 = w * r;
+        const double e0 = __builtin_fma(-q0, d, w);
+        const double q1 = __builtin_fma(e0, r, q0);
+        const double e1 = __builtin_fma(-q1, d, w);
+        return __builtin_fma(e1, r, q1);
+    }
+    return w / d;
 }
 
 __device__ __forceinline__ uint16_t tbd_pair_ids(const uint8_t* __restrict__ tid, int64_t j, int64_t n) {
@@ -1486,6 +1509,45 @@ __device__ __forceinline__ void tbd_rows(const SymTab<3>& tab, const TbdRow& c, 
     }
 }
 
+// tbd_rows without the mask selects and with div_rn, for the kernels whose absent entries meet
+// exact zeros (k_sym_zm, k_sym_zc: tb_ok operators, every neighbour outside the grid is held as
+// +0.0 and an absent in-grid entry is a +0.0 table value): such an entry's product is +-0, and
+// adding +-0 to the running sum leaves its bits unchanged — the sum starts at +0.0 and, rounding
+// to nearest, never becomes -0.0 — so every row sum has the masked sum's bits for finite x
+// (a non-finite x at an absent entry's neighbour would be discarded by the mask and propagates
+// here: an iterate that is already inf / NaN).
+__device__ __forceinline__ void zc_rows(const SymTab<3>& tab, const TbdRow& c, uint32_t m2, const double (&xv)[2][7],
+                                        bool resid, double omega, double (&out)[2]) {
+    const uint32_t t0 = c.own & 0xffu, t1 = (c.own >> 8) & 0xffu;
+    const uint32_t tr[2] = {t0, t1}, l0[2] = {c.m0 & 0xffu, t0};
+    const uint32_t l1[2] = {c.m1 & 0xffu, (c.m1 >> 8) & 0xffu}, l2[2] = {m2 & 0xffu, (m2 >> 8) & 0xffu};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const uint32_t t = tr[r];
+        double v[7];
+        v[0] = tab.v[l2[r]][3];  // a(i, i-M)  = U_2 of row i-M
+        v[1] = tab.v[l1[r]][2];  // a(i, i-nx) = U_1 of row i-nx
+        v[2] = tab.v[l0[r]][1];  // a(i, i-1)  = U_0 of row i-1
+        v[3] = tab.v[t][0];
+        v[4] = tab.v[t][1];
+        v[5] = tab.v[t][2];
+        v[6] = tab.v[t][3];
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const double p = v[k] * xv[r][k];
+            s = s + p;
+        }
+        if (resid) {
+            out[r] = c.b[r] - s;
+        } else {
+            const double u = c.b[r] - s;
+            const double w = omega * u;
+            out[r] = xv[r][3] + div_rn(w, v[3], tab.r[t]);
+        }
+    }
+}
+
 // one step k: En <- plane k+PD (loads issued), E0 = plane k (stage 0), E1 = k-1 (stage 1),
 // E2 = k-2 (stage 2, S = 3), E3 = k-3 (the -M ids of stage 2; of stage 1 when S = 2 it is E2);
 // win holds plane k+1's window on entry (loaded PD steps earlier), plane k+1+PD's on exit
@@ -1762,7 +1824,7 @@ __global__ __launch_bounds__(ZcShape<S>::threads) void k_sym_zc(int nrows, const
         if (t.pos_ok && k >= 0 && k < t.nz) {
             double xv[2][7], o[2];
             zc_gather(&sin[a][ry][0], &sin[a][ry + 1][0], &sin[a][ry + 2][0], col, xc, xm, xp, xv);
-            tbd_rows(tab, E0, E1.own, xv, S == 1 && ta.last_resid, ta.omega, o);
+            zc_rows(tab, E0, E1.own, xv, S == 1 && ta.last_resid, ta.omega, o);
             s0k = make_double2(o[0], o[1]);
             if (ta.out[0] && t.own_xy && k >= t.zs && k < t.ze)
                 *reinterpret_cast<double2*>(ta.out[0] + (int64_t)k * t.M + t.ixy) = s0k;
@@ -1776,7 +1838,7 @@ __global__ __launch_bounds__(ZcShape<S>::threads) void k_sym_zc(int nrows, const
                 (!last || t.own_xy)) {
                 double xv[2][7], o[2];
                 zc_gather(&s0l[a1][ry - 1][0], &s0l[a1][ry][0], &s0l[a1][ry + 1][0], col, s0m1, s0m2, s0k, xv);
-                tbd_rows(tab, E1, E2.own, xv, last && ta.last_resid, ta.omega, o);
+                zc_rows(tab, E1, E2.own, xv, last && ta.last_resid, ta.omega, o);
                 s1k = make_double2(o[0], o[1]);
                 if (t.own_xy && p >= t.zs && p < t.ze)
                     *reinterpret_cast<double2*>(ta.out[1] + (int64_t)p * t.M + t.ixy) = s1k;
@@ -1788,7 +1850,7 @@ __global__ __launch_bounds__(ZcShape<S>::threads) void k_sym_zc(int nrows, const
             if (t.own_xy && ry >= 2 && ry < Sh::RY - 2 && p >= t.zs && p < t.ze) {
                 double xv[2][7], o[2];
                 zc_gather(&s1l[a2][ry - 1][0], &s1l[a2][ry][0], &s1l[a2][ry + 1][0], col, s1m2, s1m3, s1k, xv);
-                tbd_rows(tab, E2, E3.own, xv, ta.last_resid, ta.omega, o);
+                zc_rows(tab, E2, E3.own, xv, ta.last_resid, ta.omega, o);
                 *reinterpret_cast<double2*>(ta.out[2] + (int64_t)p * t.M + t.ixy) = make_double2(o[0], o[1]);
             }
         }
@@ -1949,7 +2011,6 @@ __global__ __launch_bounds__(kZmThreads) void k_sym_zm(int nrows, const uint8_t*
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const uint32_t tc = tr[r];
-                const uint32_t m = tab.m[tc];
                 double v[7];
                 v[0] = tab.v[l2[r]][3];  // a(i, i-M)  = U_2 of row i-M
                 v[1] = tab.v[l1[r]][2];  // a(i, i-nx) = U_1 of row i-nx
@@ -1958,12 +2019,12 @@ __global__ __launch_bounds__(kZmThreads) void k_sym_zm(int nrows, const uint8_t*
                 v[4] = tab.v[tc][1];
                 v[5] = tab.v[tc][2];
                 v[6] = tab.v[tc][3];
+                // (absent entries meet exact zeros: no mask select, see zc_rows)
                 double sacc = 0.0;
 #pragma unroll
                 for (int q = 0; q < 7; ++q) {
                     const double p = v[q] * xv[r][q];
-                    const double u = sacc + p;
-                    sacc = ((m >> q) & 1u) ? u : sacc;
+                    sacc = sacc + p;
                 }
                 if constexpr (OP == OP_SPMV) {
                     o[r] = sacc;
@@ -1972,8 +2033,7 @@ __global__ __launch_bounds__(kZmThreads) void k_sym_zm(int nrows, const uint8_t*
                 } else {
                     const double u = bv[r] - sacc;
                     const double w = omega * u;
-                    const double q = w / v[3];
-                    o[r] = xv[r][3] + q;
+                    o[r] = xv[r][3] + div_rn(w, v[3], tab.r[tc]);
                 }
             }
             *reinterpret_cast<double2*>(y + (int64_t)k * M + ixy[h]) = make_double2(o[0], o[1]);

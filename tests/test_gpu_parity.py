@@ -1027,6 +1027,47 @@ def test_sym_zm_bit_exact(ctx, kind, shape, zch):
     assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.57), bh, 0.57)))
 
 
+def _cut_grid(n=64, cut=31):
+    """poisson3d n^3 with the couplings between x = cut and x = cut + 1 removed (both directions):
+    a tb_ok grid operator with absent entries INSIDE the grid (mask bits clear for in-grid
+    neighbours), so the row-class kernels' maskless sums (zc_rows) meet +0.0 table values."""
+    import scipy.sparse as sp
+    M = O.generate("poisson3d", n, n, n)
+    S = sp.csr_matrix((M.val, M.col, M.rowptr), shape=(M.nrows, M.ncols)).tocoo()
+    xr, xc = S.row % n, S.col % n
+    keep = ~(((S.col - S.row == 1) & (xr == cut)) | ((S.row - S.col == 1) & (xc == cut)))
+    T = sp.csr_matrix((S.data[keep], (S.row[keep], S.col[keep])), shape=S.shape)
+    T.sort_indices()
+    return O.CSR(T.indptr.astype(np.int64), T.indices.astype(np.int64), T.data.copy(), M.ncols)
+
+
+@pytest.mark.parametrize("zch", [0, 3])
+def test_row_class_kernels_absent_in_grid_entries(ctx, zch):
+    """k_sym_zm (SpMV, residual, Jacobi) and k_sym_zc (S = 2 through pamg_jacobi_residual; S = 3
+    through pipelined V-cycles elsewhere) on a grid with a cut plane of removed couplings: bit-exact
+    with the oracle, which sums present entries only."""
+    from parallel_amg_amd._lib import layout_of
+    from parallel_amg_amd.partitioned import jacobi_residual
+    M = _cut_grid()
+    Ad, _h = upload(ctx, M)
+    lay = layout_of(Ad)
+    assert lay["sym"] and lay["sym_vd"] and lay["jr_fused"], lay
+    rng = np.random.default_rng(19 + zch)
+    N = M.nrows
+    xh, bh = rng.standard_normal(N), rng.standard_normal(N)
+    x, b, y = PVector(ctx, N, 0, xh), PVector(ctx, N, 0, bh), PVector(ctx, N)
+    with _with_option("zm_chunks", zch):
+        mul(y, Ad, x)
+        assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
+        residual(y, Ad, x, b)
+        assert np.array_equal(bits(y.own_values()), bits(O.residual(M, xh, bh)))
+        t, r = PVector(ctx, N), PVector(ctx, N)
+        assert jacobi_residual(t, r, Ad, x, b, 0.66)
+    to = O.jacobi(M, xh, bh, 0.66)
+    assert np.array_equal(bits(t.own_values()), bits(to))
+    assert np.array_equal(bits(r.own_values()), bits(O.residual(M, to, bh)))
+
+
 @pytest.mark.parametrize("breaker", ["asym_value", "signed_zero", "unsorted_row", "diagonal_only"])
 def test_sym_dia_declines_what_it_cannot_reproduce(ctx, breaker):
     """A mirror that differs in one bit (or +0.0 against -0.0), a row whose storage order is
