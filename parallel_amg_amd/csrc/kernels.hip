@@ -1796,77 +1796,98 @@ __global__ __launch_bounds__(ZcShape<S>::threads) void k_sym_zc(int nrows, const
         tbd_load(e, tid, ta.b, sd, ok ? (int64_t)q * t.M + t.ixy : 0, t.n);
     };
     const double2 zero = make_double2(0.0, 0.0);
-    double2 xm = ldx(k0 - 1), xc = ldx(k0), xp = ldx(k0 + 1), xn = zero;
-    double2 hc, hn;
-    zc_halo_load<S>(hc, t, ta.in0, k0);
-    TbdRow En{}, E0{}, E1{}, E2{}, E3{};
-    ldrow(E0, k0);
-    ldrow(E1, k0 - 1);
+    // plane rings, indexed by compile-time constants in the 4-way unrolled loop (renaming, not
+    // moves: a register that receives a load is read only in the step that consumes it, so no
+    // wait for a load is forced before its consumer — a copy at the end of the step would be)
+    // X[(u + j) & 3]: in0 of plane k-1+j (j = 0..3: k-1, k, k+1, k+2 in flight); E[(u + j) & 3]:
+    // ids + b of plane k-2+j... (j = 3: k+1 in flight); HX[u & 1]: in0 halo of plane k, the
+    // other one plane k+1 in flight
+    double2 X[4], HX[2];
+    TbdRow E[4];
+    X[0] = ldx(k0 - 1);
+    X[1] = ldx(k0);
+    X[2] = ldx(k0 + 1);
+    X[3] = zero;
+    zc_halo_load<S>(HX[0], t, ta.in0, k0);
+    HX[1] = zero;
+    E[0] = TbdRow{};
+    ldrow(E[1], k0 - 1);
+    ldrow(E[2], k0);
+    E[3] = TbdRow{};
+    uint32_t e3own = 0;  // class ids of plane k-3 (stage 2's -M mirror)
     double2 s0m1 = zero, s0m2 = zero;  // stage 0 of planes k-1, k-2
     double2 s1m2 = zero, s1m3 = zero;  // stage 1 of planes k-2, k-3
     constexpr int hz = Sh::H - 1;
-    for (int k = k0; k < t.kend; ++k) {
-        const int a = k & 1, a1 = (k - 1) & 1, a2 = (k - 2) & 1;
-        // this step's LDS planes: in0 of plane k (own pair + halo), stage 0 of k-1, stage 1 of k-2
-        if (has) {
-            sin[a][ry + 1][col] = xc;
-            s0l[a1][ry][col] = s0m1;
-            if constexpr (S == 3) s1l[a2][ry][col] = s1m2;
-        }
-        zc_halo_store<S>(hc, sin[a]);
-        // next step's loads
-        xn = ldx(k + 2);
-        zc_halo_load<S>(hn, t, ta.in0, k + 1);
-        ldrow(En, k + 1);
-        __syncthreads();
-        // ---- stage 0 on plane k: a Jacobi sweep from in0
-        double2 s0k = zero;
-        if (t.pos_ok && k >= 0 && k < t.nz) {
-            double xv[2][7], o[2];
-            zc_gather(&sin[a][ry][0], &sin[a][ry + 1][0], &sin[a][ry + 2][0], col, xc, xm, xp, xv);
-            zc_rows(tab, E0, E1.own, xv, S == 1 && ta.last_resid, ta.omega, o);
-            s0k = make_double2(o[0], o[1]);
-            if (ta.out[0] && t.own_xy && k >= t.zs && k < t.ze)
-                *reinterpret_cast<double2*>(ta.out[0] + (int64_t)k * t.M + t.ixy) = s0k;
-        }
-        // ---- stage 1 on plane k-1 from stage 0 (in-plane: the LDS plane stored this step)
-        double2 s1k = zero;
-        {
-            const int p = k - 1;
-            constexpr bool last = S == 2;
-            if (t.pos_ok && ry >= 1 && ry < Sh::RY - 1 && p >= 0 && p < t.nz && p >= t.zs - hz && p < t.ze + hz &&
-                (!last || t.own_xy)) {
-                double xv[2][7], o[2];
-                zc_gather(&s0l[a1][ry - 1][0], &s0l[a1][ry][0], &s0l[a1][ry + 1][0], col, s0m1, s0m2, s0k, xv);
-                zc_rows(tab, E1, E2.own, xv, last && ta.last_resid, ta.omega, o);
-                s1k = make_double2(o[0], o[1]);
-                if (t.own_xy && p >= t.zs && p < t.ze)
-                    *reinterpret_cast<double2*>(ta.out[1] + (int64_t)p * t.M + t.ixy) = s1k;
+    for (int kb = k0; kb < t.kend; kb += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = kb + u;
+            if (k >= t.kend) break;  // uniform
+            double2& xm = X[u & 3];
+            double2& xc = X[(u + 1) & 3];
+            double2& xp = X[(u + 2) & 3];
+            double2& xn = X[(u + 3) & 3];
+            double2& hc = HX[u & 1];
+            double2& hn = HX[(u + 1) & 1];
+            TbdRow& E2 = E[u & 3];        // plane k-2
+            TbdRow& E1 = E[(u + 1) & 3];  // plane k-1
+            TbdRow& E0 = E[(u + 2) & 3];  // plane k
+            TbdRow& En = E[(u + 3) & 3];  // plane k+1 (loaded this step)
+            const int a = k & 1, a1 = (k - 1) & 1, a2 = (k - 2) & 1;
+            // this step's LDS planes: in0 of plane k (own pair + halo), stage 0 of k-1, stage 1 of k-2
+            if (has) {
+                sin[a][ry + 1][col] = xc;
+                s0l[a1][ry][col] = s0m1;
+                if constexpr (S == 3) s1l[a2][ry][col] = s1m2;
             }
-        }
-        // ---- stage 2 on plane k-2 from stage 1 (S = 3)
-        if constexpr (S == 3) {
-            const int p = k - 2;
-            if (t.own_xy && ry >= 2 && ry < Sh::RY - 2 && p >= t.zs && p < t.ze) {
+            zc_halo_store<S>(hc, sin[a]);
+            const uint32_t e3 = e3own;
+            e3own = E2.own;  // (E2 is overwritten by this step's load of plane k+1... next step)
+            // next steps' loads
+            xn = ldx(k + 2);
+            zc_halo_load<S>(hn, t, ta.in0, k + 1);
+            ldrow(En, k + 1);
+            __syncthreads();
+            // ---- stage 0 on plane k: a Jacobi sweep from in0
+            double2 s0k = zero;
+            if (t.pos_ok && k >= 0 && k < t.nz) {
                 double xv[2][7], o[2];
-                zc_gather(&s1l[a2][ry - 1][0], &s1l[a2][ry][0], &s1l[a2][ry + 1][0], col, s1m2, s1m3, s1k, xv);
-                zc_rows(tab, E2, E3.own, xv, ta.last_resid, ta.omega, o);
-                *reinterpret_cast<double2*>(ta.out[2] + (int64_t)p * t.M + t.ixy) = make_double2(o[0], o[1]);
+                zc_gather(&sin[a][ry][0], &sin[a][ry + 1][0], &sin[a][ry + 2][0], col, xc, xm, xp, xv);
+                zc_rows(tab, E0, E1.own, xv, S == 1 && ta.last_resid, ta.omega, o);
+                s0k = make_double2(o[0], o[1]);
+                if (ta.out[0] && t.own_xy && k >= t.zs && k < t.ze)
+                    *reinterpret_cast<double2*>(ta.out[0] + (int64_t)k * t.M + t.ixy) = s0k;
             }
+            // ---- stage 1 on plane k-1 from stage 0 (in-plane: the LDS plane stored this step)
+            double2 s1k = zero;
+            {
+                const int p = k - 1;
+                constexpr bool last = S == 2;
+                if (t.pos_ok && ry >= 1 && ry < Sh::RY - 1 && p >= 0 && p < t.nz && p >= t.zs - hz && p < t.ze + hz &&
+                    (!last || t.own_xy)) {
+                    double xv[2][7], o[2];
+                    zc_gather(&s0l[a1][ry - 1][0], &s0l[a1][ry][0], &s0l[a1][ry + 1][0], col, s0m1, s0m2, s0k, xv);
+                    zc_rows(tab, E1, E2.own, xv, last && ta.last_resid, ta.omega, o);
+                    s1k = make_double2(o[0], o[1]);
+                    if (t.own_xy && p >= t.zs && p < t.ze)
+                        *reinterpret_cast<double2*>(ta.out[1] + (int64_t)p * t.M + t.ixy) = s1k;
+                }
+            }
+            // ---- stage 2 on plane k-2 from stage 1 (S = 3)
+            if constexpr (S == 3) {
+                const int p = k - 2;
+                if (t.own_xy && ry >= 2 && ry < Sh::RY - 2 && p >= t.zs && p < t.ze) {
+                    double xv[2][7], o[2];
+                    zc_gather(&s1l[a2][ry - 1][0], &s1l[a2][ry][0], &s1l[a2][ry + 1][0], col, s1m2, s1m3, s1k, xv);
+                    zc_rows(tab, E2, e3, xv, ta.last_resid, ta.omega, o);
+                    *reinterpret_cast<double2*>(ta.out[2] + (int64_t)p * t.M + t.ixy) = make_double2(o[0], o[1]);
+                }
+            }
+            s0m2 = s0m1;
+            s0m1 = s0k;
+            s1m3 = s1m2;
+            s1m2 = s1k;
         }
-        // rotate the plane rings
-        xm = xc;
-        xc = xp;
-        xp = xn;
-        hc = hn;
-        s0m2 = s0m1;
-        s0m1 = s0k;
-        s1m3 = s1m2;
-        s1m2 = s1k;
-        E3 = E2;
-        E2 = E1;
-        E1 = E0;
-        E0 = En;
     }
 }
 
@@ -1965,89 +1986,99 @@ __global__ __launch_bounds__(kZmThreads) void k_sym_zm(int nrows, const uint8_t*
         if constexpr (OP == OP_SPMV) return make_double2(0.0, 0.0);
         return q < g.nz ? *reinterpret_cast<const double2*>(b + (int64_t)q * M + ixy[h]) : make_double2(0.0, 0.0);
     };
-    double2 xm[2], xc[2], xp[2], xn[2], bc[2], bn[2];
-    uint32_t idm[2], idc[2], idn[2];
-    ZmHalo hc, hn;
+    // plane rings indexed by compile-time constants in the 4-way unrolled loop (renaming: no copy
+    // of a register with a load in flight, see k_sym_zc): X[(u + j) & 3][h] = x of plane k-1+j
+    // (j = 3: k+2 in flight), ID[(u + j) & 3][h] = ids of plane k-1+j (j = 2: k+1 in flight),
+    // B[(u + j) & 1][h] = b of plane k+j, HL[(u + j) & 1] = halo of plane k+j
+    double2 X[4][2], B[2][2];
+    uint32_t ID[4][2];
+    ZmHalo HL[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        xm[h] = ldx(z0 - 1, h);
-        xc[h] = ldx(z0, h);
-        xp[h] = ldx(z0 + 1, h);
-        idm[h] = ldid(z0 - 1, h);
-        idc[h] = ldid(z0, h);
-        bc[h] = ldb(z0, h);
+        X[0][h] = ldx(z0 - 1, h);
+        X[1][h] = ldx(z0, h);
+        X[2][h] = ldx(z0 + 1, h);
+        ID[0][h] = ldid(z0 - 1, h);
+        ID[1][h] = ldid(z0, h);
+        B[0][h] = ldb(z0, h);
     }
-    zm_halo_load(hc, x, tid, x0, y0, g.nx, g.ny, g.nz, M, z0);
-    for (int k = z0; k < z1; ++k) {
-        const int sl = k & 1;
-        // plane k into LDS (own pairs and halo), then the loads the next step consumes
+    zm_halo_load(HL[0], x, tid, x0, y0, g.nx, g.ny, g.nz, M, z0);
+    for (int kb = z0; kb < z1; kb += 4) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            sx[sl][1 + ly + 8 * h][1 + px] = xc[h];
-            sid[sl][1 + ly + 8 * h][1 + px] = (uint16_t)idc[h];
-        }
-        zm_halo_store(hc, sx[sl], sid[sl]);
+        for (int u = 0; u < 4; ++u) {
+            const int k = kb + u;
+            if (k >= z1) break;  // uniform
+            double2(&xm)[2] = X[u & 3];
+            double2(&xc)[2] = X[(u + 1) & 3];
+            double2(&xp)[2] = X[(u + 2) & 3];
+            double2(&xn)[2] = X[(u + 3) & 3];
+            uint32_t(&idm)[2] = ID[u & 3];
+            uint32_t(&idc)[2] = ID[(u + 1) & 3];
+            uint32_t(&idn)[2] = ID[(u + 2) & 3];
+            double2(&bc)[2] = B[u & 1];
+            double2(&bn)[2] = B[(u + 1) & 1];
+            ZmHalo& hc = HL[u & 1];
+            ZmHalo& hn = HL[(u + 1) & 1];
+            const int sl = k & 1;
+            // plane k into LDS (own pairs and halo), then the loads the next step consumes
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            xn[h] = ldx(k + 2, h);
-            idn[h] = ldid(k + 1, h);
-            bn[h] = ldb(k + 1, h);
-        }
-        zm_halo_load(hn, x, tid, x0, y0, g.nx, g.ny, g.nz, M, k + 1);
-        __syncthreads();  // plane k's slot; the slot stored next step was last read a step ago
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int ry = 1 + ly + 8 * h, col = 1 + px;
-            const double2 lft = sx[sl][ry][col - 1], rgt = sx[sl][ry][col + 1];
-            const double2 dn = sx[sl][ry - 1][col], up = sx[sl][ry + 1][col];
-            const uint32_t idl = sid[sl][ry][col - 1], idd = sid[sl][ry - 1][col];
-            const double xv[2][7] = {{xm[h].x, dn.x, lft.y, xc[h].x, xc[h].y, up.x, xp[h].x},
-                                     {xm[h].y, dn.y, xc[h].x, xc[h].y, rgt.x, up.y, xp[h].y}};
-            const uint32_t t0 = idc[h] & 0xffu, t1 = idc[h] >> 8;
-            const uint32_t tr[2] = {t0, t1}, l0[2] = {idl >> 8, t0};
-            const uint32_t l1[2] = {idd & 0xffu, idd >> 8}, l2[2] = {idm[h] & 0xffu, idm[h] >> 8};
-            const double bv[2] = {bc[h].x, bc[h].y};
-            double o[2];
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                const uint32_t tc = tr[r];
-                double v[7];
-                v[0] = tab.v[l2[r]][3];  // a(i, i-M)  = U_2 of row i-M
-                v[1] = tab.v[l1[r]][2];  // a(i, i-nx) = U_1 of row i-nx
-                v[2] = tab.v[l0[r]][1];  // a(i, i-1)  = U_0 of row i-1
-                v[3] = tab.v[tc][0];
-                v[4] = tab.v[tc][1];
-                v[5] = tab.v[tc][2];
-                v[6] = tab.v[tc][3];
-                // (absent entries meet exact zeros: no mask select, see zc_rows)
-                double sacc = 0.0;
-#pragma unroll
-                for (int q = 0; q < 7; ++q) {
-                    const double p = v[q] * xv[r][q];
-                    sacc = sacc + p;
-                }
-                if constexpr (OP == OP_SPMV) {
-                    o[r] = sacc;
-                } else if constexpr (OP == OP_RESID) {
-                    o[r] = bv[r] - sacc;
-                } else {
-                    const double u = bv[r] - sacc;
-                    const double w = omega * u;
-                    o[r] = xv[r][3] + div_rn(w, v[3], tab.r[tc]);
-                }
+            for (int h = 0; h < 2; ++h) {
+                sx[sl][1 + ly + 8 * h][1 + px] = xc[h];
+                sid[sl][1 + ly + 8 * h][1 + px] = (uint16_t)idc[h];
             }
-            *reinterpret_cast<double2*>(y + (int64_t)k * M + ixy[h]) = make_double2(o[0], o[1]);
-        }
+            zm_halo_store(hc, sx[sl], sid[sl]);
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            xm[h] = xc[h];
-            xc[h] = xp[h];
-            xp[h] = xn[h];
-            idm[h] = idc[h];
-            idc[h] = idn[h];
-            bc[h] = bn[h];
+            for (int h = 0; h < 2; ++h) {
+                xn[h] = ldx(k + 2, h);
+                idn[h] = ldid(k + 1, h);
+                bn[h] = ldb(k + 1, h);
+            }
+            zm_halo_load(hn, x, tid, x0, y0, g.nx, g.ny, g.nz, M, k + 1);
+            __syncthreads();  // plane k's slot; the slot stored next step was last read a step ago
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int ry = 1 + ly + 8 * h, col = 1 + px;
+                const double2 lft = sx[sl][ry][col - 1], rgt = sx[sl][ry][col + 1];
+                const double2 dn = sx[sl][ry - 1][col], up = sx[sl][ry + 1][col];
+                const uint32_t idl = sid[sl][ry][col - 1], idd = sid[sl][ry - 1][col];
+                const double xv[2][7] = {{xm[h].x, dn.x, lft.y, xc[h].x, xc[h].y, up.x, xp[h].x},
+                                         {xm[h].y, dn.y, xc[h].x, xc[h].y, rgt.x, up.y, xp[h].y}};
+                const uint32_t t0 = idc[h] & 0xffu, t1 = idc[h] >> 8;
+                const uint32_t tr[2] = {t0, t1}, l0[2] = {idl >> 8, t0};
+                const uint32_t l1[2] = {idd & 0xffu, idd >> 8}, l2[2] = {idm[h] & 0xffu, idm[h] >> 8};
+                const double bv[2] = {bc[h].x, bc[h].y};
+                double o[2];
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const uint32_t tc = tr[r];
+                    double v[7];
+                    v[0] = tab.v[l2[r]][3];  // a(i, i-M)  = U_2 of row i-M
+                    v[1] = tab.v[l1[r]][2];  // a(i, i-nx) = U_1 of row i-nx
+                    v[2] = tab.v[l0[r]][1];  // a(i, i-1)  = U_0 of row i-1
+                    v[3] = tab.v[tc][0];
+                    v[4] = tab.v[tc][1];
+                    v[5] = tab.v[tc][2];
+                    v[6] = tab.v[tc][3];
+                    // (absent entries meet exact zeros: no mask select, see zc_rows)
+                    double sacc = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) {
+                        const double p = v[q] * xv[r][q];
+                        sacc = sacc + p;
+                    }
+                    if constexpr (OP == OP_SPMV) {
+                        o[r] = sacc;
+                    } else if constexpr (OP == OP_RESID) {
+                        o[r] = bv[r] - sacc;
+                    } else {
+                        const double u2 = bv[r] - sacc;
+                        const double w = omega * u2;
+                        o[r] = xv[r][3] + div_rn(w, v[3], tab.r[tc]);
+                    }
+                }
+                *reinterpret_cast<double2*>(y + (int64_t)k * M + ixy[h]) = make_double2(o[0], o[1]);
+            }
         }
-        hc = hn;
     }
     (void)nrows;
 }
