@@ -75,7 +75,7 @@ def main():
     ap.add_argument("--permute", type=int, default=None, metavar="SEED",
                     help="apply a seeded random symmetric permutation to the problem before setup "
                          "(destroys the grid numbering, as an FE mesh ordering would; 1 part only)")
-    ap.add_argument("--reorder", choices=["auto", "off", "on"], default="auto",
+    ap.add_argument("--reorder", choices=["auto", "off", "on", "agg"], default="auto",
                     help="locality permutation of the level operators inside the device layout "
                          "(AMGSolver reorder; one part; bits unchanged)")
     ap.add_argument("--pmc", choices=["auto", "committed", "off"], default="auto",

@@ -17,7 +17,7 @@ from .partitioned import Context, PSparseMatrix, PVector, _release
 OPS = ("jacobi_pre", "residual", "restrict", "prolong", "jacobi_post", "coarse")
 
 
-REORDER = {"off": 0, "auto": 1, "on": 2}
+REORDER = {"off": 0, "auto": 1, "on": 2, "agg": 3}
 
 
 def plan_tag(level: int, op: str) -> int:
@@ -72,7 +72,19 @@ class AMGSolver:
         # keeps its numbering (its dense inverse sums in column order)
         self.perm = [None] * H.nlevels
         self.span = [None] * H.nlevels
-        if H.nparts == 1 and mode:
+        if H.nparts == 1 and mode == REORDER["agg"]:
+            # levels 1 .. L-2 in the order of their coarse aggregates: the nodes
+            # of one level-(l+1) aggregate become a contiguous run — R_l's rows read runs of the
+            # level-l vector instead of ~25 scattered lines — each aggregate's nodes in their own
+            # order, the aggregates in coarse-row order; level 0 keeps its grid layout
+            for l in range(1, H.nlevels - 1):
+                agg = H.levels[l][part].agg
+                if agg is None or len(agg) != H.levels[l][part].A.nrows:
+                    continue
+                agg = np.asarray(agg, np.int64)
+                key = np.where(agg < 0, np.int64(1) << 40, agg)
+                self.perm[l] = np.argsort(key, kind="stable").astype(np.int64)
+        elif H.nparts == 1 and mode:
             from .hcsr import locality_order
             for l in range(H.nlevels - 1):
                 order, before, after = locality_order(H.levels[l][part].A, mode)
