@@ -304,7 +304,9 @@ def main():
     # the instance name as rocprofv3 demangles it (every template argument, defaults included)
     tf = lambda v: "true" if v else "false"  # noqa: E731
     if pipelined:
-        if lay.get("sym_vd"):  # k_sym_tbd<S, PD, TY> (8-line tiles run one plane ahead)
+        if lay.get("sym_vd") and _option("tb_zc"):  # the z-marching chain (round 5)
+            kname = "k_sym_zc<3>"
+        elif lay.get("sym_vd"):  # k_sym_tbd<S, PD, TY> (8-line tiles run one plane ahead)
             ty = _option("tb_ty")
             kname = f"k_sym_tbd<3, {1 if ty == 8 else _tb_pd()}, {ty}>"
         else:
@@ -393,8 +395,8 @@ def main():
             "samples_ms_per_step": [round(t / args.steps * 1e3, 4) for t in times],
             "roofline": {
                 "kernel": kname + (" (level-0 chain of the pipelined cycles, one launch per cycle: post-smoothing "
-                                   "Jacobi -> next pre-smoothing Jacobi -> residual, temporally blocked over the "
-                                   "symmetric diagonal-class layout" + (" with its row-class dictionary" if lay.get("sym_vd")
+                                   "Jacobi -> next pre-smoothing Jacobi -> residual, temporally blocked (z-marching, "
+                                   "one barrier per plane) over the symmetric diagonal-class layout" + (" with its row-class dictionary" if lay.get("sym_vd")
                                                                         else "") +
                                    ", the matrix streamed once; stores the pre-smoothed iterate and the residual)"
                                    if pipelined else
