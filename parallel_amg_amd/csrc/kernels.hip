@@ -1264,7 +1264,11 @@ __device__ __forceinline__ bool tb_ctx_init(TbCtx<S>& t, const TbGeom& g, int nr
     const int per = (ntiles + 7) / 8;
     const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
     if (lin >= ntiles) return false;
-    const int ty = lin % g.tiles_y, tx = (lin / g.tiles_y) % g.tiles_x, zc = lin / (g.tiles_x * g.tiles_y);
+    // y-fastest: an XCD's tiles are one x column of the grid (its y halos shared in its L2); x-fastest
+    // (TbGeom::xfast): whole rows of tiles, so the 128-B lines a tile's x halo touches are read once per
+    // XCD instead of by two XCDs each
+    const int ty = g.xfast ? (lin / g.tiles_x) % g.tiles_y : lin % g.tiles_y;
+    const int tx = g.xfast ? lin % g.tiles_x : (lin / g.tiles_y) % g.tiles_x, zc = lin / (g.tiles_x * g.tiles_y);
     if (g.zlo + zc * g.zlen >= g.zhi) return false;  // (a chunk past the output range: uniform)
     const int x0 = tx * kTbX, y0 = ty * TY;
     t.x0 = x0;
@@ -1966,7 +1970,11 @@ __global__ __launch_bounds__(kZmThreads) void k_sym_zm(int nrows, const uint8_t*
     const int per = (ntiles + 7) / 8;
     const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);  // consecutive tiles on one XCD
     if (lin >= ntiles) return;  // the whole workgroup, before any barrier
-    const int ty = lin % g.tiles_y, tx = (lin / g.tiles_y) % g.tiles_x, zc = lin / (g.tiles_x * g.tiles_y);
+    // y-fastest: an XCD's tiles are one x column of the grid (its y halos shared in its L2); x-fastest
+    // (TbGeom::xfast): whole rows of tiles, so the 128-B lines a tile's x halo touches are read once per
+    // XCD instead of by two XCDs each
+    const int ty = g.xfast ? (lin / g.tiles_x) % g.tiles_y : lin % g.tiles_y;
+    const int tx = g.xfast ? lin % g.tiles_x : (lin / g.tiles_y) % g.tiles_x, zc = lin / (g.tiles_x * g.tiles_y);
     const int z0 = zc * g.zlen, z1 = min(g.nz, z0 + g.zlen);
     if (z0 >= z1) return;
     const int x0 = tx * kTbX, y0 = ty * kTbY;
@@ -2415,6 +2423,7 @@ void launch_sym_nu(const pamg_mat& A, const double* x, const double* b, double* 
             (int64_t)sd.nbands * sd.band >= A.nrows && A.nrows == (int64_t)sd.tb.nx * sd.tb.ny * sd.tb.nz &&
             A.nrows % 2 == 0) {
             TbGeom g = sd.tb;
+            g.xfast = options().zm_xfast;
             const int tiles = g.tiles_x * g.tiles_y;
             // z chunks: ~4 workgroups per CU (1024), chunks of >= 16 planes; zm_chunks overrides
             int zc = options().zm_chunks > 0 ? options().zm_chunks : std::min((1024 + tiles - 1) / tiles, g.nz / 16);
@@ -2508,6 +2517,7 @@ void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s) {
     g.zchunks = (span + g.zlen - 1) / g.zlen;
     const int ntiles = g.tiles_x * g.tiles_y * g.zchunks;
     const int grid = (ntiles + 7) / 8 * 8;
+    g.xfast = options().tb_xfast;
     if (sd.vd_n && options().tb_ty == 8) {
         // 8-line tiles (Options::tb_ty): twice the tiles per plane, half the LDS per workgroup
         // (two workgroups per CU); the z split recomputed for the tile count

@@ -155,6 +155,8 @@ struct Options {
     int chain_store_x = 0;     // 1: the pipelined chain also stores its post-smoothed iterate (never read)
     int tb_zc = 1;             // 1: the level-0 blocked passes (row-class dictionary) march along z with one barrier
                                //    per plane (k_sym_zc); 0: k_sym_tbd
+    int tb_xfast = 0;          // blocked passes: tiles x-fastest (an XCD takes whole rows of tiles) instead of y-fastest
+    int zm_xfast = 0;          // the same for k_sym_zm
     int sym_zm = 1;            // 1: one-sweep ops of a whole one-part row-class grid operator march along z
                                //    (k_sym_zm); 0: k_rows_symd
     int zm_chunks = 0;         // z chunks per tile column of k_sym_zm (0: ~4 workgroups per CU)
@@ -186,6 +188,7 @@ struct TbGeom {
     int tiles_x = 0, tiles_y = 0;   // kTbX x kTbY tiles of a plane
     int zchunks = 1, zlen = 0;      // planes per workgroup (the last chunk may be shorter)
     int zlo = 0, zhi = 0;           // output planes [zlo, zhi) of a launch (set by launch_sym_tb)
+    int xfast = 0;                  // tile order: 0 y-fastest, 1 x-fastest (kernels.hip tb_ctx_init)
 };
 struct SymDia {
     int nu = 0;                     // upper offset classes
