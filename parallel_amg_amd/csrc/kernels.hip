@@ -2422,8 +2422,7 @@ void launch_sym_nu(const pamg_mat& A, const double* x, const double* b, double* 
         if (sd.vd_n && sd.tb_ok && !sd.tb_part && options().sym_zm && sd.plane0 == 0 &&
             (int64_t)sd.nbands * sd.band >= A.nrows && A.nrows == (int64_t)sd.tb.nx * sd.tb.ny * sd.tb.nz &&
             A.nrows % 2 == 0) {
-            TbGeom g = sd.tb;
-            g.xfast = options().zm_xfast;
+            TbGeom g = sd.tb;  // (y-fastest tiles: x-fastest measured +-2 %, profiles/r05_l/)
             const int tiles = g.tiles_x * g.tiles_y;
             // z chunks: ~4 workgroups per CU (1024), chunks of >= 16 planes; zm_chunks overrides
             int zc = options().zm_chunks > 0 ? options().zm_chunks : std::min((1024 + tiles - 1) / tiles, g.nz / 16);

@@ -155,8 +155,8 @@ struct Options {
     int chain_store_x = 0;     // 1: the pipelined chain also stores its post-smoothed iterate (never read)
     int tb_zc = 1;             // 1: the level-0 blocked passes (row-class dictionary) march along z with one barrier
                                //    per plane (k_sym_zc); 0: k_sym_tbd
-    int tb_xfast = 0;          // blocked passes: tiles x-fastest (an XCD takes whole rows of tiles) instead of y-fastest
-    int zm_xfast = 0;          // the same for k_sym_zm
+    int tb_xfast = 1;          // blocked passes: tiles x-fastest (an XCD takes whole rows of tiles; chain -0.9 %,
+                               // S = 2 pass -1.1 %, same-box A/B profiles/r05_l/) or y-fastest (0)
     int sym_zm = 1;            // 1: one-sweep ops of a whole one-part row-class grid operator march along z
                                //    (k_sym_zm); 0: k_rows_symd
     int zm_chunks = 0;         // z chunks per tile column of k_sym_zm (0: ~4 workgroups per CU)

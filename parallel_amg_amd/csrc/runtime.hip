@@ -3462,7 +3462,6 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "sym_zm" && (value == 0 || value == 1)) o.sym_zm = (int)value;
     else if (k == "tb_zc" && (value == 0 || value == 1)) o.tb_zc = (int)value;
     else if (k == "tb_xfast" && (value == 0 || value == 1)) o.tb_xfast = (int)value;
-    else if (k == "zm_xfast" && (value == 0 || value == 1)) o.zm_xfast = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
     else if (k == "tb_ty" && (value == 8 || value == 16)) o.tb_ty = (int)value;
     else if (k == "chain_store_x" && (value == 0 || value == 1)) o.chain_store_x = (int)value;
@@ -3504,7 +3503,6 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "sym_zm") *value = o.sym_zm;
     else if (k == "tb_zc") *value = o.tb_zc;
     else if (k == "tb_xfast") *value = o.tb_xfast;
-    else if (k == "zm_xfast") *value = o.zm_xfast;
     else if (k == "zm_chunks") *value = o.zm_chunks;
     else if (k == "tb_ty") *value = o.tb_ty;
     else if (k == "chain_store_x") *value = o.chain_store_x;
