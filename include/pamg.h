@@ -191,7 +191,9 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * bit 6: the tile-major set carries 8-bit per-tile value dictionaries (value_dict);
  * bit 7: the symmetric layout stores a 1-byte row class per row, its values in a table of
  * <= 64 (mask, diagonal, upper values) tuples (sym_vd); bit 8: the tile-major set stages each
- * tile's x runs in LDS and sums one row per lane (x_stage_tiles, k_rows_xsr). */
+ * tile's x runs in LDS and sums one row per lane (x_stage_tiles, k_rows_xsr); bit 9: the set runs in
+ * the sliced-ELL layout (ell: one row per lane, per-group 8-bit column-offset and value dictionaries;
+ * then out[8] = the kernel's grid). */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[10]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */

@@ -2091,6 +2091,90 @@ __global__ __launch_bounds__(kZmThreads) void k_sym_zm(int nrows, const uint8_t*
     (void)nrows;
 }
 
+// k_rows_ell: the sliced-ELL layout (pamg::EllSet; round 5, the level-1 operator). One row per
+// lane, a workgroup = kEllGroup consecutive rows = 4 slices; the group's two tables (column offsets
+// and values, <= 256 entries each) are staged in LDS once; a lane then walks its row in storage
+// order, 4 nonzeros per dword pair of index bytes: offset and value from LDS, x gathered at row +
+// offset (the k-th entries of 64 consecutive rows are at nearby columns: few lines per wave-load).
+// Products rounded and summed left to right from +0.0 in storage order, the padded tail of a
+// row (k >= its length) selected away: the bits of every other row kernel (SPEC §S3). Groups in
+// XCD-contiguous order: block b on XCD b % 8 takes the (b / 8)-th group of that XCD's eighth, so an
+// XCD's L2 holds the x window its consecutive rows reuse.
+template <int OP>
+__global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int2* __restrict__ smeta,
+                                                        const uint32_t* __restrict__ cw, const uint32_t* __restrict__ vw,
+                                                        const uint8_t* __restrict__ len, const int4* __restrict__ gmeta,
+                                                        const int* __restrict__ otab, const double* __restrict__ vtab,
+                                                        int ngroups, const double* __restrict__ x,
+                                                        const double* __restrict__ b, double* __restrict__ y,
+                                                        double omega) {
+    __shared__ int lo[256];
+    __shared__ double lv[256];
+    const int per = (ngroups + 7) / 8;
+    const int g = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (g >= ngroups) return;  // the whole workgroup, before the barrier
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int4 gm = gmeta[g];
+    const int i = g * kEllGroup + tid;
+    const bool in = i < nrows;
+    const int ic = in ? i : nrows - 1;
+    const int2 sm = smeta[ic / kEllW];  // (one slice per wave)
+    const int L = in ? (int)len[i] : 0;
+    const uint32_t* __restrict__ cp = cw + sm.x + lane;
+    const uint32_t* __restrict__ vp = vw + sm.x + lane;
+    const int nq = (sm.y + 3) >> 2;
+    uint32_t c4 = nq > 0 ? cp[0] : 0u, v4 = nq > 0 ? vp[0] : 0u;
+    double pb = 0.0, px = 0.0, py = 0.0;
+    if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[ic];
+    if constexpr (OP == OP_JACOBI) px = x[ic];
+    if constexpr (OP == OP_PROLONG) py = y[ic];
+    const int ot = gm.x + (tid < gm.y ? tid : 0), vt = gm.z + (tid < gm.w ? tid : 0);
+    const int otv = otab[ot];
+    const double vtv = vtab[vt];
+    if (tid < gm.y) lo[tid] = otv;
+    if (tid < gm.w) lv[tid] = vtv;
+    __syncthreads();
+    double s = 0.0, dg = 0.0;
+    for (int q = 0; q < nq; ++q) {
+        const uint32_t cq = c4, vq = v4;
+        if (q + 1 < nq) {  // the next dword pair in flight while this one is used
+            c4 = cp[(q + 1) * kEllW];
+            v4 = vp[(q + 1) * kEllW];
+        }
+        int of[4];
+        double vv[4], xv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            of[e] = lo[(cq >> (8 * e)) & 255u];
+            vv[e] = lv[(vq >> (8 * e)) & 255u];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[e] = x[4 * q + e < L ? ic + of[e] : ic];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool ok = 4 * q + e < L;
+            const double p = vv[e] * xv[e];
+            const double t = s + p;
+            s = ok ? t : s;
+            if constexpr (OP == OP_JACOBI) dg = ok && of[e] == 0 ? vv[e] : dg;
+        }
+    }
+    double out;
+    if constexpr (OP == OP_SPMV) {
+        out = s;
+    } else if constexpr (OP == OP_RESID) {
+        out = pb - s;
+    } else if constexpr (OP == OP_JACOBI) {
+        const double u = pb - s;
+        const double v = omega * u;
+        const double w = v / dg;
+        out = px + w;
+    } else {
+        out = py + s;
+    }
+    if (in) y[i] = out;
+}
+
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_rows_long(
     const int* __restrict__ rows, const int* __restrict__ rowptr, const int* __restrict__ col,
@@ -2491,6 +2575,12 @@ template <int OP>
 void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
                     double* y, double omega, hipStream_t s) {
     if (ts.sym) launch_sym<OP>(A, x, b, y, omega, s);
+    if (ts.ell) {
+        const EllSet& E = A.ell;
+        const int grid = (int)((E.ngroups + 7) / 8 * 8);
+        k_rows_ell<OP><<<grid, kEllGroup, 0, s>>>((int)A.nrows, E.d_smeta, E.d_ci, E.d_vi, E.d_len, E.d_gmeta, E.d_otab,
+                                                  E.d_vtab, (int)E.ngroups, x, b, y, omega);
+    }
     if (ts.n_short > 0) {
         if (ts.tile_nnz == 1024) launch_tile<OP, 1024>(A, ts, x, b, y, omega, s);
         else if (ts.tile_nnz == 4096) launch_tile<OP, 4096>(A, ts, x, b, y, omega, s);

@@ -109,6 +109,9 @@ struct TileSet {
     // symmetric diagonal-class layout (Options::sym_dia; interior set of a square operator,
     // pamg_mat::sym): the set's rows run in k_rows_sym instead of tiles
     bool sym = false;
+    // sliced-ELL layout (pamg_mat::ell; the whole interior set of a square operator): the set's rows run in
+    // k_rows_ell instead of tiles
+    bool ell = false;
     int max_short_len = 0;    // longest row in a short tile
     int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
@@ -161,6 +164,9 @@ struct Options {
                                //    (k_sym_zm); 0: k_rows_symd
     int zm_chunks = 0;         // z chunks per tile column of k_sym_zm (0: ~4 workgroups per CU)
     int xsr_kernel = 0;        // staged sets: 0 row lanes (k_rows_xsr), 1 nonzero lanes (k_rows_tm, 2048-nonzero tiles)
+    int ell = 1;               // 1: sliced ELL with per-group 8-bit dictionaries for square operators whose every row
+                               //    is interior, where the tables fit (EllSet; the level-1 operator)
+    int ell_min_rows = 65536;  // ... with at least this many rows
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
 };
@@ -190,6 +196,26 @@ struct TbGeom {
     int zlo = 0, zhi = 0;           // output planes [zlo, zhi) of a launch (set by launch_sym_tb)
     int xfast = 0;                  // tile order: 0 y-fastest, 1 x-fastest (kernels.hip tb_ctx_init)
 };
+// Sliced ELL with per-group dictionaries (Options::ell; round 5, the level-1 operator): rows in
+// slices of kEllW consecutive rows (one per lane of a wave), kEllGroup rows (a workgroup) sharing
+// two tables of <= 256 entries — the rows' column offsets (col - row) and values (bit patterns).
+// A slice stores its padded nonzeros k = 0 .. maxlen-1 as one column-index byte and one value-index
+// byte per row, 4 consecutive k of a row packed in a dword, lanes interleaved: dword (k / 4, lane) at
+// start + (k / 4) * kEllW + lane. Rows keep their storage order (the products are summed in it).
+constexpr int kEllW = 64;
+constexpr int kEllGroup = 256;
+struct EllSet {
+    int64_t nslices = 0, ngroups = 0;
+    int2* d_smeta = nullptr;     // per slice: (first dword of its index streams, maxlen)
+    uint32_t* d_ci = nullptr;    // column-index stream
+    uint32_t* d_vi = nullptr;    // value-index stream
+    uint8_t* d_len = nullptr;    // per row: its length
+    int4* d_gmeta = nullptr;     // per group: (offset-table start, entries, value-table start, entries)
+    int* d_otab = nullptr;       // the groups' offset tables, concatenated
+    double* d_vtab = nullptr;    // the groups' value tables, concatenated
+    int64_t words = 0, otab_n = 0, vtab_n = 0;
+};
+
 struct SymDia {
     int nu = 0;                     // upper offset classes
     int off[kSymMaxU] = {};         // ascending positive offsets
@@ -292,6 +318,7 @@ struct pamg_mat {
     pamg::SymDia sym;        // the interior set's symmetric diagonal-class layout (TileSet::sym)
     pamg::TileSet interior;  // rows with own columns only (overlap with the exchange)
     pamg::TileSet boundary;  // rows with >= 1 ghost column
+    pamg::EllSet ell;        // the interior set's sliced-ELL layout (TileSet::ell)
     int64_t stream_bytes = 0;  // matrix bytes one apply reads (values, columns, row pointers, tiles)
 };
 

@@ -1312,6 +1312,140 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
     return PAMG_OK;
 }
 
+// Sliced ELL with per-group dictionaries (Options::ell, pamg::EllSet): a square operator whose
+// rows are all interior, in slices of kEllW rows padded to the slice's longest row, kEllGroup
+// rows sharing one table of column offsets (col - row) and one of values (bit patterns), each of
+// <= 256 entries. Declines (leaves the tile layouts to the caller) where a table would be larger or
+// a row longer than 255. Rows keep their storage order, so the kernel sums every row's products in
+// the SPEC §S3 order.
+int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci, const double* val) {
+    using pamg::kEllGroup;
+    using pamg::kEllW;
+    const int64_t n = A->nrows;
+    const int64_t ns = (n + kEllW - 1) / kEllW, ng = (n + kEllGroup - 1) / kEllGroup;
+    std::vector<int> slen(ns, 0);
+    std::atomic<bool> ok{true};
+    par_for(ns, [&](int64_t a, int64_t b) {
+        for (int64_t q = a; q < b; ++q) {
+            int m = 0;
+            for (int64_t i = q * kEllW; i < std::min(n, (q + 1) * kEllW); ++i) m = std::max<int>(m, (int)(rp[i + 1] - rp[i]));
+            if (m > 255) ok = false;
+            slen[q] = m;
+        }
+    });
+    if (!ok) return PAMG_OK;
+    std::vector<int2> smeta(ns);
+    int64_t words = 0;
+    for (int64_t q = 0; q < ns; ++q) {
+        smeta[q] = make_int2((int)words, slen[q]);
+        words += (int64_t)kEllW * ((slen[q] + 3) / 4);
+        if (words >= INT32_MAX) return PAMG_OK;
+    }
+    // per group: sorted distinct offsets and value bit patterns
+    std::vector<std::vector<int>> goff(ng);
+    std::vector<std::vector<uint64_t>> gval(ng);
+    par_for(ng, [&](int64_t a, int64_t b) {
+        std::vector<int> o;
+        std::vector<uint64_t> v;
+        for (int64_t g = a; g < b && ok; ++g) {
+            o.clear();
+            v.clear();
+            const int64_t r1 = std::min(n, (g + 1) * kEllGroup);
+            for (int64_t i = g * kEllGroup; i < r1; ++i)
+                for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                    o.push_back(ci[k] - (int)i);
+                    uint64_t u;
+                    std::memcpy(&u, &val[k], 8);
+                    v.push_back(u);
+                }
+            std::sort(o.begin(), o.end());
+            o.erase(std::unique(o.begin(), o.end()), o.end());
+            std::sort(v.begin(), v.end());
+            v.erase(std::unique(v.begin(), v.end()), v.end());
+            if (o.size() > 256 || v.size() > 256) {
+                ok = false;
+                return;
+            }
+            goff[g] = o;
+            gval[g] = v;
+        }
+    });
+    if (!ok) return PAMG_OK;
+    std::vector<int4> gmeta(ng);
+    int64_t on = 0, vn = 0;
+    for (int64_t g = 0; g < ng; ++g) {
+        gmeta[g] = make_int4((int)on, (int)goff[g].size(), (int)vn, (int)gval[g].size());
+        on += (int64_t)goff[g].size();
+        vn += (int64_t)gval[g].size();
+    }
+    std::vector<int> otab(on + 1, 0);
+    std::vector<double> vtab(vn + 1, 0.0);
+    par_for(ng, [&](int64_t a, int64_t b) {
+        for (int64_t g = a; g < b; ++g) {
+            std::copy(goff[g].begin(), goff[g].end(), otab.begin() + gmeta[g].x);
+            for (size_t e = 0; e < gval[g].size(); ++e) std::memcpy(&vtab[gmeta[g].z + e], &gval[g][e], 8);
+        }
+    });
+    std::vector<uint32_t> cw(words + 1, 0u), vw(words + 1, 0u);
+    std::vector<uint8_t> len(n + kVecPad, 0);
+    par_for(ns, [&](int64_t a, int64_t b) {
+        for (int64_t q = a; q < b; ++q) {
+            const int64_t g = q * kEllW / kEllGroup;
+            const auto& o = goff[g];
+            const auto& v = gval[g];
+            for (int lane = 0; lane < kEllW; ++lane) {
+                const int64_t i = q * kEllW + lane;
+                if (i >= n) break;
+                len[i] = (uint8_t)(rp[i + 1] - rp[i]);
+                for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                    const int kk = (int)(k - rp[i]);
+                    const uint32_t co = (uint32_t)(std::lower_bound(o.begin(), o.end(), ci[k] - (int)i) - o.begin());
+                    uint64_t u;
+                    std::memcpy(&u, &val[k], 8);
+                    const uint32_t vo = (uint32_t)(std::lower_bound(v.begin(), v.end(), u) - v.begin());
+                    const int64_t w = smeta[q].x + (int64_t)(kk / 4) * kEllW + lane;
+                    cw[w] |= co << (8 * (kk % 4));
+                    vw[w] |= vo << (8 * (kk % 4));
+                }
+            }
+        }
+    });
+    pamg::EllSet& E = A->ell;
+    pamg_ctx* ctx = A->ctx;
+    E.nslices = ns;
+    E.ngroups = ng;
+    E.words = words;
+    E.otab_n = on;
+    E.vtab_n = vn;
+    CHECK(dalloc(&E.d_smeta, ns));
+    CHECK(dalloc(&E.d_ci, words + 1));
+    CHECK(dalloc(&E.d_vi, words + 1));
+    CHECK(dalloc(&E.d_len, n + kVecPad));
+    CHECK(dalloc(&E.d_gmeta, ng));
+    CHECK(dalloc(&E.d_otab, on + 1));
+    CHECK(dalloc(&E.d_vtab, vn + 1));
+    CHECK(h2d(ctx, E.d_smeta, smeta.data(), sizeof(int2) * ns));
+    CHECK(h2d(ctx, E.d_ci, cw.data(), sizeof(uint32_t) * (words + 1)));
+    CHECK(h2d(ctx, E.d_vi, vw.data(), sizeof(uint32_t) * (words + 1)));
+    CHECK(h2d(ctx, E.d_len, len.data(), len.size()));
+    CHECK(h2d(ctx, E.d_gmeta, gmeta.data(), sizeof(int4) * ng));
+    CHECK(h2d(ctx, E.d_otab, otab.data(), sizeof(int) * (on + 1)));
+    CHECK(h2d(ctx, E.d_vtab, vtab.data(), sizeof(double) * (vn + 1)));
+    A->interior.ell = true;
+    return PAMG_OK;
+}
+
+void free_ell(pamg::EllSet& E) {
+    dfree(E.d_smeta);
+    dfree(E.d_ci);
+    dfree(E.d_vi);
+    dfree(E.d_len);
+    dfree(E.d_gmeta);
+    dfree(E.d_otab);
+    dfree(E.d_vtab);
+    E = pamg::EllSet{};
+}
+
 void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_short);
     dfree(ts.d_long);
@@ -2588,6 +2722,12 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         CHECK(build_sym_dia(A.get(), rp, ci, val, inner, band));
     if (A->interior.sym) inner.clear();  // the interior rows run in k_rows_sym, not in tiles
     tr.mark("sym dia");
+    if (pamg::options().ell && !A->interior.sym && n_own_cols == nrows && bnd.empty() && nrows > 0 &&
+        nrows >= pamg::options().ell_min_rows) {
+        CHECK(build_ell(A.get(), rp, ci, val));
+        if (A->interior.ell) inner.clear();  // the rows run in k_rows_ell, not in tiles
+        tr.mark("ell");
+    }
     std::vector<int> rp32(nrows + 1);
     for (int64_t i = 0; i <= nrows; ++i) rp32[i] = (int)rp[i];
     CHECK(dalloc(&A->d_rowptr, nrows + 1));
@@ -2641,8 +2781,13 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     if (A->interior.sym)
         A->stream_bytes += A->sym.vd_n ? nrows + (int64_t)A->sym.vd_n * (8 * (A->sym.nu + 1) + 4)
                                        : nrows * (A->sym.mask_bytes + 8 + 8 * (int64_t)A->sym.nu);
+    // sliced ELL: two index bytes per padded nonzero, a length byte per row, the slice and group
+    // descriptors and the group tables
+    if (A->interior.ell)
+        A->stream_bytes += 8 * A->ell.words + nrows + 8 * A->ell.nslices + 16 * A->ell.ngroups + 4 * A->ell.otab_n +
+                           8 * A->ell.vtab_n;
     for (const pamg::TileSet* t : {&A->interior, &A->boundary}) {
-        if (t->sym) continue;  // counted above
+        if (t->sym || t->ell) continue;  // counted above
         const int64_t ns = t->n_short, nz = t->nnz_short;
         int64_t b = 8 * (int64_t)t->n_long + 12 * t->nnz_long;
         const bool base = t->c24 && !t->cd;
@@ -2761,6 +2906,7 @@ int pamg_mat_destroy(pamg_mat* A) {
     dfree(A->sym.d_mtab);
     free_tiles(A->interior);
     free_tiles(A->boundary);
+    free_ell(A->ell);
     pamg_ctx* owner = A->ctx;
     delete A;
     ctx_unref(owner);
@@ -2795,7 +2941,8 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
              (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0) |
-             (t.sym && A->sym.vd_n ? 128 : 0) | (t.tm && t.xsr ? 256 : 0);
+             (t.sym && A->sym.vd_n ? 128 : 0) | (t.tm && t.xsr ? 256 : 0) | (t.ell ? 512 : 0);
+    if (t.ell) out[8] = (int)A->ell.ngroups;  // k_rows_ell's grid
     if (t.sym) {  // the symmetric diagonal-class layout: upper classes, k_rows_sym's grid
         out[4] = A->sym.nu;
         out[8] = A->sym.nbands * 8 * A->sym.eighth;
@@ -3462,6 +3609,8 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "sym_zm" && (value == 0 || value == 1)) o.sym_zm = (int)value;
     else if (k == "tb_zc" && (value == 0 || value == 1)) o.tb_zc = (int)value;
     else if (k == "tb_xfast" && (value == 0 || value == 1)) o.tb_xfast = (int)value;
+    else if (k == "ell" && (value == 0 || value == 1)) o.ell = (int)value;
+    else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
     else if (k == "tb_ty" && (value == 8 || value == 16)) o.tb_ty = (int)value;
     else if (k == "chain_store_x" && (value == 0 || value == 1)) o.chain_store_x = (int)value;
@@ -3503,6 +3652,8 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "sym_zm") *value = o.sym_zm;
     else if (k == "tb_zc") *value = o.tb_zc;
     else if (k == "tb_xfast") *value = o.tb_xfast;
+    else if (k == "ell") *value = o.ell;
+    else if (k == "ell_min_rows") *value = o.ell_min_rows;
     else if (k == "zm_chunks") *value = o.zm_chunks;
     else if (k == "tb_ty") *value = o.tb_ty;
     else if (k == "chain_store_x") *value = o.chain_store_x;

@@ -1054,6 +1054,104 @@ def test_sym_zm_bit_exact(ctx, kind, shape, zch):
     assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.57), bh, 0.57)))
 
 
+def _ell_cases(kind):
+    """Square operators for the sliced-ELL layout: a SPEC grid (7- / 5-point, ragged last group),
+    a random SPD pattern, and a matrix with empty and single-entry rows."""
+    if kind == "grid3d":
+        return O.generate("poisson3d", 19, 19, 19)
+    if kind == "grid2d":
+        return O.generate("poisson2d", 150, 150)
+    if kind == "random":  # a 7-point pattern with values from a 24-entry palette, diagonal 10
+        M = O.generate("poisson3d", 17, 17, 17)
+        pal = np.random.default_rng(9).standard_normal(24)
+        val = pal[np.random.default_rng(10).integers(0, 24, M.nnz)]
+        rows = np.repeat(np.arange(M.nrows), np.diff(M.rowptr))
+        val[M.col == rows] = 10.0
+        return O.CSR(M.rowptr.copy(), M.col.copy(), val, M.ncols)
+    n = 3000
+    rng = np.random.default_rng(4)
+    rows, cols, vals = [], [], []
+    for i in range(n):
+        if i % 97 == 0:
+            continue  # an empty row
+        k = 1 if i % 13 == 0 else int(rng.integers(2, 40))
+        cs = np.unique(np.clip(i + rng.integers(-60, 60, k), 0, n - 1))
+        rows += [i] * len(cs)
+        cols += cs.tolist()
+        vals += (rng.integers(1, 9, len(cs)) * 0.25).tolist()
+    import scipy.sparse as sp
+    T = sp.csr_matrix((vals, (rows, cols)), shape=(n, n))
+    T.sort_indices()
+    return O.CSR(T.indptr.astype(np.int64), T.indices.astype(np.int64), T.data.copy(), n)
+
+
+@pytest.mark.parametrize("kind", ["grid3d", "grid2d", "random", "ragged"])
+def test_ell_bit_exact(ctx, kind):
+    """k_rows_ell (sliced ELL, per-group 8-bit offset and value dictionaries; round 5): SpMV and
+    residual bit-exact with the oracle, and two Jacobi sweeps where every row has its diagonal;
+    the same results as the tile layouts on the same matrix."""
+    from parallel_amg_amd._lib import layout_of
+    M = _ell_cases(kind)
+    with _with_option("ell_min_rows", 0), _with_option("sym_dia", 0):
+        A, _h = upload(ctx, M)
+        with _with_option("ell", 0):
+            B, _h2 = upload(ctx, M)
+    assert layout_of(A)["ell"] and not layout_of(B)["ell"], (layout_of(A), layout_of(B))
+    rng = np.random.default_rng(3)
+    xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
+    for D in (A, B):
+        x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
+        mul(y, D, x)
+        assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
+        residual(y, D, x, b)
+        assert np.array_equal(bits(y.own_values()), bits(O.residual(M, xh, bh)))
+        if kind != "ragged":
+            t = PVector(ctx, M.nrows)
+            jacobi(x, D, b, t, 0.57, 2)
+            assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.57), bh, 0.57)))
+
+
+def test_ell_declines_what_does_not_fit(ctx):
+    """More than 256 distinct values in a group (random values on a 7-point grid) or a row longer
+    than 255: the tile layouts, still bit-exact."""
+    from parallel_amg_amd._lib import layout_of
+    M = O.generate("poisson3d", 12, 12, 12)
+    M = O.CSR(M.rowptr.copy(), M.col.copy(), np.random.default_rng(1).standard_normal(M.nnz), M.ncols)
+    n = 400
+    dense = O.CSR(np.arange(0, n * n + 1, n, dtype=np.int64), np.tile(np.arange(n, dtype=np.int64), n),
+                  np.ones(n * n), n)
+    for Mx in (M, dense):
+        with _with_option("ell_min_rows", 0), _with_option("sym_dia", 0):
+            A, _h = upload(ctx, Mx)
+        assert not layout_of(A)["ell"]
+        xh = np.random.default_rng(2).standard_normal(Mx.nrows)
+        x, y = PVector(ctx, Mx.nrows, 0, xh), PVector(ctx, Mx.nrows)
+        mul(y, A, x)
+        assert np.array_equal(bits(y.own_values()), bits(O.spmv(Mx, xh)))
+
+
+def test_ell_level1_operator_128(ctx):
+    """The level-1 operator of the 128^3 hierarchy (263,552 rows, 30 nonzeros per row: what the
+    512^3 cycle runs per V-cycle twice) in the sliced-ELL layout: residual and Jacobi bit-exact with
+    the oracle."""
+    from parallel_amg_amd._lib import layout_of
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 128)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=ctx)
+    M1 = H.levels[1][0].A
+    D = PSparseMatrix(ctx, M1)
+    assert layout_of(D)["ell"], layout_of(D)
+    Mo = O.CSR(M1.rowptr.copy(), M1.col.astype(np.int64), M1.val.copy(), M1.ncols)
+    rng = np.random.default_rng(8)
+    xh, bh = rng.standard_normal(M1.nrows), rng.standard_normal(M1.nrows)
+    x, b, y = PVector(ctx, M1.nrows, 0, xh), PVector(ctx, M1.nrows, 0, bh), PVector(ctx, M1.nrows)
+    residual(y, D, x, b)
+    assert np.array_equal(bits(y.own_values()), bits(O.residual(Mo, xh, bh)))
+    t = PVector(ctx, M1.nrows)
+    jacobi(x, D, b, t, 0.61, 1)
+    assert np.array_equal(bits(x.own_values()), bits(O.jacobi(Mo, xh, bh, 0.61)))
+
+
 def _cut_grid(n=64, cut=31):
     """poisson3d n^3 with the couplings between x = cut and x = cut + 1 removed (both directions):
     a tb_ok grid operator with absent entries INSIDE the grid (mask bits clear for in-grid
