@@ -1060,7 +1060,7 @@ def _ell_cases(kind):
     if kind == "grid3d":
         return O.generate("poisson3d", 19, 19, 19)
     if kind == "grid2d":
-        return O.generate("poisson2d", 150, 150)
+        return O.generate("poisson2d", 150, 150, 1)
     if kind == "random":  # a 7-point pattern with values from a 24-entry palette, diagonal 10
         M = O.generate("poisson3d", 17, 17, 17)
         pal = np.random.default_rng(9).standard_normal(24)
