@@ -2100,8 +2100,8 @@ __global__ __launch_bounds__(kZmThreads) void k_sym_zm(int nrows, const uint8_t*
 // row (k >= its length) selected away: the bits of every other row kernel (SPEC §S3). Groups in
 // XCD-contiguous order: block b on XCD b % 8 takes the (b / 8)-th group of that XCD's eighth, so an
 // XCD's L2 holds the x window its consecutive rows reuse.
-template <int OP>
-__global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int2* __restrict__ smeta,
+template <int OP, bool ANC>
+__global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __restrict__ anc, const int2* __restrict__ smeta,
                                                         const uint32_t* __restrict__ cw, const uint32_t* __restrict__ vw,
                                                         const uint8_t* __restrict__ len, const int4* __restrict__ gmeta,
                                                         const int* __restrict__ otab, const double* __restrict__ vtab,
@@ -2120,6 +2120,7 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int2* _
     const int ic = in ? i : nrows - 1;
     const int2 sm = smeta[ic / kEllW];  // (one slice per wave)
     const int L = in ? (int)len[i] : 0;
+    const int base = ANC ? anc[ic] : ic;  // offsets from the row (square) or its first column (anchored)
     const uint32_t* __restrict__ cp = cw + sm.x + lane;
     const uint32_t* __restrict__ vp = vw + sm.x + lane;
     const int nq = (sm.y + 3) >> 2;
@@ -2149,7 +2150,7 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int2* _
             vv[e] = lv[(vq >> (8 * e)) & 255u];
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) xv[e] = x[4 * q + e < L ? ic + of[e] : ic];
+        for (int e = 0; e < 4; ++e) xv[e] = x[4 * q + e < L ? base + of[e] : base];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const bool ok = 4 * q + e < L;
@@ -2578,8 +2579,13 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
     if (ts.ell) {
         const EllSet& E = A.ell;
         const int grid = (int)((E.ngroups + 7) / 8 * 8);
-        k_rows_ell<OP><<<grid, kEllGroup, 0, s>>>((int)A.nrows, E.d_smeta, E.d_ci, E.d_vi, E.d_len, E.d_gmeta, E.d_otab,
-                                                  E.d_vtab, (int)E.ngroups, x, b, y, omega);
+        if (E.d_anc)
+            k_rows_ell<OP, true><<<grid, kEllGroup, 0, s>>>((int)A.nrows, E.d_anc, E.d_smeta, E.d_ci, E.d_vi, E.d_len,
+                                                            E.d_gmeta, E.d_otab, E.d_vtab, (int)E.ngroups, x, b, y, omega);
+        else
+            k_rows_ell<OP, false><<<grid, kEllGroup, 0, s>>>((int)A.nrows, nullptr, E.d_smeta, E.d_ci, E.d_vi, E.d_len,
+                                                             E.d_gmeta, E.d_otab, E.d_vtab, (int)E.ngroups, x, b, y,
+                                                             omega);
     }
     if (ts.n_short > 0) {
         if (ts.tile_nnz == 1024) launch_tile<OP, 1024>(A, ts, x, b, y, omega, s);

@@ -167,6 +167,7 @@ struct Options {
     int ell = 1;               // 1: sliced ELL with per-group 8-bit dictionaries for square operators whose every row
                                //    is interior, where the tables fit (EllSet; the level-1 operator)
     int ell_min_rows = 65536;  // ... with at least this many rows
+    int ell_restrict = 1;      // 1: also restrictions (fewer rows than columns), offsets from each row's first column
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
 };
@@ -213,6 +214,7 @@ struct EllSet {
     int4* d_gmeta = nullptr;     // per group: (offset-table start, entries, value-table start, entries)
     int* d_otab = nullptr;       // the groups' offset tables, concatenated
     double* d_vtab = nullptr;    // the groups' value tables, concatenated
+    int* d_anc = nullptr;        // anchored (rectangular operators): per row the column its offsets start from
     int64_t words = 0, otab_n = 0, vtab_n = 0;
 };
 

@@ -1318,10 +1318,14 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
 // <= 256 entries. Declines (leaves the tile layouts to the caller) where a table would be larger or
 // a row longer than 255. Rows keep their storage order, so the kernel sums every row's products in
 // the SPEC §S3 order.
-int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci, const double* val) {
+// Rectangular operators (anchored: a restriction) take their offsets from each row's first column
+// (col - col_first(row)), the anchors stored per row.
+int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci, const double* val,
+              bool anchored) {
     using pamg::kEllGroup;
     using pamg::kEllW;
     const int64_t n = A->nrows;
+    auto base_of = [&](int64_t i) -> int { return anchored ? (rp[i + 1] > rp[i] ? ci[rp[i]] : 0) : (int)i; };
     const int64_t ns = (n + kEllW - 1) / kEllW, ng = (n + kEllGroup - 1) / kEllGroup;
     std::vector<int> slen(ns, 0);
     std::atomic<bool> ok{true};
@@ -1353,7 +1357,7 @@ int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
             const int64_t r1 = std::min(n, (g + 1) * kEllGroup);
             for (int64_t i = g * kEllGroup; i < r1; ++i)
                 for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-                    o.push_back(ci[k] - (int)i);
+                    o.push_back(ci[k] - base_of(i));
                     uint64_t u;
                     std::memcpy(&u, &val[k], 8);
                     v.push_back(u);
@@ -1399,7 +1403,7 @@ int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
                 len[i] = (uint8_t)(rp[i + 1] - rp[i]);
                 for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
                     const int kk = (int)(k - rp[i]);
-                    const uint32_t co = (uint32_t)(std::lower_bound(o.begin(), o.end(), ci[k] - (int)i) - o.begin());
+                    const uint32_t co = (uint32_t)(std::lower_bound(o.begin(), o.end(), ci[k] - base_of(i)) - o.begin());
                     uint64_t u;
                     std::memcpy(&u, &val[k], 8);
                     const uint32_t vo = (uint32_t)(std::lower_bound(v.begin(), v.end(), u) - v.begin());
@@ -1431,6 +1435,14 @@ int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
     CHECK(h2d(ctx, E.d_gmeta, gmeta.data(), sizeof(int4) * ng));
     CHECK(h2d(ctx, E.d_otab, otab.data(), sizeof(int) * (on + 1)));
     CHECK(h2d(ctx, E.d_vtab, vtab.data(), sizeof(double) * (vn + 1)));
+    if (anchored) {
+        std::vector<int> anc(n + kVecPad, 0);
+        par_for(n, [&](int64_t a, int64_t b) {
+            for (int64_t i = a; i < b; ++i) anc[i] = base_of(i);
+        });
+        CHECK(dalloc(&E.d_anc, n + kVecPad));
+        CHECK(h2d(ctx, E.d_anc, anc.data(), sizeof(int) * anc.size()));
+    }
     A->interior.ell = true;
     return PAMG_OK;
 }
@@ -1443,6 +1455,7 @@ void free_ell(pamg::EllSet& E) {
     dfree(E.d_gmeta);
     dfree(E.d_otab);
     dfree(E.d_vtab);
+    dfree(E.d_anc);
     E = pamg::EllSet{};
 }
 
@@ -2722,9 +2735,11 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         CHECK(build_sym_dia(A.get(), rp, ci, val, inner, band));
     if (A->interior.sym) inner.clear();  // the interior rows run in k_rows_sym, not in tiles
     tr.mark("sym dia");
-    if (pamg::options().ell && !A->interior.sym && n_own_cols == nrows && bnd.empty() && nrows > 0 &&
-        nrows >= pamg::options().ell_min_rows) {
-        CHECK(build_ell(A.get(), rp, ci, val));
+    // square operators (offsets from the row) and restrictions (fewer rows than columns; offsets from
+    // each row's first column)
+    if (pamg::options().ell && !A->interior.sym && n_own_cols >= nrows && bnd.empty() && nrows > 0 &&
+        nrows >= pamg::options().ell_min_rows && (n_own_cols == nrows || pamg::options().ell_restrict)) {
+        CHECK(build_ell(A.get(), rp, ci, val, n_own_cols != nrows));
         if (A->interior.ell) inner.clear();  // the rows run in k_rows_ell, not in tiles
         tr.mark("ell");
     }
@@ -2785,7 +2800,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     // descriptors and the group tables
     if (A->interior.ell)
         A->stream_bytes += 8 * A->ell.words + nrows + 8 * A->ell.nslices + 16 * A->ell.ngroups + 4 * A->ell.otab_n +
-                           8 * A->ell.vtab_n;
+                           8 * A->ell.vtab_n + (A->ell.d_anc ? 4 * nrows : 0);
     for (const pamg::TileSet* t : {&A->interior, &A->boundary}) {
         if (t->sym || t->ell) continue;  // counted above
         const int64_t ns = t->n_short, nz = t->nnz_short;
@@ -3610,6 +3625,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "tb_zc" && (value == 0 || value == 1)) o.tb_zc = (int)value;
     else if (k == "tb_xfast" && (value == 0 || value == 1)) o.tb_xfast = (int)value;
     else if (k == "ell" && (value == 0 || value == 1)) o.ell = (int)value;
+    else if (k == "ell_restrict" && (value == 0 || value == 1)) o.ell_restrict = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
     else if (k == "tb_ty" && (value == 8 || value == 16)) o.tb_ty = (int)value;
@@ -3653,6 +3669,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "tb_zc") *value = o.tb_zc;
     else if (k == "tb_xfast") *value = o.tb_xfast;
     else if (k == "ell") *value = o.ell;
+    else if (k == "ell_restrict") *value = o.ell_restrict;
     else if (k == "ell_min_rows") *value = o.ell_min_rows;
     else if (k == "zm_chunks") *value = o.zm_chunks;
     else if (k == "tb_ty") *value = o.tb_ty;

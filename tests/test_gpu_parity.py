@@ -1130,6 +1130,29 @@ def test_ell_declines_what_does_not_fit(ctx):
         assert np.array_equal(bits(y.own_values()), bits(O.spmv(Mx, xh)))
 
 
+def test_ell_restriction_128(ctx):
+    """The 128^3 hierarchy's restriction R_0 (263,552 coarse rows reading the 2.1M-entry fine vector,
+    29 nonzeros per row) in the anchored sliced-ELL layout (offsets from each row's first column):
+    y = R r bit-exact with the oracle; declined with ell_restrict 0."""
+    from parallel_amg_amd._lib import layout_of
+    be = pa.SequentialBackend(1)
+    A, offs, xs = pa.generate_problem(be, "poisson3d", 128)
+    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=ctx)
+    R0 = H.levels[0][0].R
+    D = PSparseMatrix(ctx, R0)
+    assert layout_of(D)["ell"], layout_of(D)
+    with _with_option("ell_restrict", 0):
+        D2 = PSparseMatrix(ctx, R0)
+    assert not layout_of(D2)["ell"]
+    Mo = O.CSR(R0.rowptr.copy(), R0.col.astype(np.int64), R0.val.copy(), R0.ncols)
+    rh = np.random.default_rng(12).standard_normal(R0.ncols)
+    r = PVector(ctx, R0.ncols, 0, rh)
+    for M in (D, D2):
+        y = PVector(ctx, R0.nrows)
+        mul(y, M, r)
+        assert np.array_equal(bits(y.own_values()), bits(O.spmv(Mo, rh)))
+
+
 def test_ell_level1_operator_128(ctx):
     """The level-1 operator of the 128^3 hierarchy (263,552 rows, 30 nonzeros per row: what the
     512^3 cycle runs per V-cycle twice) in the sliced-ELL layout: residual and Jacobi bit-exact with
