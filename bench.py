@@ -304,11 +304,8 @@ def main():
     # the instance name as rocprofv3 demangles it (every template argument, defaults included)
     tf = lambda v: "true" if v else "false"  # noqa: E731
     if pipelined:
-        if lay.get("sym_vd") and _option("tb_zc"):  # the z-marching chain (round 5)
+        if lay.get("sym_vd"):  # the z-marching chain over the row-class dictionary (round 5)
             kname = "k_sym_zc<3>"
-        elif lay.get("sym_vd"):  # k_sym_tbd<S, PD, TY> (8-line tiles run one plane ahead)
-            ty = _option("tb_ty")
-            kname = f"k_sym_tbd<3, {1 if ty == 8 else _tb_pd()}, {ty}>"
         else:
             kname = "k_sym_tb<3>"
         post_ms = float(fused["chain3_ms"])
@@ -498,11 +495,6 @@ def _option(key: str) -> int:
     v = ctypes.c_int64()
     _lib.call("pamg_get_option", key.encode(), ctypes.byref(v))
     return int(v.value)
-
-
-def _tb_pd() -> int:
-    """The row-class chain's prefetch depth (libpamg option tb_pd, a template argument of k_sym_tbd)."""
-    return _option("tb_pd")
 
 
 def _sym_kname(op: int, lay: dict) -> str:

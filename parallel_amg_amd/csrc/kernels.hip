@@ -158,8 +158,6 @@ __global__ __launch_bounds__(kBlock) void k_rows_tile2(
     // CD (column dictionary, 4 or 8 bits per nonzero): column = row + ctab[index], with the
     // tile set's <= 16 / <= 256 distinct offsets (a stencil's 7 for A0) in LDS; every
     // position's row (lrow, tile-local) is marked by the lane that owns the row (RL8 scan)
-    // (with VD: per-tile dictionaries of a prolongator whose values are 4-bit indices too,
-    // Options::vd_col_dict)
     static_assert(CD == 0 || (RL8 && !C24), "column dictionary: 8-bit rows");
     __shared__ int ltab[CD != 0 ? BS : 1];
     __shared__ __attribute__((aligned(4))) uint8_t lrow[CD ? TNNZ + 8 : 4];
@@ -387,25 +385,17 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     const uint8_t* __restrict__ trlen, int rs, const int* __restrict__ ctab, int ctab_n,
     const double* __restrict__ x, const double* __restrict__ b, double* __restrict__ y,
     double omega, const int* __restrict__ tanc = nullptr, const XStage xst = XStage{},
-    const uint8_t* __restrict__ tvidx = nullptr, const double* __restrict__ tvtab = nullptr, int vt = 0,
-    const uint16_t* __restrict__ xpos = nullptr, const int* __restrict__ xmeta = nullptr) {
+    const uint8_t* __restrict__ tvidx = nullptr, const double* __restrict__ tvtab = nullptr, int vt = 0) {
     // ANC (anchored dictionary): column = the row's first column (slot anchors, tanc) +
     // table[index] instead of row + table[index]
     static_assert(!ANC || CD != 0, "anchored columns are dictionary columns");
     static_assert(!XS || (CD != 0 && !ANC), "x staging needs row-relative dictionary columns");
     static_assert(!PT || (CD != 0 && !ANC), "per-tile tables: row-relative");
-    // XS && PT (TileSet::xsr, launched with Options::xsr_kernel = 1): per-tile x staging — the
-    // tile's run table (xmeta) and entry positions (xpos) from the upload, the runs loaded after
-    // the first barrier, products reading x from LDS (the k_rows_xsr staging inside this body)
-    constexpr bool XSP = XS && PT;
-    static_assert(!XSP || (CD == 8 && TNNZ == 2048), "per-tile staging: 8-bit tables, 2048-nonzero tiles");
+    static_assert(!(XS && PT), "x staging uses the set-wide table");
     constexpr int BS = kBlock;
     constexpr int G = TNNZ / (4 * BS);
     static_assert(G >= 1 && TNNZ % (4 * BS) == 0, "tile budget must be a multiple of 4 x block");
-    // XSP: the staged x runs and the products share one array (a barrier between the last x read
-    // and the first product store), so the staging costs no occupancy
-    constexpr int NPROD = XSP && kXsrCap2048 > TNNZ + 8 ? kXsrCap2048 : TNNZ + 8;
-    __shared__ __attribute__((aligned(16))) double lprod[NPROD];
+    __shared__ __attribute__((aligned(16))) double lprod[TNNZ + 8];
     __shared__ double ldiag[OP == OP_JACOBI ? BS : 1];
     __shared__ int lwt[BS / 64];
     // XS keeps only the table's LDS positions (kXsIoff + index): 16 / 128 entries, so the
@@ -413,15 +403,12 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     // 2048-nonzero tiles keep per-tile tables of <= kTmSmallTab entries (checked at upload,
     // build_tile_major), so one more block fits per CU (512^3 A1: residual 7 -> 8, Jacobi 6 -> 7
     // waves per SIMD; -2.4 % / -4.6 %, profiles/r03_lds/)
-    constexpr int NTAB = CD == 0 ? 1 : XSP ? kTmSmallTab : XS ? (CD == 4 ? 16 : kXsIoff)
-                       : PT && TNNZ == 2048 ? kTmSmallTab : BS;
+    constexpr int NTAB = CD == 0 ? 1 : XS ? (CD == 4 ? 16 : kXsIoff) : PT && TNNZ == 2048 ? kTmSmallTab : BS;
     constexpr int NVT = TNNZ == 2048 ? kTmSmallTab : BS;
     __shared__ int ltab[NTAB];
     __shared__ __attribute__((aligned(4))) uint8_t lrow[TNNZ + 8];
     __shared__ int lanc[ANC ? BS : 1];
-    __shared__ double lxs_own[XS && !XSP ? kXsCap + 1 : 1];  // + 1: the dump slot of lanes past a run
-    double* const lxs = XSP ? lprod : lxs_own;
-    __shared__ int lmeta[XSP ? kXsMeta : 1];
+    __shared__ double lxs[XS ? kXsCap + 1 : 1];  // + 1: the dump slot of lanes past a run
     __shared__ double lvt[VD8 ? NVT : 1];        // the tile's value table (vt <= NVT entries)
 
     const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -435,11 +422,8 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     // value stream last: the scan, the row map and the x gathers then proceed while the
     // values are still in flight (previously the scan's wait on the row lengths also waited
     // for the whole value stream, and the gathers' wait on the columns for b / x).
-    int tabv = 0, ancv = 0, mv = 0;
-    if constexpr (XSP) {
-        mv = xmeta[(size_t)t * kXsMeta + (tid < kXsMeta ? tid : 0)];
-        tabv = xpos[(size_t)t * ctab_n + (tid < ctab_n ? tid : ctab_n - 1)];
-    } else if constexpr (XS) tabv = ctab[kXsIoff + (tid < NTAB ? tid : NTAB - 1)];
+    int tabv = 0, ancv = 0;
+    if constexpr (XS) tabv = ctab[kXsIoff + (tid < NTAB ? tid : NTAB - 1)];
     else if constexpr (PT) tabv = ctab[(size_t)t * ctab_n + (tid < ctab_n ? tid : ctab_n - 1)];
     else if constexpr (CD != 0) tabv = ctab[tid];  // the table is allocated with 256 entries
     const size_t rsl = (size_t)t * rs + (tid < rs ? tid : rs - 1);
@@ -473,7 +457,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
         if constexpr (OP == OP_PROLONG) py = y[r];
     }
     double xsv[XS ? kXsMaxClusters : 1];
-    if constexpr (XS && !XSP) {
+    if constexpr (XS) {
 #pragma unroll
         for (int c = 0; c < kXsMaxClusters; ++c) {
             xsv[c] = 0.0;
@@ -501,13 +485,10 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     if constexpr (VD8) lvt[tid < NVT ? tid : NVT - 1] = vtv;  // every lane (lanes past vt repeat the last entry)
     // every lane stores its entry (unconditionally: a conditional store lets the compiler sink
     // the table load into the branch, behind the value stream)
-    if constexpr (XSP) {
-        if (tid < NTAB) ltab[tid] = tabv;
-        if (tid < kXsMeta) lmeta[tid] = mv;
-    } else if constexpr (XS) ltab[tid < NTAB ? tid : NTAB - 1] = tabv;  // lanes past NTAB rewrite the last entry's value
+    if constexpr (XS) ltab[tid < NTAB ? tid : NTAB - 1] = tabv;  // lanes past NTAB rewrite the last entry's value
     else if constexpr (CD != 0) ltab[tid < NTAB ? tid : NTAB - 1] = tabv;  // (lanes past ctab_n: the last entry)
     if constexpr (ANC) lanc[tid] = tid < rs ? ancv : 0;
-    if constexpr (XS && !XSP) {
+    if constexpr (XS) {
 #pragma unroll
         for (int c = 0; c < kXsMaxClusters; ++c)
             if (c < xst.ncl) lxs[tid < xst.stride ? c * xst.stride + tid : kXsCap] = xsv[c];
@@ -528,36 +509,12 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     constexpr bool NEED_ROWS = CD != 0 || OP == OP_JACOBI;
     int re = 0;
     if constexpr (VD8 && !NEED_ROWS) __syncthreads();  // lvt
-    int xzix = -1;
     if constexpr (NEED_ROWS) {
-        __syncthreads();  // lwt, ltab (, lmeta)
+        __syncthreads();  // lwt, ltab
         re = row_end();
-        if constexpr (XSP) {  // the x runs: staged element e of run c is x[r0 + omin_c + e - base_c]
-            constexpr int NE = (kXsrCap2048 + BS - 1) / BS;
-            const int ncl = lmeta[0], tot = lmeta[2];
-            xzix = lmeta[1];
-            double xe[NE];
-#pragma unroll
-            for (int j = 0; j < NE; ++j) {
-                const int e = tid + j * BS;
-                int lo = 0, hi = ncl - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (lmeta[3 + kXsrMaxRuns + mid] <= e) lo = mid;
-                    else hi = mid - 1;
-                }
-                const int64_t g = (int64_t)r0 + lmeta[3 + lo] + (e - lmeta[3 + kXsrMaxRuns + lo]);
-                xe[j] = x[e < tot && g >= 0 && g < xst.ncols ? g : 0];
-            }
-            if (tid < nr)
-                for (int p = re - rl_len; p < re; ++p) lrow[p] = (uint8_t)tid;
-#pragma unroll
-            for (int j = 0; j < NE; ++j)
-                if (tid + j * BS < tot) lxs[tid + j * BS] = xe[j];
-        } else if (tid < nr) {
+        if (tid < nr)
             for (int p = re - rl_len; p < re; ++p) lrow[p] = (uint8_t)tid;
-        }
-        __syncthreads();  // lrow (, lxs)
+        __syncthreads();  // lrow
     }
 
     double xv[G][4];
@@ -575,11 +532,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
                 // product is discarded), so every LDS read stays inside lxs
                 const int rid = q + e < cnt ? (int)((rw >> (8 * e)) & 255u) : 0;
                 cc[j][e] = ix;
-                if constexpr (XSP) {  // padding bytes index no table entry: slot 0 for them too
-                    xv[j][e] = q + e < cnt ? lxs[ltab[ix] + rid] : 0.0;
-                } else {
-                    xv[j][e] = lxs[ltab[ix] + rid];
-                }
+                xv[j][e] = lxs[ltab[ix] + rid];
             }
             continue;
         }
@@ -600,7 +553,6 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
 #pragma unroll
         for (int e = 0; e < 4; ++e) xv[j][e] = x[q + e < cnt ? cc[j][e] : 0];
     }
-    if constexpr (XSP) __syncthreads();  // every staged x read before the products overwrite it
 #pragma unroll
     for (int j = 0; j < G; ++j) {
         const int q = 4 * (tid + j * BS);
@@ -623,7 +575,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
             p[e] = ok ? vv[e] * xv[j][e] : 0.0;
             if constexpr (OP == OP_JACOBI) {
                 const int rl = (int)((rw >> (8 * e)) & 255u);
-                if (ok && (XSP ? cc[j][e] == xzix : XS ? cc[j][e] == xst.zix : cc[j][e] - r0 == rl)) ldiag[rl] = vv[e];
+                if (ok && (XS ? cc[j][e] == xst.zix : cc[j][e] - r0 == rl)) ldiag[rl] = vv[e];
             }
         }
         *reinterpret_cast<double2*>(&lprod[q]) = make_double2(p[0], p[1]);
@@ -649,150 +601,6 @@ __global__ __launch_bounds__(kBlock) void k_rows_tm(
     }
     if (tid < nr) y[r0 + tid] = out;
 }
-// k_rows_xsr: tile-major slots with per-tile 8-bit column and value dictionaries (TileSet::xsr;
-// the 512^3 level-1 operator: 31 nonzeros per row, 567 distinct values), x staged in LDS, one
-// row per lane. A tile's loads are coalesced and issued at entry — its column- and value-index
-// streams (one byte each per nonzero), its dictionary tables (entry -> LDS position, index ->
-// value) and its run table — then, after one barrier, its x runs: staged element e of run c is
-// x[r0 + omin_c + e - base_c], a lane loads elements tid, tid + 256, ... After a second barrier
-// each lane walks its own row in storage order and reads everything from LDS: x of entry ix for
-// row tid at lxs[pos[ix] + tid]. No x gather from L2 (k_rows_tm's per-nonzero round trip: 2048
-// lines per tile for ~1250 staged doubles here), no row map, no product staging. Products
-// rounded, summed left to right from +0.0 in storage order (SPEC §S3): every row kernel's bits.
-template <int OP, int TNNZ>
-__global__ __launch_bounds__(kBlock) void k_rows_xsr(
-    const int4* __restrict__ tiles, const uint8_t* __restrict__ tcidx, const uint8_t* __restrict__ tvidx,
-    const double* __restrict__ tvtab, int vt, const uint8_t* __restrict__ trlen, int rs,
-    const uint16_t* __restrict__ xpos, int ctab_n, const int* __restrict__ xmeta, const double* __restrict__ x,
-    int64_t ncols, const double* __restrict__ b, double* __restrict__ y, double omega) {
-    constexpr int BS = kBlock;
-    constexpr int NB = TNNZ / BS;  // index-stream bytes per lane (8 or 16)
-    static_assert(NB == 8 || NB == 16, "2048- or 4096-nonzero tiles");
-    constexpr int NT = TNNZ == 2048 ? kTmSmallTab : BS;  // table entries (upload limit)
-    constexpr int CAP = TNNZ == 2048 ? kXsrCap2048 : kXsrCap4096;
-    constexpr int NE = (CAP + BS - 1) / BS;              // staged elements per lane
-    static_assert(kXsMeta <= BS, "one run-table entry per lane");
-    __shared__ __attribute__((aligned(16))) uint8_t lix[TNNZ];
-    __shared__ __attribute__((aligned(16))) uint8_t lvx[TNNZ];
-    __shared__ uint16_t lpos[NT];
-    __shared__ double lvt[NT];
-    __shared__ double lxs[CAP];
-    __shared__ int lmeta[kXsMeta];
-    __shared__ int lwt[BS / 64];
-
-    const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    const int4 d = tiles[t];
-    const int r0 = d.x, nr = d.y - d.x;
-    const size_t sb = (size_t)t * TNNZ;
-    // ---- every load that depends on no other one, the run table first
-    const int mv = xmeta[(size_t)t * kXsMeta + (tid < kXsMeta ? tid : 0)];
-    const int rlv = (int)trlen[(size_t)t * rs + (tid < rs ? tid : rs - 1)];
-    uint4 ci4, vi4;
-    uint2 ci2, vi2;
-    if constexpr (NB == 16) {
-        ci4 = *reinterpret_cast<const uint4*>(tcidx + sb + 16 * tid);
-        vi4 = *reinterpret_cast<const uint4*>(tvidx + sb + 16 * tid);
-    } else {
-        ci2 = *reinterpret_cast<const uint2*>(tcidx + sb + 8 * tid);
-        vi2 = *reinterpret_cast<const uint2*>(tvidx + sb + 8 * tid);
-    }
-    const uint16_t posv = xpos[(size_t)t * ctab_n + (tid < ctab_n ? tid : ctab_n - 1)];
-    const double vtv = tvtab[(size_t)t * vt + (tid < vt ? tid : vt - 1)];
-    double pb = 0.0, px = 0.0, py = 0.0;
-    {
-        const int r = r0 + (tid < nr ? tid : 0);
-        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[r];
-        if constexpr (OP == OP_JACOBI) px = x[r];
-        if constexpr (OP == OP_PROLONG) py = y[r];
-    }
-    if (tid < kXsMeta) lmeta[tid] = mv;
-    if constexpr (NB == 16) {
-        *reinterpret_cast<uint4*>(&lix[16 * tid]) = ci4;
-        *reinterpret_cast<uint4*>(&lvx[16 * tid]) = vi4;
-    } else {
-        *reinterpret_cast<uint2*>(&lix[8 * tid]) = ci2;
-        *reinterpret_cast<uint2*>(&lvx[8 * tid]) = vi2;
-    }
-    if (tid < NT) {
-        lpos[tid] = posv;
-        lvt[tid] = vtv;
-    }
-    const int rl_len = tid < nr ? rlv : 0;
-    const int rl_inc = wave_incl_scan(rl_len);
-    if (lane == 63) lwt[tid >> 6] = rl_inc;
-    __syncthreads();  // lmeta, lwt
-    // ---- the x runs: element e belongs to the last run whose base is <= e (binary search)
-    const int ncl = lmeta[0], zix = lmeta[1], tot = lmeta[2];
-    const int* __restrict__ omin = &lmeta[3];
-    const int* __restrict__ base = &lmeta[3 + kXsrMaxRuns];
-    double xe[NE];
-#pragma unroll
-    for (int j = 0; j < NE; ++j) {
-        const int e = tid + j * BS;
-        int lo = 0, hi = ncl - 1;
-        while (lo < hi) {  // (uniform trip count per lane; <= 5 steps)
-            const int mid = (lo + hi + 1) >> 1;
-            if (base[mid] <= e) lo = mid;
-            else hi = mid - 1;
-        }
-        const int64_t g = (int64_t)r0 + omin[lo] + (e - base[lo]);
-        const bool ok = e < tot && g >= 0 && g < ncols;
-        xe[j] = x[ok ? g : 0];
-    }
-#pragma unroll
-    for (int j = 0; j < NE; ++j)
-        if (tid + j * BS < tot) lxs[tid + j * BS] = xe[j];
-    int pre = 0;
-#pragma unroll
-    for (int q = 0; q < BS / 64; ++q) pre += q < (tid >> 6) ? lwt[q] : 0;
-    const int ke = pre + rl_inc, kb = ke - rl_len;
-    __syncthreads();  // lxs
-    // ---- one row per lane, storage order; batches of 4 read ahead of the dependent adds
-    double s = 0.0, dg = 0.0;
-    int k = kb;
-    for (; k + 4 <= ke; k += 4) {
-        uint32_t ix[4], vx[4];
-        double xv[4], vv[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            ix[e] = lix[k + e];
-            vx[e] = lvx[k + e];
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            xv[e] = lxs[lpos[ix[e]] + tid];
-            vv[e] = lvt[vx[e]];
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const double p = vv[e] * xv[e];
-            s = s + p;
-            if constexpr (OP == OP_JACOBI) dg = (int)ix[e] == zix ? vv[e] : dg;
-        }
-    }
-    for (; k < ke; ++k) {
-        const uint32_t ix = lix[k];
-        const double vv = lvt[lvx[k]];
-        const double p = vv * lxs[lpos[ix] + tid];
-        s = s + p;
-        if constexpr (OP == OP_JACOBI) dg = (int)ix == zix ? vv : dg;
-    }
-    double out;
-    if constexpr (OP == OP_SPMV) {
-        out = s;
-    } else if constexpr (OP == OP_RESID) {
-        out = pb - s;
-    } else if constexpr (OP == OP_JACOBI) {
-        const double u = pb - s;
-        const double v = omega * u;
-        const double w = v / dg;
-        out = px + w;
-    } else {
-        out = py + s;
-    }
-    if (tid < nr) y[r0 + tid] = out;
-}
-
 // k_rows_sym: the symmetric diagonal-class layout (pamg::SymDia). One row per lane; every
 // operand is a coalesced stream over consecutive rows — the diagonal, the NU upper-value
 // arrays U_c[i], their mirrors U_c[i - o_c] (the lower values: the same lines a block o_c rows
@@ -1018,7 +826,7 @@ template <int OP, int NU, int CH = 1>
 __global__ __launch_bounds__(kBlock) void k_rows_symd(
     int nrows, int ncols, const uint8_t* __restrict__ tid, const double* __restrict__ vtab,
     const uint32_t* __restrict__ mtab, int nv, const SymDia sd, const double* __restrict__ x,
-    const double* __restrict__ b, double* __restrict__ y, double omega, bool pair_ids = true, int main = -1) {
+    const double* __restrict__ b, double* __restrict__ y, double omega) {
     constexpr int RB = 2 * kBlock;  // rows per unit
     constexpr int P = CH < 2 ? CH : 2;
     static_assert(CH % P == 0, "units in pairs");
@@ -1027,8 +835,6 @@ __global__ __launch_bounds__(kBlock) void k_rows_symd(
     const int xcd = bid & 7, u0 = (bid >> 3) * CH;
     const int nunits = sd.nbands * sd.eighth;
     const int64_t n = nrows;
-    double vmain[NU + 1] = {};  // the main class's values and mask (fast path; main >= 0)
-    uint32_t mmain = 0;
 #pragma unroll 1
     for (int k0 = 0; k0 < CH; k0 += P) {
         int64_t ib[P];
@@ -1051,19 +857,8 @@ __global__ __launch_bounds__(kBlock) void k_rows_symd(
 #pragma unroll
             for (int c = 0; c < NU; ++c) {
                 const int o = sd.off[NU - 1 - c];
-                // the mirror rows' ids as one 2-byte load where the pair is aligned (even o), and
-                // for o = 1 the byte below the own pair (the other one is row ib's own id)
-                if (pair_ids && o == 1) {
-                    tl[q][0][c] = (uint32_t)tbd_pair_ids(tid, ib[q] - 2, n) >> 8;
-                    tl[q][1][c] = tw[q] & 0xffu;
-                } else if (pair_ids && (o & 1) == 0) {
-                    const uint32_t w = tbd_pair_ids(tid, ib[q] - o, n);
-                    tl[q][0][c] = w & 0xffu;
-                    tl[q][1][c] = w >> 8;
-                } else {
-                    tl[q][0][c] = tid_at(tid, ib[q] - o, n);
-                    tl[q][1][c] = tid_at(tid, ib[q] + 1 - o, n);
-                }
+                tl[q][0][c] = tid_at(tid, ib[q] - o, n);
+                tl[q][1][c] = tid_at(tid, ib[q] + 1 - o, n);
                 const double2 xx = ld_pair(x, ib[q] - o, ncols, (o & 1) == 0);
                 xv[q][0][c] = xx.x;
                 xv[q][1][c] = xx.y;
@@ -1088,39 +883,19 @@ __global__ __launch_bounds__(kBlock) void k_rows_symd(
         if (k0 == 0) {  // (uniform)
             symtab_fill<NU>(tab, vtab, mtab, nv);
             __syncthreads();
-            if (main >= 0) {
-#pragma unroll
-                for (int c = 0; c <= NU; ++c) vmain[c] = tab.v[main][c];
-                mmain = tab.m[main];
-            }
         }
 #pragma unroll
         for (int q = 0; q < P; ++q) {
-            // fast path (main >= 0): every row of the wave and every mirror row is of the main
-            // class — its values are the same table entry for all of them, read once (broadcast)
-            bool mine = main >= 0 && (tw[q] & 0xffu) == (uint32_t)main && (tw[q] >> 8) == (uint32_t)main;
-#pragma unroll
-            for (int c = 0; c < NU; ++c) mine = mine && tl[q][0][c] == (uint32_t)main && tl[q][1][c] == (uint32_t)main;
-            const bool fast = __all(mine);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const uint32_t t = r == 0 ? (tw[q] & 0xffu) : (tw[q] >> 8);
-                uint32_t m;
+                const uint32_t m = tab.m[t];
                 double v[2 * NU + 1];
-                if (fast) {
-                    m = mmain;
 #pragma unroll
-                    for (int c = 0; c <= NU; ++c) v[NU + c] = vmain[c];
+                for (int c = 0; c < NU; ++c) v[c] = tab.v[tl[q][r][c]][1 + (NU - 1 - c)];
+                v[NU] = tab.v[t][0];
 #pragma unroll
-                    for (int c = 0; c < NU; ++c) v[c] = v[NU + NU - c];  // U_c of the same class
-                } else {
-                    m = tab.m[t];
-#pragma unroll
-                    for (int c = 0; c < NU; ++c) v[c] = tab.v[tl[q][r][c]][1 + (NU - 1 - c)];
-                    v[NU] = tab.v[t][0];
-#pragma unroll
-                    for (int c = 0; c < NU; ++c) v[NU + 1 + c] = tab.v[t][1 + c];
-                }
+                for (int c = 0; c < NU; ++c) v[NU + 1 + c] = tab.v[t][1 + c];
                 double s = 0.0;
 #pragma unroll
                 for (int k = 0; k < 2 * NU + 1; ++k) {
@@ -1167,7 +942,7 @@ constexpr int kTbPX = (kTbX + 4) / 2;  // row pairs per line: x0-2 .. x0+kTbX+1
 constexpr int kTbLW = kTbX + 8;        // LDS line: column x - x0 + 4 (even for even x; pads 0-1, kTbX+6-7)
 
 template <int S, int TY = kTbY>
-struct TbShape {                                 // TY: tile height (Options::tb_ty; kTbY by default)
+struct TbShape {                                 // TY: tile height (kTbY)
     static constexpr int H = S - 1;              // stage-0 halo in y and z
     static constexpr int RY = TY + 2 * H;        // grid lines of stage 0
     static constexpr int NT = kTbPX * RY;        // threads with a row pair
@@ -1253,7 +1028,7 @@ struct TbCtx {
     int x0, y0;           // the tile's first grid point
 };
 
-// The workgroup's tile and the thread's row pair (k_sym_tb / k_sym_tbd); false: no tile (the
+// The workgroup's tile and the thread's row pair (k_sym_tb / k_sym_zc); false: no tile (the
 // whole workgroup returns before any barrier). Tiles: consecutive tiles on one XCD (block b runs
 // on XCD b % 8; speed only), ordered y-fastest so that the tiles sharing the wide y halos
 // (kTbX + 4 points x S-1 lines) sit on one XCD.
@@ -1447,16 +1222,11 @@ __global__ __launch_bounds__(TbShape<S>::threads) void k_sym_tb(int nrows, const
     }
 }
 
-// ---- k_sym_tbd<S>: k_sym_tb over the row-class dictionary (SymDia::vd_n). Same tiles, halos,
-// LDS rings and row expressions (so the same bits); what differs is what a thread holds per plane
-// and when it loads it. Per row pair and plane it holds the two class ids, the mirror rows' ids
-// (i-1; i-nx, i+1-nx; i-M, i+1-M: the pair's ids one plane down) and b — 5 registers instead of
-// k_sym_tb's 17 doubles — so the plane ring runs one plane ahead of the computation. At step k a
-// thread stores the in0 window of plane k+1 (loaded during step k-1), then issues the loads of
-// plane k+1's ids and b and of plane k+2's window; none of them is consumed in this step (they are
-// kept as loaded, unpacked), so the HBM latency overlaps the three stages of the current plane
-// (k_sym_tb waits for its own loads before its first barrier: one full latency per plane).
-// Values come from the class table in LDS at use.
+// ---- The row-class dictionary's blocked passes (k_sym_zc below): what a thread holds per row pair
+// and plane — the two class ids, the mirror rows' ids (i-1; i-nx, i+1-nx; the -M mirrors are the
+// pair's ids one plane down) and b — narrow until use, so no instruction touches a load's result
+// before the step that consumes it. Values come from the class table in LDS at use. (Round 4's
+// k_sym_tbd — three LDS plane rings and three barriers per plane — is replaced by k_sym_zc.)
 struct TbdRow {    // one row pair on one plane, as loaded (narrow types: widened at use, so no
     uint16_t own;  // instruction touches a load's result before the step that consumes it)
     uint8_t m0;    // class ids: own = row i (bits 0-7), row i+1 (8-15); m0 = row i-1;
@@ -1476,44 +1246,9 @@ __device__ __forceinline__ void tbd_load(TbdRow& c, const uint8_t* __restrict__ 
     c.b[1] = bb.y;
 }
 
-// the pair's outputs: k_rows_symd's values for the 7 classes -M, -nx, -1, 0, +1, +nx, +M (m2: the
-// pair's ids one plane down, whose U_2 are this plane's -M values), then tb_rows' arithmetic
-__device__ __forceinline__ void tbd_rows(const SymTab<3>& tab, const TbdRow& c, uint32_t m2, const double (&xv)[2][7],
-                                         bool resid, double omega, double (&out)[2]) {
-    const uint32_t t0 = c.own & 0xffu, t1 = (c.own >> 8) & 0xffu;
-    const uint32_t tr[2] = {t0, t1}, l0[2] = {c.m0 & 0xffu, t0};
-    const uint32_t l1[2] = {c.m1 & 0xffu, (c.m1 >> 8) & 0xffu}, l2[2] = {m2 & 0xffu, (m2 >> 8) & 0xffu};
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const uint32_t t = tr[r];
-        const uint32_t m = tab.m[t];
-        double v[7];
-        v[0] = tab.v[l2[r]][3];  // a(i, i-M)  = U_2 of row i-M
-        v[1] = tab.v[l1[r]][2];  // a(i, i-nx) = U_1 of row i-nx
-        v[2] = tab.v[l0[r]][1];  // a(i, i-1)  = U_0 of row i-1
-        v[3] = tab.v[t][0];
-        v[4] = tab.v[t][1];
-        v[5] = tab.v[t][2];
-        v[6] = tab.v[t][3];
-        double s = 0.0;
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-            const double p = v[k] * xv[r][k];
-            const double u = s + p;
-            s = ((m >> k) & 1u) ? u : s;
-        }
-        if (resid) {
-            out[r] = c.b[r] - s;
-        } else {
-            const double u = c.b[r] - s;
-            const double w = omega * u;
-            const double q = w / v[3];
-            out[r] = xv[r][3] + q;
-        }
-    }
-}
-
-// tbd_rows without the mask selects and with div_rn, for the kernels whose absent entries meet
+// The pair's outputs: k_rows_symd's values for the 7 classes -M, -nx, -1, 0, +1, +nx, +M (m2: the
+// pair's ids one plane down, whose U_2 are this plane's -M values), then k_rows_symd's arithmetic
+// without its mask selects and with div_rn — for the kernels whose absent entries meet
 // exact zeros (k_sym_zm, k_sym_zc: tb_ok operators, every neighbour outside the grid is held as
 // +0.0 and an absent in-grid entry is a +0.0 table value): such an entry's product is +-0, and
 // adding +-0 to the running sum leaves its bits unchanged — the sum starts at +0.0 and, rounding
@@ -1552,152 +1287,8 @@ __device__ __forceinline__ void zc_rows(const SymTab<3>& tab, const TbdRow& c, u
     }
 }
 
-// one step k: En <- plane k+PD (loads issued), E0 = plane k (stage 0), E1 = k-1 (stage 1),
-// E2 = k-2 (stage 2, S = 3), E3 = k-3 (the -M ids of stage 2; of stage 1 when S = 2 it is E2);
-// win holds plane k+1's window on entry (loaded PD steps earlier), plane k+1+PD's on exit
-template <int S, int PD, int TY>
-__device__ __forceinline__ void tbd_step(int k, TbdRow& En, const TbdRow& E0, const TbdRow& E1, const TbdRow& E2,
-                                         const TbdRow& E3, TbWin<S>& win, const TbCtx<S>& t,
-                                         const uint8_t* __restrict__ tid, const SymDia& sd, const TbArgs& ta,
-                                         const SymTab<3>& tab, double (*l0)[TbShape<S, TY>::RY][kTbLW],
-                                         double (*l1)[TbShape<S, TY>::RY][kTbLW],
-                                         double (*xin)[TbShape<S, TY>::XL][kTbLW]) {
-    using Sh = TbShape<S, TY>;
-    if (k >= t.kend) return;  // uniform: the whole workgroup
-    tb_win_store<S, TY>(win, xin, tb_mod3(k + 1));  // loaded PD steps ago
-    tb_win_load<S, TY>(win, t, ta.in0, k + 1 + PD);
-    {
-        const int p = k + PD;
-        const bool ok = t.pos_ok && p >= 0 && p < t.nz;
-        tbd_load(En, tid, ta.b, sd, ok ? (int64_t)p * t.M + t.ixy : 0, t.n);
-    }
-    __syncthreads();  // xin (planes k-1 .. k+1)
-    // ---- stage 0 on plane k: a Jacobi sweep from in0
-    {
-        double o[2] = {0.0, 0.0};
-        if (t.pos_ok && k >= 0 && k < t.nz) {
-            double xv[2][7];
-            tb_gather_lds<Sh::XL>(xin, tb_mod3(k - 1), tb_mod3(k), tb_mod3(k + 1), t.ry + 1, t.col, xv);
-            tbd_rows(tab, E0, E1.own, xv, S == 1 && ta.last_resid, ta.omega, o);
-            // (out[0] NULL: the stage-0 result only feeds stage 1 — the pipeline's post-smoothed
-            // iterate, which no later launch reads; uniform branch)
-            if (ta.out[0] && t.own_xy && k >= t.zs && k < t.ze)
-                *reinterpret_cast<double2*>(ta.out[0] + (int64_t)k * t.M + t.ixy) = make_double2(o[0], o[1]);
-        }
-        if (t.ry >= 0) *reinterpret_cast<double2*>(&l0[tb_mod3(k)][t.ry][t.col]) = make_double2(o[0], o[1]);
-    }
-    __syncthreads();
-    // ---- stage 1 on plane k-1 from stage 0's ring
-    {
-        const int p = k - 1;
-        constexpr bool last = S == 2;
-        constexpr int hz = Sh::H - 1;
-        double o[2] = {0.0, 0.0};
-        const bool act = t.pos_ok && t.ry >= 1 && t.ry < Sh::RY - 1 && p >= 0 && p < t.nz && p >= t.zs - hz &&
-                         p < t.ze + hz && (!last || t.own_xy);
-        if (act) {
-            double xv[2][7];
-            tb_gather_lds<Sh::RY>(l0, tb_mod3(p - 1), tb_mod3(p), tb_mod3(p + 1), t.ry, t.col, xv);
-            tbd_rows(tab, E1, E2.own, xv, last && ta.last_resid, ta.omega, o);
-            if (t.own_xy && p >= t.zs && p < t.ze)
-                *reinterpret_cast<double2*>(ta.out[1] + (int64_t)p * t.M + t.ixy) = make_double2(o[0], o[1]);
-        }
-        if constexpr (S == 3) {
-            if (t.ry >= 0) *reinterpret_cast<double2*>(&l1[tb_mod3(p)][t.ry][t.col]) = make_double2(o[0], o[1]);
-        }
-    }
-    __syncthreads();  // S = 3: stage 2 reads l1; S = 2: the next step's stage 0 rewrites l0
-    // ---- stage 2 on plane k-2 from stage 1's ring (S = 3)
-    if constexpr (S == 3) {
-        const int p = k - 2;
-        if (t.own_xy && t.ry >= 2 && t.ry < Sh::RY - 2 && p >= t.zs && p < t.ze) {
-            double xv[2][7], o[2];
-            tb_gather_lds<Sh::RY>(l1, tb_mod3(p - 1), tb_mod3(p), tb_mod3(p + 1), t.ry, t.col, xv);
-            tbd_rows(tab, E2, E3.own, xv, ta.last_resid, ta.omega, o);
-            *reinterpret_cast<double2*>(ta.out[2] + (int64_t)p * t.M + t.ixy) = make_double2(o[0], o[1]);
-        }
-    }
-}
-
-// PD (Options::tb_pd): how many planes ahead the loads run — 1: a ring of S + 2 planes and one
-// window register set; 2: S + 3 planes and two window sets used in alternation
-template <int S, int PD, int TY = kTbY>
-__global__ __launch_bounds__((TbShape<S, TY>::threads)) void k_sym_tbd(int nrows, const uint8_t* __restrict__ tid,
-                                                                  const double* __restrict__ vtab,
-                                                                  const uint32_t* __restrict__ mtab, int nv,
-                                                                  const SymDia sd, const TbArgs ta) {
-    using Sh = TbShape<S, TY>;
-    static_assert(PD == 1 || PD == 2, "one or two planes ahead");
-    __shared__ __attribute__((aligned(16))) double l0[3][Sh::RY][kTbLW];
-    __shared__ __attribute__((aligned(16))) double l1[S == 3 ? 3 : 1][Sh::RY][kTbLW];
-    __shared__ __attribute__((aligned(16))) double xin[3][Sh::XL][kTbLW];
-    __shared__ __attribute__((aligned(16))) SymTab<3> tab;
-    TbCtx<S> t;
-    if (!tb_ctx_init<S, TY>(t, sd.tb, nrows)) return;  // the whole workgroup, before any barrier
-    symtab_fill<3>(tab, vtab, mtab, nv);           // (read after the first step's barrier)
-    const int k0 = t.zs - Sh::H;
-    TbWin<S> wa, wb;
-    {  // the in0 windows of planes k0-1 and k0; planes k0+1 (.. k0+PD) stay in registers
-#pragma unroll
-        for (int q = -1; q <= 0; ++q) {
-            tb_win_load<S, TY>(wa, t, ta.in0, k0 + q);
-            tb_win_store<S, TY>(wa, xin, tb_mod3(k0 + q));
-        }
-        tb_win_load<S, TY>(wa, t, ta.in0, k0 + 1);
-        if constexpr (PD == 2) tb_win_load<S, TY>(wb, t, ta.in0, k0 + 2);
-    }
-    // the plane ring (planes k+PD .. k-S), rotated by the unrolled loop; planes k0-1 .. k0+PD-1 first
-    TbdRow e0{}, e1{}, e2{}, e3{}, e4{}, e5{};
-    auto load = [&](TbdRow& e, int p) {
-        const bool ok = t.pos_ok && p >= 0 && p < t.nz;
-        tbd_load(e, tid, ta.b, sd, ok ? (int64_t)p * t.M + t.ixy : 0, t.n);
-    };
-    constexpr int R = PD + S + 1;  // ring entries
-    load(R == 4 ? e3 : R == 5 ? e4 : e5, k0 - 1);
-    load(e0, k0);
-    if constexpr (PD == 2) load(e1, k0 + 1);
-    if constexpr (S == 2 && PD == 1) {  // planes k+1, k, k-1, k-2
-        for (int k = k0; k < t.kend; k += 4) {
-            tbd_step<S, PD, TY>(k, e1, e0, e3, e2, e2, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 1, e2, e1, e0, e3, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 2, e3, e2, e1, e0, e0, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 3, e0, e3, e2, e1, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
-        }
-    } else if constexpr (S == 3 && PD == 1) {  // planes k+1, k, k-1, k-2, k-3
-        for (int k = k0; k < t.kend; k += 5) {
-            tbd_step<S, PD, TY>(k, e1, e0, e4, e3, e2, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 1, e2, e1, e0, e4, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 2, e3, e2, e1, e0, e4, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 3, e4, e3, e2, e1, e0, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 4, e0, e4, e3, e2, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
-        }
-    } else if constexpr (S == 2) {  // PD 2: planes k+2, k+1, k, k-1, k-2; windows wa / wb alternate
-        for (int k = k0; k < t.kend; k += 10) {
-            tbd_step<S, PD, TY>(k, e2, e0, e4, e3, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 1, e3, e1, e0, e4, e4, wb, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 2, e4, e2, e1, e0, e0, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 3, e0, e3, e2, e1, e1, wb, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 4, e1, e4, e3, e2, e2, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 5, e2, e0, e4, e3, e3, wb, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 6, e3, e1, e0, e4, e4, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 7, e4, e2, e1, e0, e0, wb, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 8, e0, e3, e2, e1, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 9, e1, e4, e3, e2, e2, wb, t, tid, sd, ta, tab, l0, l1, xin);
-        }
-    } else {  // S 3, PD 2: planes k+2, k+1, k, k-1, k-2, k-3; windows wa / wb alternate
-        for (int k = k0; k < t.kend; k += 6) {
-            tbd_step<S, PD, TY>(k, e2, e0, e5, e4, e3, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 1, e3, e1, e0, e5, e4, wb, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 2, e4, e2, e1, e0, e5, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 3, e5, e3, e2, e1, e0, wb, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 4, e0, e4, e3, e2, e1, wa, t, tid, sd, ta, tab, l0, l1, xin);
-            tbd_step<S, PD, TY>(k + 5, e1, e5, e4, e3, e2, wb, t, tid, sd, ta, tab, l0, l1, xin);
-        }
-    }
-}
-
-// ---- k_sym_zc<S>: the S dependent sweeps of k_sym_tbd (same tiles, halos, activity ranges,
-// row expressions — so the same bits) restructured the way k_sym_zm marches (round 5): every
+// ---- k_sym_zc<S>: S dependent sweeps over the row-class dictionary (k_sym_tb's tiles, halos,
+// activity ranges and row expressions — so its bits) marching the way k_sym_zm does (round 5): every
 // thread owns one row pair of stage 0's region for the whole z range, so the z neighbours of
 // every stage (in0 of planes k-1, k+1; stage 0 of k-2, k; stage 1 of k-3, k-1) sit in its own
 // registers, and only in-plane neighbours go through LDS — one double-buffered plane per stage.
@@ -2362,25 +1953,6 @@ template <int OP, int TNNZ, bool PT>
 void launch_tile2_cd(const pamg_mat& A, const TileSet& ts, const double* x, const double* b, double* y,
                      double omega, hipStream_t s) {
     const int n = ts.n_short;
-    if (PT && ts.vd) {  // per-tile column dictionaries + 4-bit value dictionaries (Options::vd_col_dict)
-        if (ts.anc && ts.cd == 4)
-            k_rows_tile2<OP, TNNZ, false, true, true, 4, true, true><<<n, kBlock, 0, s>>>(
-                ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, A.d_vidx,
-                ts.d_vtab, A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n, A.d_anc16, ts.d_abase);
-        else if (ts.anc)
-            k_rows_tile2<OP, TNNZ, false, true, true, 8, true, true><<<n, kBlock, 0, s>>>(
-                ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, A.d_vidx,
-                ts.d_vtab, A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n, A.d_anc16, ts.d_abase);
-        else if (ts.cd == 4)
-            k_rows_tile2<OP, TNNZ, false, true, true, 4, true><<<n, kBlock, 0, s>>>(
-                ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, A.d_vidx,
-                ts.d_vtab, A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n);
-        else
-            k_rows_tile2<OP, TNNZ, false, true, true, 8, true><<<n, kBlock, 0, s>>>(
-                ts.d_short, A.d_rowptr, A.d_col, A.d_val, x, b, y, omega, nullptr, nullptr, nullptr, A.d_vidx,
-                ts.d_vtab, A.d_rlen, A.d_cidx, ts.d_ctab, ts.ctab_n);
-        return;
-    }
     if (PT && ts.anc) {
         if (ts.cd == 4)
             k_rows_tile2<OP, TNNZ, false, false, true, 4, true, true><<<n, kBlock, 0, s>>>(
@@ -2450,23 +2022,6 @@ template <int OP, int TNNZ>
 void launch_tile(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
                  double* y, double omega, hipStream_t s) {
     const int n = ts.n_short;
-    if constexpr (TNNZ == 2048 || TNNZ == 4096) {
-        if (ts.tm && ts.xsr && TNNZ == 2048 && options().xsr_kernel == 1 && ts.pt && ts.cd == 8 && ts.tm_vt) {
-            XStage xs{};
-            xs.ncols = (int)A.ncols;
-            k_rows_tm<OP, 2048, 8, false, true, true, true><<<n, kBlock, 0, s>>>(
-                ts.d_short, nullptr, ts.d_tm_cidx, nullptr, nullptr, nullptr, ts.d_tm_rlen, ts.tm_rs, nullptr,
-                ts.ctab_n, x, b, y, omega, nullptr, xs, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt, ts.d_xpos,
-                ts.d_xmeta);
-            return;
-        }
-        if (ts.tm && ts.xsr) {
-            k_rows_xsr<OP, TNNZ><<<n, kBlock, 0, s>>>(ts.d_short, ts.d_tm_cidx, ts.d_tm_vidx, ts.d_tm_vtab, ts.tm_vt,
-                                                     ts.d_tm_rlen, ts.tm_rs, ts.d_xpos, ts.ctab_n, ts.d_xmeta, x,
-                                                     A.ncols, b, y, omega);
-            return;
-        }
-    }
     if (ts.tm) {
         if (ts.tm_vt)
             launch_tm<OP, TNNZ, true>(A, ts, x, b, y, omega, s);
@@ -2526,22 +2081,17 @@ void launch_sym_nu(const pamg_mat& A, const double* x, const double* b, double* 
         if constexpr (NU <= 3) {
             if (ch == 2) {
                 k_rows_symd<OP, NU, 2><<<g, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab,
-                                                            sd.d_mtab, sd.vd_n, sd, x, b, y, omega,
-                                                            options().symd_pair_ids != 0,
-                                                            options().symd_fast ? sd.vd_main : -1);
+                                                            sd.d_mtab, sd.vd_n, sd, x, b, y, omega);
                 return;
             }
             if (ch == 4) {
                 k_rows_symd<OP, NU, 4><<<g, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab,
-                                                            sd.d_mtab, sd.vd_n, sd, x, b, y, omega,
-                                                            options().symd_pair_ids != 0,
-                                                            options().symd_fast ? sd.vd_main : -1);
+                                                            sd.d_mtab, sd.vd_n, sd, x, b, y, omega);
                 return;
             }
         }
         k_rows_symd<OP, NU><<<grid, kBlock, 0, s>>>((int)A.nrows, (int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab,
-                                                  sd.vd_n, sd, x, b, y, omega, options().symd_pair_ids != 0,
-                                                  options().symd_fast ? sd.vd_main : -1);
+                                                  sd.vd_n, sd, x, b, y, omega);
         return;
     }
     if (sd.rpl == 2) {
@@ -2613,45 +2163,13 @@ void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s) {
     const int ntiles = g.tiles_x * g.tiles_y * g.zchunks;
     const int grid = (ntiles + 7) / 8 * 8;
     g.xfast = options().tb_xfast;
-    if (sd.vd_n && options().tb_ty == 8) {
-        // 8-line tiles (Options::tb_ty): twice the tiles per plane, half the LDS per workgroup
-        // (two workgroups per CU); the z split recomputed for the tile count
-        g.tiles_y = g.ny / 8;
-        g.zchunks = std::max(1, std::min((g.zchunks + 1) / 2, span / 2 > 0 ? span / 2 : 1));
-        g.zlen = (span + g.zchunks - 1) / g.zchunks;
-        g.zchunks = (span + g.zlen - 1) / g.zlen;
-        const int gr = (g.tiles_x * g.tiles_y * g.zchunks + 7) / 8 * 8;
-        if (ta.nstages == 2)
-            k_sym_tbd<2, 1, 8><<<gr, TbShape<2, 8>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab,
-                                                                    sd.vd_n, sd, ta);
-        else
-            k_sym_tbd<3, 1, 8><<<gr, TbShape<3, 8>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab,
-                                                                    sd.vd_n, sd, ta);
-        return;
-    }
-    if (sd.vd_n && options().tb_zc) {
+    if (sd.vd_n) {
         if (ta.nstages == 2)
             k_sym_zc<2><<<grid, ZcShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n, sd,
                                                              ta);
         else
             k_sym_zc<3><<<grid, ZcShape<3>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n, sd,
                                                              ta);
-        return;
-    }
-    if (sd.vd_n) {
-        const bool pd2 = options().tb_pd == 2;
-        if (ta.nstages == 2 && pd2)
-            k_sym_tbd<2, 2><<<grid, TbShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
-                                                                 sd, ta);
-        else if (ta.nstages == 2)
-            k_sym_tbd<2, 1><<<grid, TbShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
-                                                                 sd, ta);
-        else if (pd2)
-            k_sym_tbd<3, 2><<<grid, TbShape<3>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
-                                                                 sd, ta);
-        else
-            k_sym_tbd<3, 1><<<grid, TbShape<3>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
-                                                                 sd, ta);
         return;
     }
     if (ta.nstages == 2)

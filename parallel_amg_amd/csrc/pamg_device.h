@@ -35,17 +35,6 @@ struct XStage {
     int ncl = 0, stride = 0, zix = -1, ncols = 0;
     int omin[kXsMaxClusters] = {}, wid[kXsMaxClusters] = {};
 };
-// Per-tile x staging with row lanes (TileSet::xsr; kernels.hip k_rows_xsr): for tile-major sets
-// with per-tile row-relative 8-bit dictionaries and 8-bit value dictionaries (the 512^3 level-1
-// operator), each tile's offsets are clustered into <= kXsrMaxRuns runs of x, staged in LDS by
-// coalesced loads (staged element e of run c is x[r0 + omin_c + e - base_c]); per tile:
-// [ncl, zix, tot, omin_0 .. omin_{R-1}, base_0 .. base_{R-1}] in d_xmeta (kXsMeta ints) and each
-// dictionary entry's LDS position in d_xpos (uint16).
-constexpr int kXsrMaxRuns = 40;
-constexpr int kXsMeta = 3 + 2 * kXsrMaxRuns;
-constexpr int kXsrCap2048 = 2200;   // staged doubles per tile (17 KiB: 7 blocks per CU), 2048-nonzero tiles
-constexpr int kXsrCap4096 = 2560;   //                                  4096-nonzero tiles
-
 enum RowOp : int {
     OP_SPMV = 0,     // y = A x
     OP_RESID = 1,    // y = b - A x
@@ -86,10 +75,6 @@ struct TileSet {
     // x staging (Options::x_stage): see XStage
     bool xs = false;
     XStage xst;
-    // per-tile x staging with row lanes (Options::x_stage_tiles): see kXsMeta
-    bool xsr = false;
-    int* d_xmeta = nullptr;
-    uint16_t* d_xpos = nullptr;
     // tile-major copies (Options::tile_major; kernels.hip k_rows_tm): tile t's values and
     // column stream at t * tile_nnz, its row lengths at t * tm_rs, zero-padded
     bool tm = false;
@@ -142,28 +127,14 @@ struct Options {
     int sym_rows = 2;          // rows per lane of its kernel (1 | 2)
     int jr_fuse = 1;           // 1: temporally blocked level-0 Jacobi -> residual / cross-cycle pipeline where the
                                //    operator is a grid stencil (k_sym_tb)
-    int tb_pd = 2;             // planes the row-class chain's loads run ahead (k_sym_tbd<S, PD>: 1 or 2;
-                               // 2: -0.5 % chain time, same-box A/B profiles/r04_g_pd/)
-    int x_stage_tiles = 0;     // 1: per-tile x staging with row lanes for per-tile dictionary sets (k_rows_xsr)
     int symd_chunks = 2;       // 512-row units per block of k_rows_symd (1, 2 or 4; 2: SpMV -2 %, residual and
                                // Jacobi -4..-5 %, 4: -1..-2 %; same-box A/B profiles/r04_g_c2/, r04_g_c4/)
-    int tb_ty = 16;            // tile height of the row-class chain (k_sym_tbd): 16, or 8 (half the LDS: two
-                               // workgroups per CU)
-    int symd_fast = 0;         // launch-time: waves whose rows and mirrors are all of the main class take its
-                               // values from registers (no per-row table reads; +0.3 %, more VGPRs:
-                               // profiles/r04_m_fast/)
-    int symd_pair_ids = 0;     // launch-time: k_rows_symd loads mirror-row class ids as aligned pairs
-                               // (+0.3…1 %: profiles/r04_m_pid/)
-    int vd_col_dict = 0;       // upload: per-tile column dictionaries also for 4-bit value-dictionary sets
     int chain_store_x = 0;     // 1: the pipelined chain also stores its post-smoothed iterate (never read)
-    int tb_zc = 1;             // 1: the level-0 blocked passes (row-class dictionary) march along z with one barrier
-                               //    per plane (k_sym_zc); 0: k_sym_tbd
     int tb_xfast = 1;          // blocked passes: tiles x-fastest (an XCD takes whole rows of tiles; chain -0.9 %,
                                // S = 2 pass -1.1 %, same-box A/B profiles/r05_l/) or y-fastest (0)
     int sym_zm = 1;            // 1: one-sweep ops of a whole one-part row-class grid operator march along z
                                //    (k_sym_zm); 0: k_rows_symd
     int zm_chunks = 0;         // z chunks per tile column of k_sym_zm (0: ~4 workgroups per CU)
-    int xsr_kernel = 0;        // staged sets: 0 row lanes (k_rows_xsr), 1 nonzero lanes (k_rows_tm, 2048-nonzero tiles)
     int ell = 1;               // 1: sliced ELL with per-group 8-bit dictionaries for square operators whose every row
                                //    is interior, where the tables fit (EllSet; the level-1 operator)
     int ell_min_rows = 65536;  // ... with at least this many rows

@@ -582,18 +582,11 @@ int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vect
         pamg::TileSet* ts = sets[q];
         if (!opt.col_dict || ts->n_short == 0 || ts->max_short_len > 255)
             continue;
-        // a set with 4-bit value dictionaries (the prolongators) takes per-tile column
-        // dictionaries in the descriptor kernel only (Options::vd_col_dict), its values staying
-        // 4-bit indices
-        if (ts->vd && !(opt.vd_col_dict && opt.col_dict_tile)) continue;
+        // a set with 4-bit value dictionaries (the prolongators) keeps its 24-bit columns
+        // (per-tile column dictionaries there measured 8 % slower)
+        if (ts->vd) continue;
         if (idx.empty()) idx.assign((size_t)A->nnz + kVecPad, 0);
         const std::vector<int4>& tiles = *tl[q];
-        if (ts->vd) {
-            ts->anc = false;
-            ts->pt = false;
-            CHECK(build_tile_dicts(A, rp, ci, tiles, ts, &idx, &tab[q], &anc16));
-            continue;
-        }
         const int64_t nt = (int64_t)tiles.size();
         // Offset of a nonzero: col - row (row-relative: stencils), or col - the row's first
         // column (anchored: rows of a repeated shape whose columns do not follow the row
@@ -767,93 +760,6 @@ int build_x_stage(pamg_mat* A, pamg::TileSet* ts, int rs) {
     }
     HIPC(hipMemcpy(ts->d_ctab, tab.data(), sizeof(int) * 256, hipMemcpyHostToDevice));
     ts->xs = true;
-    return PAMG_OK;
-}
-
-// Per-tile x staging with row lanes (Options::x_stage_tiles, pamg::kXsMeta, k_rows_xsr) for a
-// tile-major set with per-tile row-relative 8-bit dictionaries and 8-bit value dictionaries: per
-// tile, the offsets its nonzeros use, sorted, split into runs where the gap exceeds kXsGap (a
-// run of offsets [a, b] stages x[r0 + a .. r0 + nr - 1 + b]: nr + b - a doubles), and each
-// entry's LDS position; declined (the set keeps k_rows_tm) when a tile needs more than
-// kXsrMaxRuns runs or more doubles than the kernel's LDS holds.
-int build_x_stage_tiles(pamg_mat* A, pamg::TileSet* ts, const std::vector<int64_t>& rp, const std::vector<int>& ci,
-                        const std::vector<int4>& tiles, const std::vector<uint8_t>& idx8) {
-    using pamg::kXsMeta;
-    using pamg::kXsrMaxRuns;
-    ts->xsr = false;
-    if (!pamg::options().x_stage_tiles || !ts->tm || !ts->pt || ts->anc || ts->cd != 8 || !ts->tm_vt ||
-        (ts->tile_nnz != 2048 && ts->tile_nnz != 4096) || ts->ctab_n > (ts->tile_nnz == 2048 ? pamg::kTmSmallTab : 256))
-        return PAMG_OK;
-    const int64_t nt = (int64_t)tiles.size();
-    const int cap = ts->tile_nnz == 2048 ? pamg::kXsrCap2048 : pamg::kXsrCap4096;
-    const int tn = ts->ctab_n;
-    std::vector<uint16_t> pos((size_t)nt * tn + kVecPad, 0);
-    std::vector<int> meta((size_t)nt * kXsMeta + kVecPad, 0);
-    std::atomic<int64_t> staged{0};
-    std::atomic<int> worst_runs{0}, worst_tot{0};
-    par_for(nt, [&](int64_t a, int64_t b) {
-        std::vector<std::pair<int, int>> ent;  // (offset, dictionary index) of the used entries
-        int wr = 0, wt = 0;
-        for (int64_t t = a; t < b; ++t) {
-            const int4 d = tiles[t];
-            const int nr = d.y - d.x;
-            int off[256];
-            bool used[256] = {};
-            for (int r = d.x; r < d.y; ++r)
-                for (int64_t k = rp[r]; k < rp[r + 1]; ++k) {
-                    const int ix = idx8[k];
-                    off[ix] = ci[k] - r;
-                    used[ix] = true;
-                }
-            ent.clear();
-            for (int ix = 0; ix < 256; ++ix)
-                if (used[ix]) ent.emplace_back(off[ix], ix);
-            std::sort(ent.begin(), ent.end());
-            int* m = &meta[(size_t)t * kXsMeta];
-            int ncl = 0, tot = 0, zix = -1, cmin = 0, cmax = 0;
-            for (size_t q = 0; q <= ent.size(); ++q) {
-                const bool brk = q == ent.size() || (q > 0 && ent[q].first - cmax > pamg::kXsGap);
-                if (q > 0 && brk) {  // close the run [cmin, cmax]
-                    if (ncl < kXsrMaxRuns) {
-                        m[3 + ncl] = cmin;
-                        m[3 + kXsrMaxRuns + ncl] = tot;
-                    }
-                    ++ncl;
-                    tot += nr + (cmax - cmin);
-                }
-                if (q == ent.size()) break;
-                const int o = ent[q].first;
-                if (q == 0 || brk) cmin = o;
-                cmax = o;
-                if (o == 0) zix = ent[q].second;
-                pos[(size_t)t * tn + ent[q].second] = (uint16_t)std::min(tot + (o - cmin), 65535);
-            }
-            m[0] = ncl;
-            m[1] = zix;
-            m[2] = tot;
-            wr = std::max(wr, ncl);
-            wt = std::max(wt, tot);
-            staged += tot;
-        }
-        int cur = worst_runs.load();
-        while (wr > cur && !worst_runs.compare_exchange_weak(cur, wr)) {
-        }
-        cur = worst_tot.load();
-        while (wt > cur && !worst_tot.compare_exchange_weak(cur, wt)) {
-        }
-    });
-    const bool fits = worst_runs.load() <= kXsrMaxRuns && worst_tot.load() <= cap;
-    if (UploadTrace{}.on)
-        std::fprintf(stderr, "[pamg upload nnz=%lld] per-tile x staging: %lld tiles, %.0f doubles per tile, worst "
-                     "tile %d runs / %d doubles (limits %d / %d) -> %s\n", (long long)A->nnz, (long long)nt,
-                     (double)staged.load() / (double)std::max<int64_t>(nt, 1), worst_runs.load(), worst_tot.load(),
-                     kXsrMaxRuns, cap, fits ? "staged" : "declined");
-    if (!fits) return PAMG_OK;
-    CHECK(dalloc(&ts->d_xmeta, (int64_t)meta.size()));
-    CHECK(h2d(A->ctx, ts->d_xmeta, meta.data(), sizeof(int) * meta.size()));
-    CHECK(dalloc(&ts->d_xpos, (int64_t)pos.size()));
-    CHECK(h2d(A->ctx, ts->d_xpos, pos.data(), sizeof(uint16_t) * pos.size()));
-    ts->xsr = true;
     return PAMG_OK;
 }
 
@@ -1035,7 +941,6 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
         ts->tm_rs = rs;
         ts->tm = true;
         CHECK(build_x_stage(A, ts, rs));
-        CHECK(build_x_stage_tiles(A, ts, rp, ci, tiles, idx8));
     }
     return PAMG_OK;
 }
@@ -1476,9 +1381,6 @@ void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_tm_vtab);
     ts.tm_vt = 0;
     dfree(ts.d_abase);
-    dfree(ts.d_xmeta);
-    dfree(ts.d_xpos);
-    ts.xsr = false;
     ts.anc = ts.pt = ts.xs = false;
     ts.tm = false;
     ts.tm_rs = 0;
@@ -2956,7 +2858,7 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
              (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0) |
-             (t.sym && A->sym.vd_n ? 128 : 0) | (t.tm && t.xsr ? 256 : 0) | (t.ell ? 512 : 0);
+             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0);
     if (t.ell) out[8] = (int)A->ell.ngroups;  // k_rows_ell's grid
     if (t.sym) {  // the symmetric diagonal-class layout: upper classes, k_rows_sym's grid
         out[4] = A->sym.nu;
@@ -3618,22 +3520,14 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "sym_rows" && (value == 1 || value == 2)) o.sym_rows = (int)value;
     else if (k == "jr_fuse" && (value == 0 || value == 1)) o.jr_fuse = (int)value;
     else if (k == "sym_vd" && (value == 0 || value == 1)) o.sym_vd = (int)value;
-    else if (k == "x_stage_tiles" && (value == 0 || value == 1)) o.x_stage_tiles = (int)value;
-    else if (k == "xsr_kernel" && (value == 0 || value == 1)) o.xsr_kernel = (int)value;
     else if (k == "symd_chunks" && (value == 1 || value == 2 || value == 4)) o.symd_chunks = (int)value;
     else if (k == "sym_zm" && (value == 0 || value == 1)) o.sym_zm = (int)value;
-    else if (k == "tb_zc" && (value == 0 || value == 1)) o.tb_zc = (int)value;
     else if (k == "tb_xfast" && (value == 0 || value == 1)) o.tb_xfast = (int)value;
     else if (k == "ell" && (value == 0 || value == 1)) o.ell = (int)value;
     else if (k == "ell_restrict" && (value == 0 || value == 1)) o.ell_restrict = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
-    else if (k == "tb_ty" && (value == 8 || value == 16)) o.tb_ty = (int)value;
     else if (k == "chain_store_x" && (value == 0 || value == 1)) o.chain_store_x = (int)value;
-    else if (k == "vd_col_dict" && (value == 0 || value == 1)) o.vd_col_dict = (int)value;
-    else if (k == "symd_pair_ids" && (value == 0 || value == 1)) o.symd_pair_ids = (int)value;
-    else if (k == "symd_fast" && (value == 0 || value == 1)) o.symd_fast = (int)value;
-    else if (k == "tb_pd" && (value == 1 || value == 2)) o.tb_pd = (int)value;
     else return fail(PAMG_E_ARG, "set_option: unknown key or bad value: %s=%lld", key, (long long)value);
     return PAMG_OK;
 }
@@ -3662,22 +3556,14 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "sym_rows") *value = o.sym_rows;
     else if (k == "jr_fuse") *value = o.jr_fuse;
     else if (k == "sym_vd") *value = o.sym_vd;
-    else if (k == "x_stage_tiles") *value = o.x_stage_tiles;
-    else if (k == "xsr_kernel") *value = o.xsr_kernel;
     else if (k == "symd_chunks") *value = o.symd_chunks;
     else if (k == "sym_zm") *value = o.sym_zm;
-    else if (k == "tb_zc") *value = o.tb_zc;
     else if (k == "tb_xfast") *value = o.tb_xfast;
     else if (k == "ell") *value = o.ell;
     else if (k == "ell_restrict") *value = o.ell_restrict;
     else if (k == "ell_min_rows") *value = o.ell_min_rows;
     else if (k == "zm_chunks") *value = o.zm_chunks;
-    else if (k == "tb_ty") *value = o.tb_ty;
     else if (k == "chain_store_x") *value = o.chain_store_x;
-    else if (k == "vd_col_dict") *value = o.vd_col_dict;
-    else if (k == "symd_pair_ids") *value = o.symd_pair_ids;
-    else if (k == "symd_fast") *value = o.symd_fast;
-    else if (k == "tb_pd") *value = o.tb_pd;
     else return fail(PAMG_E_ARG, "get_option: unknown key %s", key);
     return PAMG_OK;
 }

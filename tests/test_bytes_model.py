@@ -47,7 +47,7 @@ def test_per_part_bytes_scale_with_the_slab():
 
 
 def test_chain_bytes_per_launch_512():
-    """The pipelined chain's algorithmic bytes (bench.py roofline for k_sym_tbd<3>): the matrix
+    """The pipelined chain's algorithmic bytes (bench.py roofline for k_sym_zc<3>): the matrix
     once, in0 and b, and the outputs it stores — the pre-smoothed iterate and the residual
     (chain_store_x 0, the default), plus the post-smoothed iterate with chain_store_x 1."""
     n = 512 ** 3

@@ -1001,13 +1001,11 @@ def test_sym_dia_bit_exact(ctx, kind, n, seed, order, rows, vd):
 @pytest.mark.parametrize("kind,n", [("poisson3d", 40), ("poisson2d", 80), ("aniso3d", 20), ("poisson3d", 7),
                                     ("poisson3d", 33)])
 @pytest.mark.parametrize("order", [0, 1])
-@pytest.mark.parametrize("ch", [2, 4])
-@pytest.mark.parametrize("pid", [1, 0])
-def test_symd_units_per_block_bit_exact(ctx, kind, n, order, ch, pid):
+@pytest.mark.parametrize("ch", [1, 2, 4])
+def test_symd_units_per_block_bit_exact(ctx, kind, n, order, ch):
     """k_rows_symd with CH 512-row units per block (symd_chunks; a unit count that CH does not
-    divide leaves the last block's tail units idle), with (pid 1) or without (0) the mirror ids
-    as pair loads and the main-class register fast path: SpMV, residual, Jacobi bit-exact with
-    the oracle."""
+    divide leaves the last block's tail units idle): SpMV, residual, Jacobi bit-exact with the
+    oracle."""
     from parallel_amg_amd._lib import layout_of
     M = _sym_grid(kind, n)
     with _with_option("tile_order", order), _with_option("sym_rows", 2), _with_option("sym_vd", 1):
@@ -1016,7 +1014,7 @@ def test_symd_units_per_block_bit_exact(ctx, kind, n, order, ch, pid):
     rng = np.random.default_rng(n + ch)
     xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
     x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
-    with _with_option("symd_chunks", ch), _with_option("symd_pair_ids", pid), _with_option("symd_fast", pid):
+    with _with_option("symd_chunks", ch):
         mul(y, A, x)
         assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
         residual(y, A, x, b)
@@ -1396,24 +1394,15 @@ def _grid_prolongator(n, nvals, seed):
 
 
 @pytest.mark.parametrize("n,nvals", [(64, 6), (48, 16), (32, 3)])
-def test_prolongator_column_and_value_dictionaries_bit_exact(ctx, n, nvals):
-    """vd_col_dict: a prolongator whose tiles hold <= 16 values (4-bit value dictionaries, the
-    512^3 P0's layout) also takes per-tile column dictionaries (anchored or row-relative) in the
-    descriptor kernel instead of 24-bit columns: SpMV, residual and prolongate-add bit-exact with
-    the oracle, and fewer streamed bytes than without."""
+def test_prolongator_value_dictionaries_bit_exact(ctx, n, nvals):
+    """A prolongator whose tiles hold <= 16 values (the 512^3 P0's layout: 4-bit value
+    dictionaries beside 24-bit columns): SpMV, residual and prolongate-add bit-exact with the
+    oracle."""
     from parallel_amg_amd._lib import layout_of
     M = _grid_prolongator(n, nvals, n)
-    rng = np.random.default_rng(n)
-    with _with_option("vd_col_dict", 0):
-        A0 = _layout_ops_match_oracle(ctx, M, rng)
-    lay0, sb0 = layout_of(A0), A0.stream_bytes
-    del A0
-    with _with_option("vd_col_dict", 1):
-        A1 = _layout_ops_match_oracle(ctx, M, rng)
-    lay1 = layout_of(A1)
+    A0 = _layout_ops_match_oracle(ctx, M, np.random.default_rng(n))
+    lay0 = layout_of(A0)
     assert lay0["vd"] and lay0["cd"] == 0, lay0
-    assert lay1["vd"] and lay1["cd"] in (4, 8) and lay1["per_tile"], lay1
-    assert A1.stream_bytes < sb0
 
 
 @pytest.mark.parametrize("kind,shape", [("poisson3d", (128, 128, 128)), ("aniso3d", (128, 128, 128)),
@@ -1421,7 +1410,7 @@ def test_prolongator_column_and_value_dictionaries_bit_exact(ctx, n, nvals):
                                         ("aniso3d", (192, 48, 7))])
 @pytest.mark.parametrize("vd", [1, 0])
 def test_jacobi_residual_op_bit_exact(ctx, kind, shape, vd):
-    """pamg_jacobi_residual: the temporally blocked pass (k_sym_tb, S = 2; k_sym_tbd over the
+    """pamg_jacobi_residual: the temporally blocked pass (k_sym_tb, S = 2; k_sym_zc over the
     row-class dictionary) against the two separate sweeps on random x, b — t and r bit for bit,
     repeated, and the separate sweeps against the oracle; grids whose tiles split the planes into
     z chunks, and a grid with fewer planes than a chunk."""
@@ -1552,49 +1541,12 @@ def level1_128(ctx):
     return O.CSR(M.rowptr.copy(), M.col.astype(np.int64), M.val.copy(), M.ncols)
 
 
-# (4096-nonzero tiles of this operator exceed the staging caps — kXsrCap4096 staged values — and
-# keep the gathering kernel; the 512^3 A1 runs 2048-nonzero tiles)
-@pytest.mark.parametrize("tnnz,xk", [(2048, 0), (2048, 1)])
-def test_row_lane_x_staging_bit_exact(ctx, level1_128, tnnz, xk):
-    """Per-tile x staging (x_stage_tiles) on a coarse AMG operator in tile-major slots with
-    per-tile column and value dictionaries — row lanes (k_rows_xsr, xsr_kernel 0) or nonzero
-    lanes (k_rows_tm with the staged runs, xsr_kernel 1): SpMV, residual, Jacobi (in-row diagonal
-    by the tile's offset-0 entry) and the oracle's bits; the same upload without the staging
-    (k_rows_tm gathering x) gives the same bits."""
-    from parallel_amg_amd._lib import layout_of
-    M = level1_128
-    rng = np.random.default_rng(tnnz)
-    xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
-    outs = []
-    for xst in (1, 0):
-        with _with_option("tile_nnz", tnnz), _with_option("tile_major", 2), _with_option("x_stage_tiles", xst):
-            A, _h = upload(ctx, M)
-        lay = layout_of(A)
-        assert lay["tm"] and lay["per_tile"] and lay["cd"] == 8 and lay["tm_vd"], lay
-        assert lay["xsr"] == bool(xst), lay
-        x, b, y = PVector(ctx, M.nrows, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
-        with _with_option("xsr_kernel", xk):
-            mul(y, A, x)
-            sp = y.own_values()
-            residual(y, A, x, b)
-            rs = y.own_values()
-            t = PVector(ctx, M.nrows)
-            jacobi(x, A, b, t, 0.61, 2)
-        outs.append((sp, rs, x.own_values()))
-        del A
-    assert np.array_equal(bits(outs[0][0]), bits(O.spmv(M, xh)))
-    assert np.array_equal(bits(outs[0][1]), bits(O.residual(M, xh, bh)))
-    assert np.array_equal(bits(outs[0][2]), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.61), bh, 0.61)))
-    for a, c in zip(outs[0], outs[1]):
-        assert np.array_equal(bits(a), bits(c))
-
-
 @pytest.mark.parametrize("kind", ["poisson3d", "aniso3d"])
-@pytest.mark.parametrize("key,val", [("tb_pd", 2), ("tb_pd", 1), ("tb_ty", 8), ("chain_store_x", 1)])
-def test_chain_two_planes_ahead_bit_exact(ctx, kind, key, val):
-    """The chain's variants — tb_pd = 2 / 1 (k_sym_tbd<S, PD>: loads two planes ahead with two
-    window register sets in alternation, or one) and tb_ty = 8 (8-line tiles, two workgroups per
-    CU): the fused pre-smoothing pass and pipelined cycles keep the oracle's bits."""
+@pytest.mark.parametrize("key,val", [("chain_store_x", 1), ("tb_xfast", 0), ("tb_xfast", 1)])
+def test_chain_variants_bit_exact(ctx, kind, key, val):
+    """The chain's options — chain_store_x (the unread post-smoothed iterate stored too) and
+    tb_xfast (tile order x- or y-fastest): the fused pre-smoothing pass and pipelined cycles keep
+    the oracle's bits."""
     from parallel_amg_amd._lib import layout_of
     from parallel_amg_amd.partitioned import jacobi_residual
     be = pa.SequentialBackend(1)

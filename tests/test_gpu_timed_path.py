@@ -2,16 +2,16 @@
 part, the library defaults.
 
 bench.py times ``S.vcycle_async(x, b, K)``: with jr_fuse on, stationary runs of K >= 2 cycles
-take the cross-cycle pipeline (``vcycle_pipe``: one ``k_sym_tb<3>`` launch per cycle boundary —
+take the cross-cycle pipeline (``vcycle_pipe``: one ``k_sym_zc<3>`` launch per cycle boundary —
 the level-0 post-smoothing of cycle k, the pre-smoothing and residual of cycle k + 1 — five
 captured graphs, the iterate alternating between ``t[0]`` and ``u0``). At 512^3 that kernel runs
 a geometry no smaller test reaches (8 x 32 xy tiles, one z chunk of all 512 planes per
-workgroup, 256 workgroups), so these tests pin it against separate, unfused cycles at this size:
+workgroup, 256 workgroups), and the level-1 operator runs in the sliced-ELL layout, so these tests
+pin the timed path at this size:
 
 * K pipelined cycles through graph replay == K separate cycles (jr_fuse off, eager), bit for
   bit, from x = 0 and continued from a non-zero iterate (the bench's warm-up then timed runs);
-* the temporally blocked pre-smoothing pass ``k_sym_tb<2>`` == Jacobi then residual, bit for bit.
-
+* the temporally blocked pre-smoothing pass ``k_sym_zc<2>`` == Jacobi then residual, bit for bit;
 * the oracle (oracle/pamg_oracle.c, OpenMP) run on the same 512^3 hierarchy (its level operators
   handed over by ``O.hierarchy_from_levels``, as bench.py's cpu_baseline does) for 3 V-cycles from
   x = 0 on the same b == the pipelined, graph-replayed cycles bench.py times, bit for bit
@@ -66,6 +66,7 @@ def test_timed_path_geometry(h512):
     lay = layout_of(S.A[0])
     assert lay["sym"] and lay["jr_fused"] and lay["cd_offsets"] == 3, lay
     assert S.L == 6
+    assert layout_of(S.A_dev[1])["ell"] and layout_of(S.R[0])["ell"], (layout_of(S.A_dev[1]), layout_of(S.R[0]))
 
 
 def test_pipelined_cycles_512_bit_exact(ctx, h512):
@@ -122,7 +123,7 @@ def test_timed_path_512_matches_oracle(ctx, h512):
 
 
 def test_blocked_pre_smoothing_512_bit_exact(ctx, h512):
-    """k_sym_tb<2> (Jacobi -> residual in one pass) == the two separate sweeps, random x, b."""
+    """k_sym_zc<2> (Jacobi -> residual in one pass) == the two separate sweeps (k_sym_zm), random x, b."""
     S, _b = h512
     A0 = S.A[0]
     n = A0.nrows
@@ -139,30 +140,3 @@ def test_blocked_pre_smoothing_512_bit_exact(ctx, h512):
         del t, r
     assert np.array_equal(bits(out[0][0]), bits(out[1][0]))
     assert np.array_equal(bits(out[0][1]), bits(out[1][1]))
-
-
-def test_level1_row_lane_staging_512_bit_exact(ctx, h512):
-    """The 512^3 level-1 operator (16.8M rows, 517M nonzeros) with per-tile x staging and row
-    lanes (k_rows_xsr, x_stage_tiles; off by default: measured slower): its residual
-    and Jacobi give the bits of the bench's layout (k_rows_tm, oracle-pinned at smaller sizes)."""
-    S, _b = h512
-    A1 = S.A_dev[1]
-    assert not layout_of(A1)["xsr"], layout_of(A1)
-    lp = S._H.levels[1][0]
-    with option("x_stage_tiles", 1):
-        from parallel_amg_amd.partitioned import PSparseMatrix
-        B1 = PSparseMatrix(ctx, lp.A, lp.planA)
-    assert layout_of(B1)["xsr"]
-    from parallel_amg_amd.partitioned import jacobi, residual
-    n = A1.nrows
-    rng = np.random.default_rng(5)
-    xh, bh = rng.standard_normal(n), rng.standard_normal(n)
-    outs = []
-    for M in (A1, B1):
-        x, b, y, t = PVector(ctx, n, 0, xh), PVector(ctx, n, 0, bh), PVector(ctx, n), PVector(ctx, n)
-        residual(y, M, x, b)
-        jacobi(x, M, b, t, S.omega[1], 1)
-        outs.append((y.own_values(), x.own_values()))
-    del B1
-    assert np.array_equal(bits(outs[0][0]), bits(outs[1][0]))
-    assert np.array_equal(bits(outs[0][1]), bits(outs[1][1]))

@@ -16,7 +16,6 @@
 #   world      the in-process device-world tests (tests/test_gpu_local_world.py)
 #   stream / chain / sub   parity subsets: streamed sweeps; chain variants; -k "$SUB_K"
 #   cab        tools/cycle_ab.py: same-box A/B of a cycle-level option (CAB_ARGS overrides)
-#   census     tools/xsr_census.py 512 (per-tile x-run census of the level-1 operator)
 # Output: gpurun_out/TAG/.
 set -euo pipefail
 export TMPDIR=/tmp
@@ -41,7 +40,7 @@ for step in "$@"; do
         timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "sym_zm or symd_units" -m gpu > "$OUT/stream.log" 2>&1
         ;;
     chain)
-        timeout -k 10 400 $PYT tests/test_gpu_parity.py -k "chain_two_planes or jacobi_residual_op or pipelined_cycles" -m gpu > "$OUT/chain.log" 2>&1
+        timeout -k 10 400 $PYT tests/test_gpu_parity.py -k "chain_variants or jacobi_residual_op or pipelined_cycles" -m gpu > "$OUT/chain.log" 2>&1
         ;;
     cab)
         timeout -k 10 500 python3 -u tools/cycle_ab.py ${CAB_ARGS:---ab chain_store_x=1,0} > "$OUT/cycle_ab.jsonl" 2> "$OUT/cycle_ab.err"
@@ -51,9 +50,6 @@ for step in "$@"; do
         ;;
     world)
         timeout -k 10 600 $PYT tests/test_gpu_local_world.py -m gpu > "$OUT/world.log" 2>&1
-        ;;
-    census)
-        timeout -k 10 300 python3 -u tools/xsr_census.py 512 > "$OUT/census.txt" 2>&1
         ;;
     bench)
         timeout -k 10 700 python3 -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log"

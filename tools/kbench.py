@@ -63,7 +63,7 @@ def main():
     ap.add_argument("--mats", default=None, help="comma list of level matrices to run (e.g. R0,A1); default all")
     ap.add_argument("--ab", default=None,
                     help="launch-time option to A/B on the same upload: KEY (values 0,1,0,1) or KEY=a,b "
-                         "(a,b,a,b; e.g. tb_pd=1,2)")
+                         "(a,b,a,b; e.g. symd_chunks=1,2)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="extra pamg_set_option before the uploads (e.g. band_pct=50)")
     args = ap.parse_args()

@@ -70,7 +70,7 @@ def main():
         rec = {"level": l, "rows": int(lp.A.nrows), "nnz": int(lp.A.nnz), "whole": bool(whole), "ms": {}}
         Ad = PSparseMatrix(ctx, lp.A, None if whole else lp.planA)
         lay = layout_of(Ad)
-        rec["A_layout"] = {k: lay[k] for k in ("sym", "sym_vd", "jr_fused", "tm", "xsr", "tile_nnz")}
+        rec["A_layout"] = {k: lay[k] for k in ("sym", "sym_vd", "jr_fused", "tm", "ell", "tile_nnz")}
         for op in ((1, 2, 4, 5) if l == 0 and lay["jr_fused"] else (1, 2)):
             rec["ms"][f"A_{OPNAME[op]}"] = round(time_op(ctx, Ad, op, a.reps), 4)
         del Ad
