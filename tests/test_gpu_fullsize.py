@@ -52,7 +52,8 @@ def test_fine_512_layouts_agree(ctx):
     the symmetric diagonal-class layout with its row-class dictionary (default) and without it,
     tile-major slots + 4-bit column dictionary
     (+ x staging), variant 1 with the dictionary, 24-bit columns + 8-bit row lengths, plain
-    32-bit CSR tiles, and the tile path's default (8-bit per-tile value dictionaries)."""
+    32-bit CSR tiles, the tile path's default (8-bit per-tile value dictionaries) and the sliced-ELL
+    layout."""
     import ctypes
     from parallel_amg_amd._lib import call, layout_of
     from parallel_amg_amd.partitioned import jacobi
@@ -64,11 +65,13 @@ def test_fine_512_layouts_agree(ctx):
     xh = rng.standard_normal(N)
     bh = rng.standard_normal(N)
     b = PVector(ctx, N, 0, bh)
-    layouts = [{}, {"sym_vd": 0}, {"sym_dia": 0, "value_dict": 0}, {"sym_dia": 0, "tile_major": 0, "value_dict": 0},
-               {"sym_dia": 0, "tile_major": 0, "col_dict": 0, "value_dict": 0},
-               {"sym_dia": 0, "tile_major": 0, "col_dict": 0, "col24": 0, "row_len8": 0, "value_dict": 0},
-               {"sym_dia": 0}]  # the tile path's default: 8-bit per-tile value dictionaries in tile-major slots
-    keys = ("sym_dia", "tile_major", "col_dict", "col24", "row_len8", "value_dict", "sym_vd")
+    layouts = [{}, {"sym_vd": 0}, {"sym_dia": 0, "value_dict": 0, "ell": 0},
+               {"sym_dia": 0, "tile_major": 0, "value_dict": 0, "ell": 0},
+               {"sym_dia": 0, "tile_major": 0, "col_dict": 0, "value_dict": 0, "ell": 0},
+               {"sym_dia": 0, "tile_major": 0, "col_dict": 0, "col24": 0, "row_len8": 0, "value_dict": 0, "ell": 0},
+               {"sym_dia": 0, "ell": 0},  # the tile path's default: 8-bit per-tile value dictionaries in tile-major slots
+               {"sym_dia": 0}]  # the sliced-ELL layout (what a square operator without the stencil layout takes)
+    keys = ("sym_dia", "tile_major", "col_dict", "col24", "row_len8", "value_dict", "sym_vd", "ell")
     old = []
     for k in keys:
         v = ctypes.c_int64()
@@ -98,6 +101,7 @@ def test_fine_512_layouts_agree(ctx):
     assert seen[1]["tm"] and seen[1]["cd"] == 4 and seen[1]["x_stage"] and not seen[2]["tm"] and seen[2]["cd"] == 4
     assert seen[3]["cd"] == 0 and seen[3]["c24"] and not seen[4]["c24"]
     assert seen[5]["tm"] and seen[5]["tm_vd"]
+    assert seen[6]["ell"] and not seen[5]["ell"]
 
 
 @pytest.fixture(scope="module")
