@@ -140,3 +140,22 @@ def test_blocked_pre_smoothing_512_bit_exact(ctx, h512):
         del t, r
     assert np.array_equal(bits(out[0][0]), bits(out[1][0]))
     assert np.array_equal(bits(out[0][1]), bits(out[1][1]))
+
+
+def test_pcg_512_matches_oracle(ctx, h512):
+    """Time to solution at the benchmarked size: PCG with one V-cycle as the preconditioner (SPEC
+    §S8, bench.py's time_to_solution leg) against the oracle's PCG on the same 512^3 hierarchy —
+    the same iteration count and residual history to 1e-6 (dot products reduce in a different
+    order, so the iterates agree to rounding, not bit for bit)."""
+    from oracle import oracle as O
+    S, b = h512
+    H = S._H
+    lv = [H.levels[l][0] for l in range(H.nlevels)]
+    Ho = O.hierarchy_from_levels([p.A for p in lv], [p.P for p in lv[:-1]], [p.R for p in lv[:-1]],
+                                 [p.omega for p in lv], H.ainv)
+    _xo, ko, ho = Ho.pcg(b.own_values(), 1e-8, 60)
+    del Ho
+    x = S.new_vector()
+    k, hist = S.pcg(x, b, 1e-8, 60)
+    assert k == ko, (k, ko, hist[-3:], ho[-3:])
+    np.testing.assert_allclose(hist, ho, rtol=1e-6)
