@@ -78,6 +78,16 @@ int set_device(const pamg_ctx* ctx) {
 
 // ---- host side of the upload: threads for the per-nonzero passes, pinned staging for copies
 // Threads: OMP_NUM_THREADS if set (16 on the GPU box), else the hardware count, at most 64.
+// Zero device memory in the context's stream order and wait for it: hipMemset runs on the
+// null stream, which the context's non-blocking streams do not wait for, so a kernel enqueued
+// right after it could run first (found in round 5: PCG's first initial residual raced with the
+// zeroing of its freshly allocated vectors).
+int dzero(pamg_ctx* ctx, void* p, size_t bytes) {
+    HIPC(hipMemsetAsync(p, 0, bytes, ctx->s_comp));
+    HIPC(hipStreamSynchronize(ctx->s_comp));
+    return PAMG_OK;
+}
+
 int host_threads() {
     static const int n = [] {
         const char* e = std::getenv("OMP_NUM_THREADS");
@@ -2652,7 +2662,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     CHECK(dalloc(&A->d_val, nnz + kVecPad));
     CHECK(h2d(ctx, A->d_rowptr, rp32.data(), sizeof(int) * (nrows + 1)));
     CHECK(h2d(ctx, A->d_col, ci.data(), sizeof(int) * (nnz + kVecPad)));
-    HIPC(hipMemset(A->d_val, 0, sizeof(double) * (nnz + kVecPad)));
+    CHECK(dzero(ctx, A->d_val, sizeof(double) * (nnz + kVecPad)));
     if (nnz) CHECK(h2d(ctx, A->d_val, val, sizeof(double) * nnz));
     if (has_all_diag && nrows > 0) {
         CHECK(dalloc(&A->d_diag, nrows));
@@ -3030,14 +3040,14 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
         if (l > 0) {
             CHECK(dalloc(&H->x[l], n));
             CHECK(dalloc(&H->b[l], n));
-            HIPC(hipMemset(H->x[l], 0, sizeof(double) * n));
-            HIPC(hipMemset(H->b[l], 0, sizeof(double) * n));
+            CHECK(dzero(ctx, H->x[l], sizeof(double) * n));
+            CHECK(dzero(ctx, H->b[l], sizeof(double) * n));
         }
         if (l < L - 1) {
             CHECK(dalloc(&H->t[l], n));
             CHECK(dalloc(&H->r[l], n));
-            HIPC(hipMemset(H->t[l], 0, sizeof(double) * n));
-            HIPC(hipMemset(H->r[l], 0, sizeof(double) * n));
+            CHECK(dzero(ctx, H->t[l], sizeof(double) * n));
+            CHECK(dzero(ctx, H->r[l], sizeof(double) * n));
         }
     }
     // coarsest level
@@ -3058,7 +3068,7 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
     if (nr > 1) {
         CHECK(dalloc(&H->d_bgather, (int64_t)nr * H->cmax + n_rep + kVecPad));
         CHECK(dalloc(&H->d_bsend, H->cmax + kVecPad));
-        HIPC(hipMemset(H->d_bsend, 0, sizeof(double) * (H->cmax + kVecPad)));
+        CHECK(dzero(ctx, H->d_bsend, sizeof(double) * (H->cmax + kVecPad)));
     }
     H->prof_ms.assign((size_t)L * 6, 0.0);
     ctx_ref(ctx);
@@ -3162,8 +3172,8 @@ int pamg_hier_set_perm(pamg_hier* H, int64_t n, const int64_t* perm) {
     CHECK(dalloc(&H->px, n + kVecPad));
     CHECK(dalloc(&H->pb, n + kVecPad));
     HIPC(hipMemcpy(H->d_perm, p.data(), sizeof(int) * n, hipMemcpyHostToDevice));
-    HIPC(hipMemset(H->px, 0, sizeof(double) * (n + kVecPad)));
-    HIPC(hipMemset(H->pb, 0, sizeof(double) * (n + kVecPad)));
+    CHECK(dzero(H->ctx, H->px, sizeof(double) * (n + kVecPad)));
+    CHECK(dzero(H->ctx, H->pb, sizeof(double) * (n + kVecPad)));
     return PAMG_OK;
 }
 
@@ -3272,7 +3282,7 @@ static int vcycle_pipe(pamg_hier* H, double* x, const double* b, int ncycles) {
     if (!H->u0) {
         const int64_t n = H->nown[0] + (H->A[0]->plan ? H->A[0]->plan->n_ghost : 0) + kVecPad;
         CHECK(dalloc(&H->u0, n));
-        HIPC(hipMemset(H->u0, 0, sizeof(double) * n));
+        CHECK(dzero(H->ctx, H->u0, sizeof(double) * n));
     }
     const int K = ncycles;
     auto seg_of = [K](int k) { return k == 0 ? 0 : k < K ? (k % 2 == 1 ? 1 : 2) : ((K - 1) % 2 == 1 ? 4 : 3); };
@@ -3450,7 +3460,7 @@ int pamg_pcg(pamg_ctx* ctx, pamg_hier* H, pamg_vec* x, const pamg_vec* b, double
         CHECK(dalloc(&H->pcg_p, cap));
         CHECK(dalloc(&H->pcg_q, cap));
         for (double* p : {H->pcg_r, H->pcg_z, H->pcg_p, H->pcg_q})
-            HIPC(hipMemset(p, 0, sizeof(double) * cap));
+            CHECK(dzero(ctx, p, sizeof(double) * cap));
     }
     hipStream_t s = ctx->s_comp;
     double *r = H->pcg_r, *z = H->pcg_z, *p = H->pcg_p, *q = H->pcg_q;
@@ -3577,7 +3587,7 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
     if (!H->u0) {
         const int64_t n = H->nown[0] + (H->A[0]->plan ? H->A[0]->plan->n_ghost : 0) + kVecPad;
         CHECK(dalloc(&H->u0, n));
-        HIPC(hipMemset(H->u0, 0, sizeof(double) * n));
+        CHECK(dzero(H->ctx, H->u0, sizeof(double) * n));
     }
     hipEvent_t e0, e1;
     HIPC(hipEventCreate(&e0));
@@ -3619,7 +3629,7 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
         const int64_t len = part_tb ? (A->plan ? A->plan->n_own + A->plan->n_ghost : A->ncols) : A->nrows;
         for (double*& p : scratch) {
             CHECK(dalloc(&p, std::max<int64_t>(len, A->nrows) + kVecPad));
-            HIPC(hipMemset(p, 0, sizeof(double) * (size_t)(std::max<int64_t>(len, A->nrows) + kVecPad)));
+            CHECK(dzero(ctx, p, sizeof(double) * (size_t)(std::max<int64_t>(len, A->nrows) + kVecPad)));
         }
     }
     pamg::TbArgs ta;
