@@ -1707,10 +1707,11 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __
     const int tid = threadIdx.x, lane = tid & 63;
     const int4 gm = gmeta[g];
     const int i = g * kEllGroup + tid;
-    const bool in = i < nrows;
-    const int ic = in ? i : nrows - 1;
+    const int ic = i < nrows ? i : nrows - 1;
+    const int L8 = i < nrows ? (int)len[i] : kEllSkip;
+    const bool in = L8 != kEllSkip;  // (a boundary row of a part: the boundary tiles compute it)
     const int2 sm = smeta[ic / kEllW];  // (one slice per wave)
-    const int L = in ? (int)len[i] : 0;
+    const int L = in ? L8 : 0;
     const int base = ANC ? anc[ic] : ic;  // offsets from the row (square) or its first column (anchored)
     const uint32_t* __restrict__ cp = cw + sm.x + lane;
     const uint32_t* __restrict__ vp = vw + sm.x + lane;

@@ -176,6 +176,7 @@ struct TbGeom {
 // start + (k / 4) * kEllW + lane. Rows keep their storage order (the products are summed in it).
 constexpr int kEllW = 64;
 constexpr int kEllGroup = 256;
+constexpr int kEllSkip = 255;  // length byte of a row outside the set (several parts: a boundary row)
 struct EllSet {
     int64_t nslices = 0, ngroups = 0;
     int2* d_smeta = nullptr;     // per slice: (first dword of its index streams, maxlen)

@@ -1235,11 +1235,21 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
 // the SPEC §S3 order.
 // Rectangular operators (anchored: a restriction) take their offsets from each row's first column
 // (col - col_first(row)), the anchors stored per row.
+// Several parts: the set is the interior rows only (`inner`, ascending); the slices still span every
+// row index, the boundary rows marked skipped (length byte kEllSkip: no load, no store — the
+// boundary tiles compute them after the exchange).
 int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci, const double* val,
-              bool anchored) {
+              bool anchored, const std::vector<int>& inner) {
     using pamg::kEllGroup;
+    using pamg::kEllSkip;
     using pamg::kEllW;
     const int64_t n = A->nrows;
+    std::vector<char> in_set;
+    if ((int64_t)inner.size() != n) {
+        in_set.assign(n, 0);
+        for (int i : inner) in_set[i] = 1;
+    }
+    auto member = [&](int64_t i) { return in_set.empty() || in_set[i]; };
     auto base_of = [&](int64_t i) -> int { return anchored ? (rp[i + 1] > rp[i] ? ci[rp[i]] : 0) : (int)i; };
     const int64_t ns = (n + kEllW - 1) / kEllW, ng = (n + kEllGroup - 1) / kEllGroup;
     std::vector<int> slen(ns, 0);
@@ -1247,8 +1257,9 @@ int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
     par_for(ns, [&](int64_t a, int64_t b) {
         for (int64_t q = a; q < b; ++q) {
             int m = 0;
-            for (int64_t i = q * kEllW; i < std::min(n, (q + 1) * kEllW); ++i) m = std::max<int>(m, (int)(rp[i + 1] - rp[i]));
-            if (m > 255) ok = false;
+            for (int64_t i = q * kEllW; i < std::min(n, (q + 1) * kEllW); ++i)
+                if (member(i)) m = std::max<int>(m, (int)(rp[i + 1] - rp[i]));
+            if (m >= kEllSkip) ok = false;
             slen[q] = m;
         }
     });
@@ -1271,7 +1282,7 @@ int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
             v.clear();
             const int64_t r1 = std::min(n, (g + 1) * kEllGroup);
             for (int64_t i = g * kEllGroup; i < r1; ++i)
-                for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                for (int64_t k = rp[i]; k < (member(i) ? rp[i + 1] : rp[i]); ++k) {
                     o.push_back(ci[k] - base_of(i));
                     uint64_t u;
                     std::memcpy(&u, &val[k], 8);
@@ -1315,6 +1326,10 @@ int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
             for (int lane = 0; lane < kEllW; ++lane) {
                 const int64_t i = q * kEllW + lane;
                 if (i >= n) break;
+                if (!member(i)) {
+                    len[i] = (uint8_t)kEllSkip;
+                    continue;
+                }
                 len[i] = (uint8_t)(rp[i + 1] - rp[i]);
                 for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
                     const int kk = (int)(k - rp[i]);
@@ -2649,9 +2664,11 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     tr.mark("sym dia");
     // square operators (offsets from the row) and restrictions (fewer rows than columns; offsets from
     // each row's first column)
-    if (pamg::options().ell && !A->interior.sym && n_own_cols >= nrows && bnd.empty() && nrows > 0 &&
-        nrows >= pamg::options().ell_min_rows && (n_own_cols == nrows || pamg::options().ell_restrict)) {
-        CHECK(build_ell(A.get(), rp, ci, val, n_own_cols != nrows));
+    // (several parts: the interior rows, when they are most of the operator)
+    if (pamg::options().ell && !A->interior.sym && n_own_cols >= nrows && nrows > 0 &&
+        (int64_t)inner.size() * 10 >= (int64_t)nrows * 9 && nrows >= pamg::options().ell_min_rows &&
+        (n_own_cols == nrows || pamg::options().ell_restrict)) {
+        CHECK(build_ell(A.get(), rp, ci, val, n_own_cols != nrows, inner));
         if (A->interior.ell) inner.clear();  // the rows run in k_rows_ell, not in tiles
         tr.mark("ell");
     }

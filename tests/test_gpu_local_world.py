@@ -113,6 +113,39 @@ def test_local_world_vcycle_bit_exact(built, nparts, kind, n, max_coarse, agglom
             assert np.array_equal(bits(gv), bits(got_x[gid]))
 
 
+@pytest.mark.parametrize("nparts,kind,n", [(3, "poisson2d", 60), (4, "poisson3d", 24), (2, "aniso3d", 20)])
+def test_local_world_ell_interior_rows_bit_exact(built, nparts, kind, n):
+    """Several parts with the sliced-ELL layout on every level's interior rows (ell_min_rows 0,
+    sym_dia 0: level 0 too; the boundary rows — ghost columns — stay in tiles and run after the
+    exchange, marked skipped in the slices): b = A x* and x after 4 V-cycles are the oracle's
+    multi-part bits, ghosts NaN-poisoned."""
+    ncycles = 4
+    with option("poison_ghosts", 1), option("ell_min_rows", 0), option("sym_dia", 0):
+        W = LocalWorld(nparts)
+        try:
+            be = pa.SequentialBackend(nparts)
+            A, offs, xs = pa.generate_problem(be, kind, n)
+            H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=60, agglomerate=0), device=W.ctxs[0])
+            S = [AMGSolver(W.ctxs[p], H, part=p) for p in range(nparts)]
+            assert any(layout_of(s.A[0])["ell"] for s in S)
+            A0 = [s.A[0] for s in S]
+            xst = [PVector(W.ctxs[p], A0[p].n_own_cols, A0[p].n_ghost, xs[p]) for p in range(nparts)]
+            b = [PVector(W.ctxs[p], A0[p].nrows) for p in range(nparts)]
+            W.run(lambda p: mul(b[p], A0[p], xst[p]))
+            x = [s.new_vector() for s in S]
+            W.run(lambda p: S[p].vcycle(x[p], b[p], ncycles))
+            got_b = np.concatenate([v.own_values() for v in b])
+            got_x = np.concatenate([v.own_values() for v in x])
+        finally:
+            del S
+            W.close()
+    Ao = O.generate(kind, *O.grid_shape(kind, n))
+    bo = O.spmv(Ao, O.xstar(Ao.nrows))
+    Ho = O.setup(Ao, nparts=nparts, max_coarse=60, agglomerate=0)
+    assert np.array_equal(bits(got_b), bits(bo))
+    assert np.array_equal(bits(got_x), bits(Ho.solve(bo, ncycles)))
+
+
 def test_baseline_config0_golden(built):
     """BASELINE.json configs[0] — 2D 5-pt Poisson 256 x 256, 2 parts, the PartitionedArrays
     sequential-backend shape — on the HIP path (both parts in one process, the device world) against
