@@ -268,7 +268,7 @@ int pamg_bench_rowop(pamg_ctx* ctx, const pamg_mat* A, int op, pamg_vec* x, cons
                      pamg_vec* y, double omega, int reps, double* avg_ms);
 
 /* Micro-benchmark hook of the cross-cycle pipeline: `reps` launches of its level-0 chain kernel
- * (post-smoothing -> next pre-smoothing -> residual, k_sym_tb<3>) on the hierarchy's own level-0
+ * (post-smoothing -> next pre-smoothing -> residual, k_sym_zc<3>) on the hierarchy's own level-0
  * buffers and the given x / b (x is overwritten); average ms per launch (HIP events).
  * PAMG_E_STATE when the hierarchy does not qualify (one part, V(1,1), jr_fuse, level 0 with
  * pamg_mat_layout bit 5). */
@@ -282,8 +282,13 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
  * temporally blocked level-0 passes of the V-cycle and the cross-cycle pipeline, read at graph
  * capture), "long_tiles_min" (1..255 nonzeros per row from which sets of >= 32 x 4096
  * nonzeros per CU take 2048-nonzero tiles), "band_pct" / "band_pct_restrict" (percent scale of the banded
- * order's band; the second for operators with fewer rows than columns), "tile_major" (0 | 1 where measured faster | 2 every eligible set). Applied at
- * every exchange:
+ * order's band; the second for operators with fewer rows than columns), "tile_major" (0 | 1 where measured faster | 2 every eligible set),
+ * "sym_vd" (0 | 1: row-class dictionary of the symmetric layout), "ell" (0 | 1: sliced ELL for
+ * large square operators with all own columns), "ell_restrict" (0 | 1: also restrictions, with
+ * anchored offsets), "ell_min_rows" (rows from which ELL is taken). Read at launch:
+ * "sym_zm" (0 | 1: z-marching single sweeps of the symmetric layout), "zm_chunks" (0 = auto |
+ * z chunks per column of k_sym_zm), "tb_xfast" (0 | 1: x-fastest tile order of the chain),
+ * "symd_chunks" (1 | 2 | 4), "chain_store_x" (0 | 1). Applied at every exchange:
  * "poison_ghosts" (0 | 1, debug: NaN-fill the ghost slots before each exchange). */
 int pamg_set_option(const char* key, int64_t value);
 int pamg_get_option(const char* key, int64_t* value);
