@@ -193,7 +193,10 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * <= 64 (mask, diagonal, upper values) tuples (sym_vd); bit 8: the tile-major set stages each
  * tile's x runs in LDS and sums one row per lane (x_stage_tiles, k_rows_xsr); bit 9: the set runs in
  * the sliced-ELL layout (ell: one row per lane, per-group 8-bit column-offset and value dictionaries;
- * then out[8] = the kernel's grid). */
+ * then out[8] = the kernel's grid); bit 10: the set runs in the neighbour-coded prolongation layout
+ * (pnc: a prolongation over a 7-point grid uploaded earlier on the same context, each column named
+ * by the grid neighbour whose anchor it is; then out[3] = the value table's entries, out[4] = the
+ * pattern table's, out[8] = the kernel's grid). */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[10]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
@@ -285,7 +288,8 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
  * order's band; the second for operators with fewer rows than columns), "tile_major" (0 | 1 where measured faster | 2 every eligible set),
  * "sym_vd" (0 | 1: row-class dictionary of the symmetric layout), "ell" (0 | 1: sliced ELL for
  * large square operators with all own columns), "ell_restrict" (0 | 1: also restrictions, with
- * anchored offsets), "ell_min_rows" (rows from which ELL is taken). Read at launch:
+ * anchored offsets), "ell_min_rows" (rows from which ELL is taken), "pnc" (0 | 1: neighbour-coded
+ * prolongations over a grid uploaded earlier on the context). Read at launch:
  * "sym_zm" (0 | 1: z-marching single sweeps of the symmetric layout), "zm_chunks" (0 = auto |
  * z chunks per column of k_sym_zm), "tb_xfast" (0 | 1: x-fastest tile order of the chain),
  * "symd_chunks" (1 | 2 | 4), "chain_store_x" (0 | 1). Applied at every exchange:

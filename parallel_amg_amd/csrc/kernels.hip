@@ -1768,6 +1768,76 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __
     if (in) y[i] = out;
 }
 
+// k_rows_pnc: the neighbour-coded prolongation (pamg::PncSet; round 5, the 512^3 P0). One row per
+// lane, about 8 workgroups per CU, each staging the two global tables (<= 1024 pattern words, <= 128
+// values) in LDS once and then walking 256-row blocks: at step t the workgroups of XCD j (block b
+// runs on XCD b % 8) take consecutive blocks of the j-th eighth of the rows, so each XCD moves one
+// window along its rows and its L2 holds the window's coarse entries and the anchors of the planes
+// next to it. A lane loads its row's record and the anchors of its 7 grid points (clamped to the
+// row itself off the grid: no code names such a point), takes each entry's column from its code and
+// sums value * x[column] left to right from +0.0 in storage order (SPEC S3), as the other row
+// kernels do.
+template <int OP>
+__global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, const int* __restrict__ anc,
+                                                  const uint2* __restrict__ rec, const uint32_t* __restrict__ ptab,
+                                                  int npat, const double* __restrict__ vtab, int nval,
+                                                  const double* __restrict__ x, const double* __restrict__ b,
+                                                  double* __restrict__ y, double omega) {
+    __shared__ uint32_t lp[kPncPatMax];
+    __shared__ double lv[kPncValMax];
+    for (int t = threadIdx.x; t < npat; t += 256) lp[t] = ptab[t];
+    for (int t = threadIdx.x; t < nval; t += 256) lv[t] = vtab[t];
+    __syncthreads();
+    const int nblk = (nrows + 255) >> 8;
+    const int per = (nblk + 7) >> 3;  // blocks of an XCD's eighth
+    const int slots = gridDim.x >> 3;  // workgroups per XCD
+    const int g0 = (blockIdx.x & 7) * per, g1 = min(nblk, g0 + per);
+    for (int g = g0 + (int)(blockIdx.x >> 3); g < g1; g += slots) {
+        const int i = (g << 8) + (int)threadIdx.x;
+        if (i >= nrows) continue;  // (no barrier in the loop)
+        const uint2 r = rec[i];
+        const int a0 = anc[i];
+        const int an1 = anc[i >= 1 ? i - 1 : i], an2 = anc[i + 1 < nrows ? i + 1 : i];
+        const int an3 = anc[i >= nx ? i - nx : i], an4 = anc[i + nx < nrows ? i + nx : i];
+        const int an5 = anc[i >= M ? i - M : i], an6 = anc[i + M < nrows ? i + M : i];
+        double pb = 0.0, px = 0.0, py = 0.0;
+        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[i];
+        if constexpr (OP == OP_JACOBI) px = x[i];
+        if constexpr (OP == OP_PROLONG) py = y[i];
+        const uint32_t pw = lp[r.x & 1023u];
+        const int L = (int)(pw & 7u);
+        const uint64_t rr = ((uint64_t)r.y << 32) | r.x;
+        double s = 0.0, dg = 0.0;
+#pragma unroll
+        for (int k = 0; k < kPncMaxLen; ++k) {
+            const uint32_t c = (pw >> (3 + 3 * k)) & 7u;
+            const int col = c == 0 ? a0 : c == 1 ? an1 : c == 2 ? an2 : c == 3 ? an3 : c == 4 ? an4 : c == 5 ? an5 : an6;
+            const bool ok = k < L;
+            const double v = lv[(uint32_t)(rr >> (10 + 7 * k)) & 127u];
+            double xv = 0.0;
+            if (ok) xv = x[col];
+            const double p = v * xv;
+            const double t = s + p;
+            s = ok ? t : s;
+            if constexpr (OP == OP_JACOBI) dg = ok && col == i ? v : dg;
+        }
+        double out;
+        if constexpr (OP == OP_SPMV) {
+            out = s;
+        } else if constexpr (OP == OP_RESID) {
+            out = pb - s;
+        } else if constexpr (OP == OP_JACOBI) {
+            const double u = pb - s;
+            const double v = omega * u;
+            const double w = v / dg;
+            out = px + w;
+        } else {
+            out = py + s;
+        }
+        y[i] = out;
+    }
+}
+
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_rows_long(
     const int* __restrict__ rows, const int* __restrict__ rowptr, const int* __restrict__ col,
@@ -2137,6 +2207,11 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
             k_rows_ell<OP, false><<<grid, kEllGroup, 0, s>>>((int)A.nrows, nullptr, E.d_smeta, E.d_ci, E.d_vi, E.d_len,
                                                              E.d_gmeta, E.d_otab, E.d_vtab, (int)E.ngroups, x, b, y,
                                                              omega);
+    }
+    if (ts.pnc) {
+        const PncSet& P = A.pnc;
+        k_rows_pnc<OP><<<P.grid, 256, 0, s>>>((int)A.nrows, P.nx, P.nx * P.ny, P.d_anc, P.d_rec, P.d_ptab, P.npat,
+                                              P.d_vtab, P.nval, x, b, y, omega);
     }
     if (ts.n_short > 0) {
         if (ts.tile_nnz == 1024) launch_tile<OP, 1024>(A, ts, x, b, y, omega, s);

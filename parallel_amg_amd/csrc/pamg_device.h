@@ -7,6 +7,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <array>
 #include <vector>
 
 #include "pamg_common.h"
@@ -97,6 +98,9 @@ struct TileSet {
     // sliced-ELL layout (pamg_mat::ell; the whole interior set of a square operator): the set's rows run in
     // k_rows_ell instead of tiles
     bool ell = false;
+    // neighbour-coded prolongation (pamg_mat::pnc; the whole set of a prolongation over a registered grid):
+    // the rows run in k_rows_pnc instead of tiles
+    bool pnc = false;
     int max_short_len = 0;    // longest row in a short tile
     int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
@@ -139,6 +143,7 @@ struct Options {
                                //    is interior, where the tables fit (EllSet; the level-1 operator)
     int ell_min_rows = 65536;  // ... with at least this many rows
     int ell_restrict = 1;      // 1: also restrictions (fewer rows than columns), offsets from each row's first column
+    int pnc = 1;               // 1: neighbour-coded prolongations over a grid registered on the context (PncSet)
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
 };
@@ -188,6 +193,27 @@ struct EllSet {
     double* d_vtab = nullptr;    // the groups' value tables, concatenated
     int* d_anc = nullptr;        // anchored (rectangular operators): per row the column its offsets start from
     int64_t words = 0, otab_n = 0, vtab_n = 0;
+};
+
+// Neighbour-coded prolongation (Options::pnc; round 5, the 512^3 P0): a prolongation (more rows than
+// columns, one part) whose rows are the points of a 7-point grid uploaded earlier on the same
+// context (pamg_ctx::grids), each of its columns being the anchor of one of the points i, i-1,
+// i+1, i-nx, i+nx, i-M, i+M (codes 0..6) — the anchor of a row being the column of its largest
+// value (in smoothed aggregation: the point's own aggregate; P = (I - w D^-1 A) P_tent reaches
+// the aggregates of the point's stencil neighbours). Per row: the anchor (4 B) and a 64-bit record:
+// bits 0-9 a pattern id (a global table of <= kPncPatMax words: bits 0-2 the row length, 3 + 3k
+// the k-th entry's neighbour code), bits 10 + 7k the k-th entry's value index (a global table of
+// <= kPncValMax bit patterns). 12 B per row against 3.5 B per nonzero + 1 B per row in tiles. Rows
+// keep their storage order (SPEC S3 sums).
+constexpr int kPncPatMax = 1024, kPncValMax = 128, kPncMaxLen = 7;
+struct PncSet {
+    int nx = 0, ny = 0, nz = 0;
+    int* d_anc = nullptr;       // nrows (+ pad)
+    uint2* d_rec = nullptr;     // nrows (+ pad): the 64-bit records as (low, high) dwords
+    uint32_t* d_ptab = nullptr;
+    double* d_vtab = nullptr;
+    int npat = 0, nval = 0;
+    int grid = 0;               // workgroups of k_rows_pnc (a multiple of 8)
 };
 
 struct SymDia {
@@ -245,6 +271,10 @@ struct pamg_ctx {
     // created on first use on this context's device and owned by the context
     char* stage[2] = {nullptr, nullptr};
     hipEvent_t stage_done[2] = {nullptr, nullptr};
+    // 7-point grids of the square operators uploaded on this context in the temporally blocked
+    // layout (SymDia::tb_ok): (rows, nx, ny, nz) — a later prolongation with as many rows may take
+    // the neighbour-coded layout over one of them (pamg::PncSet)
+    std::vector<std::array<int64_t, 4>> grids;
 };
 
 void ctx_ref(pamg_ctx* ctx);
@@ -293,6 +323,7 @@ struct pamg_mat {
     pamg::TileSet interior;  // rows with own columns only (overlap with the exchange)
     pamg::TileSet boundary;  // rows with >= 1 ghost column
     pamg::EllSet ell;        // the interior set's sliced-ELL layout (TileSet::ell)
+    pamg::PncSet pnc;        // the neighbour-coded prolongation layout (TileSet::pnc)
     int64_t stream_bytes = 0;  // matrix bytes one apply reads (values, columns, row pointers, tiles)
 };
 

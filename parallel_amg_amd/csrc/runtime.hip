@@ -1217,6 +1217,11 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
             g.zhi = nz;
             sd.tb_ok = whole;
             sd.tb_part = part;
+            if (whole) {  // (a later prolongation over this grid may take the neighbour-coded layout)
+                const std::array<int64_t, 4> gk{n, nx, ny, nz};
+                auto& gs = A->ctx->grids;
+                if (std::find(gs.begin(), gs.end(), gk) == gs.end()) gs.push_back(gk);
+            }
             sd.part_lo = part ? plo : 0;
             sd.part_hi = part ? phi : nz;
         }
@@ -1375,6 +1380,123 @@ int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
     }
     A->interior.ell = true;
     return PAMG_OK;
+}
+
+// Neighbour-coded prolongation (Options::pnc, pamg::PncSet): every row's columns named by the
+// grid neighbours whose anchors they are. Declines (leaves the tile layouts to the caller) where a
+// row is longer than kPncMaxLen, a column is no neighbour's anchor, or a table would overflow.
+int build_pnc(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci, const double* val,
+              const std::array<int64_t, 4>& grid) {
+    using pamg::kPncMaxLen;
+    const int64_t n = A->nrows;
+    const int64_t nx = grid[1], ny = grid[2], nz = grid[3], M = nx * ny;
+    if (n != nx * ny * nz || n <= 0) return PAMG_OK;
+    std::vector<int> anc(n + kVecPad, 0);
+    std::atomic<bool> ok{true};
+    par_for(n, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b && ok; ++i) {
+            if (rp[i + 1] - rp[i] > kPncMaxLen) {
+                ok = false;
+                return;
+            }
+            int64_t best = rp[i];
+            for (int64_t k = rp[i] + 1; k < rp[i + 1]; ++k)
+                if (val[k] > val[best]) best = k;
+            anc[i] = rp[i + 1] > rp[i] ? ci[best] : 0;
+        }
+    });
+    if (!ok) return PAMG_OK;
+    // pass 1: each row's pattern word (length, codes) and the distinct patterns and values
+    std::vector<uint32_t> pw(n);
+    std::mutex mu;
+    std::vector<uint32_t> pats;
+    std::vector<uint64_t> vals;
+    const int64_t d[7] = {0, -1, 1, -nx, nx, -M, M};
+    par_for(n, [&](int64_t a, int64_t b) {
+        std::vector<uint32_t> lp;
+        std::vector<uint64_t> lv;
+        for (int64_t i = a; i < b && ok; ++i) {
+            const int64_t x = i % nx, y = (i / nx) % ny, z = i / M;
+            const bool in[7] = {true, x > 0, x < nx - 1, y > 0, y < ny - 1, z > 0, z < nz - 1};
+            uint32_t w = (uint32_t)(rp[i + 1] - rp[i]);
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                int c = 0;
+                while (c < 7 && !(in[c] && anc[i + d[c]] == ci[k])) ++c;
+                if (c == 7) {
+                    ok = false;
+                    return;
+                }
+                w |= (uint32_t)c << (3 + 3 * (k - rp[i]));
+                uint64_t u;
+                std::memcpy(&u, &val[k], 8);
+                lv.push_back(u);
+            }
+            pw[i] = w;
+            lp.push_back(w);
+            if (lp.size() > 4096 || lv.size() > 4096) {
+                std::sort(lp.begin(), lp.end());
+                lp.erase(std::unique(lp.begin(), lp.end()), lp.end());
+                std::sort(lv.begin(), lv.end());
+                lv.erase(std::unique(lv.begin(), lv.end()), lv.end());
+                if (lp.size() > (size_t)pamg::kPncPatMax || lv.size() > (size_t)pamg::kPncValMax) {
+                    ok = false;
+                    return;
+                }
+            }
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        pats.insert(pats.end(), lp.begin(), lp.end());
+        vals.insert(vals.end(), lv.begin(), lv.end());
+        std::sort(pats.begin(), pats.end());
+        pats.erase(std::unique(pats.begin(), pats.end()), pats.end());
+        std::sort(vals.begin(), vals.end());
+        vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+    });
+    if (!ok || pats.size() > (size_t)pamg::kPncPatMax || vals.size() > (size_t)pamg::kPncValMax) return PAMG_OK;
+    // pass 2: the records (pattern id, value indices)
+    std::vector<uint2> rec(n + kVecPad, make_uint2(0u, 0u));
+    par_for(n, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            uint64_t r = (uint64_t)(std::lower_bound(pats.begin(), pats.end(), pw[i]) - pats.begin());
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                uint64_t u;
+                std::memcpy(&u, &val[k], 8);
+                const uint64_t vi = (uint64_t)(std::lower_bound(vals.begin(), vals.end(), u) - vals.begin());
+                r |= vi << (10 + 7 * (k - rp[i]));
+            }
+            rec[i] = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
+        }
+    });
+    std::vector<double> vtab(vals.size());
+    for (size_t e = 0; e < vals.size(); ++e) std::memcpy(&vtab[e], &vals[e], 8);
+    pamg::PncSet& P = A->pnc;
+    pamg_ctx* ctx = A->ctx;
+    P.nx = (int)nx;
+    P.ny = (int)ny;
+    P.nz = (int)nz;
+    P.npat = (int)pats.size();
+    P.nval = (int)vals.size();
+    // about 8 workgroups per CU, a multiple of 8 (kernels.hip k_rows_pnc: XCD-contiguous windows)
+    const int64_t groups = (n + 255) / 256;
+    P.grid = (int)std::max<int64_t>(8, std::min<int64_t>(groups, (int64_t)device_cus() * 8) / 8 * 8);
+    CHECK(dalloc(&P.d_anc, n + kVecPad));
+    CHECK(dalloc(&P.d_rec, n + kVecPad));
+    CHECK(dalloc(&P.d_ptab, (int64_t)pats.size()));
+    CHECK(dalloc(&P.d_vtab, (int64_t)vals.size()));
+    CHECK(h2d(ctx, P.d_anc, anc.data(), sizeof(int) * anc.size()));
+    CHECK(h2d(ctx, P.d_rec, rec.data(), sizeof(uint2) * rec.size()));
+    CHECK(h2d(ctx, P.d_ptab, pats.data(), sizeof(uint32_t) * pats.size()));
+    CHECK(h2d(ctx, P.d_vtab, vtab.data(), sizeof(double) * vtab.size()));
+    A->interior.pnc = true;
+    return PAMG_OK;
+}
+
+void free_pnc(pamg::PncSet& P) {
+    dfree(P.d_anc);
+    dfree(P.d_rec);
+    dfree(P.d_ptab);
+    dfree(P.d_vtab);
+    P = pamg::PncSet{};
 }
 
 void free_ell(pamg::EllSet& E) {
@@ -2672,6 +2794,16 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         if (A->interior.ell) inner.clear();  // the rows run in k_rows_ell, not in tiles
         tr.mark("ell");
     }
+    // a prolongation over a 7-point grid uploaded earlier on this context: neighbour-coded rows
+    if (pamg::options().pnc && n_own_cols < nrows && ncols == n_own_cols && (int64_t)inner.size() == nrows) {
+        for (const auto& g : ctx->grids)
+            if (g[0] == nrows) {
+                CHECK(build_pnc(A.get(), rp, ci, val, g));
+                break;
+            }
+        if (A->interior.pnc) inner.clear();  // the rows run in k_rows_pnc, not in tiles
+        tr.mark("pnc");
+    }
     std::vector<int> rp32(nrows + 1);
     for (int64_t i = 0; i <= nrows; ++i) rp32[i] = (int)rp[i];
     CHECK(dalloc(&A->d_rowptr, nrows + 1));
@@ -2730,8 +2862,10 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     if (A->interior.ell)
         A->stream_bytes += 8 * A->ell.words + nrows + 8 * A->ell.nslices + 16 * A->ell.ngroups + 4 * A->ell.otab_n +
                            8 * A->ell.vtab_n + (A->ell.d_anc ? 4 * nrows : 0);
+    // neighbour-coded prolongation: the anchor and the record per row, the two tables
+    if (A->interior.pnc) A->stream_bytes += 12 * nrows + 4 * A->pnc.npat + 8 * A->pnc.nval;
     for (const pamg::TileSet* t : {&A->interior, &A->boundary}) {
-        if (t->sym || t->ell) continue;  // counted above
+        if (t->sym || t->ell || t->pnc) continue;  // counted above
         const int64_t ns = t->n_short, nz = t->nnz_short;
         int64_t b = 8 * (int64_t)t->n_long + 12 * t->nnz_long;
         const bool base = t->c24 && !t->cd;
@@ -2851,6 +2985,7 @@ int pamg_mat_destroy(pamg_mat* A) {
     free_tiles(A->interior);
     free_tiles(A->boundary);
     free_ell(A->ell);
+    free_pnc(A->pnc);
     pamg_ctx* owner = A->ctx;
     delete A;
     ctx_unref(owner);
@@ -2885,8 +3020,13 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
              (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0) |
-             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0);
+             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0) | (t.pnc ? 1024 : 0);
     if (t.ell) out[8] = (int)A->ell.ngroups;  // k_rows_ell's grid
+    if (t.pnc) {  // the pattern and value tables, k_rows_pnc's grid
+        out[3] = A->pnc.nval;
+        out[4] = A->pnc.npat;
+        out[8] = A->pnc.grid;
+    }
     if (t.sym) {  // the symmetric diagonal-class layout: upper classes, k_rows_sym's grid
         out[4] = A->sym.nu;
         out[8] = A->sym.nbands * 8 * A->sym.eighth;
@@ -3552,6 +3692,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "tb_xfast" && (value == 0 || value == 1)) o.tb_xfast = (int)value;
     else if (k == "ell" && (value == 0 || value == 1)) o.ell = (int)value;
     else if (k == "ell_restrict" && (value == 0 || value == 1)) o.ell_restrict = (int)value;
+    else if (k == "pnc" && (value == 0 || value == 1)) o.pnc = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
     else if (k == "chain_store_x" && (value == 0 || value == 1)) o.chain_store_x = (int)value;
@@ -3588,6 +3729,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "tb_xfast") *value = o.tb_xfast;
     else if (k == "ell") *value = o.ell;
     else if (k == "ell_restrict") *value = o.ell_restrict;
+    else if (k == "pnc") *value = o.pnc;
     else if (k == "ell_min_rows") *value = o.ell_min_rows;
     else if (k == "zm_chunks") *value = o.zm_chunks;
     else if (k == "chain_store_x") *value = o.chain_store_x;

@@ -1573,3 +1573,65 @@ def test_chain_variants_bit_exact(ctx, kind, key, val):
     Ho = O.setup(Ao, max_coarse=1000)
     xo = Ho.solve(O.spmv(Ao, O.xstar(Ao.nrows)), 5)
     assert np.array_equal(bits(x.own_values()), bits(xo))
+
+
+def _grid_hierarchy_P0(nx, ny, nz):
+    """The level-0 prolongation of the SA hierarchy of a 7-point Poisson grid (host setup)."""
+    M = O.generate("poisson3d", nx, ny, nz)
+    n = M.nrows
+    A = {0: HCSR.from_arrays(M.rowptr, M.col.astype(np.int32), M.val, n)}
+    H = pa.build_hierarchy(pa.SequentialBackend(1), A, np.array([0, n], np.int64), pa.SAParams(max_coarse=100))
+    lp = H.levels[0][0]
+    P = lp.P
+    return lp.A, O.CSR(P.rowptr.copy(), P.col.astype(np.int64), P.val.copy(), P.ncols)
+
+
+@pytest.mark.parametrize("shape", [(64, 16, 12), (128, 32, 20), (64, 64, 64)])
+def test_prolongation_neighbour_coded_bit_exact(ctx, shape):
+    """k_rows_pnc (round 5: the prolongation's columns named by the grid neighbours whose anchors
+    they are — 12 B per row): a level-0 prolongation uploaded after its grid operator takes the
+    layout, and its SpMV, residual and prolongate-add are bit-exact with the oracle; with the
+    option off the tile layouts give the same bits."""
+    from parallel_amg_amd._lib import layout_of
+    A0, P = _grid_hierarchy_P0(*shape)
+    Ad = PSparseMatrix(ctx, A0)
+    assert layout_of(Ad)["jr_fused"], layout_of(Ad)  # (the grid is registered on the context)
+    D = _layout_ops_match_oracle(ctx, P, np.random.default_rng(sum(shape)))
+    lay = layout_of(D)
+    assert lay["pnc"] and lay["cd"] <= 128 and lay["cd_offsets"] <= 1024, lay
+    with _with_option("pnc", 0):
+        T = _layout_ops_match_oracle(ctx, P, np.random.default_rng(sum(shape)))
+    assert not layout_of(T)["pnc"]
+    del Ad
+
+
+def test_prolongation_neighbour_coded_declines(ctx):
+    """A column that is no neighbour's anchor, a row longer than 7, or no grid of the prolongation's
+    row count on the context: the tile layouts, still bit-exact."""
+    from parallel_amg_amd._lib import layout_of
+    A0, P = _grid_hierarchy_P0(64, 16, 10)
+    Ad = PSparseMatrix(ctx, A0)
+    assert layout_of(Ad)["jr_fused"]
+    # one entry of row 500 moved to a far column (kept sorted, values unchanged)
+    col = P.col.copy()
+    r0, r1 = P.rowptr[500], P.rowptr[501]
+    far = P.ncols - 1 if col[r1 - 1] < P.ncols - 1 else 0
+    if far > col[r1 - 1]:
+        col[r1 - 1] = far
+    else:
+        col[r0] = far
+    moved = O.CSR(P.rowptr.copy(), col, P.val.copy(), P.ncols)
+    # row 700 given 8 entries (the first columns not in it)
+    rows = [P.col[P.rowptr[i]:P.rowptr[i + 1]].tolist() for i in range(P.nrows)]
+    vals = [P.val[P.rowptr[i]:P.rowptr[i + 1]].tolist() for i in range(P.nrows)]
+    extra = [c for c in range(P.ncols) if c not in rows[700]][:8 - len(rows[700])]
+    rows[700] = sorted(rows[700] + extra)
+    vals[700] = (vals[700] + [0.125] * len(extra))[:8]
+    rp = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
+    long8 = O.CSR(rp, np.concatenate(rows).astype(np.int64), np.concatenate(vals), P.ncols)
+    # a grid whose operator never took the blocked layout (nx = 40: not a multiple of the tile)
+    A1, P1 = _grid_hierarchy_P0(40, 16, 10)
+    for M in (moved, long8, P1):
+        D = _layout_ops_match_oracle(ctx, M, np.random.default_rng(5))
+        assert not layout_of(D)["pnc"]
+    del Ad

@@ -91,6 +91,9 @@ def main():
             mats[f"P{l}"] = (lp.P, lp.planP)
     print(f"# setup {time.time() - t:.1f}s", file=sys.stderr, flush=True)
     ops = [int(o) for o in args.ops.split(",")]
+    # the grid operator first: a prolongation over its grid may take the neighbour-coded layout
+    # (PncSet: the upload looks the grid up on the context)
+    grid_op = PSparseMatrix(ctx, *mats["A0"])  # noqa: F841 (kept alive: its grid stays registered)
     for cfg in args.configs.split(","):
         given = [int(v) for v in cfg.split(":")]
         vals = given + [1024, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1][len(given):]  # library defaults for missing fields
