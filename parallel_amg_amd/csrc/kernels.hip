@@ -633,6 +633,13 @@ struct SymMask {
     }
 };
 
+// the grid plane of band j of a plane-window launch (launch_sym_planes): plane0 + j, the planes from
+// gap_at on shifted by gap (two windows in one launch)
+__device__ __forceinline__ int sym_plane(const SymDia& sd, int j) {
+    const int p = sd.plane0 + j;
+    return p >= sd.gap_at ? p + sd.gap : p;
+}
+
 template <int OP, int NU>
 __global__ __launch_bounds__(kBlock) void k_rows_sym(
     int nrows, int ncols, const uint8_t* __restrict__ mask, const double* __restrict__ dg,
@@ -640,7 +647,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_sym(
     const double* __restrict__ b, double* __restrict__ y, double omega) {
     const int bid = blockIdx.x, tid = threadIdx.x;
     const int xcd = bid & 7, j = bid >> 3;
-    const int plane = sd.plane0 + j / sd.eighth, blk = xcd * sd.eighth + j % sd.eighth;
+    const int plane = sym_plane(sd, j / sd.eighth), blk = xcd * sd.eighth + j % sd.eighth;
     const int64_t lo = (int64_t)plane * sd.band;
     const int64_t i64 = lo + (int64_t)blk * kBlock + tid;
     const int64_t hi = lo + sd.band < nrows ? lo + sd.band : nrows;
@@ -703,7 +710,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_sym2(
     constexpr int RB = 2 * kBlock;  // rows per block
     const int bid = blockIdx.x, tid = threadIdx.x;
     const int xcd = bid & 7, j = bid >> 3;
-    const int plane = sd.plane0 + j / sd.eighth, blk = xcd * sd.eighth + j % sd.eighth;
+    const int plane = sym_plane(sd, j / sd.eighth), blk = xcd * sd.eighth + j % sd.eighth;
     const int64_t lo = (int64_t)plane * sd.band;
     const int64_t i0 = lo + (int64_t)blk * RB + 2 * tid;
     const int64_t hi = lo + sd.band < nrows ? lo + sd.band : nrows;
@@ -844,7 +851,7 @@ __global__ __launch_bounds__(kBlock) void k_rows_symd(
 #pragma unroll
         for (int q = 0; q < P; ++q) {
             const int u = u0 + k0 + q;
-            const int plane = sd.plane0 + u / sd.eighth, blk = xcd * sd.eighth + u % sd.eighth;
+            const int plane = sym_plane(sd, u / sd.eighth), blk = xcd * sd.eighth + u % sd.eighth;
             const int64_t lo = (int64_t)plane * sd.band;
             const int64_t i0 = lo + (int64_t)blk * RB + 2 * tidx;
             const int64_t hi = lo + sd.band < nrows ? lo + sd.band : nrows;
@@ -1777,6 +1784,44 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __
 // row itself off the grid: no code names such a point), takes each entry's column from its code and
 // sums value * x[column] left to right from +0.0 in storage order (SPEC S3), as the other row
 // kernels do.
+// what a lane loads for its row of a block before the pattern is known (k_rows_pnc)
+struct PncRow {
+    uint2 rec;
+    int an[7];   // anchors of the points i, i-1, i+1, i-nx, i+nx, i-M, i+M (clamped to i off the grid)
+    double p0;   // y (prolongate-add), b (residual, Jacobi)
+    double p1;   // x_i (Jacobi)
+};
+
+template <int OP>
+__device__ __forceinline__ void pnc_load(PncRow& r, int i, int nrows, int nx, int M, const int* __restrict__ anc,
+                                         const uint2* __restrict__ rec, const double* __restrict__ x,
+                                         const double* __restrict__ b, const double* __restrict__ y) {
+    const int ic = i < nrows ? i : nrows - 1;
+    r.rec = rec[ic];
+    r.an[0] = anc[ic];
+    r.an[1] = anc[ic >= 1 ? ic - 1 : ic];
+    r.an[2] = anc[ic + 1 < nrows ? ic + 1 : ic];
+    r.an[3] = anc[ic >= nx ? ic - nx : ic];
+    r.an[4] = anc[ic + nx < nrows ? ic + nx : ic];
+    r.an[5] = anc[ic >= M ? ic - M : ic];
+    r.an[6] = anc[ic + M < nrows ? ic + M : ic];
+    r.p0 = 0.0;
+    r.p1 = 0.0;
+    if constexpr (OP == OP_RESID || OP == OP_JACOBI) r.p0 = b[ic];
+    if constexpr (OP == OP_PROLONG) r.p0 = y[ic];
+    if constexpr (OP == OP_JACOBI) r.p1 = x[ic];
+}
+
+// k_rows_pnc: the neighbour-coded prolongation (pamg::PncSet; round 5, the 512^3 P0). One row per
+// lane, about 8 workgroups per CU, each staging the two global tables (<= 1024 pattern words, <= 128
+// values) in LDS once and then walking 256-row blocks: at step t the workgroups of XCD j (block b
+// runs on XCD b % 8) take consecutive blocks of the j-th eighth of the rows, so each XCD moves one
+// window along its rows and its L2 holds the window's coarse entries and the anchors of the planes
+// next to it. A lane loads its row's record and the anchors of its 7 grid points (clamped to the
+// row itself off the grid: no code names such a point), takes each entry's column from its code and
+// sums value * x[column] left to right from +0.0 in storage order (SPEC S3), as the other row
+// kernels do. The next block's record, anchors and y are loaded while this block's x gathers are in
+// flight (issued after them, so waiting for the gathers never waits for the prefetch).
 template <int OP>
 __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, const int* __restrict__ anc,
                                                   const uint2* __restrict__ rec, const uint32_t* __restrict__ ptab,
@@ -1787,54 +1832,62 @@ __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, cons
     __shared__ double lv[kPncValMax];
     for (int t = threadIdx.x; t < npat; t += 256) lp[t] = ptab[t];
     for (int t = threadIdx.x; t < nval; t += 256) lv[t] = vtab[t];
-    __syncthreads();
     const int nblk = (nrows + 255) >> 8;
     const int per = (nblk + 7) >> 3;  // blocks of an XCD's eighth
     const int slots = gridDim.x >> 3;  // workgroups per XCD
     const int g0 = (blockIdx.x & 7) * per, g1 = min(nblk, g0 + per);
-    for (int g = g0 + (int)(blockIdx.x >> 3); g < g1; g += slots) {
+    int g = g0 + (int)(blockIdx.x >> 3);
+    PncRow cur;
+    if (g < g1) pnc_load<OP>(cur, (g << 8) + (int)threadIdx.x, nrows, nx, M, anc, rec, x, b, y);
+    __syncthreads();  // (the tables; the first block's loads already in flight)
+    for (; g < g1; g += slots) {
         const int i = (g << 8) + (int)threadIdx.x;
-        if (i >= nrows) continue;  // (no barrier in the loop)
-        const uint2 r = rec[i];
-        const int a0 = anc[i];
-        const int an1 = anc[i >= 1 ? i - 1 : i], an2 = anc[i + 1 < nrows ? i + 1 : i];
-        const int an3 = anc[i >= nx ? i - nx : i], an4 = anc[i + nx < nrows ? i + nx : i];
-        const int an5 = anc[i >= M ? i - M : i], an6 = anc[i + M < nrows ? i + M : i];
-        double pb = 0.0, px = 0.0, py = 0.0;
-        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[i];
-        if constexpr (OP == OP_JACOBI) px = x[i];
-        if constexpr (OP == OP_PROLONG) py = y[i];
-        const uint32_t pw = lp[r.x & 1023u];
+        const uint32_t pw = lp[cur.rec.x & 1023u];
         const int L = (int)(pw & 7u);
-        const uint64_t rr = ((uint64_t)r.y << 32) | r.x;
-        double s = 0.0, dg = 0.0;
+        int col[kPncMaxLen];
+        double xv[kPncMaxLen];
 #pragma unroll
         for (int k = 0; k < kPncMaxLen; ++k) {
             const uint32_t c = (pw >> (3 + 3 * k)) & 7u;
-            const int col = c == 0 ? a0 : c == 1 ? an1 : c == 2 ? an2 : c == 3 ? an3 : c == 4 ? an4 : c == 5 ? an5 : an6;
+            // (a select chain, no branches; a padded entry loads the first entry's x again, so every
+            // lane issues the same straight-line loads and the wait below counts them exactly)
+            const int c01 = c & 1u ? cur.an[1] : cur.an[0];
+            const int c23 = c & 1u ? cur.an[3] : cur.an[2];
+            const int c45 = c & 1u ? cur.an[5] : cur.an[4];
+            const int c03 = c & 2u ? c23 : c01;
+            const int c47 = c & 2u ? cur.an[6] : c45;
+            col[k] = c & 4u ? c47 : c03;
+            xv[k] = x[k < L ? col[k] : col[0]];
+        }
+        // (unconditional — the last block reloads itself — so the waits below count exactly)
+        PncRow nxt;
+        pnc_load<OP>(nxt, ((g + slots < g1 ? g + slots : g) << 8) + (int)threadIdx.x, nrows, nx, M, anc, rec, x, b, y);
+        const uint64_t rr = ((uint64_t)cur.rec.y << 32) | cur.rec.x;
+        double s = 0.0, dg = 0.0;
+#pragma unroll
+        for (int k = 0; k < kPncMaxLen; ++k) {
             const bool ok = k < L;
             const double v = lv[(uint32_t)(rr >> (10 + 7 * k)) & 127u];
-            double xv = 0.0;
-            if (ok) xv = x[col];
-            const double p = v * xv;
+            const double p = v * xv[k];
             const double t = s + p;
             s = ok ? t : s;
-            if constexpr (OP == OP_JACOBI) dg = ok && col == i ? v : dg;
+            if constexpr (OP == OP_JACOBI) dg = ok && col[k] == i ? v : dg;
         }
         double out;
         if constexpr (OP == OP_SPMV) {
             out = s;
         } else if constexpr (OP == OP_RESID) {
-            out = pb - s;
+            out = cur.p0 - s;
         } else if constexpr (OP == OP_JACOBI) {
-            const double u = pb - s;
+            const double u = cur.p0 - s;
             const double v = omega * u;
             const double w = v / dg;
-            out = px + w;
+            out = cur.p1 + w;
         } else {
-            out = py + s;
+            out = cur.p0 + s;
         }
-        y[i] = out;
+        if (i < nrows) y[i] = out;
+        cur = nxt;
     }
 }
 
@@ -2255,11 +2308,22 @@ void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s) {
 }
 
 void launch_sym_planes(const pamg_mat& A, int op, int p0, int p1, const double* x, const double* b, double* y,
-                       double omega, hipStream_t s) {
+                       double omega, hipStream_t s, int p2, int p3) {
+    if (p1 < p0) p1 = p0;
+    if (p3 < p2) p3 = p2;
+    if (p1 == p0) {  // one window: the second
+        p0 = p2;
+        p1 = p3;
+        p2 = p3 = 0;
+    }
     if (p1 <= p0) return;
-    pamg_mat B = A;  // shallow: the same device arrays, a plane window
+    pamg_mat B = A;  // shallow: the same device arrays, a plane window (or two)
     B.sym.plane0 = p0;
-    B.sym.nbands = p1 - p0;
+    B.sym.nbands = (p1 - p0) + (p3 - p2);
+    if (p3 > p2) {
+        B.sym.gap_at = p1;
+        B.sym.gap = p2 - p1;
+    }
     switch (op) {
         case OP_RESID: launch_sym<OP_RESID>(B, x, b, y, omega, s); break;
         case OP_JACOBI: launch_sym<OP_JACOBI>(B, x, b, y, omega, s); break;

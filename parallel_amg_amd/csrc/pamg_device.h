@@ -231,6 +231,7 @@ struct SymDia {
     bool tb_part = false;
     int part_lo = 0, part_hi = 0;   // the set's planes [part_lo, part_hi) (the others read ghosts)
     int plane0 = 0;                 // first plane of a plane-range launch of k_rows_sym / sym2
+    int gap_at = 1 << 30, gap = 0;  // ... whose planes from gap_at on are shifted by gap (a second window)
     TbGeom tb;
     uint8_t* d_mask = nullptr;      // nrows (+ pad) masks of 1 byte (2 nu + 1 <= 7) or 2 bytes
     int mask_bytes = 2;
@@ -351,9 +352,10 @@ struct TbArgs {
 };
 constexpr int kTbX = 64, kTbY = 16;  // output tile of a workgroup (grid points in x, y)
 void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s);
-// a row operation of the symmetric set on the grid planes [p0, p1) only (band = one plane)
+// a row operation of the symmetric set on the grid planes [p0, p1) and [p2, p3) only (band = one
+// plane; p1 <= p2), one launch
 void launch_sym_planes(const pamg_mat& A, int op, int p0, int p1, const double* x, const double* b, double* y,
-                       double omega, hipStream_t s);
+                       double omega, hipStream_t s, int p2 = 0, int p3 = 0);
 // dst[i] = src[perm[i]] (gather), or dst[perm[i]] = src[i] (scatter)
 void launch_permute(int64_t n, const int* perm, const double* src, double* dst, bool scatter, hipStream_t s);
 void launch_axpby(int64_t n, double a, const double* x, double b, double* y, hipStream_t s);

@@ -1867,8 +1867,8 @@ int sweeps_part(pamg_ctx* ctx, const pamg_mat* A, int S, const double* in0, doub
             v,
             [&]() {
                 if (q == 0) pamg::launch_sym_tb(*A, ta, s);
-                pamg::launch_sym_planes(*A, op, sd.part_lo, zlo, v, b, out[q], w, s);
-                pamg::launch_sym_planes(*A, op, zhi, sd.part_hi, v, b, out[q], w, s);
+                // the set's planes next to the neighbour parts, both sides in one launch
+                pamg::launch_sym_planes(*A, op, sd.part_lo, zlo, v, b, out[q], w, s, zhi, sd.part_hi);
             },
             [&]() { pamg::launch_rows(*A, A->boundary, op, v, b, v, out[q], w, s); }));
     }

@@ -6,7 +6,7 @@ set -euo pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:-zm}
 mkdir -p $O
-KB="python3 -u tools/kbench.py --n 512 --levels 1 --ops ${OPS:-0,2,4,5} --reps 3 --configs 1024"
+KB="python3 -u tools/kbench.py ${KB_ARGS:---n 512 --levels 1 --ops ${OPS:-0,2,4,5} --reps 3 --configs 1024}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- $KB > $O/kt.jsonl 2> $O/kt.err
 echo "trace done"
 i=0
