@@ -1784,64 +1784,68 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __
 // row itself off the grid: no code names such a point), takes each entry's column from its code and
 // sums value * x[column] left to right from +0.0 in storage order (SPEC S3), as the other row
 // kernels do.
-// what a lane loads for its row of a block before the pattern is known (k_rows_pnc)
+// what a lane loads for its row of a block before the pattern is known (k_rows_pnc): the record,
+// the anchors of the in-plane neighbours, y / b / x; the z neighbours' anchors come from the
+// z-march's registers
 struct PncRow {
     uint2 rec;
-    int an[7];   // anchors of the points i, i-1, i+1, i-nx, i+nx, i-M, i+M (clamped to i off the grid)
+    int an[5];   // anchors of the points i, i-1, i+1, i-nx, i+nx (clamped to i off the plane)
     double p0;   // y (prolongate-add), b (residual, Jacobi)
     double p1;   // x_i (Jacobi)
 };
 
 template <int OP>
-__device__ __forceinline__ void pnc_load(PncRow& r, int i, int nrows, int nx, int M, const int* __restrict__ anc,
+__device__ __forceinline__ void pnc_load(PncRow& r, int i, int nrows, int nx, const int* __restrict__ anc,
                                          const uint2* __restrict__ rec, const double* __restrict__ x,
                                          const double* __restrict__ b, const double* __restrict__ y) {
-    const int ic = i < nrows ? i : nrows - 1;
-    r.rec = rec[ic];
-    r.an[0] = anc[ic];
-    r.an[1] = anc[ic >= 1 ? ic - 1 : ic];
-    r.an[2] = anc[ic + 1 < nrows ? ic + 1 : ic];
-    r.an[3] = anc[ic >= nx ? ic - nx : ic];
-    r.an[4] = anc[ic + nx < nrows ? ic + nx : ic];
-    r.an[5] = anc[ic >= M ? ic - M : ic];
-    r.an[6] = anc[ic + M < nrows ? ic + M : ic];
+    r.rec = rec[i];
+    r.an[0] = anc[i];
+    r.an[1] = anc[i >= 1 ? i - 1 : i];
+    r.an[2] = anc[i + 1 < nrows ? i + 1 : i];
+    r.an[3] = anc[i >= nx ? i - nx : i];
+    r.an[4] = anc[i + nx < nrows ? i + nx : i];
     r.p0 = 0.0;
     r.p1 = 0.0;
-    if constexpr (OP == OP_RESID || OP == OP_JACOBI) r.p0 = b[ic];
-    if constexpr (OP == OP_PROLONG) r.p0 = y[ic];
-    if constexpr (OP == OP_JACOBI) r.p1 = x[ic];
+    if constexpr (OP == OP_RESID || OP == OP_JACOBI) r.p0 = b[i];
+    if constexpr (OP == OP_PROLONG) r.p0 = y[i];
+    if constexpr (OP == OP_JACOBI) r.p1 = x[i];
 }
 
 // k_rows_pnc: the neighbour-coded prolongation (pamg::PncSet; round 5, the 512^3 P0). One row per
-// lane, about 8 workgroups per CU, each staging the two global tables (<= 1024 pattern words, <= 128
-// values) in LDS once and then walking 256-row blocks: at step t the workgroups of XCD j (block b
-// runs on XCD b % 8) take consecutive blocks of the j-th eighth of the rows, so each XCD moves one
-// window along its rows and its L2 holds the window's coarse entries and the anchors of the planes
-// next to it. A lane loads its row's record and the anchors of its 7 grid points (clamped to the
-// row itself off the grid: no code names such a point), takes each entry's column from its code and
-// sums value * x[column] left to right from +0.0 in storage order (SPEC S3), as the other row
-// kernels do. The next block's record, anchors and y are loaded while this block's x gathers are in
-// flight (issued after them, so waiting for the gathers never waits for the prefetch).
+// lane; a workgroup owns a 256-point block of a plane (M % 256 == 0) and marches it along z over a
+// chunk of planes, so the anchors of the z neighbours (i - M, i + M) are the ones it loaded for the
+// previous plane and prefetches for the next — each anchor leaves HBM once; the in-plane neighbours'
+// anchors (i +- 1: the same lines; i +- nx: the blocks next to it, marched by the workgroups beside
+// it on the same XCD) come from the caches. The two global tables (<= 1024 pattern words, <= 128
+// values) sit in LDS. A lane takes each entry's column from its code and sums value * x[column]
+// left to right from +0.0 in storage order (SPEC S3), as the other row kernels do. The next plane's
+// record, anchors and y are loaded under this plane's x gathers; every gather is issued (a padded
+// entry reloads the first entry's x), so the loads are straight-line and the waits count exactly.
 template <int OP>
-__global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, const int* __restrict__ anc,
-                                                  const uint2* __restrict__ rec, const uint32_t* __restrict__ ptab,
-                                                  int npat, const double* __restrict__ vtab, int nval,
+__global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int nz, int zlen,
+                                                  const int* __restrict__ anc, const uint2* __restrict__ rec,
+                                                  const uint32_t* __restrict__ ptab, int npat,
+                                                  const double* __restrict__ vtab, int nval,
                                                   const double* __restrict__ x, const double* __restrict__ b,
                                                   double* __restrict__ y, double omega) {
     __shared__ uint32_t lp[kPncPatMax];
     __shared__ double lv[kPncValMax];
+    const int nxb = M >> 8;                                    // 256-point blocks of a plane
+    const int units = nxb * ((nz + zlen - 1) / zlen);
+    const int per = (units + 7) >> 3;
+    const int u = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // consecutive units on one XCD
+    if (u >= units) return;  // the whole workgroup, before the barrier
     for (int t = threadIdx.x; t < npat; t += 256) lp[t] = ptab[t];
     for (int t = threadIdx.x; t < nval; t += 256) lv[t] = vtab[t];
-    const int nblk = (nrows + 255) >> 8;
-    const int per = (nblk + 7) >> 3;  // blocks of an XCD's eighth
-    const int slots = gridDim.x >> 3;  // workgroups per XCD
-    const int g0 = (blockIdx.x & 7) * per, g1 = min(nblk, g0 + per);
-    int g = g0 + (int)(blockIdx.x >> 3);
+    const int z0 = (u / nxb) * zlen, z1 = min(nz, z0 + zlen);
+    const int ixy = ((u % nxb) << 8) + (int)threadIdx.x;
     PncRow cur;
-    if (g < g1) pnc_load<OP>(cur, (g << 8) + (int)threadIdx.x, nrows, nx, M, anc, rec, x, b, y);
-    __syncthreads();  // (the tables; the first block's loads already in flight)
-    for (; g < g1; g += slots) {
-        const int i = (g << 8) + (int)threadIdx.x;
+    pnc_load<OP>(cur, z0 * M + ixy, nrows, nx, anc, rec, x, b, y);
+    int am = anc[z0 > 0 ? (z0 - 1) * M + ixy : ixy];          // anchors of planes z - 1 and z + 1
+    int ap = anc[z0 + 1 < nz ? (z0 + 1) * M + ixy : ixy];
+    __syncthreads();  // (the tables; the first plane's loads already in flight)
+    for (int z = z0; z < z1; ++z) {
+        const int i = z * M + ixy;
         const uint32_t pw = lp[cur.rec.x & 1023u];
         const int L = (int)(pw & 7u);
         int col[kPncMaxLen];
@@ -1849,19 +1853,20 @@ __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, cons
 #pragma unroll
         for (int k = 0; k < kPncMaxLen; ++k) {
             const uint32_t c = (pw >> (3 + 3 * k)) & 7u;
-            // (a select chain, no branches; a padded entry loads the first entry's x again, so every
-            // lane issues the same straight-line loads and the wait below counts them exactly)
+            // codes 0 self, 1 i-1, 2 i+1, 3 i-nx, 4 i+nx, 5 i-M, 6 i+M: a select chain, no branches
             const int c01 = c & 1u ? cur.an[1] : cur.an[0];
             const int c23 = c & 1u ? cur.an[3] : cur.an[2];
-            const int c45 = c & 1u ? cur.an[5] : cur.an[4];
+            const int c45 = c & 1u ? am : cur.an[4];
             const int c03 = c & 2u ? c23 : c01;
-            const int c47 = c & 2u ? cur.an[6] : c45;
+            const int c47 = c & 2u ? ap : c45;
             col[k] = c & 4u ? c47 : c03;
             xv[k] = x[k < L ? col[k] : col[0]];
         }
-        // (unconditional — the last block reloads itself — so the waits below count exactly)
+        // the next plane (the last one reloads its own plane), and the anchors two planes on
+        const int zn = z + 1 < z1 ? z + 1 : z;
         PncRow nxt;
-        pnc_load<OP>(nxt, ((g + slots < g1 ? g + slots : g) << 8) + (int)threadIdx.x, nrows, nx, M, anc, rec, x, b, y);
+        pnc_load<OP>(nxt, zn * M + ixy, nrows, nx, anc, rec, x, b, y);
+        const int ap2 = anc[zn + 1 < nz ? (zn + 1) * M + ixy : zn * M + ixy];
         const uint64_t rr = ((uint64_t)cur.rec.y << 32) | cur.rec.x;
         double s = 0.0, dg = 0.0;
 #pragma unroll
@@ -1879,15 +1884,17 @@ __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, cons
         } else if constexpr (OP == OP_RESID) {
             out = cur.p0 - s;
         } else if constexpr (OP == OP_JACOBI) {
-            const double u = cur.p0 - s;
-            const double v = omega * u;
+            const double uu = cur.p0 - s;
+            const double v = omega * uu;
             const double w = v / dg;
             out = cur.p1 + w;
         } else {
             out = cur.p0 + s;
         }
-        if (i < nrows) y[i] = out;
+        y[i] = out;
+        am = cur.an[0];
         cur = nxt;
+        ap = ap2;
     }
 }
 
@@ -2263,8 +2270,8 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
     }
     if (ts.pnc) {
         const PncSet& P = A.pnc;
-        k_rows_pnc<OP><<<P.grid, 256, 0, s>>>((int)A.nrows, P.nx, P.nx * P.ny, P.d_anc, P.d_rec, P.d_ptab, P.npat,
-                                              P.d_vtab, P.nval, x, b, y, omega);
+        k_rows_pnc<OP><<<P.grid, 256, 0, s>>>((int)A.nrows, P.nx, P.nx * P.ny, P.nz, P.zlen, P.d_anc, P.d_rec, P.d_ptab,
+                                              P.npat, P.d_vtab, P.nval, x, b, y, omega);
     }
     if (ts.n_short > 0) {
         if (ts.tile_nnz == 1024) launch_tile<OP, 1024>(A, ts, x, b, y, omega, s);

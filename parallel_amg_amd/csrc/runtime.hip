@@ -152,6 +152,29 @@ int h2d(pamg_ctx* ctx, void* dst, const void* src, size_t bytes) {
 }
 
 // PAMG_TRACE_UPLOAD=1: per-phase host times of each matrix upload on stderr
+// std::vector storage whose sizing constructor leaves the elements uninitialised: the upload's
+// column and row-pointer copies (up to 3.75 GB at 512^3) are filled by parallel loops, not zeroed
+// first on one thread
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) {}
+    template <class U, class... Args>
+    void construct(U* p, Args&&... args) {
+        if constexpr (sizeof...(Args) == 0)
+            ::new ((void*)p) U;
+        else
+            ::new ((void*)p) U(std::forward<Args>(args)...);
+    }
+};
+using IdxVec = std::vector<int, NoInitAlloc<int>>;
+using PtrVec = std::vector<int64_t, NoInitAlloc<int64_t>>;
+
 struct UploadTrace {
     bool on = std::getenv("PAMG_TRACE_UPLOAD") != nullptr;
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
@@ -251,7 +274,7 @@ int build_value_dict(const std::vector<int4>& tiles, const double* val, pamg::Ti
 // and the largest gap inside the chunk), then merged per column in chunk order: the values of
 // one sequential pass. A matrix whose chunks together span more than ~2x the columns (no band
 // structure) takes the sequential pass.
-std::vector<int> column_reuse_gaps(const std::vector<int64_t>& rp, const std::vector<int>& ci, int64_t nrows,
+std::vector<int> column_reuse_gaps(const PtrVec& rp, const IdxVec& ci, int64_t nrows,
                                    int64_t ncols) {
     std::vector<int> gap(ncols, 0);
     const int nch = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, nrows / 65536));
@@ -326,8 +349,8 @@ std::vector<int> column_reuse_gaps(const std::vector<int64_t>& rp, const std::ve
     return gap;
 }
 
-int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows, bool square,
-                pamg::TileSet* ts, int64_t band, const std::vector<int>& ci,
+int build_tiles(const PtrVec& rp, const std::vector<int>& rows, bool square,
+                pamg::TileSet* ts, int64_t band, const IdxVec& ci,
                 std::vector<uint16_t>* lo, std::vector<uint8_t>* hi, const double* val,
                 std::vector<uint8_t>* vidx, std::vector<int4>* tiles_out, bool tall = false) {
     const auto& opt = pamg::options();
@@ -471,7 +494,7 @@ int build_tiles(const std::vector<int64_t>& rp, const std::vector<int>& rows, bo
 // as a 16-bit delta from a per-tile base: the prolongators, a few per tile). The form
 // with fewer bytes is taken, and only if it streams less than the 24-bit columns; it runs in
 // the descriptor kernel (k_rows_tile2), not in tile-major slots.
-int build_tile_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci,
+int build_tile_dicts(pamg_mat* A, const PtrVec& rp, const IdxVec& ci,
                      const std::vector<int4>& tiles, pamg::TileSet* ts, std::vector<uint8_t>* idx,
                      std::vector<int>* tab, std::vector<uint16_t>* anc16) {
     const int64_t nt = (int64_t)tiles.size();
@@ -579,7 +602,7 @@ int build_tile_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vec
 // column as row + table[index] (exact); its rows come from the 8-bit row lengths, so a
 // dictionary set also turns rl8 on. Against the 24-bit stream this saves 2.5 B/nonzero
 // (4-bit) or 2 B/nonzero (8-bit) of the 11-12 B a nonzero streams.
-int build_col_dicts(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci,
+int build_col_dicts(pamg_mat* A, const PtrVec& rp, const IdxVec& ci,
                     const std::vector<int4>& t_in, const std::vector<int4>& t_bd,
                     std::vector<uint8_t>* idx8) {
     const auto& opt = pamg::options();
@@ -778,8 +801,8 @@ int build_x_stage(pamg_mat* A, pamg::TileSet* ts, int rs) {
 // columns, tile t's values, column stream and row lengths are copied to fixed, zero-padded
 // slots (t * tile_nnz, t * tm_rs), so the kernel addresses every pre-gather load from its
 // block index. The CSR arrays stay resident for the other variants and the long rows.
-int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>& rp,
-                     const std::vector<int>& ci, const double* val,
+int build_tile_major(pamg_mat* A, int64_t n_own_cols, const PtrVec& rp,
+                     const IdxVec& ci, const double* val,
                      const std::vector<int4>& t_in, const std::vector<int4>& t_bd,
                      const std::vector<uint16_t>& lo, const std::vector<uint8_t>& hi,
                      const std::vector<uint8_t>& idx8) {
@@ -960,7 +983,7 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const std::vector<int64_t>
 // interior row's entries in strictly ascending offset order (so the kernel's ascending sum is
 // the storage-order sum of SPEC §S3), and every lower entry bit-identical to its mirror
 // a(i-o, i) in row i-o. Otherwise nothing is built and the rows keep their tiles.
-int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci, const double* val,
+int build_sym_dia(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val,
                   const std::vector<int>& inner, int64_t band) {
     using pamg::kSymMaxU;
     const int64_t n = A->nrows;
@@ -1002,10 +1025,23 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
     sd.ld = (n + 63) / 64 * 64 + 64;
     const int mb = 2 * nu + 1 <= 7 ? 1 : 2;  // mask bytes per row (kernels.hip SymMask)
     const uint32_t in_flag = mb == 1 ? 0x80u : 0x8000u;
-    std::vector<uint16_t> mask(n + kVecPad, 0);
-    std::vector<double> dg(n + kVecPad, 0.0), up((size_t)nu * sd.ld, 0.0);
-    std::vector<char> in_set(n, 0);
-    for (int i : inner) in_set[i] = 1;
+    // (zeroed by parallel loops: 5 GB at 512^3)
+    std::vector<uint16_t, NoInitAlloc<uint16_t>> mask(n + kVecPad);
+    std::vector<double, NoInitAlloc<double>> dg(n + kVecPad), up((size_t)nu * sd.ld);
+    std::vector<char, NoInitAlloc<char>> in_set(n);
+    par_for(n + kVecPad, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            mask[i] = 0;
+            dg[i] = 0.0;
+            if (i < n) in_set[i] = 0;
+        }
+    });
+    par_for((int64_t)up.size(), [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) up[i] = 0.0;
+    });
+    par_for((int64_t)inner.size(), [&](int64_t a, int64_t b) {
+        for (int64_t q = a; q < b; ++q) in_set[inner[q]] = 1;
+    });
     auto cls = [&](int o) { return (int)(std::lower_bound(offs.begin(), offs.end(), o) - offs.begin()); };
     std::atomic<bool> bad{false};
     par_for(n, [&](int64_t a, int64_t b) {
@@ -1243,7 +1279,7 @@ int build_sym_dia(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector
 // Several parts: the set is the interior rows only (`inner`, ascending); the slices still span every
 // row index, the boundary rows marked skipped (length byte kEllSkip: no load, no store — the
 // boundary tiles compute them after the exchange).
-int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci, const double* val,
+int build_ell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val,
               bool anchored, const std::vector<int>& inner) {
     using pamg::kEllGroup;
     using pamg::kEllSkip;
@@ -1276,30 +1312,61 @@ int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
         words += (int64_t)kEllW * ((slen[q] + 3) / 4);
         if (words >= INT32_MAX) return PAMG_OK;
     }
-    // per group: sorted distinct offsets and value bit patterns
+    // per group, one pass: an entry's offset and value take the index of their first appearance in
+    // the group (open addressing over 512 slots, stamped per group instead of cleared), and the index
+    // bytes go straight into the slice streams (a slice lies in one group: no two threads share a word)
     std::vector<std::vector<int>> goff(ng);
     std::vector<std::vector<uint64_t>> gval(ng);
+    std::vector<uint32_t> cw(words + 1, 0u), vw(words + 1, 0u);
+    std::vector<uint8_t> len(n + kVecPad, 0);
     par_for(ng, [&](int64_t a, int64_t b) {
+        constexpr int kSlots = 512;
+        std::vector<int> okey(kSlots), oid(kSlots), ostamp(kSlots, -1), vid(kSlots), vstamp(kSlots, -1);
+        std::vector<uint64_t> vkey(kSlots);
         std::vector<int> o;
         std::vector<uint64_t> v;
         for (int64_t g = a; g < b && ok; ++g) {
+            const int stamp = (int)(g - a);
             o.clear();
             v.clear();
             const int64_t r1 = std::min(n, (g + 1) * kEllGroup);
-            for (int64_t i = g * kEllGroup; i < r1; ++i)
-                for (int64_t k = rp[i]; k < (member(i) ? rp[i + 1] : rp[i]); ++k) {
-                    o.push_back(ci[k] - base_of(i));
+            for (int64_t i = g * kEllGroup; i < r1; ++i) {
+                if (!member(i)) {
+                    len[i] = (uint8_t)kEllSkip;
+                    continue;
+                }
+                len[i] = (uint8_t)(rp[i + 1] - rp[i]);
+                const int64_t q = i / kEllW, lane = i % kEllW;
+                const int base = base_of(i);
+                for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                    const int kk = (int)(k - rp[i]);
+                    const int off = ci[k] - base;
+                    uint32_t h = ((uint32_t)off * 0x9E3779B1u) >> 23;
+                    while (ostamp[h] == stamp && okey[h] != off) h = (h + 1) & (kSlots - 1);
+                    if (ostamp[h] != stamp) {
+                        ostamp[h] = stamp;
+                        okey[h] = off;
+                        oid[h] = (int)o.size();
+                        o.push_back(off);
+                    }
                     uint64_t u;
                     std::memcpy(&u, &val[k], 8);
-                    v.push_back(u);
+                    uint32_t hv = (uint32_t)((u ^ (u >> 29)) * 0x9E3779B97F4A7C15ull >> 55);
+                    while (vstamp[hv] == stamp && vkey[hv] != u) hv = (hv + 1) & (kSlots - 1);
+                    if (vstamp[hv] != stamp) {
+                        vstamp[hv] = stamp;
+                        vkey[hv] = u;
+                        vid[hv] = (int)v.size();
+                        v.push_back(u);
+                    }
+                    if (o.size() > 256 || v.size() > 256) {
+                        ok = false;
+                        return;
+                    }
+                    const int64_t w = smeta[q].x + (int64_t)(kk / 4) * kEllW + lane;
+                    cw[w] |= (uint32_t)oid[h] << (8 * (kk % 4));
+                    vw[w] |= (uint32_t)vid[hv] << (8 * (kk % 4));
                 }
-            std::sort(o.begin(), o.end());
-            o.erase(std::unique(o.begin(), o.end()), o.end());
-            std::sort(v.begin(), v.end());
-            v.erase(std::unique(v.begin(), v.end()), v.end());
-            if (o.size() > 256 || v.size() > 256) {
-                ok = false;
-                return;
             }
             goff[g] = o;
             gval[g] = v;
@@ -1319,34 +1386,6 @@ int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
         for (int64_t g = a; g < b; ++g) {
             std::copy(goff[g].begin(), goff[g].end(), otab.begin() + gmeta[g].x);
             for (size_t e = 0; e < gval[g].size(); ++e) std::memcpy(&vtab[gmeta[g].z + e], &gval[g][e], 8);
-        }
-    });
-    std::vector<uint32_t> cw(words + 1, 0u), vw(words + 1, 0u);
-    std::vector<uint8_t> len(n + kVecPad, 0);
-    par_for(ns, [&](int64_t a, int64_t b) {
-        for (int64_t q = a; q < b; ++q) {
-            const int64_t g = q * kEllW / kEllGroup;
-            const auto& o = goff[g];
-            const auto& v = gval[g];
-            for (int lane = 0; lane < kEllW; ++lane) {
-                const int64_t i = q * kEllW + lane;
-                if (i >= n) break;
-                if (!member(i)) {
-                    len[i] = (uint8_t)kEllSkip;
-                    continue;
-                }
-                len[i] = (uint8_t)(rp[i + 1] - rp[i]);
-                for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
-                    const int kk = (int)(k - rp[i]);
-                    const uint32_t co = (uint32_t)(std::lower_bound(o.begin(), o.end(), ci[k] - base_of(i)) - o.begin());
-                    uint64_t u;
-                    std::memcpy(&u, &val[k], 8);
-                    const uint32_t vo = (uint32_t)(std::lower_bound(v.begin(), v.end(), u) - v.begin());
-                    const int64_t w = smeta[q].x + (int64_t)(kk / 4) * kEllW + lane;
-                    cw[w] |= co << (8 * (kk % 4));
-                    vw[w] |= vo << (8 * (kk % 4));
-                }
-            }
         }
     });
     pamg::EllSet& E = A->ell;
@@ -1385,12 +1424,12 @@ int build_ell(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
 // Neighbour-coded prolongation (Options::pnc, pamg::PncSet): every row's columns named by the
 // grid neighbours whose anchors they are. Declines (leaves the tile layouts to the caller) where a
 // row is longer than kPncMaxLen, a column is no neighbour's anchor, or a table would overflow.
-int build_pnc(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int>& ci, const double* val,
+int build_pnc(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val,
               const std::array<int64_t, 4>& grid) {
     using pamg::kPncMaxLen;
     const int64_t n = A->nrows;
     const int64_t nx = grid[1], ny = grid[2], nz = grid[3], M = nx * ny;
-    if (n != nx * ny * nz || n <= 0) return PAMG_OK;
+    if (n != nx * ny * nz || n <= 0 || M % 256 != 0) return PAMG_OK;  // (k_rows_pnc: 256-point blocks of a plane)
     std::vector<int> anc(n + kVecPad, 0);
     std::atomic<bool> ok{true};
     par_for(n, [&](int64_t a, int64_t b) {
@@ -1413,6 +1452,12 @@ int build_pnc(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
     std::vector<uint64_t> vals;
     const int64_t d[7] = {0, -1, 1, -nx, nx, -M, M};
     par_for(n, [&](int64_t a, int64_t b) {
+        // this chunk's distinct patterns and values (open addressing; the tables' limits are far below
+        // the slot counts, so a chunk past them stops)
+        constexpr int kPS = 4096, kVS = 1024;
+        std::vector<uint32_t> pkey(kPS, 0xffffffffu);
+        std::vector<uint64_t> vkey(kVS);
+        std::vector<char> vused(kVS, 0);
         std::vector<uint32_t> lp;
         std::vector<uint64_t> lv;
         for (int64_t i = a; i < b && ok; ++i) {
@@ -1429,16 +1474,25 @@ int build_pnc(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
                 w |= (uint32_t)c << (3 + 3 * (k - rp[i]));
                 uint64_t u;
                 std::memcpy(&u, &val[k], 8);
-                lv.push_back(u);
+                uint32_t h = (uint32_t)((u ^ (u >> 29)) * 0x9E3779B97F4A7C15ull >> 54);
+                while (vused[h] && vkey[h] != u) h = (h + 1) & (kVS - 1);
+                if (!vused[h]) {
+                    vused[h] = 1;
+                    vkey[h] = u;
+                    lv.push_back(u);
+                    if (lv.size() > (size_t)pamg::kPncValMax) {
+                        ok = false;
+                        return;
+                    }
+                }
             }
             pw[i] = w;
-            lp.push_back(w);
-            if (lp.size() > 4096 || lv.size() > 4096) {
-                std::sort(lp.begin(), lp.end());
-                lp.erase(std::unique(lp.begin(), lp.end()), lp.end());
-                std::sort(lv.begin(), lv.end());
-                lv.erase(std::unique(lv.begin(), lv.end()), lv.end());
-                if (lp.size() > (size_t)pamg::kPncPatMax || lv.size() > (size_t)pamg::kPncValMax) {
+            uint32_t h = (w * 0x9E3779B1u) >> 20;
+            while (pkey[h] != 0xffffffffu && pkey[h] != w) h = (h + 1) & (kPS - 1);
+            if (pkey[h] == 0xffffffffu) {
+                pkey[h] = w;
+                lp.push_back(w);
+                if (lp.size() > (size_t)pamg::kPncPatMax) {
                     ok = false;
                     return;
                 }
@@ -1476,9 +1530,13 @@ int build_pnc(pamg_mat* A, const std::vector<int64_t>& rp, const std::vector<int
     P.nz = (int)nz;
     P.npat = (int)pats.size();
     P.nval = (int)vals.size();
-    // about 8 workgroups per CU, a multiple of 8 (kernels.hip k_rows_pnc: XCD-contiguous windows)
-    const int64_t groups = (n + 255) / 256;
-    P.grid = (int)std::max<int64_t>(8, std::min<int64_t>(groups, (int64_t)device_cus() * 8) / 8 * 8);
+    // about 8 workgroups per CU, each marching one 256-point block of a plane along z over zlen planes
+    // (kernels.hip k_rows_pnc), the grid a multiple of 8
+    const int64_t nxb = M / 256, want = (int64_t)device_cus() * 8;
+    const int64_t zch = std::max<int64_t>(1, std::min<int64_t>(nz, (want + nxb - 1) / nxb));
+    P.zlen = (int)((nz + zch - 1) / zch);
+    const int64_t units = nxb * ((nz + P.zlen - 1) / P.zlen);
+    P.grid = (int)((units + 7) / 8 * 8);
     CHECK(dalloc(&P.d_anc, n + kVecPad));
     CHECK(dalloc(&P.d_rec, n + kVecPad));
     CHECK(dalloc(&P.d_ptab, (int64_t)pats.size()));
@@ -2695,12 +2753,25 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     CHECK(set_device(ctx));
     UploadTrace tr;
     tr.nnz = nnz;
-    std::vector<int64_t> rp(nrows + 1);
-    std::vector<int> ci(nnz + kVecPad, 0);
-    for (int64_t i = 0; i <= nrows; ++i) rp[i] = rowptr[i] - index_base;
-    for (int64_t i = 0; i < nrows; ++i)
-        if (rp[i + 1] < rp[i]) return fail(PAMG_E_ARG, "mat_upload: rowptr not monotone at %lld", (long long)i);
+    PtrVec rp(nrows + 1);
+    IdxVec ci(nnz + kVecPad);
+    {
+        std::atomic<int64_t> bad_row{INT64_MAX};
+        par_for(nrows + 1, [&](int64_t a, int64_t b) {
+            for (int64_t i = a; i < b; ++i) {
+                rp[i] = rowptr[i] - index_base;
+                if (i > 0 && rowptr[i] < rowptr[i - 1]) {
+                    int64_t cur = bad_row.load();
+                    while (i - 1 < cur && !bad_row.compare_exchange_weak(cur, i - 1)) {
+                    }
+                }
+            }
+        });
+        if (bad_row.load() != INT64_MAX)
+            return fail(PAMG_E_ARG, "mat_upload: rowptr not monotone at %lld", (long long)bad_row.load());
+    }
     if (rp[0] != 0) return fail(PAMG_E_ARG, "mat_upload: rowptr[0] != index_base");
+    for (int k = 0; k < kVecPad; ++k) ci[nnz + k] = 0;
     {
         std::atomic<int64_t> bad_at{INT64_MAX};
         par_for(nnz, [&](int64_t a, int64_t b) {
@@ -2754,15 +2825,31 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         }
         if (!all) has_all_diag = false;
     });
-    for (int64_t i = 0; i < nrows; ++i) (ghost_row[i] ? bnd : inner).push_back((int)i);
+    std::atomic<int64_t> n_ghost_rows{0};
+    par_for(nrows, [&](int64_t a, int64_t b) {
+        int64_t c = 0;
+        for (int64_t i = a; i < b; ++i) c += ghost_row[i];
+        n_ghost_rows += c;
+    });
+    if (n_ghost_rows.load() == 0) {  // (one part: every row interior, listed in parallel)
+        inner.resize(nrows);
+        par_for(nrows, [&](int64_t a, int64_t b) {
+            for (int64_t i = a; i < b; ++i) inner[i] = (int)i;
+        });
+    } else {
+        for (int64_t i = 0; i < nrows; ++i) (ghost_row[i] ? bnd : inner).push_back((int)i);
+    }
     std::vector<char>().swap(ghost_row);
     tr.mark("classify");
     // The row distance at which rows share x entries, for the banded tile order: per own
     // column the largest gap between consecutive rows that read it (one grid plane for a
     // stencil, one aggregate layer for a restriction); band = its 90th percentile over the
-    // columns. (Sequential: the gaps depend on the row order.)
-    int64_t band = 0;
-    {
+    // columns. (Sequential: the gaps depend on the row order.) Computed when a layout that
+    // uses it is tried (the symmetric layout, tiles): not for rows that all go to ELL / pnc.
+    int64_t band = -1;
+    auto get_band = [&]() -> int64_t {
+        if (band >= 0) return band;
+        band = 0;
         std::vector<int> max_gap = column_reuse_gaps(rp, ci, nrows, n_own_cols);
         auto end = std::remove(max_gap.begin(), max_gap.end(), 0);
         const size_t m = (size_t)(end - max_gap.begin());
@@ -2778,10 +2865,11 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
             const int pct = nrows < n_own_cols ? pamg::options().band_pct_restrict : pamg::options().band_pct;
             if (pct != 100) band = std::max<int64_t>(1, band * pct / 100);
         }
-    }
-    tr.mark("band");
+        tr.mark("band");
+        return band;
+    };
     if (pamg::options().sym_dia && n_own_cols == nrows && has_all_diag && !inner.empty())
-        CHECK(build_sym_dia(A.get(), rp, ci, val, inner, band));
+        CHECK(build_sym_dia(A.get(), rp, ci, val, inner, get_band()));
     if (A->interior.sym) inner.clear();  // the interior rows run in k_rows_sym, not in tiles
     tr.mark("sym dia");
     // square operators (offsets from the row) and restrictions (fewer rows than columns; offsets from
@@ -2804,15 +2892,21 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         if (A->interior.pnc) inner.clear();  // the rows run in k_rows_pnc, not in tiles
         tr.mark("pnc");
     }
-    std::vector<int> rp32(nrows + 1);
-    for (int64_t i = 0; i <= nrows; ++i) rp32[i] = (int)rp[i];
-    CHECK(dalloc(&A->d_rowptr, nrows + 1));
-    CHECK(dalloc(&A->d_col, nnz + kVecPad));
-    CHECK(dalloc(&A->d_val, nnz + kVecPad));
-    CHECK(h2d(ctx, A->d_rowptr, rp32.data(), sizeof(int) * (nrows + 1)));
-    CHECK(h2d(ctx, A->d_col, ci.data(), sizeof(int) * (nnz + kVecPad)));
-    CHECK(dzero(ctx, A->d_val, sizeof(double) * (nnz + kVecPad)));
-    if (nnz) CHECK(h2d(ctx, A->d_val, val, sizeof(double) * nnz));
+    // the CSR copies: read by the tile and long-row kernels only, so not uploaded when every row
+    // runs in the symmetric, ELL or neighbour-coded layout (the 512^3 A0, A1, R0, P0: 29 GB less)
+    if (!inner.empty() || !bnd.empty()) {
+        std::vector<int> rp32(nrows + 1);
+        par_for(nrows + 1, [&](int64_t a, int64_t b) {
+            for (int64_t i = a; i < b; ++i) rp32[i] = (int)rp[i];
+        });
+        CHECK(dalloc(&A->d_rowptr, nrows + 1));
+        CHECK(dalloc(&A->d_col, nnz + kVecPad));
+        CHECK(dalloc(&A->d_val, nnz + kVecPad));
+        CHECK(h2d(ctx, A->d_rowptr, rp32.data(), sizeof(int) * (nrows + 1)));
+        CHECK(h2d(ctx, A->d_col, ci.data(), sizeof(int) * (nnz + kVecPad)));
+        CHECK(dzero(ctx, A->d_val, sizeof(double) * (nnz + kVecPad)));
+        if (nnz) CHECK(h2d(ctx, A->d_val, val, sizeof(double) * nnz));
+    }
     if (has_all_diag && nrows > 0) {
         CHECK(dalloc(&A->d_diag, nrows));
         CHECK(h2d(ctx, A->d_diag, diag.data(), sizeof(double) * nrows));
@@ -2824,8 +2918,9 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         std::vector<int4> t_in, t_bd;
         const bool square = n_own_cols == nrows;
         const bool tall = n_own_cols < nrows;  // a prolongation's shape
-        CHECK(build_tiles(rp, inner, square, &A->interior, band, ci, &lo, &hi, val, &vidx, &t_in, tall));
-        CHECK(build_tiles(rp, bnd, square, &A->boundary, band, ci, &lo, &hi, val, &vidx, &t_bd, tall));
+        const int64_t tb = inner.empty() && bnd.empty() ? 0 : get_band();
+        CHECK(build_tiles(rp, inner, square, &A->interior, tb, ci, &lo, &hi, val, &vidx, &t_in, tall));
+        CHECK(build_tiles(rp, bnd, square, &A->boundary, tb, ci, &lo, &hi, val, &vidx, &t_bd, tall));
         tr.mark("tiles");
         std::vector<uint8_t> idx8;
         CHECK(build_col_dicts(A.get(), rp, ci, t_in, t_bd, &idx8));
