@@ -1813,14 +1813,18 @@ __device__ __forceinline__ void pnc_load(PncRow& r, int i, int nrows, int nx, co
 
 // k_rows_pnc: the neighbour-coded prolongation (pamg::PncSet; round 5, the 512^3 P0). One row per
 // lane; a workgroup owns a 256-point block of a plane (M % 256 == 0) and marches it along z over a
-// chunk of planes, so the anchors of the z neighbours (i - M, i + M) are the ones it loaded for the
-// previous plane and prefetches for the next — each anchor leaves HBM once; the in-plane neighbours'
-// anchors (i +- 1: the same lines; i +- nx: the blocks next to it, marched by the workgroups beside
-// it on the same XCD) come from the caches. The two global tables (<= 1024 pattern words, <= 128
-// values) sit in LDS. A lane takes each entry's column from its code and sums value * x[column]
-// left to right from +0.0 in storage order (SPEC S3), as the other row kernels do. The next plane's
-// record, anchors and y are loaded under this plane's x gathers; every gather is issued (a padded
-// entry reloads the first entry's x), so the loads are straight-line and the waits count exactly.
+// chunk of planes — as kPncStreams interleaved streams (the chunk cut in as many parts, a plane of each per
+// step: independent gather sets in flight per lane) — so the anchors of the z neighbours (i - M,
+// i + M) are the ones it loaded for the previous plane and prefetches for the next: each anchor
+// leaves HBM once; the in-plane neighbours' anchors (i +- 1: the same lines; i +- nx: the blocks
+// next to it, marched by the workgroups beside it on the same XCD) come from the caches. The two
+// global tables (<= 1024 pattern words, <= 128 values) sit in LDS. A lane takes each entry's column
+// from its code and sums value * x[column] left to right from +0.0 in storage order (SPEC S3), as
+// the other row kernels do. The next planes' records, anchors and y are loaded under this step's x
+// gathers; every gather is issued (a padded entry reloads the first entry's x), so the loads are
+// straight-line and the waits count exactly.
+constexpr int kPncStreams = 2;
+
 template <int OP>
 __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int nz, int zlen,
                                                   const int* __restrict__ anc, const uint2* __restrict__ rec,
@@ -1828,6 +1832,7 @@ __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int 
                                                   const double* __restrict__ vtab, int nval,
                                                   const double* __restrict__ x, const double* __restrict__ b,
                                                   double* __restrict__ y, double omega) {
+    constexpr int NS = kPncStreams;
     __shared__ uint32_t lp[kPncPatMax];
     __shared__ double lv[kPncValMax];
     const int nxb = M >> 8;                                    // 256-point blocks of a plane
@@ -1837,64 +1842,88 @@ __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int 
     if (u >= units) return;  // the whole workgroup, before the barrier
     for (int t = threadIdx.x; t < npat; t += 256) lp[t] = ptab[t];
     for (int t = threadIdx.x; t < nval; t += 256) lv[t] = vtab[t];
-    const int z0 = (u / nxb) * zlen, z1 = min(nz, z0 + zlen);
+    const int zc0 = (u / nxb) * zlen, zc1 = min(nz, zc0 + zlen);
+    const int part = (zc1 - zc0 + NS - 1) / NS;  // planes per stream
     const int ixy = ((u % nxb) << 8) + (int)threadIdx.x;
-    PncRow cur;
-    pnc_load<OP>(cur, z0 * M + ixy, nrows, nx, anc, rec, x, b, y);
-    int am = anc[z0 > 0 ? (z0 - 1) * M + ixy : ixy];          // anchors of planes z - 1 and z + 1
-    int ap = anc[z0 + 1 < nz ? (z0 + 1) * M + ixy : ixy];
-    __syncthreads();  // (the tables; the first plane's loads already in flight)
-    for (int z = z0; z < z1; ++z) {
-        const int i = z * M + ixy;
-        const uint32_t pw = lp[cur.rec.x & 1023u];
-        const int L = (int)(pw & 7u);
-        int col[kPncMaxLen];
-        double xv[kPncMaxLen];
+    int zs[NS], ze[NS], zl[NS];
 #pragma unroll
-        for (int k = 0; k < kPncMaxLen; ++k) {
-            const uint32_t c = (pw >> (3 + 3 * k)) & 7u;
-            // codes 0 self, 1 i-1, 2 i+1, 3 i-nx, 4 i+nx, 5 i-M, 6 i+M: a select chain, no branches
-            const int c01 = c & 1u ? cur.an[1] : cur.an[0];
-            const int c23 = c & 1u ? cur.an[3] : cur.an[2];
-            const int c45 = c & 1u ? am : cur.an[4];
-            const int c03 = c & 2u ? c23 : c01;
-            const int c47 = c & 2u ? ap : c45;
-            col[k] = c & 4u ? c47 : c03;
-            xv[k] = x[k < L ? col[k] : col[0]];
-        }
-        // the next plane (the last one reloads its own plane), and the anchors two planes on
-        const int zn = z + 1 < z1 ? z + 1 : z;
-        PncRow nxt;
-        pnc_load<OP>(nxt, zn * M + ixy, nrows, nx, anc, rec, x, b, y);
-        const int ap2 = anc[zn + 1 < nz ? (zn + 1) * M + ixy : zn * M + ixy];
-        const uint64_t rr = ((uint64_t)cur.rec.y << 32) | cur.rec.x;
-        double s = 0.0, dg = 0.0;
+    for (int q = 0; q < NS; ++q) {
+        zs[q] = zc0 + q * part;
+        ze[q] = min(zc1, zs[q] + part);
+        zl[q] = ze[q] > zs[q] ? ze[q] - 1 : zc1 - 1;  // a stream's last plane (an empty stream re-walks the chunk's)
+    }
+    PncRow cur[NS];
+    int am[NS], ap[NS];
 #pragma unroll
-        for (int k = 0; k < kPncMaxLen; ++k) {
-            const bool ok = k < L;
-            const double v = lv[(uint32_t)(rr >> (10 + 7 * k)) & 127u];
-            const double p = v * xv[k];
-            const double t = s + p;
-            s = ok ? t : s;
-            if constexpr (OP == OP_JACOBI) dg = ok && col[k] == i ? v : dg;
+    for (int q = 0; q < NS; ++q) {
+        const int z = min(zs[q], zl[q]);
+        pnc_load<OP>(cur[q], z * M + ixy, nrows, nx, anc, rec, x, b, y);
+        am[q] = anc[z > 0 ? (z - 1) * M + ixy : ixy];          // anchors of planes z - 1 and z + 1
+        ap[q] = anc[z + 1 < nz ? (z + 1) * M + ixy : ixy];
+    }
+    __syncthreads();  // (the tables; the first planes' loads already in flight)
+    for (int j = 0; j < part; ++j) {
+        int zq[NS], L[NS], col[NS][kPncMaxLen];
+        double xv[NS][kPncMaxLen];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            zq[q] = min(zs[q] + j, zl[q]);
+            const uint32_t pw = lp[cur[q].rec.x & 1023u];
+            L[q] = (int)(pw & 7u);
+#pragma unroll
+            for (int k = 0; k < kPncMaxLen; ++k) {
+                const uint32_t c = (pw >> (3 + 3 * k)) & 7u;
+                // codes 0 self, 1 i-1, 2 i+1, 3 i-nx, 4 i+nx, 5 i-M, 6 i+M: a select chain, no branches
+                const int c01 = c & 1u ? cur[q].an[1] : cur[q].an[0];
+                const int c23 = c & 1u ? cur[q].an[3] : cur[q].an[2];
+                const int c45 = c & 1u ? am[q] : cur[q].an[4];
+                const int c03 = c & 2u ? c23 : c01;
+                const int c47 = c & 2u ? ap[q] : c45;
+                col[q][k] = c & 4u ? c47 : c03;
+                xv[q][k] = x[k < L[q] ? col[q][k] : col[q][0]];
+            }
         }
-        double out;
-        if constexpr (OP == OP_SPMV) {
-            out = s;
-        } else if constexpr (OP == OP_RESID) {
-            out = cur.p0 - s;
-        } else if constexpr (OP == OP_JACOBI) {
-            const double uu = cur.p0 - s;
-            const double v = omega * uu;
-            const double w = v / dg;
-            out = cur.p1 + w;
-        } else {
-            out = cur.p0 + s;
+        // the next planes (a stream's last plane reloads itself), and the anchors two planes on
+        PncRow nxt[NS];
+        int ap2[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int zn = min(zq[q] + 1, zl[q]);
+            pnc_load<OP>(nxt[q], zn * M + ixy, nrows, nx, anc, rec, x, b, y);
+            ap2[q] = anc[zn + 1 < nz ? (zn + 1) * M + ixy : zn * M + ixy];
         }
-        y[i] = out;
-        am = cur.an[0];
-        cur = nxt;
-        ap = ap2;
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int i = zq[q] * M + ixy;
+            const uint64_t rr = ((uint64_t)cur[q].rec.y << 32) | cur[q].rec.x;
+            double s = 0.0, dg = 0.0;
+#pragma unroll
+            for (int k = 0; k < kPncMaxLen; ++k) {
+                const bool ok = k < L[q];
+                const double v = lv[(uint32_t)(rr >> (10 + 7 * k)) & 127u];
+                const double p = v * xv[q][k];
+                const double t = s + p;
+                s = ok ? t : s;
+                if constexpr (OP == OP_JACOBI) dg = ok && col[q][k] == i ? v : dg;
+            }
+            double out;
+            if constexpr (OP == OP_SPMV) {
+                out = s;
+            } else if constexpr (OP == OP_RESID) {
+                out = cur[q].p0 - s;
+            } else if constexpr (OP == OP_JACOBI) {
+                const double uu = cur[q].p0 - s;
+                const double v = omega * uu;
+                const double w = v / dg;
+                out = cur[q].p1 + w;
+            } else {
+                out = cur[q].p0 + s;
+            }
+            if (zs[q] + j < ze[q]) y[i] = out;
+            am[q] = cur[q].an[0];
+            cur[q] = nxt[q];
+            ap[q] = ap2[q];
+        }
     }
 }
 
@@ -2253,6 +2282,37 @@ void launch_sym(const pamg_mat& A, const double* x, const double* b, double* y, 
     }
 }
 
+// planes per unit of k_rows_pnc: the chunking whose units fill the chip in the fewest equal rounds —
+// makespan ~ ceil(units / resident workgroups) x (planes per unit) — the resident count from the
+// kernel's occupancy (queried once), so no round runs a short tail of workgroups
+template <int OP>
+int pnc_zlen(const PncSet& P) {
+    static int resident = 0;
+    if (resident == 0) {
+        int per_cu = 0, dev = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rows_pnc<OP>, 256, 0) != hipSuccess || per_cu < 1)
+            per_cu = 4;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+        resident = per_cu * cus;
+    }
+    const int64_t nxb = (int64_t)P.nx * P.ny / 256;
+    int best = P.nz;
+    int64_t best_t = INT64_MAX;
+    for (int zch = 1; zch <= P.nz; ++zch) {
+        const int zlen = (P.nz + zch - 1) / zch;
+        if (zch > 1 && (P.nz + zlen - 1) / zlen != zch) continue;  // (the same chunking as a smaller zch)
+        const int64_t rounds = (nxb * zch + resident - 1) / resident;
+        const int64_t t = rounds * ((zlen + kPncStreams - 1) / kPncStreams + 2);  // streams per unit + a prologue
+        if (t < best_t) {
+            best_t = t;
+            best = zlen;
+        }
+    }
+    return best;
+}
+
 template <int OP>
 void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
                     double* y, double omega, hipStream_t s) {
@@ -2270,8 +2330,10 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
     }
     if (ts.pnc) {
         const PncSet& P = A.pnc;
-        k_rows_pnc<OP><<<P.grid, 256, 0, s>>>((int)A.nrows, P.nx, P.nx * P.ny, P.nz, P.zlen, P.d_anc, P.d_rec, P.d_ptab,
-                                              P.npat, P.d_vtab, P.nval, x, b, y, omega);
+        const int zlen = pnc_zlen<OP>(P);
+        const int nxb = P.nx * P.ny / 256, units = nxb * ((P.nz + zlen - 1) / zlen);
+        k_rows_pnc<OP><<<(units + 7) / 8 * 8, 256, 0, s>>>((int)A.nrows, P.nx, P.nx * P.ny, P.nz, zlen, P.d_anc, P.d_rec,
+                                                           P.d_ptab, P.npat, P.d_vtab, P.nval, x, b, y, omega);
     }
     if (ts.n_short > 0) {
         if (ts.tile_nnz == 1024) launch_tile<OP, 1024>(A, ts, x, b, y, omega, s);

@@ -213,8 +213,7 @@ struct PncSet {
     uint32_t* d_ptab = nullptr;
     double* d_vtab = nullptr;
     int npat = 0, nval = 0;
-    int zlen = 0;               // planes a workgroup of k_rows_pnc marches (one 256-point block of a plane each)
-    int grid = 0;               // workgroups of k_rows_pnc (a multiple of 8)
+    int grid = 0;               // workgroups of k_rows_pnc at upload (the launcher re-derives its chunking)
 };
 
 struct SymDia {

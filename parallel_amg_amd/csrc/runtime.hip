@@ -1530,13 +1530,8 @@ int build_pnc(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
     P.nz = (int)nz;
     P.npat = (int)pats.size();
     P.nval = (int)vals.size();
-    // about 8 workgroups per CU, each marching one 256-point block of a plane along z over zlen planes
-    // (kernels.hip k_rows_pnc), the grid a multiple of 8
-    const int64_t nxb = M / 256, want = (int64_t)device_cus() * 8;
-    const int64_t zch = std::max<int64_t>(1, std::min<int64_t>(nz, (want + nxb - 1) / nxb));
-    P.zlen = (int)((nz + zch - 1) / zch);
-    const int64_t units = nxb * ((nz + P.zlen - 1) / P.zlen);
-    P.grid = (int)((units + 7) / 8 * 8);
+    // (reported by pamg_mat_layout: the launcher picks the chunking, kernels.hip pnc_zlen)
+    P.grid = (int)((M / 256 + 7) / 8 * 8);
     CHECK(dalloc(&P.d_anc, n + kVecPad));
     CHECK(dalloc(&P.d_rec, n + kVecPad));
     CHECK(dalloc(&P.d_ptab, (int64_t)pats.size()));
