@@ -2869,9 +2869,9 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     tr.mark("sym dia");
     // square operators (offsets from the row) and restrictions (fewer rows than columns; offsets from
     // each row's first column)
-    // (several parts: the interior rows, when they are most of the operator)
+    // (several parts: the interior rows, when they are >= 3/4 of the operator — a 512^3 z-slab part's level 1)
     if (pamg::options().ell && !A->interior.sym && n_own_cols >= nrows && nrows > 0 &&
-        (int64_t)inner.size() * 10 >= (int64_t)nrows * 9 && nrows >= pamg::options().ell_min_rows &&
+        (int64_t)inner.size() * 4 >= (int64_t)nrows * 3 && nrows >= pamg::options().ell_min_rows &&
         (n_own_cols == nrows || pamg::options().ell_restrict)) {
         CHECK(build_ell(A.get(), rp, ci, val, n_own_cols != nrows, inner));
         if (A->interior.ell) inner.clear();  // the rows run in k_rows_ell, not in tiles

@@ -113,7 +113,7 @@ def test_local_world_vcycle_bit_exact(built, nparts, kind, n, max_coarse, agglom
             assert np.array_equal(bits(gv), bits(got_x[gid]))
 
 
-# (a part takes ELL where >= 90 % of its rows are interior: 60 planes in 3 slabs leave the middle
+# (a part takes ELL where >= 75 % of its rows are interior: 60 planes in 3 slabs leave the middle
 # slab 18 of its 20 planes)
 @pytest.mark.parametrize("nparts,kind,n", [(3, "poisson2d", 60), (3, "poisson3d", 60), (2, "aniso3d", 20)])
 def test_local_world_ell_interior_rows_bit_exact(built, nparts, kind, n):
