@@ -2879,11 +2879,10 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     }
     // a prolongation over a 7-point grid uploaded earlier on this context: neighbour-coded rows
     if (pamg::options().pnc && n_own_cols < nrows && ncols == n_own_cols && (int64_t)inner.size() == nrows) {
-        for (const auto& g : ctx->grids)
-            if (g[0] == nrows) {
-                CHECK(build_pnc(A.get(), rp, ci, val, g));
-                break;
-            }
+        // (every registered grid of this row count, the latest first: grids of one size but other
+        // shapes may be registered too, and the neighbour check decides)
+        for (auto g = ctx->grids.rbegin(); g != ctx->grids.rend() && !A->interior.pnc; ++g)
+            if ((*g)[0] == nrows) CHECK(build_pnc(A.get(), rp, ci, val, *g));
         if (A->interior.pnc) inner.clear();  // the rows run in k_rows_pnc, not in tiles
         tr.mark("pnc");
     }
