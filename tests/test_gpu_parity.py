@@ -1635,3 +1635,18 @@ def test_prolongation_neighbour_coded_declines(ctx):
         D = _layout_ops_match_oracle(ctx, M, np.random.default_rng(5))
         assert not layout_of(D)["pnc"]
     del Ad
+
+
+def test_prolongation_neighbour_coded_same_size_grids(ctx):
+    """Two 7-point grids of the same row count and different shapes registered on the context (the
+    prolongation's own uploaded first, the other after): the upload tries each and finds its own."""
+    from parallel_amg_amd._lib import layout_of
+    A0, P = _grid_hierarchy_P0(64, 32, 12)          # 24576 rows
+    own = PSparseMatrix(ctx, A0)
+    decoy_M = O.generate("poisson3d", 128, 16, 12)  # 24576 rows too
+    decoy = PSparseMatrix(ctx, HCSR.from_arrays(decoy_M.rowptr, decoy_M.col.astype(np.int32), decoy_M.val,
+                                                decoy_M.nrows))
+    assert layout_of(own)["jr_fused"] and layout_of(decoy)["jr_fused"]
+    D = _layout_ops_match_oracle(ctx, P, np.random.default_rng(8))
+    assert layout_of(D)["pnc"], layout_of(D)
+    del own, decoy
