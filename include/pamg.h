@@ -288,7 +288,8 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
  * order's band; the second for operators with fewer rows than columns), "tile_major" (0 | 1 where measured faster | 2 every eligible set),
  * "sym_vd" (0 | 1: row-class dictionary of the symmetric layout), "ell" (0 | 1: sliced ELL for
  * large square operators with all own columns), "ell_restrict" (0 | 1: also restrictions, with
- * anchored offsets), "ell_min_rows" (rows from which ELL is taken), "pnc" (0 | 1: neighbour-coded
+ * anchored offsets), "ell_min_rows" (rows from which ELL is taken), "ell_yblock" (0 | lines: the
+ * blocked group order of a restriction over a grid), "pnc" (0 | 1: neighbour-coded
  * prolongations over a grid uploaded earlier on the context). Read at launch:
  * "sym_zm" (0 | 1: z-marching single sweeps of the symmetric layout), "zm_chunks" (0 = auto |
  * z chunks per column of k_sym_zm), "tb_xfast" (0 | 1: x-fastest tile order of the chain),

@@ -1699,7 +1699,8 @@ __global__ __launch_bounds__(kZmThreads) void k_sym_zm(int nrows, const uint8_t*
 // XCD-contiguous order: block b on XCD b % 8 takes the (b / 8)-th group of that XCD's eighth, so an
 // XCD's L2 holds the x window its consecutive rows reuse.
 template <int OP, bool ANC>
-__global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __restrict__ anc, const int2* __restrict__ smeta,
+__global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __restrict__ gorder,
+                                                        const int* __restrict__ anc, const int2* __restrict__ smeta,
                                                         const uint32_t* __restrict__ cw, const uint32_t* __restrict__ vw,
                                                         const uint8_t* __restrict__ len, const int4* __restrict__ gmeta,
                                                         const int* __restrict__ otab, const double* __restrict__ vtab,
@@ -1709,8 +1710,9 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __
     __shared__ int lo[256];
     __shared__ double lv[256];
     const int per = (ngroups + 7) / 8;
-    const int g = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (g >= ngroups) return;  // the whole workgroup, before the barrier
+    const int gi = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (gi >= ngroups) return;  // the whole workgroup, before the barrier
+    const int g = gorder ? gorder[gi] : gi;  // (a restriction's blocked order: EllSet::d_gorder)
     const int tid = threadIdx.x, lane = tid & 63;
     const int4 gm = gmeta[g];
     const int i = g * kEllGroup + tid;
@@ -2321,12 +2323,13 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
         const EllSet& E = A.ell;
         const int grid = (int)((E.ngroups + 7) / 8 * 8);
         if (E.d_anc)
-            k_rows_ell<OP, true><<<grid, kEllGroup, 0, s>>>((int)A.nrows, E.d_anc, E.d_smeta, E.d_ci, E.d_vi, E.d_len,
-                                                            E.d_gmeta, E.d_otab, E.d_vtab, (int)E.ngroups, x, b, y, omega);
+            k_rows_ell<OP, true><<<grid, kEllGroup, 0, s>>>((int)A.nrows, E.d_gorder, E.d_anc, E.d_smeta, E.d_ci, E.d_vi,
+                                                              E.d_len, E.d_gmeta, E.d_otab, E.d_vtab, (int)E.ngroups, x, b,
+                                                              y, omega);
         else
-            k_rows_ell<OP, false><<<grid, kEllGroup, 0, s>>>((int)A.nrows, nullptr, E.d_smeta, E.d_ci, E.d_vi, E.d_len,
-                                                             E.d_gmeta, E.d_otab, E.d_vtab, (int)E.ngroups, x, b, y,
-                                                             omega);
+            k_rows_ell<OP, false><<<grid, kEllGroup, 0, s>>>((int)A.nrows, E.d_gorder, nullptr, E.d_smeta, E.d_ci, E.d_vi,
+                                                               E.d_len, E.d_gmeta, E.d_otab, E.d_vtab, (int)E.ngroups, x, b,
+                                                               y, omega);
     }
     if (ts.pnc) {
         const PncSet& P = A.pnc;

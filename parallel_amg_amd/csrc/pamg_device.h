@@ -143,6 +143,9 @@ struct Options {
                                //    is interior, where the tables fit (EllSet; the level-1 operator)
     int ell_min_rows = 65536;  // ... with at least this many rows
     int ell_restrict = 1;      // 1: also restrictions (fewer rows than columns), offsets from each row's first column
+    int ell_yblock = 16;       // restrictions over a grid: groups processed in (y-block of this many lines, z, y)
+                               //    order within each XCD's eighth (0: row order; 512^3 R0 0.81 -> 0.745 ms for any
+                               //    block of 2..64 lines, profiles/r05_r/); read at upload
     int pnc = 1;               // 1: neighbour-coded prolongations over a grid registered on the context (PncSet)
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
@@ -192,6 +195,10 @@ struct EllSet {
     int* d_otab = nullptr;       // the groups' offset tables, concatenated
     double* d_vtab = nullptr;    // the groups' value tables, concatenated
     int* d_anc = nullptr;        // anchored (rectangular operators): per row the column its offsets start from
+    // a restriction over a registered grid (its columns are the grid's points): the groups in a
+    // processing order whose in-flight window is a compact (y, z) block of the grid instead of whole
+    // planes (Options::ell_yblock; kernels.hip k_rows_ell), null otherwise
+    int* d_gorder = nullptr;
     int64_t words = 0, otab_n = 0, vtab_n = 0;
 };
 

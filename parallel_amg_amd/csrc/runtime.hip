@@ -1416,6 +1416,33 @@ int build_ell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
         });
         CHECK(dalloc(&E.d_anc, n + kVecPad));
         CHECK(h2d(ctx, E.d_anc, anc.data(), sizeof(int) * anc.size()));
+        // a restriction over a registered grid (Options::ell_yblock > 0): the groups of each XCD's
+        // eighth (kernels.hip k_rows_ell) in (y / yblock, z, y) order of their first row's anchor, so
+        // the window of groups in flight is a compact (y, z) block of the grid, not whole planes
+        const int yb = pamg::options().ell_yblock;
+        for (const auto& gr : ctx->grids)
+            if (yb > 0 && gr[0] == A->ncols) {
+                const int64_t gnx = gr[1], gny = gr[2], gM = gr[1] * gr[2];
+                std::vector<int64_t> key(ng);
+                par_for(ng, [&](int64_t a, int64_t b) {
+                    for (int64_t g = a; g < b; ++g) {
+                        const int64_t c = anc[g * kEllGroup];
+                        const int64_t y = (c / gnx) % gny, z = c / gM;
+                        key[g] = ((y / yb) << 40) | (z << 20) | y;
+                    }
+                });
+                const int64_t per = (ng + 7) / 8;
+                std::vector<int> order(ng);
+                for (int64_t g = 0; g < ng; ++g) order[g] = (int)g;
+                for (int64_t e = 0; e < 8; ++e) {
+                    const int64_t lo = std::min(ng, e * per), hi = std::min(ng, (e + 1) * per);
+                    std::stable_sort(order.begin() + lo, order.begin() + hi,
+                                     [&](int p, int q) { return key[p] < key[q]; });
+                }
+                CHECK(dalloc(&E.d_gorder, ng));
+                CHECK(h2d(ctx, E.d_gorder, order.data(), sizeof(int) * ng));
+                break;
+            }
     }
     A->interior.ell = true;
     return PAMG_OK;
@@ -1553,6 +1580,7 @@ void free_pnc(pamg::PncSet& P) {
 }
 
 void free_ell(pamg::EllSet& E) {
+    dfree(E.d_gorder);
     dfree(E.d_smeta);
     dfree(E.d_ci);
     dfree(E.d_vi);
@@ -3782,6 +3810,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "ell" && (value == 0 || value == 1)) o.ell = (int)value;
     else if (k == "ell_restrict" && (value == 0 || value == 1)) o.ell_restrict = (int)value;
     else if (k == "pnc" && (value == 0 || value == 1)) o.pnc = (int)value;
+    else if (k == "ell_yblock" && value >= 0 && value <= 65536) o.ell_yblock = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
     else if (k == "chain_store_x" && (value == 0 || value == 1)) o.chain_store_x = (int)value;
@@ -3819,6 +3848,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "ell") *value = o.ell;
     else if (k == "ell_restrict") *value = o.ell_restrict;
     else if (k == "pnc") *value = o.pnc;
+    else if (k == "ell_yblock") *value = o.ell_yblock;
     else if (k == "ell_min_rows") *value = o.ell_min_rows;
     else if (k == "zm_chunks") *value = o.zm_chunks;
     else if (k == "chain_store_x") *value = o.chain_store_x;
