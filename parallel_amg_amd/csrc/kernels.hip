@@ -1815,7 +1815,7 @@ __device__ __forceinline__ void pnc_load(PncRow& r, int i, int nrows, int nx, co
 
 // k_rows_pnc: the neighbour-coded prolongation (pamg::PncSet; round 5, the 512^3 P0). One row per
 // lane; a workgroup owns a 256-point block of a plane (M % 256 == 0) and marches it along z over a
-// chunk of planes — as kPncStreams interleaved streams (the chunk cut in as many parts, a plane of each per
+// chunk of planes — as NS interleaved streams (the chunk cut in as many parts, a plane of each per
 // step: independent gather sets in flight per lane) — so the anchors of the z neighbours (i - M,
 // i + M) are the ones it loaded for the previous plane and prefetches for the next: each anchor
 // leaves HBM once; the in-plane neighbours' anchors (i +- 1: the same lines; i +- nx: the blocks
@@ -1825,16 +1825,13 @@ __device__ __forceinline__ void pnc_load(PncRow& r, int i, int nrows, int nx, co
 // the other row kernels do. The next planes' records, anchors and y are loaded under this step's x
 // gathers; every gather is issued (a padded entry reloads the first entry's x), so the loads are
 // straight-line and the waits count exactly.
-constexpr int kPncStreams = 2;
-
-template <int OP>
+template <int OP, int NS>
 __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int nz, int zlen,
                                                   const int* __restrict__ anc, const uint2* __restrict__ rec,
                                                   const uint32_t* __restrict__ ptab, int npat,
                                                   const double* __restrict__ vtab, int nval,
                                                   const double* __restrict__ x, const double* __restrict__ b,
                                                   double* __restrict__ y, double omega) {
-    constexpr int NS = kPncStreams;
     __shared__ uint32_t lp[kPncPatMax];
     __shared__ double lv[kPncValMax];
     const int nxb = M >> 8;                                    // 256-point blocks of a plane
@@ -2287,12 +2284,12 @@ void launch_sym(const pamg_mat& A, const double* x, const double* b, double* y, 
 // planes per unit of k_rows_pnc: the chunking whose units fill the chip in the fewest equal rounds —
 // makespan ~ ceil(units / resident workgroups) x (planes per unit) — the resident count from the
 // kernel's occupancy (queried once), so no round runs a short tail of workgroups
-template <int OP>
+template <int OP, int NS>
 int pnc_zlen(const PncSet& P) {
     static int resident = 0;
     if (resident == 0) {
         int per_cu = 0, dev = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rows_pnc<OP>, 256, 0) != hipSuccess || per_cu < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rows_pnc<OP, NS>, 256, 0) != hipSuccess || per_cu < 1)
             per_cu = 4;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
@@ -2306,13 +2303,22 @@ int pnc_zlen(const PncSet& P) {
         const int zlen = (P.nz + zch - 1) / zch;
         if (zch > 1 && (P.nz + zlen - 1) / zlen != zch) continue;  // (the same chunking as a smaller zch)
         const int64_t rounds = (nxb * zch + resident - 1) / resident;
-        const int64_t t = rounds * ((zlen + kPncStreams - 1) / kPncStreams + 2);  // streams per unit + a prologue
+        const int64_t t = rounds * ((zlen + NS - 1) / NS + 2);  // streams per unit + a prologue
         if (t < best_t) {
             best_t = t;
             best = zlen;
         }
     }
     return best;
+}
+
+template <int OP, int NS>
+void launch_pnc(const pamg_mat& A, const double* x, const double* b, double* y, double omega, hipStream_t s) {
+    const PncSet& P = A.pnc;
+    const int zlen = pnc_zlen<OP, NS>(P);
+    const int nxb = P.nx * P.ny / 256, units = nxb * ((P.nz + zlen - 1) / zlen);
+    k_rows_pnc<OP, NS><<<(units + 7) / 8 * 8, 256, 0, s>>>((int)A.nrows, P.nx, P.nx * P.ny, P.nz, zlen, P.d_anc, P.d_rec,
+                                                           P.d_ptab, P.npat, P.d_vtab, P.nval, x, b, y, omega);
 }
 
 template <int OP>
@@ -2331,12 +2337,12 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
                                                                E.d_len, E.d_gmeta, E.d_otab, E.d_vtab, (int)E.ngroups, x, b,
                                                                y, omega);
     }
-    if (ts.pnc) {
-        const PncSet& P = A.pnc;
-        const int zlen = pnc_zlen<OP>(P);
-        const int nxb = P.nx * P.ny / 256, units = nxb * ((P.nz + zlen - 1) / zlen);
-        k_rows_pnc<OP><<<(units + 7) / 8 * 8, 256, 0, s>>>((int)A.nrows, P.nx, P.nx * P.ny, P.nz, zlen, P.d_anc, P.d_rec,
-                                                           P.d_ptab, P.npat, P.d_vtab, P.nval, x, b, y, omega);
+    if (ts.pnc) {  // z-streams per workgroup (Options::pnc_streams)
+        switch (options().pnc_streams) {
+            case 1: launch_pnc<OP, 1>(A, x, b, y, omega, s); break;
+            case 3: launch_pnc<OP, 3>(A, x, b, y, omega, s); break;
+            default: launch_pnc<OP, 2>(A, x, b, y, omega, s); break;
+        }
     }
     if (ts.n_short > 0) {
         if (ts.tile_nnz == 1024) launch_tile<OP, 1024>(A, ts, x, b, y, omega, s);

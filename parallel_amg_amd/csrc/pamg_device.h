@@ -147,6 +147,7 @@ struct Options {
                                //    order within each XCD's eighth (0: row order; 512^3 R0 0.81 -> 0.745 ms for any
                                //    block of 2..64 lines, profiles/r05_r/); read at upload
     int pnc = 1;               // 1: neighbour-coded prolongations over a grid registered on the context (PncSet)
+    int pnc_streams = 2;       // z-streams per k_rows_pnc workgroup (1 | 2 | 3); read at launch
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
 };
