@@ -1253,7 +1253,7 @@ int build_sym_dia(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double*
             g.zhi = nz;
             sd.tb_ok = whole;
             sd.tb_part = part;
-            if (whole) {  // (a later prolongation over this grid may take the neighbour-coded layout)
+            if (whole || part) {  // (a later prolongation / restriction over this grid: pnc, ELL group order)
                 const std::array<int64_t, 4> gk{n, nx, ny, nz};
                 auto& gs = A->ctx->grids;
                 if (std::find(gs.begin(), gs.end(), gk) == gs.end()) gs.push_back(gk);
@@ -1420,8 +1420,9 @@ int build_ell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
         // eighth (kernels.hip k_rows_ell) in (y / yblock, z, y) order of their first row's anchor, so
         // the window of groups in flight is a compact (y, z) block of the grid, not whole planes
         const int yb = pamg::options().ell_yblock;
+        const int64_t own_cols = A->plan ? A->plan->n_own : A->ncols;
         for (const auto& gr : ctx->grids)
-            if (yb > 0 && gr[0] == A->ncols) {
+            if (yb > 0 && gr[0] == own_cols) {
                 const int64_t gnx = gr[1], gny = gr[2], gM = gr[1] * gr[2];
                 std::vector<int64_t> key(ng);
                 par_for(ng, [&](int64_t a, int64_t b) {
