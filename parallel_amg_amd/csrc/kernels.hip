@@ -2286,6 +2286,7 @@ void launch_sym(const pamg_mat& A, const double* x, const double* b, double* y, 
 // kernel's occupancy (queried once), so no round runs a short tail of workgroups
 template <int OP, int NS>
 int pnc_zlen(const PncSet& P) {
+    if (options().pnc_zlen > 0) return std::min(options().pnc_zlen, P.nz);  // (a fixed chunk, for A/B)
     static int resident = 0;
     if (resident == 0) {
         int per_cu = 0, dev = 0, cus = 0;

@@ -3816,6 +3816,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "ell_restrict" && (value == 0 || value == 1)) o.ell_restrict = (int)value;
     else if (k == "pnc" && (value == 0 || value == 1)) o.pnc = (int)value;
     else if (k == "pnc_streams" && value >= 1 && value <= 3) o.pnc_streams = (int)value;
+    else if (k == "pnc_zlen" && value >= 0 && value <= 65536) o.pnc_zlen = (int)value;
     else if (k == "ell_yblock" && value >= 0 && value <= 65536) o.ell_yblock = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
@@ -3855,6 +3856,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "ell_restrict") *value = o.ell_restrict;
     else if (k == "pnc") *value = o.pnc;
     else if (k == "pnc_streams") *value = o.pnc_streams;
+    else if (k == "pnc_zlen") *value = o.pnc_zlen;
     else if (k == "ell_yblock") *value = o.ell_yblock;
     else if (k == "ell_min_rows") *value = o.ell_min_rows;
     else if (k == "zm_chunks") *value = o.zm_chunks;
