@@ -8,6 +8,7 @@
 #include <atomic>
 #include <cstdint>
 #include <array>
+#include <mutex>
 #include <vector>
 
 #include "pamg_common.h"
@@ -287,6 +288,7 @@ struct pamg_ctx {
     // layout (SymDia::tb_ok): (rows, nx, ny, nz) — a later prolongation with as many rows may take
     // the neighbour-coded layout over one of them (pamg::PncSet)
     std::vector<std::array<int64_t, 4>> grids;
+    std::mutex grids_mu;  // (uploads on one context from several host threads)
 };
 
 void ctx_ref(pamg_ctx* ctx);

@@ -983,6 +983,12 @@ int build_tile_major(pamg_mat* A, int64_t n_own_cols, const PtrVec& rp,
 // interior row's entries in strictly ascending offset order (so the kernel's ascending sum is
 // the storage-order sum of SPEC §S3), and every lower entry bit-identical to its mirror
 // a(i-o, i) in row i-o. Otherwise nothing is built and the rows keep their tiles.
+// a copy of the context's registered grids (pamg_ctx::grids)
+std::vector<std::array<int64_t, 4>> grids_of(pamg_ctx* ctx) {
+    std::lock_guard<std::mutex> lk(ctx->grids_mu);
+    return ctx->grids;
+}
+
 int build_sym_dia(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val,
                   const std::vector<int>& inner, const std::function<int64_t()>& get_band) {
     using pamg::kSymMaxU;
@@ -1259,6 +1265,7 @@ int build_sym_dia(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double*
             sd.tb_part = part;
             if (whole || part) {  // (a later prolongation / restriction over this grid: pnc, ELL group order)
                 const std::array<int64_t, 4> gk{n, nx, ny, nz};
+                std::lock_guard<std::mutex> lk(A->ctx->grids_mu);
                 auto& gs = A->ctx->grids;
                 if (std::find(gs.begin(), gs.end(), gk) == gs.end()) gs.push_back(gk);
             }
@@ -1425,7 +1432,7 @@ int build_ell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
         // the window of groups in flight is a compact (y, z) block of the grid, not whole planes
         const int yb = pamg::options().ell_yblock;
         const int64_t own_cols = A->plan ? A->plan->n_own : A->ncols;
-        for (const auto& gr : ctx->grids)
+        for (const auto& gr : grids_of(ctx))
             if (yb > 0 && gr[0] == own_cols) {
                 const int64_t gnx = gr[1], gny = gr[2], gM = gr[1] * gr[2];
                 std::vector<int64_t> key(ng);
@@ -2914,7 +2921,8 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     if (pamg::options().pnc && n_own_cols < nrows && ncols == n_own_cols && (int64_t)inner.size() == nrows) {
         // (every registered grid of this row count, the latest first: grids of one size but other
         // shapes may be registered too, and the neighbour check decides)
-        for (auto g = ctx->grids.rbegin(); g != ctx->grids.rend() && !A->interior.pnc; ++g)
+        const auto grids = grids_of(ctx);
+        for (auto g = grids.rbegin(); g != grids.rend() && !A->interior.pnc; ++g)
             if ((*g)[0] == nrows) CHECK(build_pnc(A.get(), rp, ci, val, *g));
         if (A->interior.pnc) inner.clear();  // the rows run in k_rows_pnc, not in tiles
         tr.mark("pnc");
