@@ -175,6 +175,7 @@ struct NoInitAlloc : std::allocator<T> {
 using IdxVec = std::vector<int, NoInitAlloc<int>>;
 using PtrVec = std::vector<int64_t, NoInitAlloc<int64_t>>;
 
+
 struct UploadTrace {
     bool on = std::getenv("PAMG_TRACE_UPLOAD") != nullptr;
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
@@ -2840,10 +2841,13 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     // classify rows: interior (own columns only) or boundary (>= 1 ghost column), and find
     // the diagonal (threads over row ranges)
     std::vector<int> inner, bnd;
-    std::vector<double> diag(nrows, 0.0);
+    std::vector<double> diag(n_own_cols == nrows ? nrows : 0, 0.0);  // (square operators only)
     std::vector<char> ghost_row(nrows, 0);
     std::atomic<bool> has_all_diag{n_own_cols == nrows};
-    par_for(nrows, [&](int64_t a, int64_t b) {
+    // (no ghost columns and no diagonal to find — a one-part prolongation or restriction: nothing
+    // to scan)
+    const bool scan = n_own_cols == nrows || ncols != n_own_cols;
+    if (scan) par_for(nrows, [&](int64_t a, int64_t b) {
         bool all = true;
         for (int64_t i = a; i < b; ++i) {
             bool g = false, d = false;

@@ -34,8 +34,18 @@ def main():
     del A
     t1 = time.time()
     print(f"# setup {t1 - t0:.1f}s", file=sys.stderr, flush=True)
-    S = AMGSolver(ctx, H)
-    ctx.sync()
+    if os.environ.get("UPLOAD_PROFILE"):
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        S = AMGSolver(ctx, H)
+        ctx.sync()
+        pr.disable()
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(25)
+    else:
+        S = AMGSolver(ctx, H)
+        ctx.sync()
     t2 = time.time()
     print(json.dumps({"n": a.n, "setup_s": round(t1 - t0, 2), "upload_s": round(t2 - t1, 2), "levels": S.L}))
     del S
