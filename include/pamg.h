@@ -293,8 +293,7 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
  * prolongations over a grid uploaded earlier on the context). Read at launch:
  * "sym_zm" (0 | 1: z-marching single sweeps of the symmetric layout), "zm_chunks" (0 = auto |
  * z chunks per column of k_sym_zm), "tb_xfast" (0 | 1: x-fastest tile order of the chain),
- * "symd_chunks" (1 | 2 | 4), "chain_store_x" (0 | 1), "pnc_streams" (1 | 2 | 3: z-streams per
- * k_rows_pnc workgroup), "pnc_zlen" (planes per k_rows_pnc unit; 0 = from its occupancy). Applied at every exchange:
+ * "symd_chunks" (1 | 2 | 4), "chain_store_x" (0 | 1). Applied at every exchange:
  * "poison_ghosts" (0 | 1, debug: NaN-fill the ghost slots before each exchange). */
 int pamg_set_option(const char* key, int64_t value);
 int pamg_get_option(const char* key, int64_t* value);

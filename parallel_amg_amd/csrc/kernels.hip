@@ -2281,45 +2281,19 @@ void launch_sym(const pamg_mat& A, const double* x, const double* b, double* y, 
     }
 }
 
-// planes per unit of k_rows_pnc: the chunking whose units fill the chip in the fewest equal rounds —
-// makespan ~ ceil(units / resident workgroups) x (planes per unit) — the resident count from the
-// kernel's occupancy (queried once), so no round runs a short tail of workgroups
-template <int OP, int NS>
-int pnc_zlen(const PncSet& P) {
-    if (options().pnc_zlen > 0) return std::min(options().pnc_zlen, P.nz);  // (a fixed chunk, for A/B)
-    static int resident = 0;
-    if (resident == 0) {
-        int per_cu = 0, dev = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rows_pnc<OP, NS>, 256, 0) != hipSuccess || per_cu < 1)
-            per_cu = 4;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-            cus = 256;
-        resident = per_cu * cus;
-    }
-    const int64_t nxb = (int64_t)P.nx * P.ny / 256;
-    int best = P.nz;
-    int64_t best_t = INT64_MAX;
-    for (int zch = 1; zch <= P.nz; ++zch) {
-        const int zlen = (P.nz + zch - 1) / zch;
-        if (zch > 1 && (P.nz + zlen - 1) / zlen != zch) continue;  // (the same chunking as a smaller zch)
-        const int64_t rounds = (nxb * zch + resident - 1) / resident;
-        const int64_t t = rounds * ((zlen + NS - 1) / NS + 2);  // streams per unit + a prologue
-        if (t < best_t) {
-            best_t = t;
-            best = zlen;
-        }
-    }
-    return best;
-}
+// k_rows_pnc's units: one 256-point plane block over kPncZlen planes, two z-streams per workgroup
+// (measured at 512^3, profiles/r05_ns/ and r05_zl/: one or three streams 1.33 / 1.16 ms, 8-, 16-plane
+// units and units sized to fill the chip in equal rounds 1.14 / 1.12 / 1.11 ms, against 1.09-1.10)
+constexpr int kPncZlen = 32, kPncStreams = 2;
 
-template <int OP, int NS>
+template <int OP>
 void launch_pnc(const pamg_mat& A, const double* x, const double* b, double* y, double omega, hipStream_t s) {
     const PncSet& P = A.pnc;
-    const int zlen = pnc_zlen<OP, NS>(P);
+    const int zlen = std::min(kPncZlen, P.nz);
     const int nxb = P.nx * P.ny / 256, units = nxb * ((P.nz + zlen - 1) / zlen);
-    k_rows_pnc<OP, NS><<<(units + 7) / 8 * 8, 256, 0, s>>>((int)A.nrows, P.nx, P.nx * P.ny, P.nz, zlen, P.d_anc, P.d_rec,
-                                                           P.d_ptab, P.npat, P.d_vtab, P.nval, x, b, y, omega);
+    k_rows_pnc<OP, kPncStreams><<<(units + 7) / 8 * 8, 256, 0, s>>>((int)A.nrows, P.nx, P.nx * P.ny, P.nz, zlen,
+                                                                    P.d_anc, P.d_rec, P.d_ptab, P.npat, P.d_vtab,
+                                                                    P.nval, x, b, y, omega);
 }
 
 template <int OP>
@@ -2338,13 +2312,7 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
                                                                E.d_len, E.d_gmeta, E.d_otab, E.d_vtab, (int)E.ngroups, x, b,
                                                                y, omega);
     }
-    if (ts.pnc) {  // z-streams per workgroup (Options::pnc_streams)
-        switch (options().pnc_streams) {
-            case 1: launch_pnc<OP, 1>(A, x, b, y, omega, s); break;
-            case 3: launch_pnc<OP, 3>(A, x, b, y, omega, s); break;
-            default: launch_pnc<OP, 2>(A, x, b, y, omega, s); break;
-        }
-    }
+    if (ts.pnc) launch_pnc<OP>(A, x, b, y, omega, s);
     if (ts.n_short > 0) {
         if (ts.tile_nnz == 1024) launch_tile<OP, 1024>(A, ts, x, b, y, omega, s);
         else if (ts.tile_nnz == 4096) launch_tile<OP, 4096>(A, ts, x, b, y, omega, s);

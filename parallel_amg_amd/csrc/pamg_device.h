@@ -148,10 +148,6 @@ struct Options {
                                //    order within each XCD's eighth (0: row order; 512^3 R0 0.81 -> 0.745 ms for any
                                //    block of 2..64 lines, profiles/r05_r/); read at upload
     int pnc = 1;               // 1: neighbour-coded prolongations over a grid registered on the context (PncSet)
-    int pnc_streams = 2;       // z-streams per k_rows_pnc workgroup (1 | 2 | 3); read at launch
-    int pnc_zlen = 32;         // planes per k_rows_pnc unit (0: equal rounds from the kernel's occupancy; 512^3 P0
-                               //    32: 1.09-1.10 ms, occupancy rule (74): 1.11-1.12, 16: 1.12, 8: 1.14 —
-                               //    profiles/r05_zl/); read at launch
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
 };
@@ -225,7 +221,7 @@ struct PncSet {
     uint32_t* d_ptab = nullptr;
     double* d_vtab = nullptr;
     int npat = 0, nval = 0;
-    int grid = 0;               // workgroups of k_rows_pnc at upload (the launcher re-derives its chunking)
+    int grid = 0;               // workgroups of k_rows_pnc
 };
 
 struct SymDia {

@@ -1570,8 +1570,12 @@ int build_pnc(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
     P.nz = (int)nz;
     P.npat = (int)pats.size();
     P.nval = (int)vals.size();
-    // (reported by pamg_mat_layout: the launcher picks the chunking, kernels.hip pnc_zlen)
-    P.grid = (int)((M / 256 + 7) / 8 * 8);
+    // k_rows_pnc's grid (pamg_mat_layout out[8]): one workgroup per 256-point plane block and 32-plane
+    // chunk (kernels.hip launch_pnc)
+    {
+        const int64_t zlen = std::min<int64_t>(32, nz);
+        P.grid = (int)((M / 256 * ((nz + zlen - 1) / zlen) + 7) / 8 * 8);
+    }
     CHECK(dalloc(&P.d_anc, n + kVecPad));
     CHECK(dalloc(&P.d_rec, n + kVecPad));
     CHECK(dalloc(&P.d_ptab, (int64_t)pats.size()));
@@ -3827,8 +3831,6 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "ell" && (value == 0 || value == 1)) o.ell = (int)value;
     else if (k == "ell_restrict" && (value == 0 || value == 1)) o.ell_restrict = (int)value;
     else if (k == "pnc" && (value == 0 || value == 1)) o.pnc = (int)value;
-    else if (k == "pnc_streams" && value >= 1 && value <= 3) o.pnc_streams = (int)value;
-    else if (k == "pnc_zlen" && value >= 0 && value <= 65536) o.pnc_zlen = (int)value;
     else if (k == "ell_yblock" && value >= 0 && value <= 65536) o.ell_yblock = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
@@ -3867,8 +3869,6 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "ell") *value = o.ell;
     else if (k == "ell_restrict") *value = o.ell_restrict;
     else if (k == "pnc") *value = o.pnc;
-    else if (k == "pnc_streams") *value = o.pnc_streams;
-    else if (k == "pnc_zlen") *value = o.pnc_zlen;
     else if (k == "ell_yblock") *value = o.ell_yblock;
     else if (k == "ell_min_rows") *value = o.ell_min_rows;
     else if (k == "zm_chunks") *value = o.zm_chunks;
