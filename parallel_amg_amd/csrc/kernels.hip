@@ -1867,7 +1867,8 @@ __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int 
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
             zq[q] = min(zs[q] + j, zl[q]);
-            const uint32_t pw = lp[cur[q].rec.x & 1023u];
+            const uint32_t pid = cur[q].rec.x & 1023u;
+            const uint32_t pw = pid < (uint32_t)npat ? lp[pid] : 0u;  // (kPncSkip: no entries, no store)
             L[q] = (int)(pw & 7u);
 #pragma unroll
             for (int k = 0; k < kPncMaxLen; ++k) {
@@ -1918,7 +1919,7 @@ __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int 
             } else {
                 out = cur[q].p0 + s;
             }
-            if (zs[q] + j < ze[q]) y[i] = out;
+            if (zs[q] + j < ze[q] && (cur[q].rec.x & 1023u) != (uint32_t)kPncSkip) y[i] = out;
             am[q] = cur[q].an[0];
             cur[q] = nxt[q];
             ap[q] = ap2[q];

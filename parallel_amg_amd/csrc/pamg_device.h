@@ -214,6 +214,7 @@ struct EllSet {
 // <= kPncValMax bit patterns). 12 B per row against 3.5 B per nonzero + 1 B per row in tiles. Rows
 // keep their storage order (SPEC S3 sums).
 constexpr int kPncPatMax = 1024, kPncValMax = 128, kPncMaxLen = 7;
+constexpr int kPncSkip = kPncPatMax - 1;  // pattern id of a row outside the set (several parts: a boundary row)
 struct PncSet {
     int nx = 0, ny = 0, nz = 0;
     int* d_anc = nullptr;       // nrows (+ pad)

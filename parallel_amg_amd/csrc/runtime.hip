@@ -1465,16 +1465,25 @@ int build_ell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
 // grid neighbours whose anchors they are. Declines (leaves the tile layouts to the caller) where a
 // row is longer than kPncMaxLen, a column is no neighbour's anchor, or a table would overflow.
 int build_pnc(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val,
-              const std::array<int64_t, 4>& grid) {
+              const std::array<int64_t, 4>& grid, const std::vector<int>& inner) {
     using pamg::kPncMaxLen;
+    using pamg::kPncSkip;
     const int64_t n = A->nrows;
+    // several parts: the interior rows only (the boundary rows — ghost columns — run in their tiles
+    // after the exchange; their records carry the skip pattern id)
+    std::vector<char> in_set;
+    if ((int64_t)inner.size() != n) {
+        in_set.assign(n, 0);
+        for (int i : inner) in_set[i] = 1;
+    }
+    auto member = [&](int64_t i) { return in_set.empty() || in_set[i]; };
     const int64_t nx = grid[1], ny = grid[2], nz = grid[3], M = nx * ny;
     if (n != nx * ny * nz || n <= 0 || M % 256 != 0) return PAMG_OK;  // (k_rows_pnc: 256-point blocks of a plane)
     std::vector<int> anc(n + kVecPad, 0);
     std::atomic<bool> ok{true};
     par_for(n, [&](int64_t a, int64_t b) {
         for (int64_t i = a; i < b && ok; ++i) {
-            if (rp[i + 1] - rp[i] > kPncMaxLen) {
+            if (member(i) && rp[i + 1] - rp[i] > kPncMaxLen) {
                 ok = false;
                 return;
             }
@@ -1501,6 +1510,7 @@ int build_pnc(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
         std::vector<uint32_t> lp;
         std::vector<uint64_t> lv;
         for (int64_t i = a; i < b && ok; ++i) {
+            if (!member(i)) continue;
             const int64_t x = i % nx, y = (i / nx) % ny, z = i / M;
             const bool in[7] = {true, x > 0, x < nx - 1, y > 0, y < ny - 1, z > 0, z < nz - 1};
             uint32_t w = (uint32_t)(rp[i + 1] - rp[i]);
@@ -1532,7 +1542,7 @@ int build_pnc(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
             if (pkey[h] == 0xffffffffu) {
                 pkey[h] = w;
                 lp.push_back(w);
-                if (lp.size() > (size_t)pamg::kPncPatMax) {
+                if (lp.size() > (size_t)kPncSkip) {
                     ok = false;
                     return;
                 }
@@ -1546,11 +1556,15 @@ int build_pnc(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
         std::sort(vals.begin(), vals.end());
         vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
     });
-    if (!ok || pats.size() > (size_t)pamg::kPncPatMax || vals.size() > (size_t)pamg::kPncValMax) return PAMG_OK;
+    if (!ok || pats.size() > (size_t)kPncSkip || vals.size() > (size_t)pamg::kPncValMax) return PAMG_OK;
     // pass 2: the records (pattern id, value indices)
     std::vector<uint2> rec(n + kVecPad, make_uint2(0u, 0u));
     par_for(n, [&](int64_t a, int64_t b) {
         for (int64_t i = a; i < b; ++i) {
+            if (!member(i)) {
+                rec[i] = make_uint2((uint32_t)kPncSkip, 0u);
+                continue;
+            }
             uint64_t r = (uint64_t)(std::lower_bound(pats.begin(), pats.end(), pw[i]) - pats.begin());
             for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
                 uint64_t u;
@@ -2926,12 +2940,12 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         tr.mark("ell");
     }
     // a prolongation over a 7-point grid uploaded earlier on this context: neighbour-coded rows
-    if (pamg::options().pnc && n_own_cols < nrows && ncols == n_own_cols && (int64_t)inner.size() == nrows) {
+    if (pamg::options().pnc && n_own_cols < nrows && (int64_t)inner.size() * 4 >= (int64_t)nrows * 3) {
         // (every registered grid of this row count, the latest first: grids of one size but other
         // shapes may be registered too, and the neighbour check decides)
         const auto grids = grids_of(ctx);
         for (auto g = grids.rbegin(); g != grids.rend() && !A->interior.pnc; ++g)
-            if ((*g)[0] == nrows) CHECK(build_pnc(A.get(), rp, ci, val, *g));
+            if ((*g)[0] == nrows) CHECK(build_pnc(A.get(), rp, ci, val, *g, inner));
         if (A->interior.pnc) inner.clear();  // the rows run in k_rows_pnc, not in tiles
         tr.mark("pnc");
     }
