@@ -87,7 +87,7 @@ def test_local_world_vcycle_bit_exact(built, nparts, kind, n, max_coarse, agglom
             assert itw.value == pcg[0][0]
             assert np.array_equal(hq[:itw.value + 1], np.asarray(pcg[0][1])[:itw.value + 1])
             fused = [layout_of(a)["jr_fused"] for a in A0]
-            pnc0 = [layout_of(s.P[0])["pnc"] for s in S]  # (a part's P0: interior rows neighbour-coded)
+            pnc0 = [bool(s.P) and layout_of(s.P[0])["pnc"] for s in S]  # (a part's P0: interior rows neighbour-coded)
             got_b = np.concatenate([bb.own_values() for bb in b])
             got_x = np.concatenate([xx.own_values() for xx in x])
             ghosts = [(np.asarray(pl[p].ghost_ids, np.int64), v[p].ghost_values()) for p in range(nparts)]
