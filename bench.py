@@ -330,7 +330,7 @@ def main():
     src = kernel_source_sha()
     spmv_kname = _sym_kname(0, lay) if lay.get("sym") else kname.replace("<2,", "<0,", 1)
     traffic = spmv_traffic = None
-    if live_pmc and pipelined:  # this run's own counters (the child ran op 5 = k_sym_tb<3>, op 0 = SpMV)
+    if live_pmc:  # this run's own counters (the child ran op 5 = the chain, op 2 = Jacobi, op 0 = SpMV)
         traffic = live_pmc.get(kname)
         spmv_traffic = live_pmc.get(spmv_kname)
     if args.pmc != "off":
@@ -577,7 +577,7 @@ def pmc_live(args):
         return None
     tmp = tempfile.mkdtemp(prefix="pamg_pmc_")
     kb = [sys.executable, "-u", os.path.join(ROOT, "tools", "kbench.py"), "--n", str(args.grid), "--kind", args.kind,
-          "--levels", "1", "--ops", "0,5", "--reps", "3", "--configs", f"1024:1:1:{int(args.value_dict)}",
+          "--levels", "1", "--ops", "0,2,5", "--reps", "3", "--configs", f"1024:1:1:{int(args.value_dict)}",
           ]
     for kv in args.set:
         kb += ["--set", kv]

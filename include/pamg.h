@@ -52,6 +52,10 @@ const char* pamg_last_error(void);
 int pamg_ctx_create(int device, pamg_ctx** out);
 int pamg_ctx_destroy(pamg_ctx* ctx);
 int pamg_ctx_sync(pamg_ctx* ctx);
+/* References held on the context: the caller's handle (until pamg_ctx_destroy) plus one per
+ * live plan, vector, matrix and hierarchy made on it; it is torn down when they reach 0
+ * (diagnostics and tests: a failed create must leave the count unchanged). */
+int pamg_ctx_refcount(const pamg_ctx* ctx, int* refs);
 /* Number of visible GPUs, through libpamg's own HIP runtime (a driver that must not
  * initialise another runtime in the process asks here; see INTEGRATION.md, load order). */
 int pamg_device_count(int* n);
@@ -92,8 +96,14 @@ int pamg_comm_init_host(pamg_ctx* ctx, int nranks, int rank, pamg_host_comm_fn f
  * PAMG_E_STATE instead of exchanging the wrong vectors. All-reduce / all-gather meet every rank.
  * A rank that does not arrive within 300 s, a failed collective, a failed part of a
  * pamg_world_* call or pamg_world_abort marks the world broken: every waiting and later
- * collective fails (PAMG_E_STATE) at once. pamg_world_reset clears that — call it only when no
- * rank is inside a library call. The world lives until it and all its contexts are destroyed. */
+ * collective fails (PAMG_E_STATE) at once, so no sibling waits for a part that has given up.
+ * pamg_world_reset clears that — call it only when no rank is inside a library call. The
+ * pamg_world_* calls below (and the Python LocalWorld.run over all parts) reset the world
+ * themselves once every part has returned, so one part's error (an argument error included)
+ * fails that call only; a caller driving the ranks from its own threads calls
+ * pamg_world_reset after a failure. Two parts whose tagged plans disagree on their counts
+ * fail at once (PAMG_E_STATE), also when one of them lists the other with zero counts.
+ * The world lives until it and all its contexts are destroyed. */
 typedef struct pamg_world pamg_world;
 int pamg_world_create(int nparts, pamg_world** out);
 int pamg_world_destroy(pamg_world* w);
@@ -190,13 +200,15 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * level-0 Jacobi -> residual, and the pipelined cycles' post -> pre -> residual chain; jr_fuse);
  * bit 6: the tile-major set carries 8-bit per-tile value dictionaries (value_dict);
  * bit 7: the symmetric layout stores a 1-byte row class per row, its values in a table of
- * <= 64 (mask, diagonal, upper values) tuples (sym_vd); bit 8: the tile-major set stages each
- * tile's x runs in LDS and sums one row per lane (x_stage_tiles, k_rows_xsr); bit 9: the set runs in
+ * <= 64 (mask, diagonal, upper values) tuples (sym_vd); bit 8: retired (round 5; never set —
+ * it named the per-tile x staging, deleted); bit 9: the set runs in
  * the sliced-ELL layout (ell: one row per lane, per-group 8-bit column-offset and value dictionaries;
  * then out[8] = the kernel's grid); bit 10: the set runs in the neighbour-coded prolongation layout
  * (pnc: a prolongation over a 7-point grid uploaded earlier on the same context, each column named
  * by the grid neighbour whose anchor it is; then out[3] = the value table's entries, out[4] = the
- * pattern table's, out[8] = the kernel's grid). */
+ * pattern table's, out[8] = the kernel's grid); bit 11: the set runs in the sorted sliced-ELL layout
+ * with plain values (sell: rows longest first within 256-row groups, int32 columns, f64 values;
+ * then out[8] = the kernel's grid). */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[10]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
@@ -290,7 +302,9 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
  * large square operators with all own columns), "ell_restrict" (0 | 1: also restrictions, with
  * anchored offsets), "ell_min_rows" (rows from which ELL is taken), "ell_yblock" (0 | lines: the
  * blocked group order of a restriction over a grid), "pnc" (0 | 1: neighbour-coded
- * prolongations over a grid uploaded earlier on the context). Read at launch:
+ * prolongations over a grid uploaded earlier on the context), "sell" (0 | 1: sorted sliced ELL
+ * with plain values for long-row operators the others decline), "sell_min_len" (mean nonzeros per
+ * row from which it is taken), "sell_min_rows" (rows from which it is taken). Read at launch:
  * "sym_zm" (0 | 1: z-marching single sweeps of the symmetric layout), "zm_chunks" (0 = auto |
  * z chunks per column of k_sym_zm), "tb_xfast" (0 | 1: x-fastest tile order of the chain),
  * "symd_chunks" (1 | 2 | 4), "chain_store_x" (0 | 1). Applied at every exchange:

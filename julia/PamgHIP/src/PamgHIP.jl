@@ -78,6 +78,12 @@ function Base.close(c::Context)
     nothing
 end
 sync(c::Context) = check(ccall((:pamg_ctx_sync, libpamg), Cint, (Ptr{Cvoid},), c.h))
+"References held on the context (its handle + one per live plan, vector, matrix, hierarchy)."
+function refcount(c::Context)
+    n = Ref{Cint}(0)
+    check(ccall((:pamg_ctx_refcount, libpamg), Cint, (Ptr{Cvoid}, Ptr{Cint}), c.h, n))
+    Int(n[])
+end
 function device_count()
     n = Ref{Cint}(0)
     check(ccall((:pamg_device_count, libpamg), Cint, (Ptr{Cint},), n))

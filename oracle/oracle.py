@@ -151,10 +151,28 @@ class Hierarchy:
     rho: list = field(default_factory=list)
     ainv: np.ndarray = None
     _h: int = 0
+    _nlev: int = 0
 
     @property
     def nlevels(self):
-        return len(self.A)
+        return self._nlev or len(self.A)
+
+    def csr(self, l: int, which: int) -> CSR:
+        """Level l's A (which 0), P (1) or R (2), copied out of the C hierarchy."""
+        info = np.zeros(3, np.int64)
+        lib().orc_csr_info(self._h, l, which, info)
+        nr, nc, nnz = (int(v) for v in info)
+        rp = np.empty(nr + 1, np.int64); col = np.empty(nnz, np.int64); val = np.empty(nnz)
+        lib().orc_csr_get(self._h, l, which, rp, col, val)
+        return CSR(rp, col, val, nc)
+
+    def aggregates(self, l: int) -> np.ndarray:
+        """Level l's aggregate ids (global coarse ids, -1 isolated)."""
+        info = np.zeros(3, np.int64)
+        lib().orc_csr_info(self._h, l, 0, info)
+        a = np.empty(int(info[0]), np.int64)
+        lib().orc_agg_get(self._h, l, a)
+        return a
 
     def set_sweeps(self, nu1: int, nu2: int):
         """SPEC §S6 V(nu1, nu2) (default V(1, 1))."""
@@ -181,10 +199,13 @@ class Hierarchy:
 
 
 def setup(A: CSR, nparts: int = 1, theta: float = 0.02, max_levels: int = 20,
-          max_coarse: int = 1000, offsets=None, agglomerate: int = 32768) -> Hierarchy:
+          max_coarse: int = 1000, offsets=None, agglomerate: int = 32768, fetch: bool = True) -> Hierarchy:
     """SPEC §S4-§S5 smoothed-aggregation setup (global view, decoupled by parts; `offsets`
     overrides the uniform partition of SPEC §S7; levels >= 1 with <= `agglomerate` rows are
-    one part, SPEC §S7 agglomeration — 0 disables it)."""
+    one part, SPEC §S7 agglomeration — 0 disables it). fetch=False leaves the level operators
+    in the C hierarchy (H.A / H.P / H.R / H.agg stay empty; ``H.csr(l, which)`` and
+    ``H.aggregates(l)`` copy one out on demand — for 512^3, where all of them at once would be
+    ~50 GB of host memory)."""
     L = lib()
     offs = uniform_offsets(A.nrows, nparts) if offsets is None else np.asarray(offsets, np.int64)
     nparts = len(offs) - 1
@@ -195,28 +216,22 @@ def setup(A: CSR, nparts: int = 1, theta: float = 0.02, max_levels: int = 20,
         raise RuntimeError("oracle setup: coarse Cholesky failed")
     nlev = L.orc_nlev(h)
     info = np.zeros(3, np.int64)
-
-    def get(l, which):
-        L.orc_csr_info(h, l, which, info)
-        nr, nc, nnz = (int(v) for v in info)
-        rp = np.empty(nr + 1, np.int64); col = np.empty(nnz, np.int64); val = np.empty(nnz)
-        L.orc_csr_get(h, l, which, rp, col, val)
-        return CSR(rp, col, val, nc)
-
+    get = H.csr
+    H._nlev = nlev
     for l in range(nlev):
-        H.A.append(get(l, 0))
         H.omega.append(L.orc_omega(h, l))
         H.rho.append(L.orc_rho(h, l))
         o = np.empty(nparts + 1, np.int64)
         L.orc_offs_get(h, l, o)
         H.offsets.append(o)
-        if l < nlev - 1:
-            H.P.append(get(l, 1))
-            H.R.append(get(l, 2))
-            a = np.empty(H.A[l].nrows, np.int64)
-            L.orc_agg_get(h, l, a)
-            H.agg.append(a)
-    nL = H.A[-1].nrows
+        if fetch:
+            H.A.append(get(l, 0))
+            if l < nlev - 1:
+                H.P.append(get(l, 1))
+                H.R.append(get(l, 2))
+                H.agg.append(H.aggregates(l))
+    L.orc_csr_info(h, nlev - 1, 0, info)
+    nL = int(info[0])
     H.ainv = np.empty(nL * nL)
     L.orc_ainv_get(h, H.ainv)
     H.ainv = H.ainv.reshape(nL, nL).T.copy()  # stored column-major -> row-major matrix
@@ -229,7 +244,7 @@ def hierarchy_from_levels(A, P, R, omega, ainv_colmajor) -> Hierarchy:
     the oracle V-cycle on the product's own hierarchy (bench cpu_baseline)."""
     L = lib()
     h = L.orc_hier_new(len(A))
-    H = Hierarchy(_h=h)
+    H = Hierarchy(_h=h, _nlev=len(A))
     for l, M in enumerate(A):
         for which, X in ((0, M), (1, P[l] if l < len(P) else None), (2, R[l] if l < len(R) else None)):
             if X is None:
@@ -239,3 +254,80 @@ def hierarchy_from_levels(A, P, R, omega, ainv_colmajor) -> Hierarchy:
                            X.val.ctypes.data, float(omega[l]) if which == 0 else 0.0)
     L.orc_hier_set_ainv(h, int(round(len(ainv_colmajor) ** 0.5)), np.ascontiguousarray(ainv_colmajor))
     return H
+
+
+# ---------------------------------------------------------------------------------------------
+# A second, independent restatement of SPEC §S4.2-3 (strength + standard aggregation), written
+# from the SPEC text rather than from pamg_oracle.c: the strength pattern is a scipy matrix built
+# with whole-array numpy operations, and the three passes are set operations on per-row
+# neighbour lists. It pins the two C implementations (pamg_oracle.c aggregate(), the product's
+# csrc/setup.cpp pamg_setup_aggregate), which share one formulation.
+
+def strength_matrix(A, theta: float = 0.02, offsets=None):
+    """SPEC §S4.2 as a scipy CSR pattern: entry (i, j) present iff j != i, j is owned by i's
+    part, and |a_ij| >= theta * sqrt(|a_ii * a_jj|) (product, then sqrt, then x theta — the
+    SPEC's rounding order, evaluated elementwise by numpy in IEEE double). The entries keep A's
+    storage order within each row (pass 2 reads "the first strong neighbour in storage order")."""
+    import scipy.sparse as sp
+    rp = np.asarray(A.rowptr, np.int64)
+    col = np.asarray(A.col, np.int64)
+    val = np.asarray(A.val, np.float64)
+    n = len(rp) - 1
+    offs = np.array([0, n], np.int64) if offsets is None else np.asarray(offsets, np.int64)
+    row = np.repeat(np.arange(n, dtype=np.int64), np.diff(rp))
+    on_diag = col == row
+    d = np.zeros(n)
+    d[row[on_diag]] = val[on_diag]            # the stored diagonal (0 if absent)
+    part_of = np.searchsorted(offs, np.arange(n), side="right") - 1
+    ok = ~on_diag & (col >= 0) & (col < n)
+    same = np.zeros(len(col), bool)
+    same[ok] = part_of[col[ok]] == part_of[row[ok]]
+    jj = np.where(same, col, 0)
+    thr = theta * np.sqrt(np.abs(d[row] * d[jj]))
+    strong = same & (np.abs(val) >= thr)
+    keep_rp = np.concatenate([[0], np.cumsum(np.bincount(row[strong], minlength=n))])
+    return sp.csr_matrix((np.ones(int(strong.sum())), col[strong], keep_rp), shape=(n, n))
+
+
+def aggregate_sets(A, theta: float = 0.02, offsets=None):
+    """SPEC §S4.3 standard aggregation on strength_matrix(A), per part in row order, as set
+    operations: returns (agg, coarse_offsets) with agg[i] the global coarse id (part offset +
+    creation number) or -1 for an isolated row. Pure Python: small and medium sizes only."""
+    S = strength_matrix(A, theta, offsets)
+    n = S.shape[0]
+    offs = np.array([0, n], np.int64) if offsets is None else np.asarray(offsets, np.int64)
+    nbrs = [S.indices[S.indptr[i]:S.indptr[i + 1]].tolist() for i in range(n)]
+    agg = np.full(n, -1, np.int64)
+    coffs = [0]
+    for q in range(len(offs) - 1):
+        rows = range(int(offs[q]), int(offs[q + 1]))
+        members = []                          # aggregate k -> its set of rows
+        owner = {}                            # row -> aggregate (assigned rows only)
+        isolated = {i for i in rows if not nbrs[i]}
+        first = set()                         # rows placed by pass 1
+        for i in rows:                        # pass 1: a root and its whole free neighbourhood
+            if i in owner or i in isolated:
+                continue
+            nb = set(nbrs[i])
+            if not any(j in owner for j in nb):
+                grp = nb | {i}
+                members.append(grp)
+                owner.update(dict.fromkeys(grp, len(members) - 1))
+                first |= grp
+        for i in rows:                        # pass 2: join the first pass-1 neighbour's aggregate
+            if i in owner or i in isolated:
+                continue
+            j = next((j for j in nbrs[i] if j in first), None)
+            if j is not None:
+                owner[i] = owner[j]
+                members[owner[j]].add(i)
+        for i in rows:                        # pass 3: a new aggregate of the leftovers
+            if i in owner or i in isolated:
+                continue
+            grp = {i} | {j for j in nbrs[i] if j not in owner}
+            members.append(grp)
+            owner.update(dict.fromkeys(grp, len(members) - 1))
+        for k, grp in enumerate(members):
+            agg[list(grp)] = coffs[-1] + k
+        coffs.append(coffs[-1] + len(members))
+    return agg, np.asarray(coffs, np.int64)

@@ -157,18 +157,16 @@ static int cmp_i64(const void* a, const void* b) {
     i64 x = *(const i64*)a, y = *(const i64*)b; return (x > y) - (x < y);
 }
 
-/* Gustavson C = X*Y (§S4.5): first product initialises, later ones add; row sorted. */
-static ocsr spgemm(const ocsr* X, const ocsr* Y) {
-    ocsr C; C.nr = X->nr; C.nc = Y->nc;
-    double* acc = calloc(Y->nc + 1, sizeof(double));
-    i64* mark = malloc(sizeof(i64) * (Y->nc + 1));
-    for (i64 j = 0; j < Y->nc; ++j) mark[j] = -1;
-    i64* list = malloc(sizeof(i64) * (Y->nc + 1));
-    i64 cap = X->nnz + 16;
-    C.rp = malloc(sizeof(i64) * (X->nr + 1)); C.col = malloc(sizeof(i64) * cap);
-    C.val = malloc(sizeof(double) * cap);
-    C.rp[0] = 0; i64 nnz = 0;
-    for (i64 i = 0; i < X->nr; ++i) {
+/* Gustavson C = X*Y (§S4.5): first product initialises, later ones add; row sorted.
+ * Rows are independent: blocks of rows run on OpenMP threads, each row computed exactly as in
+ * the serial loop (same products, same order), and the blocks are concatenated in row order. */
+typedef struct { i64 r0, r1, nnz, cap; i64* col; double* val; i64* len; } gblock;
+
+static void spgemm_rows(const ocsr* X, const ocsr* Y, gblock* g, double* acc, i64* mark, i64* list) {
+    g->nnz = 0; g->cap = 1024;
+    g->col = malloc(sizeof(i64) * g->cap); g->val = malloc(sizeof(double) * g->cap);
+    g->len = malloc(sizeof(i64) * (g->r1 - g->r0 + 1));
+    for (i64 i = g->r0; i < g->r1; ++i) {
         i64 m = 0;
         for (i64 a = X->rp[i]; a < X->rp[i + 1]; ++a) {
             i64 k = X->col[a]; double xv = X->val[a];
@@ -179,31 +177,82 @@ static ocsr spgemm(const ocsr* X, const ocsr* Y) {
             }
         }
         qsort(list, (size_t)m, sizeof(i64), cmp_i64);
-        if (nnz + m > cap) {
-            while (nnz + m > cap) cap *= 2;
-            C.col = realloc(C.col, sizeof(i64) * cap); C.val = realloc(C.val, sizeof(double) * cap);
+        if (g->nnz + m > g->cap) {
+            while (g->nnz + m > g->cap) g->cap *= 2;
+            g->col = realloc(g->col, sizeof(i64) * g->cap); g->val = realloc(g->val, sizeof(double) * g->cap);
         }
-        for (i64 t = 0; t < m; ++t) { C.col[nnz] = list[t]; C.val[nnz] = acc[list[t]]; ++nnz; }
-        C.rp[i + 1] = nnz;
+        for (i64 t = 0; t < m; ++t) { g->col[g->nnz] = list[t]; g->val[g->nnz] = acc[list[t]]; ++g->nnz; }
+        g->len[i - g->r0] = m;
+    }
+}
+
+static ocsr spgemm(const ocsr* X, const ocsr* Y) {
+    ocsr C; C.nr = X->nr; C.nc = Y->nc;
+    /* ~32 blocks per thread (a coarse product has few rows, each long) */
+    i64 rows_per = X->nr / (32 * (i64)omp_get_max_threads()) + 1;
+    if (rows_per > 65536) rows_per = 65536;
+    const i64 nb = (X->nr + rows_per - 1) / rows_per;
+    gblock* blk = calloc((size_t)nb + 1, sizeof(gblock));
+    for (i64 t = 0; t < nb; ++t) { blk[t].r0 = t * rows_per; blk[t].r1 = (t + 1) * rows_per < X->nr ? (t + 1) * rows_per : X->nr; }
+#pragma omp parallel
+    {
+        double* acc = calloc(Y->nc + 1, sizeof(double));
+        i64* mark = malloc(sizeof(i64) * (Y->nc + 1));
+        for (i64 j = 0; j < Y->nc; ++j) mark[j] = -1;
+        i64* list = malloc(sizeof(i64) * (Y->nc + 1));
+#pragma omp for schedule(dynamic, 1)
+        for (i64 t = 0; t < nb; ++t) spgemm_rows(X, Y, &blk[t], acc, mark, list);
+        free(acc); free(mark); free(list);
+    }
+    i64 nnz = 0;
+    for (i64 t = 0; t < nb; ++t) nnz += blk[t].nnz;
+    C.rp = malloc(sizeof(i64) * (X->nr + 1)); C.col = malloc(sizeof(i64) * (nnz + 1));
+    C.val = malloc(sizeof(double) * (nnz + 1));
+    C.rp[0] = 0;
+    i64* start = malloc(sizeof(i64) * (nb + 1));
+    start[0] = 0;
+    for (i64 t = 0; t < nb; ++t) {
+        start[t + 1] = start[t] + blk[t].nnz;
+        for (i64 i = blk[t].r0; i < blk[t].r1; ++i) C.rp[i + 1] = C.rp[i] + blk[t].len[i - blk[t].r0];
+    }
+#pragma omp parallel for schedule(dynamic, 1)
+    for (i64 t = 0; t < nb; ++t) {
+        memcpy(C.col + start[t], blk[t].col, sizeof(i64) * blk[t].nnz);
+        memcpy(C.val + start[t], blk[t].val, sizeof(double) * blk[t].nnz);
+        free(blk[t].col); free(blk[t].val); free(blk[t].len);
     }
     C.nnz = nnz;
-    free(acc); free(mark); free(list);
+    free(start); free(blk);
     return C;
 }
 
-/* R = P^T: entries of each row in ascending fine-row order (§S4.7). */
+/* R = P^T: entries of each row in ascending fine-row order (§S4.7). Each thread owns a range of
+ * R's rows (P's columns) and scans P in fine-row order, so every row of R is filled in that order. */
 static ocsr transpose(const ocsr* P) {
     ocsr R; R.nr = P->nc; R.nc = P->nr; R.nnz = P->nnz;
     R.rp = calloc(R.nr + 1, sizeof(i64));
     R.col = malloc(sizeof(i64) * (R.nnz + 1)); R.val = malloc(sizeof(double) * (R.nnz + 1));
-    for (i64 a = 0; a < P->nnz; ++a) R.rp[P->col[a] + 1]++;
-    for (i64 c = 0; c < R.nr; ++c) R.rp[c + 1] += R.rp[c];
     i64* pos = malloc(sizeof(i64) * (R.nr + 1));
-    memcpy(pos, R.rp, sizeof(i64) * (R.nr + 1));
-    for (i64 i = 0; i < P->nr; ++i)
-        for (i64 a = P->rp[i]; a < P->rp[i + 1]; ++a) {
-            i64 c = P->col[a]; R.col[pos[c]] = i; R.val[pos[c]] = P->val[a]; pos[c]++;
+#pragma omp parallel
+    {
+        const i64 nt = omp_get_num_threads(), t = omp_get_thread_num();
+        const i64 c0 = R.nr * t / nt, c1 = R.nr * (t + 1) / nt;
+        for (i64 a = 0; a < P->nnz; ++a) {
+            const i64 c = P->col[a];
+            if (c >= c0 && c < c1) R.rp[c + 1]++;
         }
+#pragma omp barrier
+#pragma omp single
+        {
+            for (i64 c = 0; c < R.nr; ++c) R.rp[c + 1] += R.rp[c];
+            memcpy(pos, R.rp, sizeof(i64) * (R.nr + 1));
+        }
+        for (i64 i = 0; i < P->nr; ++i)
+            for (i64 a = P->rp[i]; a < P->rp[i + 1]; ++a) {
+                const i64 c = P->col[a];
+                if (c >= c0 && c < c1) { R.col[pos[c]] = i; R.val[pos[c]] = P->val[a]; pos[c]++; }
+            }
+    }
     free(pos);
     return R;
 }
@@ -211,7 +260,8 @@ static ocsr transpose(const ocsr* P) {
 /* ------------------------------------------------------------------ setup §S4 */
 
 static double gershgorin(const ocsr* A) {
-    double rho = 0.0;
+    double rho = 0.0;  /* (a max: the same value in any row order) */
+#pragma omp parallel for schedule(static) reduction(max : rho)
     for (i64 i = 0; i < A->nr; ++i) {
         double s = 0.0, d = 0.0;
         for (i64 a = A->rp[i]; a < A->rp[i + 1]; ++a) {
@@ -230,14 +280,16 @@ static i64 aggregate(const ocsr* A, double theta, int nparts, const i64* offs,
                      i64* agg, i64* coffs) {
     const i64 n = A->nr;
     double* dg = malloc(sizeof(double) * (n + 1));
+#pragma omp parallel for schedule(static)
     for (i64 i = 0; i < n; ++i) {
         dg[i] = 0.0;
         for (i64 a = A->rp[i]; a < A->rp[i + 1]; ++a) if (A->col[a] == i) dg[i] = A->val[a];
     }
-    /* strong[a] for each entry */
+    /* strong[a] for each entry (rows independent) */
     char* strong = calloc(A->nnz + 1, 1);
-    int p = 0;
+#pragma omp parallel for schedule(static)
     for (i64 i = 0; i < n; ++i) {
+        int p = 0;  /* the part owning row i */
         while (i >= offs[p + 1]) ++p;
         for (i64 a = A->rp[i]; a < A->rp[i + 1]; ++a) {
             i64 j = A->col[a];
@@ -301,6 +353,7 @@ static ocsr smoothed_prolongator(const ocsr* A, const i64* agg, i64 nc, double o
     }
     T.nnz = m;
     ocsr AT = spgemm(A, &T);
+#pragma omp parallel for schedule(static)
     for (i64 i = 0; i < AT.nr; ++i) {
         double d = 0.0;
         for (i64 a = A->rp[i]; a < A->rp[i + 1]; ++a) if (A->col[a] == i) d = A->val[a];

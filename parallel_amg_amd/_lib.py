@@ -38,6 +38,7 @@ SIGNATURES = {
     "pamg_ctx_create": [i32, pvp],
     "pamg_ctx_destroy": [vp],
     "pamg_ctx_sync": [vp],
+    "pamg_ctx_refcount": [vp, C.POINTER(C.c_int)],
     "pamg_device_count": [C.POINTER(C.c_int)],
     "pamg_device_sync": [i32],
     "pamg_comm_unique_id": [C.c_char_p],
@@ -193,7 +194,8 @@ def layout_of(M, part_set: int = 0) -> dict:
             "tile_nnz": int(out[7]), "tiles": int(out[8]), "anchored": bool(out[9] & 1), "per_tile": bool(out[9] & 2),
             "x_stage": bool(out[9] & 4), "sym": bool(out[9] & 8), "sym_rows": 2 if out[9] & 16 else 1,
             "jr_fused": bool(out[9] & 32), "tm_vd": bool(out[9] & 64), "sym_vd": bool(out[9] & 128),
-            "xsr": bool(out[9] & 256), "ell": bool(out[9] & 512), "pnc": bool(out[9] & 1024)}
+            "ell": bool(out[9] & 512), "pnc": bool(out[9] & 1024),
+            "sell": bool(out[9] & 2048)}
 
 
 def last_error() -> str:

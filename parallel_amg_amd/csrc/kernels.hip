@@ -1777,6 +1777,88 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __
     if (in) y[i] = out;
 }
 
+// k_rows_sell: the sorted sliced-ELL layout with plain values (pamg::SellSet; round 6, the 512^3 R1).
+// A workgroup = a group of kEllGroup rows, sorted longest first into 4 slices of kEllW; a lane walks
+// its row: per step 4 elements, their columns and values coalesced across the wave (the k-th
+// elements of the slice's 64 rows are contiguous: 256 B of columns, 512 B of values), the next 4
+// in flight, x gathered at each column (a padded element's column is its row's last: a line the
+// row already reads), products summed left to right from +0.0 in storage order and the padding
+// selected away (SPEC §S3 bits, as every row kernel). Groups in XCD-contiguous order (k_rows_ell).
+template <int OP>
+__global__ __launch_bounds__(kEllGroup) void k_rows_sell(const int2* __restrict__ smeta, const int* __restrict__ col,
+                                                         const double* __restrict__ val, const int* __restrict__ rows,
+                                                         const uint16_t* __restrict__ lens, int ngroups,
+                                                         const double* __restrict__ x, const double* __restrict__ b,
+                                                         double* __restrict__ y, double omega) {
+    const int per = (ngroups + 7) / 8;
+    const int g = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (g >= ngroups) return;
+    const int pos = g * kEllGroup + threadIdx.x, lane = threadIdx.x & 63;
+    const int L16 = lens[pos];
+    const bool in = L16 != kSellSkip;
+    const int L = in ? L16 : 0;
+    const int row = in ? rows[pos] : 0;
+    const int2 sm = smeta[pos / kEllW];  // (one slice per wave: sm.y is wave-uniform)
+    const int* __restrict__ cp = col + sm.x + lane;
+    const double* __restrict__ vp = val + sm.x + lane;
+    double pb = 0.0, px = 0.0, py = 0.0;
+    if (in) {
+        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[row];
+        if constexpr (OP == OP_JACOBI) px = x[row];
+        if constexpr (OP == OP_PROLONG) py = y[row];
+    }
+    const int nq = (sm.y + 3) >> 2;
+    int c4[4];
+    double v4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        c4[e] = e < sm.y ? cp[e * kEllW] : 0;
+        v4[e] = e < sm.y ? vp[e * kEllW] : 0.0;
+    }
+    double s = 0.0, dg = 0.0;
+    for (int q = 0; q < nq; ++q) {
+        int cq[4];
+        double vq[4], xv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            cq[e] = c4[e];
+            vq[e] = v4[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // the next 4 elements in flight while these are used
+            const int k = 4 * (q + 1) + e;
+            if (k < sm.y) {
+                c4[e] = cp[k * kEllW];
+                v4[e] = vp[k * kEllW];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[e] = x[4 * q + e < sm.y ? cq[e] : cq[0]];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool ok = 4 * q + e < L;
+            const double p = vq[e] * xv[e];
+            const double t = s + p;
+            s = ok ? t : s;
+            if constexpr (OP == OP_JACOBI) dg = ok && cq[e] == row ? vq[e] : dg;
+        }
+    }
+    double out;
+    if constexpr (OP == OP_SPMV) {
+        out = s;
+    } else if constexpr (OP == OP_RESID) {
+        out = pb - s;
+    } else if constexpr (OP == OP_JACOBI) {
+        const double u = pb - s;
+        const double v = omega * u;
+        const double w = v / dg;
+        out = px + w;
+    } else {
+        out = py + s;
+    }
+    if (in) y[row] = out;
+}
+
 // k_rows_pnc: the neighbour-coded prolongation (pamg::PncSet; round 5, the 512^3 P0). One row per
 // lane, about 8 workgroups per CU, each staging the two global tables (<= 1024 pattern words, <= 128
 // values) in LDS once and then walking 256-row blocks: at step t the workgroups of XCD j (block b
@@ -2314,6 +2396,12 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
                                                                y, omega);
     }
     if (ts.pnc) launch_pnc<OP>(A, x, b, y, omega, s);
+    if (ts.sell) {
+        const SellSet& E = A.sell;
+        const int grid = (int)((E.ngroups + 7) / 8 * 8);
+        k_rows_sell<OP><<<grid, kEllGroup, 0, s>>>(E.d_smeta, E.d_col, E.d_val, E.d_row, E.d_len, (int)E.ngroups, x, b,
+                                                   y, omega);
+    }
     if (ts.n_short > 0) {
         if (ts.tile_nnz == 1024) launch_tile<OP, 1024>(A, ts, x, b, y, omega, s);
         else if (ts.tile_nnz == 4096) launch_tile<OP, 4096>(A, ts, x, b, y, omega, s);

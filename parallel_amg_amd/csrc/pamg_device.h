@@ -102,6 +102,9 @@ struct TileSet {
     // neighbour-coded prolongation (pamg_mat::pnc; the whole set of a prolongation over a registered grid):
     // the rows run in k_rows_pnc instead of tiles
     bool pnc = false;
+    // sorted sliced ELL with plain values (pamg_mat::sell; long-row operators the ELL dictionaries do not
+    // fit, e.g. the 512^3 R1): the set's rows run in k_rows_sell instead of tiles
+    bool sell = false;
     int max_short_len = 0;    // longest row in a short tile
     int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
@@ -150,6 +153,9 @@ struct Options {
     int pnc = 1;               // 1: neighbour-coded prolongations over a grid registered on the context (PncSet)
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
+    int sell = 1;              // 1: sorted sliced ELL (SellSet) for long-row operators the other layouts decline
+    int sell_min_len = 96;     // ... with at least this many nonzeros per row on average
+    int sell_min_rows = 32768; // ... and at least this many rows
 };
 
 // Symmetric diagonal-class layout (k_rows_sym): a square operator whose interior rows use at
@@ -177,7 +183,9 @@ struct TbGeom {
     int zlo = 0, zhi = 0;           // output planes [zlo, zhi) of a launch (set by launch_sym_tb)
     int xfast = 0;                  // tile order: 0 y-fastest, 1 x-fastest (kernels.hip tb_ctx_init)
 };
-// Sliced ELL with per-group dictionaries (Options::ell; round 5, the level-1 operator): rows in
+// Sliced ELL with per-group dictionaries (Options::ell; round 5, the level-1 operator and R0 of one
+// part; on several parts the interior rows of a part's operator, its boundary rows carrying the length
+// byte kEllSkip and running in tiles after the exchange): rows in
 // slices of kEllW consecutive rows (one per lane of a wave), kEllGroup rows (a workgroup) sharing
 // two tables of <= 256 entries — the rows' column offsets (col - row) and values (bit patterns).
 // A slice stores its padded nonzeros k = 0 .. maxlen-1 as one column-index byte and one value-index
@@ -204,15 +212,36 @@ struct EllSet {
 };
 
 // Neighbour-coded prolongation (Options::pnc; round 5, the 512^3 P0): a prolongation (more rows than
-// columns, one part) whose rows are the points of a 7-point grid uploaded earlier on the same
-// context (pamg_ctx::grids), each of its columns being the anchor of one of the points i, i-1,
-// i+1, i-nx, i+nx, i-M, i+M (codes 0..6) — the anchor of a row being the column of its largest
+// columns) whose rows are the points of a 7-point grid uploaded earlier on the same context — on one
+// part all of them; on several parts a part's interior rows, its boundary rows (ghost columns) carrying
+// the pattern id kPncSkip and running in tiles after the exchange (the grids: pamg_ctx::grids).
+// Each column of row i is the anchor of one of the points i, i-1, i+1, i-nx, i+nx, i-M, i+M (codes 0..6) — the anchor of a row being the column of its largest
 // value (in smoothed aggregation: the point's own aggregate; P = (I - w D^-1 A) P_tent reaches
 // the aggregates of the point's stencil neighbours). Per row: the anchor (4 B) and a 64-bit record:
 // bits 0-9 a pattern id (a global table of <= kPncPatMax words: bits 0-2 the row length, 3 + 3k
 // the k-th entry's neighbour code), bits 10 + 7k the k-th entry's value index (a global table of
 // <= kPncValMax bit patterns). 12 B per row against 3.5 B per nonzero + 1 B per row in tiles. Rows
 // keep their storage order (SPEC S3 sums).
+// Sorted sliced ELL with plain values (Options::sell; round 6, the 512^3 R1: ~190 nonzeros per row,
+// tens of thousands of distinct values per 256 rows and columns spread over 2^18, so neither the ELL
+// dictionaries nor 16-bit offsets fit). Rows in groups of kEllGroup consecutive rows (a workgroup);
+// inside a group the rows are ordered by length, longest first (stable), and cut into slices of kEllW
+// (one row per lane, a wave each), each slice padded to its first row's length — so a slice's rows
+// have about one length and the padding stays small (512^3 R1 ~2 % against ~20 % in row order).
+// Element k of the slice's lane-th row: column d_col[start + k * kEllW + lane] (int32, absolute) and
+// value d_val[...] (f64); a padded element repeats the row's last column with value 0 and is selected
+// away. Per sorted position: the row (d_row) and its length (d_len; kSellSkip: a position with no row,
+// or a part's boundary row computed by the tiles after the exchange). Rows keep their storage order.
+constexpr int kSellSkip = 0xffff, kSellMaxLen = 0xfffe;
+struct SellSet {
+    int64_t nslices = 0, ngroups = 0, elems = 0;
+    int2* d_smeta = nullptr;   // per slice: (first element of its streams, padded length)
+    int* d_col = nullptr;
+    double* d_val = nullptr;
+    int* d_row = nullptr;      // per sorted position (ngroups * kEllGroup)
+    uint16_t* d_len = nullptr; // per sorted position
+};
+
 constexpr int kPncPatMax = 1024, kPncValMax = 128, kPncMaxLen = 7;
 constexpr int kPncSkip = kPncPatMax - 1;  // pattern id of a row outside the set (several parts: a boundary row)
 struct PncSet {
@@ -335,6 +364,7 @@ struct pamg_mat {
     pamg::TileSet boundary;  // rows with >= 1 ghost column
     pamg::EllSet ell;        // the interior set's sliced-ELL layout (TileSet::ell)
     pamg::PncSet pnc;        // the neighbour-coded prolongation layout (TileSet::pnc)
+    pamg::SellSet sell;      // the interior set's sorted sliced-ELL layout (TileSet::sell)
     int64_t stream_bytes = 0;  // matrix bytes one apply reads (values, columns, row pointers, tiles)
 };
 

@@ -1461,6 +1461,87 @@ int build_ell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
     return PAMG_OK;
 }
 
+// Sorted sliced ELL with plain values (Options::sell, pamg::SellSet): the interior rows of an
+// operator with long rows that the ELL dictionaries decline. Within each group of kEllGroup rows the
+// rows are ordered longest first (stable), cut into slices of kEllW padded to their longest row.
+// Declines (leaves the tiles to the caller) where a row exceeds kSellMaxLen or a stream index 2^31.
+int build_sell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val, const std::vector<int>& inner) {
+    using pamg::kEllGroup;
+    using pamg::kEllW;
+    using pamg::kSellSkip;
+    const int64_t n = A->nrows;
+    std::vector<char> in_set;
+    if ((int64_t)inner.size() != n) {
+        in_set.assign(n, 0);
+        for (int i : inner) in_set[i] = 1;
+    }
+    auto member = [&](int64_t i) { return in_set.empty() || in_set[i]; };
+    const int64_t ng = (n + kEllGroup - 1) / kEllGroup, npos = ng * kEllGroup, ns = npos / kEllW;
+    std::vector<int> row(npos, 0);
+    std::vector<uint16_t> len(npos, (uint16_t)kSellSkip);
+    std::atomic<bool> ok{true};
+    par_for(ng, [&](int64_t a, int64_t b) {
+        std::vector<int> r;
+        for (int64_t g = a; g < b; ++g) {
+            r.clear();
+            for (int64_t i = g * kEllGroup; i < std::min(n, (g + 1) * kEllGroup); ++i) {
+                if (!member(i)) continue;
+                if (rp[i + 1] - rp[i] > pamg::kSellMaxLen) ok = false;
+                r.push_back((int)i);
+            }
+            std::stable_sort(r.begin(), r.end(), [&](int p, int q) { return rp[p + 1] - rp[p] > rp[q + 1] - rp[q]; });
+            for (size_t j = 0; j < r.size(); ++j) {
+                row[g * kEllGroup + (int64_t)j] = r[j];
+                len[g * kEllGroup + (int64_t)j] = (uint16_t)(rp[r[j] + 1] - rp[r[j]]);
+            }
+        }
+    });
+    if (!ok) return PAMG_OK;
+    std::vector<int2> smeta(ns);
+    int64_t elems = 0;
+    for (int64_t q = 0; q < ns; ++q) {
+        int m = 0;
+        for (int64_t j = q * kEllW; j < (q + 1) * kEllW; ++j)
+            if (len[j] != kSellSkip) m = std::max<int>(m, len[j]);
+        smeta[q] = make_int2((int)elems, m);
+        elems += (int64_t)kEllW * m;
+        if (elems >= INT32_MAX) return PAMG_OK;
+    }
+    std::vector<int> col(elems + 1, 0);
+    std::vector<double> v(elems + 1, 0.0);
+    par_for(ns, [&](int64_t a, int64_t b) {
+        for (int64_t q = a; q < b; ++q)
+            for (int lane = 0; lane < kEllW; ++lane) {
+                const int64_t j = q * kEllW + lane;
+                const int L = len[j] == kSellSkip ? 0 : len[j];
+                const int64_t r0 = L ? rp[row[j]] : 0;
+                const int pad_col = L ? ci[r0 + L - 1] : 0;  // a padded element re-reads the row's last x
+                for (int k = 0; k < smeta[q].y; ++k) {
+                    const int64_t e = smeta[q].x + (int64_t)k * kEllW + lane;
+                    col[e] = k < L ? ci[r0 + k] : pad_col;
+                    v[e] = k < L ? val[r0 + k] : 0.0;
+                }
+            }
+    });
+    pamg::SellSet& E = A->sell;
+    pamg_ctx* ctx = A->ctx;
+    E.nslices = ns;
+    E.ngroups = ng;
+    E.elems = elems;
+    CHECK(dalloc(&E.d_smeta, ns));
+    CHECK(dalloc(&E.d_col, elems + 1));
+    CHECK(dalloc(&E.d_val, elems + 1));
+    CHECK(dalloc(&E.d_row, npos));
+    CHECK(dalloc(&E.d_len, npos));
+    CHECK(h2d(ctx, E.d_smeta, smeta.data(), sizeof(int2) * ns));
+    CHECK(h2d(ctx, E.d_col, col.data(), sizeof(int) * (elems + 1)));
+    CHECK(h2d(ctx, E.d_val, v.data(), sizeof(double) * (elems + 1)));
+    CHECK(h2d(ctx, E.d_row, row.data(), sizeof(int) * npos));
+    CHECK(h2d(ctx, E.d_len, len.data(), sizeof(uint16_t) * npos));
+    A->interior.sell = true;
+    return PAMG_OK;
+}
+
 // Neighbour-coded prolongation (Options::pnc, pamg::PncSet): every row's columns named by the
 // grid neighbours whose anchors they are. Declines (leaves the tile layouts to the caller) where a
 // row is longer than kPncMaxLen, a column is no neighbour's anchor, or a table would overflow.
@@ -1623,6 +1704,15 @@ void free_ell(pamg::EllSet& E) {
     E = pamg::EllSet{};
 }
 
+void free_sell(pamg::SellSet& E) {
+    dfree(E.d_smeta);
+    dfree(E.d_col);
+    dfree(E.d_val);
+    dfree(E.d_row);
+    dfree(E.d_len);
+    E = pamg::SellSet{};
+}
+
 void free_tiles(pamg::TileSet& ts) {
     dfree(ts.d_short);
     dfree(ts.d_long);
@@ -1683,6 +1773,12 @@ struct pamg_world {
         const pamg_plan* plan = nullptr;
         hipEvent_t ready = nullptr;
         int64_t tag = 0;
+        // q is in (or has made) an exchange under plan tag zero_tag that lists p with zero counts,
+        // after zero_at exchanges with p: a p waiting for q's post #zero_at + 1 under the same tag
+        // expects a non-zero count — the two parts' plans disagree (fail at once, not
+        // after the 300 s timeout)
+        uint64_t zero_at = UINT64_MAX;
+        int64_t zero_tag = 0;
     };
     std::vector<Post> post;
     std::vector<pamg_ctx*> ctx;
@@ -1747,9 +1843,18 @@ int exchange_local(const pamg_plan* plan, double* x, hipStream_t s) {
     pamg_ctx* ctx = plan->ctx;
     pamg_world* w = ctx->world;
     const int me = ctx->rank, nn = (int)plan->nbr.size(), n = w->n;
-    std::vector<int> ks;  // neighbours this exchange pairs with
+    std::vector<int> ks, zs;  // neighbours this exchange pairs with; neighbours listed with zero counts
     for (int k = 0; k < nn; ++k)
-        if (plan->recv_off[k + 1] > plan->recv_off[k] || plan->send_off[k + 1] > plan->send_off[k]) ks.push_back(k);
+        (plan->recv_off[k + 1] > plan->recv_off[k] || plan->send_off[k + 1] > plan->send_off[k] ? ks : zs).push_back(k);
+    if (!zs.empty() && plan->tag != 0) {
+        std::lock_guard<std::mutex> lk(w->mu);
+        for (int k : zs) {
+            pamg_world::Post& p = w->post[(size_t)me * n + plan->nbr[k]];
+            p.zero_at = p.seq;
+            p.zero_tag = plan->tag;
+        }
+        w->cv.notify_all();
+    }
     if (ks.empty()) return PAMG_OK;
     HIPC(hipEventRecord(ctx->ev_ready, s));
     std::vector<uint64_t> seq(ks.size());
@@ -1773,9 +1878,19 @@ int exchange_local(const pamg_plan* plan, double* x, hipStream_t s) {
         {
             std::unique_lock<std::mutex> lk(w->mu);
             const pamg_world::Post& pq = w->post[(size_t)q * n + me];
-            if (!w->wait_locked(lk, [&] { return pq.seq >= seq[i]; }, "a neighbour part did not post its exchange within 300 s"))
+            auto zero_listed = [&] { return plan->tag != 0 && pq.zero_tag == plan->tag && pq.zero_at + 1 == seq[i]; };
+            if (!w->wait_locked(lk, [&] { return pq.seq >= seq[i] || zero_listed(); },
+                                "a neighbour part did not post its exchange within 300 s"))
                 return fail(PAMG_E_STATE, "local exchange: part %d waited for part %d: the world is broken (%s)", me, q,
                             w->why.c_str());
+            if (pq.seq < seq[i]) {
+                w->abort_locked("exchange count mismatch");
+                return fail(PAMG_E_STATE,
+                            "local exchange: part %d expects %lld ghosts from part %d and sends it %lld, but part %d's plan "
+                            "(tag %lld) lists part %d with zero counts", me,
+                            (long long)(plan->recv_off[k + 1] - plan->recv_off[k]), q,
+                            (long long)(plan->send_off[k + 1] - plan->send_off[k]), q, (long long)plan->tag, me);
+            }
             sq = pq;
             if (sq.seq != seq[i] || sq.tag != plan->tag) {
                 w->abort_locked("exchange pairing mismatch");
@@ -2334,6 +2449,12 @@ int pamg_device_count(int* n) {
     return PAMG_OK;
 }
 
+int pamg_ctx_refcount(const pamg_ctx* ctx, int* refs) {
+    if (!ctx || !refs) return fail(PAMG_E_ARG, "ctx_refcount: bad args");
+    *refs = (int)ctx->refs.load();
+    return PAMG_OK;
+}
+
 int pamg_ctx_sync(pamg_ctx* ctx) {
     if (!ctx) return fail(PAMG_E_ARG, "ctx_sync: NULL");
     HIPC(hipStreamSynchronize(ctx->s_comm));
@@ -2492,21 +2613,28 @@ int world_each(pamg_world* w, F&& f) {
     if (!w) return fail(PAMG_E_ARG, "world: NULL");
     for (int r = 0; r < w->n; ++r)
         if (!w->ctx[r]) return fail(PAMG_E_STATE, "world: rank %d has no context", r);
-    std::vector<int> rc(w->n, PAMG_OK);
+    std::vector<int> rc(w->n, PAMG_OK), order(w->n, INT32_MAX);
     std::vector<std::string> msg(w->n);
     std::vector<std::thread> th;
+    std::atomic<int> nfail{0};
     for (int r = 0; r < w->n; ++r)
         th.emplace_back([&, r] {
             rc[r] = f(r);
             if (rc[r] != PAMG_OK) {
                 msg[r] = pamg::last_error();
+                order[r] = nfail.fetch_add(1);
                 w->abort("a part's call failed");  // its siblings stop waiting for it now
             }
         });
     for (auto& t : th) t.join();
-    for (int r = 0; r < w->n; ++r)
-        if (rc[r] != PAMG_OK) return fail(rc[r], "part %d: %s", r, msg[r].c_str());
-    return PAMG_OK;
+    if (nfail.load() == 0) return PAMG_OK;
+    // the part that failed first (the cause; the others failed because the world broke)
+    const int r = (int)(std::min_element(order.begin(), order.end()) - order.begin());
+    // every part has returned (the library owns all the world's threads here), so the break
+    // that released the siblings is cleared: one part's argument error leaves the world usable
+    // for the next call
+    (void)pamg_world_reset(w);
+    return fail(rc[r], "part %d: %s", r, msg[r].c_str());
 }
 }  // namespace
 
@@ -2575,8 +2703,10 @@ int pamg_plan_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, int n_nbr,
     if (n_own >= INT32_MAX || n_own + n_ghost >= INT32_MAX)
         return fail(PAMG_E_OVERFLOW, "plan_create: sizes exceed int32");
     CHECK(set_device(ctx));
-    auto p = std::make_unique<pamg_plan>();
+    // released through pamg_plan_destroy on every error path
+    std::unique_ptr<pamg_plan, int (*)(pamg_plan*)> p(new pamg_plan, pamg_plan_destroy);
     p->ctx = ctx;
+    ctx_ref(ctx);
     p->n_own = n_own;
     p->n_ghost = n_ghost;
     p->nbr.assign(nbr_rank, nbr_rank + n_nbr);
@@ -2612,7 +2742,6 @@ int pamg_plan_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, int n_nbr,
     CHECK(dalloc(&p->d_send_idx, ns));
     CHECK(dalloc(&p->d_sendbuf, ns));
     if (ns) HIPC(hipMemcpy(p->d_send_idx, idx.data(), sizeof(int) * ns, hipMemcpyHostToDevice));
-    ctx_ref(ctx);
     *out = p.release();
     return PAMG_OK;
 }
@@ -2639,14 +2768,14 @@ int pamg_plan_destroy(pamg_plan* p) {
 int pamg_vec_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, pamg_vec** out) {
     if (!ctx || !out || n_own < 0 || n_ghost < 0) return fail(PAMG_E_ARG, "vec_create: bad args");
     CHECK(set_device(ctx));
-    auto v = std::make_unique<pamg_vec>();
+    std::unique_ptr<pamg_vec, int (*)(pamg_vec*)> v(new pamg_vec, pamg_vec_destroy);
     v->ctx = ctx;
+    ctx_ref(ctx);
     v->n_own = n_own;
     v->n_ghost = n_ghost;
     CHECK(dalloc(&v->d, n_own + n_ghost + kVecPad));
     HIPC(hipMemsetAsync(v->d, 0, sizeof(double) * (n_own + n_ghost + kVecPad), ctx->s_comp));
     HIPC(hipStreamSynchronize(ctx->s_comp));
-    ctx_ref(ctx);
     *out = v.release();
     return PAMG_OK;
 }
@@ -2852,6 +2981,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     // released through pamg_mat_destroy on every error path (no device memory leaks)
     std::unique_ptr<pamg_mat, int (*)(pamg_mat*)> A(new pamg_mat, pamg_mat_destroy);
     A->ctx = ctx;
+    ctx_ref(ctx);  // (before the first failure point: the deleter drops it)
     A->nrows = nrows;
     A->ncols = ncols;
     A->nnz = nnz;
@@ -2949,6 +3079,18 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         if (A->interior.pnc) inner.clear();  // the rows run in k_rows_pnc, not in tiles
         tr.mark("pnc");
     }
+    // long rows the ELL dictionaries decline (512^3 R1: ~190 per row, tens of thousands of values per
+    // group): sorted sliced ELL with plain values and int32 columns
+    if (pamg::options().sell && !A->interior.sym && !A->interior.ell && !A->interior.pnc && !inner.empty() &&
+        nrows >= pamg::options().sell_min_rows && (int64_t)inner.size() * 4 >= (int64_t)nrows * 3) {
+        int64_t nz_in = 0;
+        for (int i : inner) nz_in += rp[i + 1] - rp[i];
+        if (nz_in >= (int64_t)pamg::options().sell_min_len * (int64_t)inner.size()) {
+            CHECK(build_sell(A.get(), rp, ci, val, inner));
+            if (A->interior.sell) inner.clear();  // the rows run in k_rows_sell, not in tiles
+            tr.mark("sell");
+        }
+    }
     // the CSR copies: read by the tile and long-row kernels only, so not uploaded when every row
     // runs in the symmetric, ELL or neighbour-coded layout (the 512^3 A0, A1, R0, P0: 29 GB less)
     if (!inner.empty() || !bnd.empty()) {
@@ -3016,8 +3158,11 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
                            8 * A->ell.vtab_n + (A->ell.d_anc ? 4 * nrows : 0);
     // neighbour-coded prolongation: the anchor and the record per row, the two tables
     if (A->interior.pnc) A->stream_bytes += 12 * nrows + 4 * A->pnc.npat + 8 * A->pnc.nval;
+    // sorted sliced ELL: 12 B per padded element, the row and length per position, the slice descriptors
+    if (A->interior.sell)
+        A->stream_bytes += 12 * A->sell.elems + 6 * A->sell.ngroups * pamg::kEllGroup + 8 * A->sell.nslices;
     for (const pamg::TileSet* t : {&A->interior, &A->boundary}) {
-        if (t->sym || t->ell || t->pnc) continue;  // counted above
+        if (t->sym || t->ell || t->pnc || t->sell) continue;  // counted above
         const int64_t ns = t->n_short, nz = t->nnz_short;
         int64_t b = 8 * (int64_t)t->n_long + 12 * t->nnz_long;
         const bool base = t->c24 && !t->cd;
@@ -3045,7 +3190,6 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         CHECK(h2d(ctx, A->d_chi, hi.data(), sizeof(uint8_t) * hi.size()));
     }
     tr.mark("rest");
-    ctx_ref(ctx);
     *out = A.release();
     return PAMG_OK;
 }
@@ -3138,6 +3282,7 @@ int pamg_mat_destroy(pamg_mat* A) {
     free_tiles(A->boundary);
     free_ell(A->ell);
     free_pnc(A->pnc);
+    free_sell(A->sell);
     pamg_ctx* owner = A->ctx;
     delete A;
     ctx_unref(owner);
@@ -3172,8 +3317,9 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
              (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0) |
-             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0) | (t.pnc ? 1024 : 0);
+             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0) | (t.pnc ? 1024 : 0) | (t.sell ? 2048 : 0);
     if (t.ell) out[8] = (int)A->ell.ngroups;  // k_rows_ell's grid
+    if (t.sell) out[8] = (int)A->sell.ngroups;  // k_rows_sell's grid
     if (t.pnc) {  // the pattern and value tables, k_rows_pnc's grid
         out[3] = A->pnc.nval;
         out[4] = A->pnc.npat;
@@ -3283,6 +3429,10 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
     if (!ctx || !out || nlevels < 1 || !A || !omega || !ainv || n_coarse < 1)
         return fail(PAMG_E_ARG, "hier_create: bad args");
     if (nlevels > 1 && (!P || !R)) return fail(PAMG_E_ARG, "hier_create: P/R missing");
+    for (int l = 0; l < nlevels; ++l) {  // (before anything below dereferences them)
+        if (!A[l]) return fail(PAMG_E_ARG, "hier_create: A[%d] is NULL", l);
+        if (l < nlevels - 1 && (!P[l] || !R[l])) return fail(PAMG_E_ARG, "hier_create: P/R[%d] is NULL", l);
+    }
     const int L = nlevels, nr = ctx->nranks, me = ctx->rank;
     if (nr == 1 || L == 1) rep_level = L - 1;
     if (rep_level < (L > 1 ? 1 : 0) || rep_level > L - 1)
@@ -3292,6 +3442,7 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
     CHECK(set_device(ctx));
     std::unique_ptr<pamg_hier, int (*)(pamg_hier*)> H(new pamg_hier, pamg_hier_destroy);
     H->ctx = ctx;
+    ctx_ref(ctx);  // (before the first failure point: the deleter drops it)
     H->L = nlevels;
     H->rep = rep_level;
     // graph replay on one part and on RCCL multi-part runs (RCCL captures its p2p and
@@ -3380,7 +3531,6 @@ int pamg_hier_create(pamg_ctx* ctx, int nlevels, pamg_mat* const* A, pamg_mat* c
         CHECK(dzero(ctx, H->d_bsend, sizeof(double) * (H->cmax + kVecPad)));
     }
     H->prof_ms.assign((size_t)L * 6, 0.0);
-    ctx_ref(ctx);
     *out = H.release();
     return PAMG_OK;
 }
@@ -3846,6 +3996,9 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "ell_restrict" && (value == 0 || value == 1)) o.ell_restrict = (int)value;
     else if (k == "pnc" && (value == 0 || value == 1)) o.pnc = (int)value;
     else if (k == "ell_yblock" && value >= 0 && value <= 65536) o.ell_yblock = (int)value;
+    else if (k == "sell" && (value == 0 || value == 1)) o.sell = (int)value;
+    else if (k == "sell_min_len" && value >= 1 && value <= 65535) o.sell_min_len = (int)value;
+    else if (k == "sell_min_rows" && value >= 1 && value <= INT32_MAX) o.sell_min_rows = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
     else if (k == "chain_store_x" && (value == 0 || value == 1)) o.chain_store_x = (int)value;
@@ -3884,6 +4037,9 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "ell_restrict") *value = o.ell_restrict;
     else if (k == "pnc") *value = o.pnc;
     else if (k == "ell_yblock") *value = o.ell_yblock;
+    else if (k == "sell") *value = o.sell;
+    else if (k == "sell_min_len") *value = o.sell_min_len;
+    else if (k == "sell_min_rows") *value = o.sell_min_rows;
     else if (k == "ell_min_rows") *value = o.ell_min_rows;
     else if (k == "zm_chunks") *value = o.zm_chunks;
     else if (k == "chain_store_x") *value = o.chain_store_x;

@@ -158,6 +158,13 @@ class Context:
     def sync(self):
         call("pamg_ctx_sync", self._h)
 
+    def refcount(self) -> int:
+        """References held on the context (pamg_ctx_refcount): this handle + one per live plan,
+        vector, matrix and hierarchy made on it."""
+        v = C.c_int()
+        call("pamg_ctx_refcount", self._h, C.byref(v))
+        return v.value
+
     def close(self):
         _release(self, "pamg_ctx_destroy")
 
@@ -192,17 +199,20 @@ class LocalWorld:
             raise
 
     def run(self, fn, parts=None):
-        """[fn(p) for p in parts], one thread per part, concurrently; the first exception of any
-        part is raised after every thread has ended."""
+        """[fn(p) for p in parts], one thread per part, concurrently; the exception of the part
+        that failed first is raised after every thread has ended. A failing part breaks the world at once (its
+        siblings stop waiting for it); a run over all the parts resets it before raising, so the
+        world stays usable for the next run."""
         import threading
         parts = list(range(self.nparts)) if parts is None else list(parts)
-        out, err = {}, {}
+        out, err, failed = {}, {}, []  # failed: the parts in the order they failed
 
         def body(p):
             try:
                 out[p] = fn(p)
             except BaseException as e:  # noqa: BLE001 - re-raised below
                 err[p] = e
+                failed.append(p)  # (list.append is atomic under the GIL)
 
         def guarded(p):
             body(p)
@@ -217,7 +227,12 @@ class LocalWorld:
         for t in th:
             t.join()
         if err:
-            p = min(err)
+            if self._h and set(parts) == set(range(self.nparts)):
+                # every part has returned: clear the break that released the siblings, so one
+                # part's error fails this call only (a run over some of the parts
+                # leaves that to the caller's reset(), the others may still be inside a call)
+                call("pamg_world_reset", self._h)
+            p = failed[0]  # the first to fail: the cause (the others failed because the world broke)
             raise RuntimeError(f"part {p}: {err[p]!r}") from err[p]
         return [out[p] for p in parts]
 

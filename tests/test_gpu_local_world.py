@@ -151,6 +151,40 @@ def test_local_world_ell_interior_rows_bit_exact(built, nparts, kind, n):
     assert np.array_equal(bits(got_x), bits(Ho.solve(bo, ncycles)))
 
 
+@pytest.mark.parametrize("nparts,kind,n", [(3, "poisson3d", 20), (4, "elastic3d", 10)])
+def test_local_world_sell_interior_rows_bit_exact(built, nparts, kind, n):
+    """Several parts with every level's interior rows in the sorted sliced ELL (sell_min_len 1,
+    sell_min_rows 0; the symmetric, ELL and neighbour-coded layouts off): the boundary rows carry the
+    skip length and run in tiles after the exchange. b = A x* and x after 4 V-cycles are the
+    oracle's multi-part bits, ghosts NaN-poisoned."""
+    ncycles = 4
+    with option("poison_ghosts", 1), option("sell_min_rows", 0), option("sell_min_len", 1), option("sym_dia", 0), \
+            option("ell", 0), option("pnc", 0):
+        W = LocalWorld(nparts)
+        try:
+            be = pa.SequentialBackend(nparts)
+            A, offs, xs = pa.generate_problem(be, kind, n)
+            H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=60, agglomerate=0), device=W.ctxs[0])
+            S = [AMGSolver(W.ctxs[p], H, part=p) for p in range(nparts)]
+            assert any(layout_of(s.A_dev[0])["sell"] for s in S)
+            A0 = [s.A_dev[0] for s in S]
+            xst = [PVector(W.ctxs[p], A0[p].n_own_cols, A0[p].n_ghost, xs[p]) for p in range(nparts)]
+            b = [PVector(W.ctxs[p], A0[p].nrows) for p in range(nparts)]
+            W.run(lambda p: mul(b[p], A0[p], xst[p]))
+            x = [s.new_vector() for s in S]
+            W.run(lambda p: S[p].vcycle(x[p], b[p], ncycles))
+            got_b = np.concatenate([v.own_values() for v in b])
+            got_x = np.concatenate([v.own_values() for v in x])
+        finally:
+            del S
+            W.close()
+    Ao = O.generate(kind, *O.grid_shape(kind, n))
+    bo = O.spmv(Ao, O.xstar(Ao.nrows))
+    Ho = O.setup(Ao, nparts=nparts, max_coarse=60, agglomerate=0)
+    assert np.array_equal(bits(got_b), bits(bo))
+    assert np.array_equal(bits(got_x), bits(Ho.solve(bo, ncycles)))
+
+
 def test_baseline_config0_golden(built):
     """BASELINE.json configs[0] — 2D 5-pt Poisson 256 x 256, 2 parts, the PartitionedArrays
     sequential-backend shape — on the HIP path (both parts in one process, the device world) against
@@ -314,7 +348,8 @@ def test_local_world_mismatched_pairing_fails(built):
         v = [PVector(W.ctxs[p], 10, 3, np.arange(10.0) + 10 * p) for p in range(2)]
         with pytest.raises(RuntimeError, match="schedules diverged|broken"):
             W.run(lambda p: consistent(v[p], pA[p] if p == 0 else pB[p]))
-        assert W.broken
+        # (a run over all the parts clears the break once they have all returned: ADVICE r5)
+        assert not W.broken
         W.reset()
         assert not W.broken
         W.run(lambda p: consistent(v[p], pA[p]))
@@ -348,10 +383,66 @@ def test_local_world_failed_part_releases_siblings(built):
         with pytest.raises(RuntimeError, match="part 0"):
             W.run(body)
         assert time.time() - t < 60
+        assert not W.broken  # every part returned: the run reset the world itself
+        W.run(lambda p: consistent(v[p], pA[p]))
+        # a run over SOME parts leaves the break for the caller's reset (the others may be busy)
+        with pytest.raises(RuntimeError, match="part 0"):
+            W.run(body, parts=[0])
         assert W.broken
         W.reset()
         W.run(lambda p: consistent(v[p], pA[p]))
         del pA, v
+    finally:
+        W.close()
+
+
+def test_world_call_argument_error_leaves_the_world_usable(built):
+    """a pamg_world_* call whose part fails an argument check (here part 1
+    passes no plan) fails that call — the sibling waiting in its exchange is released at once —
+    and the world is reset before the call returns, so the next call runs."""
+    import time
+    from parallel_amg_amd._lib import PamgError
+    from parallel_amg_amd.partitioned import DevicePlan
+    hA, _hB = _two_plans()
+    W = LocalWorld(2)
+    try:
+        pA = [DevicePlan(W.ctxs[p], hA[p], tag=1) for p in range(2)]
+        v = [PVector(W.ctxs[p], 10, 3, np.arange(10.0) + 10 * p) for p in range(2)]
+        vs = (ctypes.c_void_p * 2)(*[x.handle.value for x in v])
+        bad = (ctypes.c_void_p * 2)(pA[0].handle.value, None)
+        good = (ctypes.c_void_p * 2)(*[q.handle.value for q in pA])
+        t = time.time()
+        with pytest.raises(PamgError, match="part 1"):
+            call("pamg_world_exchange", W._h, bad, vs)
+        assert time.time() - t < 60
+        assert not W.broken
+        call("pamg_world_exchange", W._h, good, vs)
+        assert np.array_equal(v[0].ghost_values(), [10.0, 11.0, 12.0])
+        assert np.array_equal(v[1].ghost_values(), [7.0, 8.0, 9.0])
+        del pA, v
+    finally:
+        W.close()
+
+
+def test_local_world_zero_listed_neighbour_fails_fast(built):
+    """part 0's plan expects 3 ghosts from part 1 and sends it 3, while part 1's
+    plan (same tag) lists part 0 with zero counts. Part 0 must fail at once with the count
+    mismatch, not after the 300 s pairing timeout."""
+    import time
+    from parallel_amg_amd.hierarchy import HostPlan
+    from parallel_amg_amd.partitioned import DevicePlan
+    hA, _hB = _two_plans()
+    lonely = HostPlan(n_own=10, col0=10, ghost_ids=np.zeros(0, np.int64), nbrs=[0], recv_counts=[0],
+                      send_counts=[0], send_idx=np.zeros(0, np.int64))
+    W = LocalWorld(2)
+    try:
+        plans = [DevicePlan(W.ctxs[0], hA[0], tag=7), DevicePlan(W.ctxs[1], lonely, tag=7)]
+        v = [PVector(W.ctxs[0], 10, 3, np.arange(10.0)), PVector(W.ctxs[1], 10, 0, np.arange(10.0))]
+        t = time.time()
+        with pytest.raises(RuntimeError, match="zero counts"):
+            W.run(lambda p: consistent(v[p], plans[p]))
+        assert time.time() - t < 60
+        del plans, v
     finally:
         W.close()
 
@@ -406,6 +497,60 @@ def test_local_world_part_without_neighbours(built):
     xo = Ho.solve(bo, ncycles)
     assert np.array_equal(bits(got_b), bits(bo))
     assert np.array_equal(bits(got_x), bits(xo))
+
+
+def test_failed_create_keeps_the_context_reference_count(built):
+    """a hierarchy / matrix create that fails after its object took the
+    context must give back exactly the reference it took — never one it did not — so the
+    context is torn down once, with its last user."""
+    from parallel_amg_amd import hcsr as HC
+    from parallel_amg_amd._lib import PamgError
+    from parallel_amg_amd.partitioned import Context, PSparseMatrix
+    c = Context(0)
+    assert c.refcount() == 1
+    v = PVector(c, 2, 0, np.ones(2))
+    M = HC.HCSR.from_arrays(np.array([0, 2, 4]), np.array([0, 1, 0, 1], np.int32),
+                            np.array([4.0, -1.0, -1.0, 4.0]), 2)
+    A = PSparseMatrix(c, M)
+    B = PSparseMatrix(c, HC.HCSR.from_arrays(np.array([0, 1, 2, 3]), np.array([0, 1, 2], np.int32),
+                                             np.array([2.0, 2.0, 2.0]), 3))
+    assert c.refcount() == 4
+    arrPR = (ctypes.c_void_p * 1)(A.handle.value)
+    om = np.array([2.0 / 3.0, 2.0 / 3.0])
+    ainv = np.eye(3)
+    h = ctypes.c_void_p()
+    # a NULL level is refused before anything is made
+    arrA = (ctypes.c_void_p * 2)(A.handle.value, None)
+    with pytest.raises(PamgError, match="A\\[1\\] is NULL"):
+        call("pamg_hier_create", c.handle, 2, arrA, arrPR, arrPR, om.ctypes.data_as(ctypes.c_void_p), 3,
+             ainv.ctypes.data_as(ctypes.c_void_p), 1, None, ctypes.byref(h))
+    assert c.refcount() == 4
+    # R (2 rows) does not fit the 3-row coarse level: fails after the hierarchy took the context
+    arrA = (ctypes.c_void_p * 2)(A.handle.value, B.handle.value)
+    for _ in range(3):
+        with pytest.raises(PamgError, match="shapes inconsistent"):
+            call("pamg_hier_create", c.handle, 2, arrA, arrPR, arrPR, om.ctypes.data_as(ctypes.c_void_p), 3,
+                 ainv.ctypes.data_as(ctypes.c_void_p), 1, None, ctypes.byref(h))
+        assert c.refcount() == 4
+    del B
+    assert c.refcount() == 3
+    one = (ctypes.c_void_p * 1)(A.handle.value)
+    with pytest.raises(PamgError, match="n_coarse"):  # a one-level hierarchy with the wrong coarse size
+        call("pamg_hier_create", c.handle, 1, one, None, None, om.ctypes.data_as(ctypes.c_void_p), 5,
+             ainv.ctypes.data_as(ctypes.c_void_p), 0, None, ctypes.byref(h))
+    assert c.refcount() == 3
+    # a failed plan create (send index out of range) likewise
+    from parallel_amg_amd.hierarchy import HostPlan
+    from parallel_amg_amd.partitioned import DevicePlan
+    with pytest.raises(PamgError):
+        DevicePlan(c, HostPlan(n_own=2, col0=0, ghost_ids=np.zeros(1, np.int64), nbrs=[0], recv_counts=[1],
+                               send_counts=[1], send_idx=np.array([9], np.int64)))
+    assert c.refcount() == 3
+    del A
+    assert c.refcount() == 2
+    assert np.array_equal(v.own_values(), np.ones(2))
+    del v
+    assert c.refcount() == 1
 
 
 def test_context_outlives_its_handle(built):

@@ -6,13 +6,19 @@
 # steps (each GPU step under its own time limit; the first failure ends the script):
 #   tests      the whole -m gpu suite (one process)
 #   timed      the 512^3 timed-path tests + the parity file (faster than `tests`)
-#   tp         the 512^3 timed-path tests alone (oracle parity at the benchmarked size)
+#   tp         the 512^3 timed-path tests alone (oracle parity at the benchmarked size, setup included)
+#   p8         configs[2]: the 512^3 8-part test against the oracle's 8-part setup
 #   bench      the default bench line (live PMC passes included) -> TAG/bench.json, bench.log
 #   trace      rocprofv3 --kernel-trace --stats of bench.py (5 steps, no CPU leg, no PMC)
 #   anatomy    counter anatomy of the level-0/1 row operators (A0 chain/SpMV, R0, P0, A1, R1, P1):
 #              three --pmc passes (requests by size; DRAM / L2 hits / writes; SQ wave-cycle split)
 #   part       tools/part_bench.py: one part (3 of 8 z-slabs of 512^3) timed alone (the T_8 model)
+#   gen        the general-matrix path: elastic3d 80^3 natural / permuted, 512^3 with sym_vd=0 (bench lines)
+#   gentrace   rocprofv3 kernel stats of the same three runs
+#   calib      counter calibration: tools/fetch_calib (known bytes per access width) and the row kernels
+#              (kbench) under FETCH_SIZE / WRITE_SIZE / request-size / DRAM passes -> calib.json
 #   kbench     tools/kbench.py --n 512 --levels 2 timings (KB_ARGS overrides)
+#   sell       the sorted sliced-ELL parity tests (and the ELL ones)
 #   world      the in-process device-world tests (tests/test_gpu_local_world.py)
 #   stream / chain / sub   parity subsets: streamed sweeps; chain variants; -k "$SUB_K"
 #   cab        tools/cycle_ab.py: same-box A/B of a cycle-level option (CAB_ARGS overrides)
@@ -34,7 +40,10 @@ for step in "$@"; do
         timeout -k 10 800 $PYT tests/test_gpu_timed_path.py tests/test_gpu_parity.py tests/test_gpu_local_world.py -m gpu > "$OUT/timed.log" 2>&1
         ;;
     tp)
-        timeout -k 10 500 $PYT tests/test_gpu_timed_path.py -m gpu > "$OUT/tp.log" 2>&1
+        timeout -k 10 900 $PYT -s --durations=10 tests/test_gpu_timed_path.py -m gpu > "$OUT/tp.log" 2>&1
+        ;;
+    p8)
+        timeout -k 10 1100 $PYT -s --durations=5 tests/test_gpu_configs.py -k eight_parts -m gpu > "$OUT/p8.log" 2>&1
         ;;
     stream)
         timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "sym_zm or symd_units" -m gpu > "$OUT/stream.log" 2>&1
@@ -47,6 +56,9 @@ for step in "$@"; do
         ;;
     sub)
         timeout -k 10 400 $PYT tests/test_gpu_parity.py -k "${SUB_K:-prolongator}" -m gpu > "$OUT/sub.log" 2>&1
+        ;;
+    sell)
+        timeout -k 10 400 $PYT tests/test_gpu_parity.py -k "sell or ell_restriction or ell_level1" -m gpu > "$OUT/sell.log" 2>&1
         ;;
     world)
         timeout -k 10 600 $PYT tests/test_gpu_local_world.py -m gpu > "$OUT/world.log" 2>&1
@@ -76,6 +88,41 @@ for step in "$@"; do
         ;;
     part)
         timeout -k 10 600 python3 -u tools/part_bench.py ${PART_ARGS:---n 512 --parts 8 --part 3} > "$OUT/part.json" 2> "$OUT/part.err"
+        ;;
+    gen)
+        # the general-matrix path: the elastic3d stand-in for Flan_1565 in natural
+        # and randomly renumbered order, and 512^3 without the row-class dictionary
+        timeout -k 10 400 python3 -u bench.py --kind elastic3d --grid 80 --pcg-rtol 0 > "$OUT/gen_e80.json" 2> "$OUT/gen_e80.log"
+        echo "gen e80 done"
+        timeout -k 10 400 python3 -u bench.py --kind elastic3d --grid 80 --permute 1 --pcg-rtol 0 > "$OUT/gen_e80p.json" 2> "$OUT/gen_e80p.log"
+        echo "gen e80p done"
+        timeout -k 10 600 python3 -u bench.py --set sym_vd=0 --cpu-baseline off --pcg-rtol 0 > "$OUT/gen_svd0.json" 2> "$OUT/gen_svd0.log"
+        ;;
+    gentrace)
+        for spec in "e80:--kind elastic3d --grid 80" "e80p:--kind elastic3d --grid 80 --permute 1" "svd0:--set sym_vd=0"; do
+            tag=${spec%%:*}
+            timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$tag" -o bench --output-format csv \
+                -- python3 -u bench.py ${spec#*:} --steps 5 --samples 1 --cpu-baseline off --pmc off --pcg-rtol 0 \
+                > "$OUT/prof_$tag.json" 2> "$OUT/prof_$tag.log"
+            echo "gentrace $tag done"
+        done
+        ;;
+    calib)
+        # known-byte kernels under each counter pass, then the row kernels under
+        # the same passes; tools/calib_analysis.py turns both into per-width factors and traffic
+        test -x tools/fetch_calib || hipcc --offload-arch=gfx950 -O3 -o tools/fetch_calib tools/fetch_calib.hip
+        i=0
+        for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" \
+                    "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_32B_sum"; do
+            i=$((i + 1))
+            timeout -s KILL 120 rocprofv3 --pmc $pass -d "$OUT/cal$i" -o p --output-format csv -- tools/fetch_calib \
+                > "$OUT/cal$i.jsonl" 2> "$OUT/cal$i.err"
+            echo "calib pass $i done"
+            timeout -s KILL 300 rocprofv3 --pmc $pass -d "$OUT/kb$i" -o p --output-format csv -- python3 -u tools/kbench.py $KBA \
+                > "$OUT/kb$i.jsonl" 2> "$OUT/kb$i.err"
+            echo "kbench pass $i done"
+        done
+        python3 tools/calib_analysis.py "$OUT" > "$OUT/calib.json"
         ;;
     kbench)
         timeout -k 10 400 python3 -u tools/kbench.py $KBA > "$OUT/kbench.jsonl" 2> "$OUT/kbench.err"
