@@ -3998,7 +3998,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "ell_yblock" && value >= 0 && value <= 65536) o.ell_yblock = (int)value;
     else if (k == "sell" && (value == 0 || value == 1)) o.sell = (int)value;
     else if (k == "sell_min_len" && value >= 1 && value <= 65535) o.sell_min_len = (int)value;
-    else if (k == "sell_min_rows" && value >= 1 && value <= INT32_MAX) o.sell_min_rows = (int)value;
+    else if (k == "sell_min_rows" && value >= 0 && value <= INT32_MAX) o.sell_min_rows = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
     else if (k == "chain_store_x" && (value == 0 || value == 1)) o.chain_store_x = (int)value;

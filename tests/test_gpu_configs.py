@@ -317,122 +317,3 @@ def test_config_poisson3d_512_eight_parts(built):
         assert o["lin"], f"part {p}: V(2b) != 2 V(b)"
         np.testing.assert_allclose(o["hist"], ho, rtol=1e-12)
     assert np.all(np.diff(ho) < 0) and ho[-1] < 0.5 * ho[0]
-
-
-# --------------------------------------------------------- configs[3]: aniso 256^3, 4 parts
-def test_config_aniso3d_256_four_parts(built):
-    from oracle import oracle as O
-    world, n, mc, agg, ncycles = 4, 256, 1000, 32768, 3
-    procs, q = _run(_aniso_worker, world, (n, mc, agg, ncycles))
-    # the oracle's 4-part setup runs here while the ranks set up on the GPU
-    say("oracle setup (4 parts, 16.8M rows)")
-    Ao = O.generate("aniso3d", n, n, n)
-    bo = O.spmv(Ao, O.xstar(Ao.nrows))
-    Ho = O.setup(Ao, nparts=world, max_coarse=mc, agglomerate=agg)
-    xo, ho = Ho.solve(bo, ncycles, res_hist=True)
-    say("oracle done")
-    res = _collect(procs, q, world)
-    assert all(res[r][5] == Ho.nlevels for r in range(world))
-    b = np.concatenate([res[r][2] for r in range(world)])
-    x = np.concatenate([res[r][3] for r in range(world)])
-    assert np.array_equal(bits(b), bits(bo))
-    assert np.array_equal(bits(x), bits(xo))
-    for r in range(world):
-        np.testing.assert_allclose(res[r][4], ho, rtol=1e-12)
-    assert ho[-1] < ho[0]
-
-
-# ------------------------------------------------------ configs[2]: Poisson 512^3, 8 parts
-SEED2 = 977
-
-
-def _p512_worker(rank, world, port, n, q):
-    dist = None
-    try:
-        dist = _setup_worker(rank, world, port)
-        from parallel_amg_amd.hcsr import gen_xstar
-        from parallel_amg_amd.partitioned import Context, jacobi, residual
-        be = pa.DistributedBackend()
-        A, offs, xs = pa.generate_problem(be, "poisson3d", n)
-        ctx = Context(0, be, transport="host")
-        H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000, agglomerate=32768), device=ctx)
-        del A
-        S = AMGSolver(ctx, H, part=rank)
-        A0 = S.A[0]
-        r0, r1 = int(offs[rank]), int(offs[rank + 1])
-        out = {"nlevels": H.nlevels, "rep": int(S.rep_level)}
-        # level 0, the metric's operator: SpMV / residual / Jacobi rows of this part
-        u = PVector(ctx, A0.n_own_cols, A0.n_ghost, xs[rank])
-        y = PVector(ctx, A0.nrows)
-        mul(y, A0, u)
-        out["spmv"] = digest(y.own_values())
-        c = PVector(ctx, A0.nrows, 0, gen_xstar(r0, r1 - r0, SEED2))
-        r = PVector(ctx, A0.nrows)
-        residual(r, A0, u, c)
-        out["resid"] = digest(r.own_values())
-        t = A0.new_input_vector()
-        jacobi(u, A0, c, t, S.omega[0], 1)
-        out["jacobi"] = digest(u.own_values())
-        # whole 8-part V-cycles: determinism, linearity (x 2 exact), falling residuals
-        b = y
-        x1, x2, x3 = S.new_vector(), S.new_vector(), S.new_vector()
-        h1 = S.vcycle(x1, b, 3, res_hist=True)
-        h2 = S.vcycle(x2, b, 3, res_hist=True)
-        b2 = PVector(ctx, A0.nrows, 0, 2.0 * b.own_values())
-        h3 = S.vcycle(x3, b2, 3, res_hist=True)
-        v1, v2, v3 = x1.own_values(), x2.own_values(), x3.own_values()
-        out["det"] = bool(np.array_equal(bits(v1), bits(v2)) and np.array_equal(h1, h2))
-        out["lin"] = bool(np.array_equal(bits(2.0 * v1), bits(v3)) and np.array_equal(2.0 * h1, h3))
-        out["hist"] = h1
-        q.put((rank, "ok", out))
-    except Exception:
-        import traceback
-        q.put((rank, traceback.format_exc(), None))
-    finally:
-        if dist is not None and dist.is_initialized():
-            dist.destroy_process_group()
-
-
-def test_config_poisson3d_512_eight_parts(ctx):
-    from parallel_amg_amd.hcsr import gen_xstar
-    from parallel_amg_amd.partitioned import PSparseMatrix, jacobi, residual
-    world, n = 8, 512
-    procs, q = _run(_p512_worker, world, (n,))
-    # the one-part level-0 rows of the same global operator, on this process's context
-    say("one-part 512^3 level 0")
-    be = pa.SequentialBackend(1)
-    A, offs, xs = pa.generate_problem(be, "poisson3d", n)
-    N = A[0].nrows
-    D = PSparseMatrix(ctx, A[0])
-    from parallel_amg_amd.hcsr import gershgorin
-    rho = gershgorin(A[0], 0)
-    omega = 4.0 / (3.0 * rho)
-    del A
-    u = PVector(ctx, N, 0, xs[0])
-    y = PVector(ctx, N)
-    mul(y, D, u)
-    yv = y.own_values()
-    c = PVector(ctx, N, 0, gen_xstar(0, N, SEED2))
-    r = PVector(ctx, N)
-    residual(r, D, u, c)
-    rv = r.own_values()
-    del r
-    t = PVector(ctx, N)
-    jacobi(u, D, c, t, omega, 1)
-    jv = u.own_values()
-    del D, u, y, c, t
-    say("one-part done")
-    parts = [(N * p) // world for p in range(world + 1)]
-    res = _collect(procs, q, world, timeout=900)
-    outs = [res[p][2] for p in range(world)]
-    assert len({o["nlevels"] for o in outs}) == 1 and outs[0]["nlevels"] >= 5
-    for p, o in enumerate(outs):
-        sl = slice(parts[p], parts[p + 1])
-        assert o["spmv"] == digest(yv[sl]), f"part {p}: SpMV rows differ from the one-part run"
-        assert o["resid"] == digest(rv[sl]), f"part {p}: residual rows differ"
-        assert o["jacobi"] == digest(jv[sl]), f"part {p}: Jacobi rows differ"
-        assert o["det"], f"part {p}: two 8-part V-cycle runs differ"
-        assert o["lin"], f"part {p}: V(2b) != 2 V(b)"
-        np.testing.assert_allclose(o["hist"], outs[0]["hist"], rtol=1e-12)
-    h = outs[0]["hist"]
-    assert np.all(np.diff(h) < 0) and h[-1] < 0.5 * h[0]

@@ -151,7 +151,7 @@ def test_local_world_ell_interior_rows_bit_exact(built, nparts, kind, n):
     assert np.array_equal(bits(got_x), bits(Ho.solve(bo, ncycles)))
 
 
-@pytest.mark.parametrize("nparts,kind,n", [(3, "poisson3d", 20), (4, "elastic3d", 10)])
+@pytest.mark.parametrize("nparts,kind,n", [(3, "poisson3d", 20), (2, "elastic3d", 12)])
 def test_local_world_sell_interior_rows_bit_exact(built, nparts, kind, n):
     """Several parts with every level's interior rows in the sorted sliced ELL (sell_min_len 1,
     sell_min_rows 0; the symmetric, ELL and neighbour-coded layouts off): the boundary rows carry the
@@ -166,6 +166,7 @@ def test_local_world_sell_interior_rows_bit_exact(built, nparts, kind, n):
             A, offs, xs = pa.generate_problem(be, kind, n)
             H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=60, agglomerate=0), device=W.ctxs[0])
             S = [AMGSolver(W.ctxs[p], H, part=p) for p in range(nparts)]
+            # (a part keeps the tiles where fewer than 3/4 of its rows are interior)
             assert any(layout_of(s.A_dev[0])["sell"] for s in S)
             A0 = [s.A_dev[0] for s in S]
             xst = [PVector(W.ctxs[p], A0[p].n_own_cols, A0[p].n_ghost, xs[p]) for p in range(nparts)]

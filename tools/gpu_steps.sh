@@ -14,6 +14,7 @@
 #              three --pmc passes (requests by size; DRAM / L2 hits / writes; SQ wave-cycle split)
 #   part       tools/part_bench.py: one part (3 of 8 z-slabs of 512^3) timed alone (the T_8 model)
 #   gen        the general-matrix path: elastic3d 80^3 natural / permuted, 512^3 with sym_vd=0 (bench lines)
+#   cfgs       bench lines of configs[1] (128^3) and configs[3]'s operator (aniso 256^3) on one GPU
 #   gentrace   rocprofv3 kernel stats of the same three runs
 #   calib      counter calibration: tools/fetch_calib (known bytes per access width) and the row kernels
 #              (kbench) under FETCH_SIZE / WRITE_SIZE / request-size / DRAM passes -> calib.json
@@ -97,6 +98,14 @@ for step in "$@"; do
         timeout -k 10 400 python3 -u bench.py --kind elastic3d --grid 80 --permute 1 --pcg-rtol 0 > "$OUT/gen_e80p.json" 2> "$OUT/gen_e80p.log"
         echo "gen e80p done"
         timeout -k 10 600 python3 -u bench.py --set sym_vd=0 --cpu-baseline off --pcg-rtol 0 > "$OUT/gen_svd0.json" 2> "$OUT/gen_svd0.log"
+        echo "gen svd0 done"
+        ;;
+    cfgs)
+        # the other BASELINE configs at one GPU (bench lines with their oracle parity and CPU baseline)
+        timeout -k 10 300 python3 -u bench.py --grid 128 > "$OUT/cfg_p128.json" 2> "$OUT/cfg_p128.log"
+        echo "cfg p128 done"
+        timeout -k 10 500 python3 -u bench.py --kind aniso3d --grid 256 > "$OUT/cfg_a256.json" 2> "$OUT/cfg_a256.log"
+        echo "cfg a256 done"
         ;;
     gentrace)
         for spec in "e80:--kind elastic3d --grid 80" "e80p:--kind elastic3d --grid 80 --permute 1" "svd0:--set sym_vd=0"; do
