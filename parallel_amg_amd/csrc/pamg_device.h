@@ -105,6 +105,9 @@ struct TileSet {
     // sorted sliced ELL with plain values (pamg_mat::sell; long-row operators the ELL dictionaries do not
     // fit, e.g. the 512^3 R1): the set's rows run in k_rows_sell instead of tiles
     bool sell = false;
+    // long rows with LDS-staged products (pamg_mat::d_rowptr / d_col / d_val, the CSR copy; long-row
+    // operators the ELL dictionaries do not fit, e.g. the 512^3 R1): the set's rows run in k_rows_lsr
+    bool lsr = false;
     int max_short_len = 0;    // longest row in a short tile
     int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
@@ -156,6 +159,12 @@ struct Options {
     int sell = 1;              // 1: sorted sliced ELL (SellSet) for long-row operators the other layouts decline
     int sell_min_len = 96;     // ... with at least this many nonzeros per row on average
     int sell_min_rows = 32768; // ... and at least this many rows
+    int sell_sort = 1;         // 1: rows ordered longest first within each group (less padding); 0: row order
+    int lsr = 1;               // 1: long rows with LDS-staged products (TileSet::lsr) for long-row operators the
+                               //    ELL dictionaries decline (before sell)
+    int lsr_min_len = 96;      // ... with at least this many nonzeros per row on average
+    int lsr_min_rows = 32768;  // ... and at least this many rows
+    int lsr_chunk = 32;        // elements per row per LDS chunk of k_rows_lsr (16 | 32); read at launch
 };
 
 // Symmetric diagonal-class layout (k_rows_sym): a square operator whose interior rows use at
@@ -358,6 +367,7 @@ struct pamg_mat {
     uint16_t* d_anc16 = nullptr;  // per-tile anchored dictionaries: row's first column - tile base
     double* d_val = nullptr;
     double* d_diag = nullptr;  // a_ii for square matrices (zero-guess Jacobi), else null
+    uint8_t* d_lsr_skip = nullptr;  // TileSet::lsr with boundary rows: 1 for a row the tiles compute
     const pamg_plan* plan = nullptr;
     pamg::SymDia sym;        // the interior set's symmetric diagonal-class layout (TileSet::sym)
     pamg::TileSet interior;  // rows with own columns only (overlap with the exchange)

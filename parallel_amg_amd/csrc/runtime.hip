@@ -1489,7 +1489,8 @@ int build_sell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* va
                 if (rp[i + 1] - rp[i] > pamg::kSellMaxLen) ok = false;
                 r.push_back((int)i);
             }
-            std::stable_sort(r.begin(), r.end(), [&](int p, int q) { return rp[p + 1] - rp[p] > rp[q + 1] - rp[q]; });
+            if (pamg::options().sell_sort)
+                std::stable_sort(r.begin(), r.end(), [&](int p, int q) { return rp[p + 1] - rp[p] > rp[q + 1] - rp[q]; });
             for (size_t j = 0; j < r.size(); ++j) {
                 row[g * kEllGroup + (int64_t)j] = r[j];
                 len[g * kEllGroup + (int64_t)j] = (uint16_t)(rp[r[j] + 1] - rp[r[j]]);
@@ -3080,8 +3081,25 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         tr.mark("pnc");
     }
     // long rows the ELL dictionaries decline (512^3 R1: ~190 per row, tens of thousands of values per
-    // group): sorted sliced ELL with plain values and int32 columns
-    if (pamg::options().sell && !A->interior.sym && !A->interior.ell && !A->interior.pnc && !inner.empty() &&
+    // group): the CSR copy with LDS-staged products (k_rows_lsr), else the sorted sliced ELL
+    int64_t lsr_nnz = 0;
+    if (pamg::options().lsr && !A->interior.sym && !A->interior.ell && !A->interior.pnc && !inner.empty() &&
+        nrows >= pamg::options().lsr_min_rows && (int64_t)inner.size() * 4 >= (int64_t)nrows * 3) {
+        for (int i : inner) lsr_nnz += rp[i + 1] - rp[i];
+        if (lsr_nnz >= (int64_t)pamg::options().lsr_min_len * (int64_t)inner.size()) {
+            A->interior.lsr = true;
+            A->interior.rows_short = (int64_t)inner.size();
+            if (!bnd.empty()) {  // (several parts: the boundary rows run in tiles after the exchange)
+                std::vector<uint8_t> skip(nrows + kVecPad, 0);
+                for (int i : bnd) skip[i] = 1;
+                CHECK(dalloc(&A->d_lsr_skip, nrows + kVecPad));
+                CHECK(h2d(ctx, A->d_lsr_skip, skip.data(), skip.size()));
+            }
+            inner.clear();  // the rows run in k_rows_lsr, not in tiles
+            tr.mark("lsr");
+        }
+    }
+    if (pamg::options().sell && !A->interior.sym && !A->interior.ell && !A->interior.pnc && !A->interior.lsr && !inner.empty() &&
         nrows >= pamg::options().sell_min_rows && (int64_t)inner.size() * 4 >= (int64_t)nrows * 3) {
         int64_t nz_in = 0;
         for (int i : inner) nz_in += rp[i + 1] - rp[i];
@@ -3093,7 +3111,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     }
     // the CSR copies: read by the tile and long-row kernels only, so not uploaded when every row
     // runs in the symmetric, ELL or neighbour-coded layout (the 512^3 A0, A1, R0, P0: 29 GB less)
-    if (!inner.empty() || !bnd.empty()) {
+    if (!inner.empty() || !bnd.empty() || A->interior.lsr) {
         std::vector<int> rp32(nrows + 1);
         par_for(nrows + 1, [&](int64_t a, int64_t b) {
             for (int64_t i = a; i < b; ++i) rp32[i] = (int)rp[i];
@@ -3158,11 +3176,13 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
                            8 * A->ell.vtab_n + (A->ell.d_anc ? 4 * nrows : 0);
     // neighbour-coded prolongation: the anchor and the record per row, the two tables
     if (A->interior.pnc) A->stream_bytes += 12 * nrows + 4 * A->pnc.npat + 8 * A->pnc.nval;
+    // LDS-staged long rows: the CSR copy's 12 B per nonzero and row pointers (+ the skip flags)
+    if (A->interior.lsr) A->stream_bytes += 12 * lsr_nnz + 4 * (nrows + 1) + (A->d_lsr_skip ? nrows : 0);
     // sorted sliced ELL: 12 B per padded element, the row and length per position, the slice descriptors
     if (A->interior.sell)
         A->stream_bytes += 12 * A->sell.elems + 6 * A->sell.ngroups * pamg::kEllGroup + 8 * A->sell.nslices;
     for (const pamg::TileSet* t : {&A->interior, &A->boundary}) {
-        if (t->sym || t->ell || t->pnc || t->sell) continue;  // counted above
+        if (t->sym || t->ell || t->pnc || t->sell || t->lsr) continue;  // counted above
         const int64_t ns = t->n_short, nz = t->nnz_short;
         int64_t b = 8 * (int64_t)t->n_long + 12 * t->nnz_long;
         const bool base = t->c24 && !t->cd;
@@ -3283,6 +3303,7 @@ int pamg_mat_destroy(pamg_mat* A) {
     free_ell(A->ell);
     free_pnc(A->pnc);
     free_sell(A->sell);
+    dfree(A->d_lsr_skip);
     pamg_ctx* owner = A->ctx;
     delete A;
     ctx_unref(owner);
@@ -3317,9 +3338,11 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
              (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0) |
-             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0) | (t.pnc ? 1024 : 0) | (t.sell ? 2048 : 0);
+             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0) | (t.pnc ? 1024 : 0) | (t.sell ? 2048 : 0) |
+             (t.lsr ? 4096 : 0);
     if (t.ell) out[8] = (int)A->ell.ngroups;  // k_rows_ell's grid
     if (t.sell) out[8] = (int)A->sell.ngroups;  // k_rows_sell's grid
+    if (t.lsr) out[8] = (int)((A->nrows + pamg::kBlock - 1) / pamg::kBlock);  // k_rows_lsr's workgroups
     if (t.pnc) {  // the pattern and value tables, k_rows_pnc's grid
         out[3] = A->pnc.nval;
         out[4] = A->pnc.npat;
@@ -3997,6 +4020,11 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "pnc" && (value == 0 || value == 1)) o.pnc = (int)value;
     else if (k == "ell_yblock" && value >= 0 && value <= 65536) o.ell_yblock = (int)value;
     else if (k == "sell" && (value == 0 || value == 1)) o.sell = (int)value;
+    else if (k == "sell_sort" && (value == 0 || value == 1)) o.sell_sort = (int)value;
+    else if (k == "lsr" && (value == 0 || value == 1)) o.lsr = (int)value;
+    else if (k == "lsr_min_len" && value >= 1 && value <= 65535) o.lsr_min_len = (int)value;
+    else if (k == "lsr_min_rows" && value >= 0 && value <= INT32_MAX) o.lsr_min_rows = (int)value;
+    else if (k == "lsr_chunk" && (value == 16 || value == 32)) o.lsr_chunk = (int)value;
     else if (k == "sell_min_len" && value >= 1 && value <= 65535) o.sell_min_len = (int)value;
     else if (k == "sell_min_rows" && value >= 0 && value <= INT32_MAX) o.sell_min_rows = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
@@ -4038,6 +4066,11 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "pnc") *value = o.pnc;
     else if (k == "ell_yblock") *value = o.ell_yblock;
     else if (k == "sell") *value = o.sell;
+    else if (k == "sell_sort") *value = o.sell_sort;
+    else if (k == "lsr") *value = o.lsr;
+    else if (k == "lsr_min_len") *value = o.lsr_min_len;
+    else if (k == "lsr_min_rows") *value = o.lsr_min_rows;
+    else if (k == "lsr_chunk") *value = o.lsr_chunk;
     else if (k == "sell_min_len") *value = o.sell_min_len;
     else if (k == "sell_min_rows") *value = o.sell_min_rows;
     else if (k == "ell_min_rows") *value = o.ell_min_rows;
