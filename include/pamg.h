@@ -206,11 +206,7 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * then out[8] = the kernel's grid); bit 10: the set runs in the neighbour-coded prolongation layout
  * (pnc: a prolongation over a 7-point grid uploaded earlier on the same context, each column named
  * by the grid neighbour whose anchor it is; then out[3] = the value table's entries, out[4] = the
- * pattern table's, out[8] = the kernel's grid); bit 11: the set runs in the sorted sliced-ELL layout
- * with plain values (sell: rows longest first within 256-row groups, int32 columns, f64 values;
- * then out[8] = the kernel's grid); bit 12: the set runs from the CSR copy with LDS-staged products
- * (lsr: a wave per 64 rows, chunks of each row loaded coalesced, every lane summing its own row;
- * then out[8] = the kernel's workgroups). */
+ * pattern table's, out[8] = the kernel's grid). */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[10]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
@@ -304,12 +300,7 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
  * large square operators with all own columns), "ell_restrict" (0 | 1: also restrictions, with
  * anchored offsets), "ell_min_rows" (rows from which ELL is taken), "ell_yblock" (0 | lines: the
  * blocked group order of a restriction over a grid), "pnc" (0 | 1: neighbour-coded
- * prolongations over a grid uploaded earlier on the context), "sell" (0 | 1: sorted sliced ELL
- * with plain values for long-row operators the others decline), "sell_min_len" (mean nonzeros per
- * row from which it is taken), "sell_min_rows" (rows from which it is taken), "sell_sort" (0 | 1:
- * rows longest first within each group), "lsr" (0 | 1: long rows with LDS-staged products, taken
- * before sell), "lsr_min_len", "lsr_min_rows" (its thresholds). Read at launch: "lsr_chunk"
- * (16 | 32 elements per row per LDS chunk),
+ * prolongations over a grid uploaded earlier on the context). Read at launch:
  * "sym_zm" (0 | 1: z-marching single sweeps of the symmetric layout), "zm_chunks" (0 = auto |
  * z chunks per column of k_sym_zm), "tb_xfast" (0 | 1: x-fastest tile order of the chain),
  * "symd_chunks" (1 | 2 | 4), "chain_store_x" (0 | 1). Applied at every exchange:

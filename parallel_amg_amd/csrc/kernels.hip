@@ -1777,179 +1777,6 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __
     if (in) y[i] = out;
 }
 
-// k_rows_sell: the sorted sliced-ELL layout with plain values (pamg::SellSet; round 6, the 512^3 R1).
-// A workgroup = a group of kEllGroup rows, sorted longest first into 4 slices of kEllW; a lane walks
-// its row: per step 4 elements, their columns and values coalesced across the wave (the k-th
-// elements of the slice's 64 rows are contiguous: 256 B of columns, 512 B of values), the next 4
-// in flight, x gathered at each column (a padded element's column is its row's last: a line the
-// row already reads), products summed left to right from +0.0 in storage order and the padding
-// selected away (SPEC §S3 bits, as every row kernel). Groups in XCD-contiguous order (k_rows_ell).
-template <int OP>
-__global__ __launch_bounds__(kEllGroup) void k_rows_sell(const int2* __restrict__ smeta, const int* __restrict__ col,
-                                                         const double* __restrict__ val, const int* __restrict__ rows,
-                                                         const uint16_t* __restrict__ lens, int ngroups,
-                                                         const double* __restrict__ x, const double* __restrict__ b,
-                                                         double* __restrict__ y, double omega) {
-    const int per = (ngroups + 7) / 8;
-    const int g = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (g >= ngroups) return;
-    const int pos = g * kEllGroup + threadIdx.x, lane = threadIdx.x & 63;
-    const int L16 = lens[pos];
-    const bool in = L16 != kSellSkip;
-    const int L = in ? L16 : 0;
-    const int row = in ? rows[pos] : 0;
-    const int2 sm = smeta[pos / kEllW];  // (one slice per wave: sm.y is wave-uniform)
-    const int* __restrict__ cp = col + sm.x + lane;
-    const double* __restrict__ vp = val + sm.x + lane;
-    double pb = 0.0, px = 0.0, py = 0.0;
-    if (in) {
-        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[row];
-        if constexpr (OP == OP_JACOBI) px = x[row];
-        if constexpr (OP == OP_PROLONG) py = y[row];
-    }
-    const int nq = (sm.y + 3) >> 2;
-    int c4[4];
-    double v4[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        c4[e] = e < sm.y ? cp[e * kEllW] : 0;
-        v4[e] = e < sm.y ? vp[e * kEllW] : 0.0;
-    }
-    double s = 0.0, dg = 0.0;
-    for (int q = 0; q < nq; ++q) {
-        int cq[4];
-        double vq[4], xv[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            cq[e] = c4[e];
-            vq[e] = v4[e];
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {  // the next 4 elements in flight while these are used
-            const int k = 4 * (q + 1) + e;
-            if (k < sm.y) {
-                c4[e] = cp[k * kEllW];
-                v4[e] = vp[k * kEllW];
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) xv[e] = x[4 * q + e < sm.y ? cq[e] : cq[0]];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const bool ok = 4 * q + e < L;
-            const double p = vq[e] * xv[e];
-            const double t = s + p;
-            s = ok ? t : s;
-            if constexpr (OP == OP_JACOBI) dg = ok && cq[e] == row ? vq[e] : dg;
-        }
-    }
-    double out;
-    if constexpr (OP == OP_SPMV) {
-        out = s;
-    } else if constexpr (OP == OP_RESID) {
-        out = pb - s;
-    } else if constexpr (OP == OP_JACOBI) {
-        const double u = pb - s;
-        const double v = omega * u;
-        const double w = v / dg;
-        out = px + w;
-    } else {
-        out = py + s;
-    }
-    if (in) y[row] = out;
-}
-
-// k_rows_lsr: long rows with their products staged in LDS (pamg::TileSet::lsr; round 6, the 512^3 R1:
-// ~190 nonzeros per row, values all distinct). A wave owns 64 consecutive rows of the set's CSR copy.
-// Per chunk of CH elements of every row: CH load instructions, each covering 64 / CH rows with CH
-// consecutive elements per row (columns and values coalesced; a row's consecutive entries gather x
-// from few lines), each product rounded and stored at LDS [row][k]; then every lane adds its own
-// row's CH products left to right to its running sum (SPEC §S3 order: the products rounded, summed
-// from +0.0 in storage order) — the wave's 64 rows' dependent add chains advance together instead of
-// one row at a time. Hand-offs between the two phases are wave-local (no workgroup barrier).
-template <int OP, int CH>
-__global__ __launch_bounds__(kBlock) void k_rows_lsr(int nrows, const int* __restrict__ rowptr, const int* __restrict__ col,
-                                                     const double* __restrict__ val, const uint8_t* __restrict__ skip,
-                                                     const double* __restrict__ x, const double* __restrict__ b,
-                                                     double* __restrict__ y, double omega) {
-    constexpr int RPI = 64 / CH;  // rows per load instruction
-    __shared__ double prod[kBlock / 64][64][CH + 1];
-    __shared__ int rs[kBlock / 64][64], rl[kBlock / 64][64];
-    __shared__ double dgl[OP == OP_JACOBI ? kBlock / 64 : 1][64];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // XCD-contiguous block order (block b runs on XCD b % 8 and takes the (b / 8)-th block of that
-    // XCD's eighth of the rows)
-    const int nblk = (nrows + kBlock - 1) / kBlock;
-    const int per = (nblk + 7) / 8;
-    const int blk = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (blk >= nblk) return;  // the whole workgroup (no workgroup barrier below)
-    const int r0 = blk * kBlock + w * 64, row = r0 + lane;
-    const bool in = row < nrows && !(skip && skip[row]);
-    const int a = in ? rowptr[row] : 0;
-    const int L = in ? rowptr[row + 1] - a : 0;
-    rs[w][lane] = a;
-    rl[w][lane] = L;
-    if constexpr (OP == OP_JACOBI) dgl[OP == OP_JACOBI ? w : 0][lane] = 0.0;
-    int m = L;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
-    double pb = 0.0, px = 0.0, py = 0.0;
-    if (in) {
-        if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[row];
-        if constexpr (OP == OP_JACOBI) px = x[row];
-        if constexpr (OP == OP_PROLONG) py = y[row];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int sub = lane / CH, kk = lane % CH;
-    double s = 0.0;
-    for (int c = 0; c < m; c += CH) {
-        // branch-free: an element past its row's end loads element 0 (a line in cache) and stores a
-        // product that the sum below selects away, so the loads of the unrolled iterations batch
-        for (int i0 = 0; i0 < CH; i0 += 16)
-#pragma unroll
-        for (int i = i0; i < i0 + 16; ++i) {
-            const int r = i * RPI + sub;
-            const int k = c + kk;
-            const bool ok = k < rl[w][r];
-            const int e = ok ? rs[w][r] + k : 0;
-            const int cc = col[e];
-            const double v = val[e];
-            const double p = v * x[cc];
-            if constexpr (OP == OP_JACOBI)
-                if (ok && cc == r0 + r) dgl[OP == OP_JACOBI ? w : 0][r] = v;
-            prod[w][r][kk] = p;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int n = min(CH, L - c);
-#pragma unroll
-        for (int k = 0; k < CH; ++k) {
-            const double t = s + prod[w][lane][k];
-            s = k < n ? t : s;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    double out;
-    if constexpr (OP == OP_SPMV) {
-        out = s;
-    } else if constexpr (OP == OP_RESID) {
-        out = pb - s;
-    } else if constexpr (OP == OP_JACOBI) {
-        const double u = pb - s;
-        const double v = omega * u;
-        const double wq = v / dgl[OP == OP_JACOBI ? w : 0][lane];
-        out = px + wq;
-    } else {
-        out = py + s;
-    }
-    if (in) y[row] = out;
-}
-
 // k_rows_pnc: the neighbour-coded prolongation (pamg::PncSet; round 5, the 512^3 P0). One row per
 // lane, about 8 workgroups per CU, each staging the two global tables (<= 1024 pattern words, <= 128
 // values) in LDS once and then walking 256-row blocks: at step t the workgroups of XCD j (block b
@@ -2487,21 +2314,6 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
                                                                y, omega);
     }
     if (ts.pnc) launch_pnc<OP>(A, x, b, y, omega, s);
-    if (ts.lsr) {
-        const int grid = (int)(((A.nrows + kBlock - 1) / kBlock + 7) / 8 * 8);
-        if (options().lsr_chunk == 16)
-            k_rows_lsr<OP, 16><<<grid, kBlock, 0, s>>>((int)A.nrows, A.d_rowptr, A.d_col, A.d_val, A.d_lsr_skip, x, b, y,
-                                                      omega);
-        else
-            k_rows_lsr<OP, 32><<<grid, kBlock, 0, s>>>((int)A.nrows, A.d_rowptr, A.d_col, A.d_val, A.d_lsr_skip, x, b, y,
-                                                      omega);
-    }
-    if (ts.sell) {
-        const SellSet& E = A.sell;
-        const int grid = (int)((E.ngroups + 7) / 8 * 8);
-        k_rows_sell<OP><<<grid, kEllGroup, 0, s>>>(E.d_smeta, E.d_col, E.d_val, E.d_row, E.d_len, (int)E.ngroups, x, b,
-                                                   y, omega);
-    }
     if (ts.n_short > 0) {
         if (ts.tile_nnz == 1024) launch_tile<OP, 1024>(A, ts, x, b, y, omega, s);
         else if (ts.tile_nnz == 4096) launch_tile<OP, 4096>(A, ts, x, b, y, omega, s);

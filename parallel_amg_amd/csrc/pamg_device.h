@@ -102,12 +102,6 @@ struct TileSet {
     // neighbour-coded prolongation (pamg_mat::pnc; the whole set of a prolongation over a registered grid):
     // the rows run in k_rows_pnc instead of tiles
     bool pnc = false;
-    // sorted sliced ELL with plain values (pamg_mat::sell; long-row operators the ELL dictionaries do not
-    // fit, e.g. the 512^3 R1): the set's rows run in k_rows_sell instead of tiles
-    bool sell = false;
-    // long rows with LDS-staged products (pamg_mat::d_rowptr / d_col / d_val, the CSR copy; long-row
-    // operators the ELL dictionaries do not fit, e.g. the 512^3 R1): the set's rows run in k_rows_lsr
-    bool lsr = false;
     int max_short_len = 0;    // longest row in a short tile
     int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
@@ -156,15 +150,6 @@ struct Options {
     int pnc = 1;               // 1: neighbour-coded prolongations over a grid registered on the context (PncSet)
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
-    int sell = 1;              // 1: sorted sliced ELL (SellSet) for long-row operators the other layouts decline
-    int sell_min_len = 96;     // ... with at least this many nonzeros per row on average
-    int sell_min_rows = 32768; // ... and at least this many rows
-    int sell_sort = 1;         // 1: rows ordered longest first within each group (less padding); 0: row order
-    int lsr = 1;               // 1: long rows with LDS-staged products (TileSet::lsr) for long-row operators the
-                               //    ELL dictionaries decline (before sell)
-    int lsr_min_len = 96;      // ... with at least this many nonzeros per row on average
-    int lsr_min_rows = 32768;  // ... and at least this many rows
-    int lsr_chunk = 32;        // elements per row per LDS chunk of k_rows_lsr (16 | 32); read at launch
 };
 
 // Symmetric diagonal-class layout (k_rows_sym): a square operator whose interior rows use at
@@ -231,26 +216,6 @@ struct EllSet {
 // the k-th entry's neighbour code), bits 10 + 7k the k-th entry's value index (a global table of
 // <= kPncValMax bit patterns). 12 B per row against 3.5 B per nonzero + 1 B per row in tiles. Rows
 // keep their storage order (SPEC S3 sums).
-// Sorted sliced ELL with plain values (Options::sell; round 6, the 512^3 R1: ~190 nonzeros per row,
-// tens of thousands of distinct values per 256 rows and columns spread over 2^18, so neither the ELL
-// dictionaries nor 16-bit offsets fit). Rows in groups of kEllGroup consecutive rows (a workgroup);
-// inside a group the rows are ordered by length, longest first (stable), and cut into slices of kEllW
-// (one row per lane, a wave each), each slice padded to its first row's length — so a slice's rows
-// have about one length and the padding stays small (512^3 R1 ~2 % against ~20 % in row order).
-// Element k of the slice's lane-th row: column d_col[start + k * kEllW + lane] (int32, absolute) and
-// value d_val[...] (f64); a padded element repeats the row's last column with value 0 and is selected
-// away. Per sorted position: the row (d_row) and its length (d_len; kSellSkip: a position with no row,
-// or a part's boundary row computed by the tiles after the exchange). Rows keep their storage order.
-constexpr int kSellSkip = 0xffff, kSellMaxLen = 0xfffe;
-struct SellSet {
-    int64_t nslices = 0, ngroups = 0, elems = 0;
-    int2* d_smeta = nullptr;   // per slice: (first element of its streams, padded length)
-    int* d_col = nullptr;
-    double* d_val = nullptr;
-    int* d_row = nullptr;      // per sorted position (ngroups * kEllGroup)
-    uint16_t* d_len = nullptr; // per sorted position
-};
-
 constexpr int kPncPatMax = 1024, kPncValMax = 128, kPncMaxLen = 7;
 constexpr int kPncSkip = kPncPatMax - 1;  // pattern id of a row outside the set (several parts: a boundary row)
 struct PncSet {
@@ -367,14 +332,12 @@ struct pamg_mat {
     uint16_t* d_anc16 = nullptr;  // per-tile anchored dictionaries: row's first column - tile base
     double* d_val = nullptr;
     double* d_diag = nullptr;  // a_ii for square matrices (zero-guess Jacobi), else null
-    uint8_t* d_lsr_skip = nullptr;  // TileSet::lsr with boundary rows: 1 for a row the tiles compute
     const pamg_plan* plan = nullptr;
     pamg::SymDia sym;        // the interior set's symmetric diagonal-class layout (TileSet::sym)
     pamg::TileSet interior;  // rows with own columns only (overlap with the exchange)
     pamg::TileSet boundary;  // rows with >= 1 ghost column
     pamg::EllSet ell;        // the interior set's sliced-ELL layout (TileSet::ell)
     pamg::PncSet pnc;        // the neighbour-coded prolongation layout (TileSet::pnc)
-    pamg::SellSet sell;      // the interior set's sorted sliced-ELL layout (TileSet::sell)
     int64_t stream_bytes = 0;  // matrix bytes one apply reads (values, columns, row pointers, tiles)
 };
 

@@ -1461,88 +1461,6 @@ int build_ell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
     return PAMG_OK;
 }
 
-// Sorted sliced ELL with plain values (Options::sell, pamg::SellSet): the interior rows of an
-// operator with long rows that the ELL dictionaries decline. Within each group of kEllGroup rows the
-// rows are ordered longest first (stable), cut into slices of kEllW padded to their longest row.
-// Declines (leaves the tiles to the caller) where a row exceeds kSellMaxLen or a stream index 2^31.
-int build_sell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val, const std::vector<int>& inner) {
-    using pamg::kEllGroup;
-    using pamg::kEllW;
-    using pamg::kSellSkip;
-    const int64_t n = A->nrows;
-    std::vector<char> in_set;
-    if ((int64_t)inner.size() != n) {
-        in_set.assign(n, 0);
-        for (int i : inner) in_set[i] = 1;
-    }
-    auto member = [&](int64_t i) { return in_set.empty() || in_set[i]; };
-    const int64_t ng = (n + kEllGroup - 1) / kEllGroup, npos = ng * kEllGroup, ns = npos / kEllW;
-    std::vector<int> row(npos, 0);
-    std::vector<uint16_t> len(npos, (uint16_t)kSellSkip);
-    std::atomic<bool> ok{true};
-    par_for(ng, [&](int64_t a, int64_t b) {
-        std::vector<int> r;
-        for (int64_t g = a; g < b; ++g) {
-            r.clear();
-            for (int64_t i = g * kEllGroup; i < std::min(n, (g + 1) * kEllGroup); ++i) {
-                if (!member(i)) continue;
-                if (rp[i + 1] - rp[i] > pamg::kSellMaxLen) ok = false;
-                r.push_back((int)i);
-            }
-            if (pamg::options().sell_sort)
-                std::stable_sort(r.begin(), r.end(), [&](int p, int q) { return rp[p + 1] - rp[p] > rp[q + 1] - rp[q]; });
-            for (size_t j = 0; j < r.size(); ++j) {
-                row[g * kEllGroup + (int64_t)j] = r[j];
-                len[g * kEllGroup + (int64_t)j] = (uint16_t)(rp[r[j] + 1] - rp[r[j]]);
-            }
-        }
-    });
-    if (!ok) return PAMG_OK;
-    std::vector<int2> smeta(ns);
-    int64_t elems = 0;
-    for (int64_t q = 0; q < ns; ++q) {
-        int m = 0;
-        for (int64_t j = q * kEllW; j < (q + 1) * kEllW; ++j)
-            if (len[j] != kSellSkip) m = std::max<int>(m, len[j]);
-        smeta[q] = make_int2((int)elems, m);
-        elems += (int64_t)kEllW * m;
-        if (elems >= INT32_MAX) return PAMG_OK;
-    }
-    std::vector<int> col(elems + 1, 0);
-    std::vector<double> v(elems + 1, 0.0);
-    par_for(ns, [&](int64_t a, int64_t b) {
-        for (int64_t q = a; q < b; ++q)
-            for (int lane = 0; lane < kEllW; ++lane) {
-                const int64_t j = q * kEllW + lane;
-                const int L = len[j] == kSellSkip ? 0 : len[j];
-                const int64_t r0 = L ? rp[row[j]] : 0;
-                const int pad_col = L ? ci[r0 + L - 1] : 0;  // a padded element re-reads the row's last x
-                for (int k = 0; k < smeta[q].y; ++k) {
-                    const int64_t e = smeta[q].x + (int64_t)k * kEllW + lane;
-                    col[e] = k < L ? ci[r0 + k] : pad_col;
-                    v[e] = k < L ? val[r0 + k] : 0.0;
-                }
-            }
-    });
-    pamg::SellSet& E = A->sell;
-    pamg_ctx* ctx = A->ctx;
-    E.nslices = ns;
-    E.ngroups = ng;
-    E.elems = elems;
-    CHECK(dalloc(&E.d_smeta, ns));
-    CHECK(dalloc(&E.d_col, elems + 1));
-    CHECK(dalloc(&E.d_val, elems + 1));
-    CHECK(dalloc(&E.d_row, npos));
-    CHECK(dalloc(&E.d_len, npos));
-    CHECK(h2d(ctx, E.d_smeta, smeta.data(), sizeof(int2) * ns));
-    CHECK(h2d(ctx, E.d_col, col.data(), sizeof(int) * (elems + 1)));
-    CHECK(h2d(ctx, E.d_val, v.data(), sizeof(double) * (elems + 1)));
-    CHECK(h2d(ctx, E.d_row, row.data(), sizeof(int) * npos));
-    CHECK(h2d(ctx, E.d_len, len.data(), sizeof(uint16_t) * npos));
-    A->interior.sell = true;
-    return PAMG_OK;
-}
-
 // Neighbour-coded prolongation (Options::pnc, pamg::PncSet): every row's columns named by the
 // grid neighbours whose anchors they are. Declines (leaves the tile layouts to the caller) where a
 // row is longer than kPncMaxLen, a column is no neighbour's anchor, or a table would overflow.
@@ -1703,15 +1621,6 @@ void free_ell(pamg::EllSet& E) {
     dfree(E.d_vtab);
     dfree(E.d_anc);
     E = pamg::EllSet{};
-}
-
-void free_sell(pamg::SellSet& E) {
-    dfree(E.d_smeta);
-    dfree(E.d_col);
-    dfree(E.d_val);
-    dfree(E.d_row);
-    dfree(E.d_len);
-    E = pamg::SellSet{};
 }
 
 void free_tiles(pamg::TileSet& ts) {
@@ -3080,38 +2989,9 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         if (A->interior.pnc) inner.clear();  // the rows run in k_rows_pnc, not in tiles
         tr.mark("pnc");
     }
-    // long rows the ELL dictionaries decline (512^3 R1: ~190 per row, tens of thousands of values per
-    // group): the CSR copy with LDS-staged products (k_rows_lsr), else the sorted sliced ELL
-    int64_t lsr_nnz = 0;
-    if (pamg::options().lsr && !A->interior.sym && !A->interior.ell && !A->interior.pnc && !inner.empty() &&
-        nrows >= pamg::options().lsr_min_rows && (int64_t)inner.size() * 4 >= (int64_t)nrows * 3) {
-        for (int i : inner) lsr_nnz += rp[i + 1] - rp[i];
-        if (lsr_nnz >= (int64_t)pamg::options().lsr_min_len * (int64_t)inner.size()) {
-            A->interior.lsr = true;
-            A->interior.rows_short = (int64_t)inner.size();
-            if (!bnd.empty()) {  // (several parts: the boundary rows run in tiles after the exchange)
-                std::vector<uint8_t> skip(nrows + kVecPad, 0);
-                for (int i : bnd) skip[i] = 1;
-                CHECK(dalloc(&A->d_lsr_skip, nrows + kVecPad));
-                CHECK(h2d(ctx, A->d_lsr_skip, skip.data(), skip.size()));
-            }
-            inner.clear();  // the rows run in k_rows_lsr, not in tiles
-            tr.mark("lsr");
-        }
-    }
-    if (pamg::options().sell && !A->interior.sym && !A->interior.ell && !A->interior.pnc && !A->interior.lsr && !inner.empty() &&
-        nrows >= pamg::options().sell_min_rows && (int64_t)inner.size() * 4 >= (int64_t)nrows * 3) {
-        int64_t nz_in = 0;
-        for (int i : inner) nz_in += rp[i + 1] - rp[i];
-        if (nz_in >= (int64_t)pamg::options().sell_min_len * (int64_t)inner.size()) {
-            CHECK(build_sell(A.get(), rp, ci, val, inner));
-            if (A->interior.sell) inner.clear();  // the rows run in k_rows_sell, not in tiles
-            tr.mark("sell");
-        }
-    }
     // the CSR copies: read by the tile and long-row kernels only, so not uploaded when every row
     // runs in the symmetric, ELL or neighbour-coded layout (the 512^3 A0, A1, R0, P0: 29 GB less)
-    if (!inner.empty() || !bnd.empty() || A->interior.lsr) {
+    if (!inner.empty() || !bnd.empty()) {
         std::vector<int> rp32(nrows + 1);
         par_for(nrows + 1, [&](int64_t a, int64_t b) {
             for (int64_t i = a; i < b; ++i) rp32[i] = (int)rp[i];
@@ -3176,13 +3056,8 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
                            8 * A->ell.vtab_n + (A->ell.d_anc ? 4 * nrows : 0);
     // neighbour-coded prolongation: the anchor and the record per row, the two tables
     if (A->interior.pnc) A->stream_bytes += 12 * nrows + 4 * A->pnc.npat + 8 * A->pnc.nval;
-    // LDS-staged long rows: the CSR copy's 12 B per nonzero and row pointers (+ the skip flags)
-    if (A->interior.lsr) A->stream_bytes += 12 * lsr_nnz + 4 * (nrows + 1) + (A->d_lsr_skip ? nrows : 0);
-    // sorted sliced ELL: 12 B per padded element, the row and length per position, the slice descriptors
-    if (A->interior.sell)
-        A->stream_bytes += 12 * A->sell.elems + 6 * A->sell.ngroups * pamg::kEllGroup + 8 * A->sell.nslices;
     for (const pamg::TileSet* t : {&A->interior, &A->boundary}) {
-        if (t->sym || t->ell || t->pnc || t->sell || t->lsr) continue;  // counted above
+        if (t->sym || t->ell || t->pnc) continue;  // counted above
         const int64_t ns = t->n_short, nz = t->nnz_short;
         int64_t b = 8 * (int64_t)t->n_long + 12 * t->nnz_long;
         const bool base = t->c24 && !t->cd;
@@ -3302,8 +3177,6 @@ int pamg_mat_destroy(pamg_mat* A) {
     free_tiles(A->boundary);
     free_ell(A->ell);
     free_pnc(A->pnc);
-    free_sell(A->sell);
-    dfree(A->d_lsr_skip);
     pamg_ctx* owner = A->ctx;
     delete A;
     ctx_unref(owner);
@@ -3338,11 +3211,8 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
              (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0) |
-             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0) | (t.pnc ? 1024 : 0) | (t.sell ? 2048 : 0) |
-             (t.lsr ? 4096 : 0);
+             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0) | (t.pnc ? 1024 : 0);
     if (t.ell) out[8] = (int)A->ell.ngroups;  // k_rows_ell's grid
-    if (t.sell) out[8] = (int)A->sell.ngroups;  // k_rows_sell's grid
-    if (t.lsr) out[8] = (int)((A->nrows + pamg::kBlock - 1) / pamg::kBlock);  // k_rows_lsr's workgroups
     if (t.pnc) {  // the pattern and value tables, k_rows_pnc's grid
         out[3] = A->pnc.nval;
         out[4] = A->pnc.npat;
@@ -4019,14 +3889,6 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "ell_restrict" && (value == 0 || value == 1)) o.ell_restrict = (int)value;
     else if (k == "pnc" && (value == 0 || value == 1)) o.pnc = (int)value;
     else if (k == "ell_yblock" && value >= 0 && value <= 65536) o.ell_yblock = (int)value;
-    else if (k == "sell" && (value == 0 || value == 1)) o.sell = (int)value;
-    else if (k == "sell_sort" && (value == 0 || value == 1)) o.sell_sort = (int)value;
-    else if (k == "lsr" && (value == 0 || value == 1)) o.lsr = (int)value;
-    else if (k == "lsr_min_len" && value >= 1 && value <= 65535) o.lsr_min_len = (int)value;
-    else if (k == "lsr_min_rows" && value >= 0 && value <= INT32_MAX) o.lsr_min_rows = (int)value;
-    else if (k == "lsr_chunk" && (value == 16 || value == 32)) o.lsr_chunk = (int)value;
-    else if (k == "sell_min_len" && value >= 1 && value <= 65535) o.sell_min_len = (int)value;
-    else if (k == "sell_min_rows" && value >= 0 && value <= INT32_MAX) o.sell_min_rows = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
     else if (k == "chain_store_x" && (value == 0 || value == 1)) o.chain_store_x = (int)value;
@@ -4065,14 +3927,6 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "ell_restrict") *value = o.ell_restrict;
     else if (k == "pnc") *value = o.pnc;
     else if (k == "ell_yblock") *value = o.ell_yblock;
-    else if (k == "sell") *value = o.sell;
-    else if (k == "sell_sort") *value = o.sell_sort;
-    else if (k == "lsr") *value = o.lsr;
-    else if (k == "lsr_min_len") *value = o.lsr_min_len;
-    else if (k == "lsr_min_rows") *value = o.lsr_min_rows;
-    else if (k == "lsr_chunk") *value = o.lsr_chunk;
-    else if (k == "sell_min_len") *value = o.sell_min_len;
-    else if (k == "sell_min_rows") *value = o.sell_min_rows;
     else if (k == "ell_min_rows") *value = o.ell_min_rows;
     else if (k == "zm_chunks") *value = o.zm_chunks;
     else if (k == "chain_store_x") *value = o.chain_store_x;

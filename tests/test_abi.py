@@ -115,9 +115,7 @@ OPTION_DEFAULTS = {"tile_nnz": (1024, 4096), "tile_order": (1, 0), "col24": (1, 
                    "sym_dia": (1, 0), "sym_rows": (2, 1), "jr_fuse": (1, 0), "sym_vd": (1, 0),
                    "symd_chunks": (2, 4), "chain_store_x": (0, 1), "sym_zm": (1, 0), "zm_chunks": (0, 16),
                    "tb_xfast": (1, 0), "ell": (1, 0), "ell_restrict": (1, 0), "ell_min_rows": (65536, 1024), "pnc": (1, 0),
-                   "ell_yblock": (16, 0), "sell": (1, 0), "sell_min_len": (96, 64), "sell_min_rows": (32768, 1024),
-                   "sell_sort": (1, 0), "lsr": (1, 0), "lsr_min_len": (96, 64), "lsr_min_rows": (32768, 1024),
-                   "lsr_chunk": (32, 16)}
+                   "ell_yblock": (16, 0)}
 
 
 def test_option_keys_defaults_and_docs(built):

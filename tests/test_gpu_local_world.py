@@ -151,46 +151,6 @@ def test_local_world_ell_interior_rows_bit_exact(built, nparts, kind, n):
     assert np.array_equal(bits(got_x), bits(Ho.solve(bo, ncycles)))
 
 
-@pytest.mark.parametrize("layout", ["lsr", "sell"])
-@pytest.mark.parametrize("nparts,kind,n", [(3, "poisson3d", 20), (2, "elastic3d", 12)])
-def test_local_world_long_layout_interior_rows_bit_exact(built, nparts, kind, n, layout):
-    """Several parts with every level's interior rows in a long-row layout (k_rows_lsr: the boundary
-    rows skip-flagged; k_rows_sell: they carry the skip length; both computed by the tiles after the
-    exchange; min length 1, min rows 0, the symmetric, ELL and neighbour-coded layouts off). b = A x*
-    and x after 4 V-cycles are the oracle's multi-part bits, ghosts NaN-poisoned."""
-    import contextlib
-    ncycles = 4
-    opts = ([("lsr_min_rows", 0), ("lsr_min_len", 1)] if layout == "lsr" else
-            [("lsr", 0), ("sell_min_rows", 0), ("sell_min_len", 1)])
-    with contextlib.ExitStack() as st:
-        for k, v in opts + [("poison_ghosts", 1), ("sym_dia", 0), ("ell", 0), ("pnc", 0)]:
-            st.enter_context(option(k, v))
-        W = LocalWorld(nparts)
-        try:
-            be = pa.SequentialBackend(nparts)
-            A, offs, xs = pa.generate_problem(be, kind, n)
-            H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=60, agglomerate=0), device=W.ctxs[0])
-            S = [AMGSolver(W.ctxs[p], H, part=p) for p in range(nparts)]
-            # (a part keeps the tiles where fewer than 3/4 of its rows are interior)
-            assert any(layout_of(s.A_dev[0])[layout] for s in S)
-            A0 = [s.A_dev[0] for s in S]
-            xst = [PVector(W.ctxs[p], A0[p].n_own_cols, A0[p].n_ghost, xs[p]) for p in range(nparts)]
-            b = [PVector(W.ctxs[p], A0[p].nrows) for p in range(nparts)]
-            W.run(lambda p: mul(b[p], A0[p], xst[p]))
-            x = [s.new_vector() for s in S]
-            W.run(lambda p: S[p].vcycle(x[p], b[p], ncycles))
-            got_b = np.concatenate([v.own_values() for v in b])
-            got_x = np.concatenate([v.own_values() for v in x])
-        finally:
-            del S
-            W.close()
-    Ao = O.generate(kind, *O.grid_shape(kind, n))
-    bo = O.spmv(Ao, O.xstar(Ao.nrows))
-    Ho = O.setup(Ao, nparts=nparts, max_coarse=60, agglomerate=0)
-    assert np.array_equal(bits(got_b), bits(bo))
-    assert np.array_equal(bits(got_x), bits(Ho.solve(bo, ncycles)))
-
-
 def test_baseline_config0_golden(built):
     """BASELINE.json configs[0] — 2D 5-pt Poisson 256 x 256, 2 parts, the PartitionedArrays
     sequential-backend shape — on the HIP path (both parts in one process, the device world) against

@@ -1173,163 +1173,6 @@ def test_ell_level1_operator_128(ctx):
     assert np.array_equal(bits(x.own_values()), bits(O.jacobi(Mo, xh, bh, 0.61)))
 
 
-def _long_rows(nrows, ncols, lo, hi, seed, square=False, empty_every=0):
-    """Random rows of lo..hi nonzeros (sorted distinct columns near the row's position, random
-    values; square: a dominant diagonal), every empty_every-th row empty."""
-    rng = np.random.default_rng(seed)
-    rp, cols, vals = [0], [], []
-    for i in range(nrows):
-        k = 0 if empty_every and i % empty_every == 0 else int(rng.integers(lo, hi + 1))
-        c0 = min(max(0, i * ncols // max(nrows, 1) - 4 * k), max(0, ncols - 8 * k))
-        cs = np.unique(c0 + rng.integers(0, 8 * k + 1, k)) if k else np.zeros(0, np.int64)
-        cs = cs[cs < ncols]
-        v = rng.standard_normal(len(cs))
-        if square:
-            cs = np.unique(np.append(cs, i))
-            v = rng.standard_normal(len(cs))
-            v[cs == i] = 4.0 * len(cs)
-        cols += cs.tolist()
-        vals += v.tolist()
-        rp.append(len(cols))
-    return O.CSR(np.array(rp, np.int64), np.array(cols, np.int64), np.array(vals), ncols)
-
-
-def _long_layout(layout):
-    """Options that give a long-row operator the layout under test: "lsr" (k_rows_lsr, the default
-    for such operators), "lsr16" (its 16-element chunks), "sell" / "sell_unsorted" (k_rows_sell)."""
-    import contextlib
-
-    @contextlib.contextmanager
-    def cm():
-        opts = {"lsr": [("lsr_min_rows", 0)], "lsr16": [("lsr_min_rows", 0), ("lsr_chunk", 16)],
-                "sell": [("lsr", 0), ("sell_min_rows", 0)],
-                "sell_unsorted": [("lsr", 0), ("sell_min_rows", 0), ("sell_sort", 0)]}[layout]
-        with contextlib.ExitStack() as st:
-            for k, v in opts:
-                st.enter_context(_with_option(k, v))
-            yield
-    return cm()
-
-
-LONG_LAYOUTS = ["lsr", "lsr16", "sell", "sell_unsorted"]
-
-
-@pytest.mark.parametrize("layout", LONG_LAYOUTS)
-@pytest.mark.parametrize("case", ["restriction", "restriction_ragged", "square"])
-def test_long_rows_bit_exact(ctx, case, layout):
-    """The long-row layouts (round 6; the 512^3 R1's shape): k_rows_lsr (CSR copy, products staged in
-    LDS, every lane summing its own row) and k_rows_sell (sliced ELL with plain values, rows sorted or
-    in row order): rows of 24..300 nonzeros with tens of thousands of distinct values (no dictionary
-    fits), empty rows, a ragged last group; SpMV (and on a square operator residual and two Jacobi
-    sweeps) bit-exact with the oracle and with the tile layouts on the same matrix."""
-    from parallel_amg_amd._lib import layout_of
-    if case == "restriction":
-        M = _long_rows(3000, 60000, 24, 300, 1)
-    elif case == "restriction_ragged":
-        M = _long_rows(2777, 50000, 1, 280, 2, empty_every=41)
-    else:
-        M = _long_rows(2500, 2500, 90, 200, 3, square=True)
-    key = "lsr" if layout.startswith("lsr") else "sell"
-    with _with_option("sym_dia", 0):
-        with _long_layout(layout):
-            A, _h = upload(ctx, M)
-        with _with_option("sell", 0), _with_option("lsr", 0):
-            B, _h2 = upload(ctx, M)
-    assert layout_of(A)[key] and not layout_of(B)[key], (layout_of(A), layout_of(B))
-    rng = np.random.default_rng(5)
-    xh = rng.standard_normal(M.ncols)
-    with _long_layout(layout):  # (lsr_chunk is read at launch)
-        for D in (A, B):
-            x, y = PVector(ctx, M.ncols, 0, xh), PVector(ctx, M.nrows)
-            mul(y, D, x)
-            assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
-            if case == "square":
-                bh = rng.standard_normal(M.nrows)
-                b = PVector(ctx, M.nrows, 0, bh)
-                residual(y, D, x, b)
-                assert np.array_equal(bits(y.own_values()), bits(O.residual(M, xh, bh)))
-                t = PVector(ctx, M.nrows)
-                jacobi(x, D, b, t, 0.57, 2)
-                assert np.array_equal(bits(x.own_values()), bits(O.jacobi(M, O.jacobi(M, xh, bh, 0.57), bh, 0.57)))
-
-
-def test_long_rows_decline_short_rows_and_small_operators(ctx):
-    """The long-row layouts are taken only from lsr_min_len / sell_min_len nonzeros per row on
-    average and lsr_min_rows / sell_min_rows rows (defaults 96, 32768); k_rows_lsr before k_rows_sell."""
-    from parallel_amg_amd._lib import layout_of
-    short = _long_rows(40000, 400000, 20, 60, 4)
-    small = _long_rows(3000, 60000, 150, 250, 5)
-    big = _long_rows(40000, 400000, 100, 200, 6)
-    A, _h = upload(ctx, short)
-    B, _h2 = upload(ctx, small)
-    C, _h3 = upload(ctx, big)
-    assert not any(layout_of(D)[k] for D in (A, B) for k in ("lsr", "sell"))
-    assert layout_of(C)["lsr"] and not layout_of(C)["sell"]
-    with _with_option("lsr", 0):
-        E, _h4 = upload(ctx, big)
-    assert layout_of(E)["sell"] and not layout_of(E)["lsr"]
-    xh = np.random.default_rng(6).standard_normal(big.ncols)
-    for D in (C, E):
-        x, y = PVector(ctx, big.ncols, 0, xh), PVector(ctx, big.nrows)
-        mul(y, D, x)
-        assert np.array_equal(bits(y.own_values()), bits(O.spmv(big, xh)))
-
-
-@pytest.mark.parametrize("layout", LONG_LAYOUTS)
-def test_long_rows_restriction_r1_128(ctx, layout):
-    """The 128^3 hierarchy's R_1 (the 512^3 R1's shape at a smaller size: ~200 nonzeros per row)
-    in each long-row layout: y = R r bit-exact with the oracle and with the tiles."""
-    from parallel_amg_amd._lib import layout_of
-    be = pa.SequentialBackend(1)
-    A, offs, xs = pa.generate_problem(be, "poisson3d", 128)
-    H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=ctx)
-    R1 = H.levels[1][0].R
-    assert R1.nnz > 96 * R1.nrows
-    key = "lsr" if layout.startswith("lsr") else "sell"
-    with _long_layout(layout):
-        D = PSparseMatrix(ctx, R1)
-    D2 = PSparseMatrix(ctx, R1)  # (8K rows: the tiles at the default threshold)
-    assert layout_of(D)[key] and not layout_of(D2)[key]
-    Mo = O.CSR(R1.rowptr.copy(), R1.col.astype(np.int64), R1.val.copy(), R1.ncols)
-    rh = np.random.default_rng(13).standard_normal(R1.ncols)
-    r = PVector(ctx, R1.ncols, 0, rh)
-    with _long_layout(layout):
-        for M in (D, D2):
-            y = PVector(ctx, R1.nrows)
-            mul(y, M, r)
-            assert np.array_equal(bits(y.own_values()), bits(O.spmv(Mo, rh)))
-
-
-@pytest.mark.parametrize("layout", ["lsr", "sell"])
-@pytest.mark.parametrize("kind,n", [("poisson3d", 24), ("elastic3d", 10), ("aniso3d", 16)])
-def test_vcycle_every_operator_long_layout_bit_exact(ctx, kind, n, layout):
-    """Every level's A, R and P in a long-row layout (min length 1, min rows 0; the symmetric, ELL
-    and neighbour-coded layouts off): SpMV, residual, Jacobi and prolongate-add through k_rows_lsr /
-    k_rows_sell inside whole V-cycles, x after 4 cycles equal to the oracle's."""
-    import contextlib
-    from parallel_amg_amd._lib import layout_of
-    Ao = O.generate(kind, *O.grid_shape(kind, n))
-    be = pa.SequentialBackend(1)
-    opts = ([("lsr_min_rows", 0), ("lsr_min_len", 1)] if layout == "lsr" else
-            [("lsr", 0), ("sell_min_rows", 0), ("sell_min_len", 1)])
-    with contextlib.ExitStack() as st:
-        for k, v in opts + [("sym_dia", 0), ("ell", 0), ("pnc", 0)]:
-            st.enter_context(_with_option(k, v))
-        A, offs, xs = pa.generate_problem(be, kind, n)
-        H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=50), device=ctx)
-        S = AMGSolver(ctx, H, reorder="off")
-        A0 = S.A_dev[0]
-        assert layout_of(A0)[layout] and layout_of(S.P[0])[layout] and layout_of(S.R[0])[layout]
-        b = PVector(ctx, A0.nrows)
-        mul(b, A0, PVector(ctx, A0.nrows, 0, xs[0]))
-        x = S.new_vector()
-        S.vcycle(x, b, 4)
-    bo = O.spmv(Ao, O.xstar(Ao.nrows))
-    Ho = O.setup(Ao, max_coarse=50)
-    assert np.array_equal(bits(b.own_values()), bits(bo))
-    assert np.array_equal(bits(x.own_values()), bits(Ho.solve(bo, 4)))
-
-
 def _cut_grid(n=64, cut=31):
     """poisson3d n^3 with the couplings between x = cut and x = cut + 1 removed (both directions):
     a tb_ok grid operator with absent entries INSIDE the grid (mask bits clear for in-grid

@@ -85,7 +85,8 @@ def known_kernels(out):
         if not os.path.isdir(d):
             continue
         disp = per_dispatch(d)
-        launches = [disp[k] for k in sorted(disp) if disp[k][0] != "k_flush"]
+        # the measured kernels in launch order (not the flushes, nor the runtime's memset / copy kernels)
+        launches = [disp[k] for k in sorted(disp) if disp[k][0].startswith("k_") and disp[k][0] != "k_flush"]
         for rec, (_nm, _b, c) in zip(merged, launches):
             rec["counters"].update(c)
     for rec in merged:

@@ -18,9 +18,7 @@
 #   gentrace   rocprofv3 kernel stats of the same three runs
 #   calib      counter calibration: tools/fetch_calib (known bytes per access width) and the row kernels
 #              (kbench) under FETCH_SIZE / WRITE_SIZE / request-size / DRAM passes -> calib.json
-#   sellab     R1 with and without the sorted sliced ELL (kbench, same box)
 #   kbench     tools/kbench.py --n 512 --levels 2 timings (KB_ARGS overrides)
-#   sell       the sorted sliced-ELL parity tests (and the ELL ones)
 #   world      the in-process device-world tests (tests/test_gpu_local_world.py)
 #   stream / chain / sub   parity subsets: streamed sweeps; chain variants; -k "$SUB_K"
 #   cab        tools/cycle_ab.py: same-box A/B of a cycle-level option (CAB_ARGS overrides)
@@ -58,9 +56,6 @@ for step in "$@"; do
         ;;
     sub)
         timeout -k 10 400 $PYT tests/test_gpu_parity.py -k "${SUB_K:-prolongator}" -m gpu > "$OUT/sub.log" 2>&1
-        ;;
-    sell)
-        timeout -k 10 400 $PYT tests/test_gpu_parity.py -k "sell or ell_restriction or ell_level1" -m gpu > "$OUT/sell.log" 2>&1
         ;;
     world)
         timeout -k 10 600 $PYT tests/test_gpu_local_world.py -m gpu > "$OUT/world.log" 2>&1
@@ -133,18 +128,6 @@ for step in "$@"; do
             echo "kbench pass $i done"
         done
         python3 tools/calib_analysis.py "$OUT" > "$OUT/calib.json"
-        ;;
-    sellab)
-        # R1 (512^3) and aniso 256^3's levels 2-3 in each long-row layout, same box: LDS-staged rows
-        # (k_rows_lsr, chunks of 32 / 16), the sliced ELL unsorted / sorted, the tiles
-        for v in "lsr_chunk=32" "lsr_chunk=16" "lsr=0 --set sell_sort=0" "lsr=0 --set sell_sort=1" "lsr=0 --set sell=0"; do
-            tag=$(echo "$v" | tr -c 'a-z0-9' '_')
-            timeout -k 10 400 python3 -u tools/kbench.py --n 512 --levels 2 --mats R1 --ops 0 --reps 10 --configs 1024 \
-                --set $v > "$OUT/sellab_$tag.jsonl" 2> "$OUT/sellab_$tag.err"
-            timeout -k 10 400 python3 -u tools/kbench.py --kind aniso3d --n 256 --levels 4 --mats A2,R2,A3,R3 --ops 0 \
-                --reps 10 --configs 1024 --set $v > "$OUT/sellab_a256_$tag.jsonl" 2> "$OUT/sellab_a256_$tag.err"
-            echo "sellab $v done"
-        done
         ;;
     kbench)
         timeout -k 10 400 python3 -u tools/kbench.py $KBA > "$OUT/kbench.jsonl" 2> "$OUT/kbench.err"
