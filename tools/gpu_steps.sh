@@ -18,6 +18,7 @@
 #   gentrace   rocprofv3 kernel stats of the same three runs
 #   calib      counter calibration: tools/fetch_calib (known bytes per access width) and the row kernels
 #              (kbench) under FETCH_SIZE / WRITE_SIZE / request-size / DRAM passes -> calib.json
+#   chainpmc   SQ instruction / LDS counters of the chain and the fine SpMV (one pass)
 #   kbench     tools/kbench.py --n 512 --levels 2 timings (KB_ARGS overrides)
 #   world      the in-process device-world tests (tests/test_gpu_local_world.py)
 #   stream / chain / sub   parity subsets: streamed sweeps; chain variants; -k "$SUB_K"
@@ -128,6 +129,14 @@ for step in "$@"; do
             echo "kbench pass $i done"
         done
         python3 tools/calib_analysis.py "$OUT" > "$OUT/calib.json"
+        ;;
+    chainpmc)
+        # where the level-0 chain and the fine SpMV spend their issue slots: LDS vs VALU vs memory (one pass)
+        timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
+            SQ_WAIT_INST_LDS SQ_INSTS_LDS_LOAD_BANDWIDTH SQ_LDS_BANK_CONFLICT \
+            -d "$OUT/chainpmc" -o p --output-format csv -- python3 -u tools/kbench.py --n 512 --levels 1 --mats A0 \
+            --ops 0,5 --reps 3 --configs 1024 > "$OUT/chainpmc.jsonl" 2> "$OUT/chainpmc.err"
+        python3 tools/pmc_anatomy.py "$OUT/chainpmc" > "$OUT/chainpmc.json"
         ;;
     kbench)
         timeout -k 10 400 python3 -u tools/kbench.py $KBA > "$OUT/kbench.jsonl" 2> "$OUT/kbench.err"
