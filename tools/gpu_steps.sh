@@ -19,6 +19,7 @@
 #   calib      counter calibration: tools/fetch_calib (known bytes per access width) and the row kernels
 #              (kbench) under FETCH_SIZE / WRITE_SIZE / request-size / DRAM passes -> calib.json
 #   chainpmc   SQ instruction / LDS counters of the chain and the fine SpMV (one pass)
+#   r1band     R1 with its restriction band swept (tile order A/B)
 #   kbench     tools/kbench.py --n 512 --levels 2 timings (KB_ARGS overrides)
 #   world      the in-process device-world tests (tests/test_gpu_local_world.py)
 #   stream / chain / sub   parity subsets: streamed sweeps; chain variants; -k "$SUB_K"
@@ -137,6 +138,11 @@ for step in "$@"; do
             -d "$OUT/chainpmc" -o p --output-format csv -- python3 -u tools/kbench.py --n 512 --levels 1 --mats A0 \
             --ops 0,5 --reps 3 --configs 1024 > "$OUT/chainpmc.jsonl" 2> "$OUT/chainpmc.err"
         python3 tools/pmc_anatomy.py "$OUT/chainpmc" > "$OUT/chainpmc.json"
+        ;;
+    r1band)
+        # R1's tile order: the XCD band of the restriction tiles swept (read at upload), natural order beside it
+        timeout -k 10 500 python3 -u tools/kbench.py --n 512 --levels 2 --mats R1 --ops 0 --reps 10 --configs 1024:1,1024:0 \
+            --sweep band_pct_restrict=6,12,25,50,100,200 > "$OUT/r1band.jsonl" 2> "$OUT/r1band.err"
         ;;
     kbench)
         timeout -k 10 400 python3 -u tools/kbench.py $KBA > "$OUT/kbench.jsonl" 2> "$OUT/kbench.err"

@@ -66,6 +66,9 @@ def main():
                          "(a,b,a,b; e.g. symd_chunks=1,2)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="extra pamg_set_option before the uploads (e.g. band_pct=50)")
+    ap.add_argument("--sweep", default=None, metavar="KEY=V1,V2,...",
+                    help="an upload-time option swept over values: every matrix re-uploaded per value "
+                         "(e.g. band_pct_restrict=25,50,100)")
     args = ap.parse_args()
     ab_vals = (0, 1, 0, 1)
     if args.ab and "=" in args.ab:
@@ -94,7 +97,11 @@ def main():
     # the grid operator first: a prolongation over its grid may take the neighbour-coded layout
     # (PncSet: the upload looks the grid up on the context)
     grid_op = PSparseMatrix(ctx, *mats["A0"])  # noqa: F841 (kept alive: its grid stays registered)
-    for cfg in args.configs.split(","):
+    sweep_key, sweep_vals = (args.sweep.split("=")[0], [int(v) for v in args.sweep.split("=")[1].split(",")]) \
+        if args.sweep else (None, [None])
+    for sv, cfg in itertools.product(sweep_vals, args.configs.split(",")):
+        if sweep_key:
+            set_opts(**{sweep_key: sv})
         given = [int(v) for v in cfg.split(":")]
         vals = given + [1024, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1][len(given):]  # library defaults for missing fields
         tnnz, order, c24, vd, lt, rl8, cd, tm, anc, ptd, xst, tmpt = vals[:12]
@@ -121,6 +128,8 @@ def main():
                            "format_GBps": round(fbyt / ms / 1e6, 1), "layout": layout_of(D)}
                     if abv is not None:
                         rec[args.ab] = abv
+                    if sweep_key:
+                        rec[sweep_key] = sv
                     print(json.dumps(rec), flush=True)
                 if args.ab:
                     set_opts(**{args.ab: ab_vals[0]})
