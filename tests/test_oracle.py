@@ -185,3 +185,26 @@ def test_golden_fixtures(path):
     x, hist = H.solve(b, int(g["ncycles"]), res_hist=True)
     assert sha(x) == str(g["x_sha"])
     np.testing.assert_allclose(hist, g["res_hist"], rtol=1e-12)
+
+
+def test_oracle_setup_is_thread_count_independent():
+    """The oracle's setup runs rows of its Gustavson products, transpose, strength and Gershgorin
+    loops on OpenMP threads (round 6, so the 512^3 setups finish in about a minute): every level's
+    A, P, R and aggregates must have the same bits on 1 and on 8 threads (each row is computed as
+    the serial loop computes it)."""
+    L = O.lib()
+    A = O.generate("aniso3d", 24, 24, 24)
+    got = []
+    for threads in (1, 8):
+        L.orc_set_threads(threads)
+        H = O.setup(A, nparts=3, max_coarse=40, agglomerate=0)
+        h = hashlib.sha256()
+        for l in range(H.nlevels):
+            for M in [H.A[l]] + ([H.P[l], H.R[l]] if l < H.nlevels - 1 else []):
+                for a in (M.rowptr, M.col, M.val):
+                    h.update(np.ascontiguousarray(a).tobytes())
+            if l < H.nlevels - 1:
+                h.update(H.agg[l].tobytes())
+        got.append(h.hexdigest())
+    L.orc_set_threads(os.cpu_count() or 1)
+    assert got[0] == got[1]
