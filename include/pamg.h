@@ -133,7 +133,10 @@ int pamg_plan_create(pamg_ctx* ctx, int64_t n_own, int64_t n_ghost, int n_nbr,
                      const int64_t* send_counts, const int64_t* send_idx, pamg_plan** out);
 /* Identity of the index space a plan describes (e.g. "level 2, the columns of R"), the same
  * number on every part; default 0. The in-process world refuses to pair two parts' exchanges
- * whose plans carry different tags (RCCL and the host transport ignore it). */
+ * whose plans carry different tags, and fails at once when one part's plan lists the other with
+ * zero counts while that one's plan of the same tag expects ghosts from it (RCCL and the host
+ * transport ignore tags). A tag names one index space for the life of the world (or until
+ * pamg_world_reset): plans of one tag must agree on their counts across parts. */
 int pamg_plan_set_tag(pamg_plan* plan, int64_t tag);
 int pamg_plan_destroy(pamg_plan* plan);
 
