@@ -304,7 +304,7 @@ def main():
     tf = lambda v: "true" if v else "false"  # noqa: E731
     if pipelined:
         if lay.get("sym_vd"):  # the z-marching chain over the row-class dictionary (round 5)
-            kname = "k_sym_zc<3>"
+            kname = "k_sym_zc<3, 1>"
         else:
             kname = "k_sym_tb<3>"
         post_ms = float(fused["chain3_ms"])

@@ -1362,7 +1362,7 @@ __device__ __forceinline__ void zc_gather(const double2* __restrict__ dn_line, c
     xv[0][6] = zp.x;  xv[1][6] = zp.y;
 }
 
-template <int S>
+template <int S, int AH>
 __global__ __launch_bounds__(ZcShape<S>::threads) void k_sym_zc(int nrows, const uint8_t* __restrict__ tid,
                                                                  const double* __restrict__ vtab,
                                                                  const uint32_t* __restrict__ mtab, int nv,
@@ -1404,7 +1404,11 @@ __global__ __launch_bounds__(ZcShape<S>::threads) void k_sym_zc(int nrows, const
     // X[(u + j) & 3]: in0 of plane k-1+j (j = 0..3: k-1, k, k+1, k+2 in flight); E[(u + j) & 3]:
     // ids + b of plane k-2+j... (j = 3: k+1 in flight); HX[u & 1]: in0 halo of plane k, the
     // other one plane k+1 in flight
-    double2 X[4], HX[2];
+    // AH = 2 (ids, b and the in0 halo two planes ahead): E[(u + j) & 3] = plane k-2+j with plane k+2
+    // loaded into plane k-2's slot once stage 2's copy of it is taken; HX[(u + j) & 3] = halo of
+    // plane k+j (j = 2 loaded this step)
+    static_assert(AH == 1 || AH == 2, "one or two planes ahead");
+    double2 X[4], HX[AH == 2 ? 4 : 2];
     TbdRow E[4];
     X[0] = ldx(k0 - 1);
     X[1] = ldx(k0);
@@ -1412,10 +1416,15 @@ __global__ __launch_bounds__(ZcShape<S>::threads) void k_sym_zc(int nrows, const
     X[3] = zero;
     zc_halo_load<S>(HX[0], t, ta.in0, k0);
     HX[1] = zero;
+    if constexpr (AH == 2) {
+        zc_halo_load<S>(HX[1], t, ta.in0, k0 + 1);
+        HX[2] = HX[3] = zero;
+    }
     E[0] = TbdRow{};
     ldrow(E[1], k0 - 1);
     ldrow(E[2], k0);
     E[3] = TbdRow{};
+    if constexpr (AH == 2) ldrow(E[3], k0 + 1);
     uint32_t e3own = 0;  // class ids of plane k-3 (stage 2's -M mirror)
     double2 s0m1 = zero, s0m2 = zero;  // stage 0 of planes k-1, k-2
     double2 s1m2 = zero, s1m3 = zero;  // stage 1 of planes k-2, k-3
@@ -1429,12 +1438,12 @@ __global__ __launch_bounds__(ZcShape<S>::threads) void k_sym_zc(int nrows, const
             double2& xc = X[(u + 1) & 3];
             double2& xp = X[(u + 2) & 3];
             double2& xn = X[(u + 3) & 3];
-            double2& hc = HX[u & 1];
-            double2& hn = HX[(u + 1) & 1];
-            TbdRow& E2 = E[u & 3];        // plane k-2
+            double2& hc = HX[u & (AH == 2 ? 3 : 1)];
+            double2& hn = HX[(u + AH) & (AH == 2 ? 3 : 1)];
+            TbdRow E2 = E[u & 3];         // plane k-2 (AH = 2: a copy, its slot takes plane k+2)
             TbdRow& E1 = E[(u + 1) & 3];  // plane k-1
             TbdRow& E0 = E[(u + 2) & 3];  // plane k
-            TbdRow& En = E[(u + 3) & 3];  // plane k+1 (loaded this step)
+            TbdRow& En = E[(u + (AH == 2 ? 0 : 3)) & 3];  // plane k+AH (loaded this step)
             const int a = k & 1, a1 = (k - 1) & 1, a2 = (k - 2) & 1;
             // this step's LDS planes: in0 of plane k (own pair + halo), stage 0 of k-1, stage 1 of k-2
             if (has) {
@@ -1447,8 +1456,8 @@ __global__ __launch_bounds__(ZcShape<S>::threads) void k_sym_zc(int nrows, const
             e3own = E2.own;  // (E2 is overwritten by this step's load of plane k+1... next step)
             // next steps' loads
             xn = ldx(k + 2);
-            zc_halo_load<S>(hn, t, ta.in0, k + 1);
-            ldrow(En, k + 1);
+            zc_halo_load<S>(hn, t, ta.in0, k + AH);
+            ldrow(En, k + AH);
             __syncthreads();
             // ---- stage 0 on plane k: a Jacobi sweep from in0
             double2 s0k = zero;
@@ -2341,12 +2350,14 @@ void launch_sym_tb(const pamg_mat& A, const TbArgs& ta, hipStream_t s) {
     const int grid = (ntiles + 7) / 8 * 8;
     g.xfast = options().tb_xfast;
     if (sd.vd_n) {
+        // ids, b and the in0 halo two planes ahead for S = 2 (-2 %), one for S = 3 (two: +2.7 %;
+        // same-box A/B, profiles/r06_j/)
         if (ta.nstages == 2)
-            k_sym_zc<2><<<grid, ZcShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n, sd,
-                                                             ta);
+            k_sym_zc<2, 2><<<grid, ZcShape<2>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
+                                                                sd, ta);
         else
-            k_sym_zc<3><<<grid, ZcShape<3>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n, sd,
-                                                             ta);
+            k_sym_zc<3, 1><<<grid, ZcShape<3>::threads, 0, s>>>((int)A.nrows, sd.d_tid, sd.d_vtab, sd.d_mtab, sd.vd_n,
+                                                                sd, ta);
         return;
     }
     if (ta.nstages == 2)

@@ -1545,8 +1545,8 @@ def level1_128(ctx):
 @pytest.mark.parametrize("key,val", [("chain_store_x", 1), ("tb_xfast", 0), ("tb_xfast", 1)])
 def test_chain_variants_bit_exact(ctx, kind, key, val):
     """The chain's options — chain_store_x (the unread post-smoothed iterate stored too) and
-    tb_xfast (tile order x- or y-fastest): the fused pre-smoothing pass and pipelined cycles keep
-    the oracle's bits."""
+    tb_xfast (tile order x- or y-fastest): the fused pre-smoothing pass (k_sym_zc<2, 2>) and
+    pipelined cycles (k_sym_zc<3, 1>) keep the oracle's bits."""
     from parallel_amg_amd._lib import layout_of
     from parallel_amg_amd.partitioned import jacobi_residual
     be = pa.SequentialBackend(1)
