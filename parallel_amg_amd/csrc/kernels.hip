@@ -1786,6 +1786,78 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __
     if (in) y[i] = out;
 }
 
+// k_rows_rpat: pattern-dictionary rows (pamg::RpatSet; round 6, the 512^3 R0). One row per lane, a
+// workgroup per kEllGroup rows (the groups in the ELL's blocked order where the columns are a
+// registered grid); every workgroup stages the entry, pattern and value tables (<= kRpatEnt + kRpatMax
+// + 256 words; 1,249 + 58 + 41 at 512^3) in LDS, then a lane walks its pattern's entries 4 per step —
+// their x gathers issued together, a step past the row's end re-reading its last entry — x at the
+// row's first column + offset, products rounded and summed left to right from +0.0 in storage order,
+// the entries past the end selected away (SPEC S3: the bits of every other row kernel).
+template <int OP>
+__global__ __launch_bounds__(kEllGroup) void k_rows_rpat(int nrows, const int* __restrict__ gorder,
+                                                         const int* __restrict__ anc, const uint8_t* __restrict__ pid,
+                                                         const int2* __restrict__ pmeta, int npat,
+                                                         const uint32_t* __restrict__ pent, int nent,
+                                                         const double* __restrict__ vtab, int nval, int ngroups,
+                                                         const double* __restrict__ x, const double* __restrict__ b,
+                                                         double* __restrict__ y, double omega) {
+    __shared__ uint32_t le[kRpatEnt];
+    __shared__ int2 lm[kRpatMax];
+    __shared__ double lv[256];
+    const int per = (ngroups + 7) / 8;
+    const int gi = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (gi >= ngroups) return;  // the whole workgroup, before the barrier
+    const int g = gorder ? gorder[gi] : gi;
+    const int tid = threadIdx.x;
+    const int i = g * kEllGroup + tid;
+    const int ic = i < nrows ? i : nrows - 1;
+    const int p = i < nrows ? (int)pid[i] : kRpatSkip;  // (kRpatSkip: a boundary row of a part, or past the end)
+    const int a = anc[ic];
+    double pb = 0.0, px = 0.0, py = 0.0;
+    if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[ic];
+    if constexpr (OP == OP_JACOBI) px = x[ic];
+    if constexpr (OP == OP_PROLONG) py = y[ic];
+    for (int t = tid; t < nent; t += kEllGroup) le[t] = pent[t];
+    for (int t = tid; t < npat; t += kEllGroup) lm[t] = pmeta[t];
+    for (int t = tid; t < nval; t += kEllGroup) lv[t] = vtab[t];
+    __syncthreads();
+    const bool in = p != kRpatSkip;
+    const int2 m = in ? lm[p] : make_int2(0, 0);
+    const int L = m.y;
+    double s = 0.0, dg = 0.0;
+    for (int q = 0; q < L; q += 4) {
+        uint32_t w[4];
+        double xv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = le[m.x + min(q + e, L - 1)];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[e] = x[a + (int)(w[e] & 0xffffffu)];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool ok = q + e < L;
+            const double v = lv[w[e] >> 24];
+            const double pr = v * xv[e];
+            const double t = s + pr;
+            s = ok ? t : s;
+            if constexpr (OP == OP_JACOBI) dg = ok && a + (int)(w[e] & 0xffffffu) == i ? v : dg;
+        }
+    }
+    double out;
+    if constexpr (OP == OP_SPMV) {
+        out = s;
+    } else if constexpr (OP == OP_RESID) {
+        out = pb - s;
+    } else if constexpr (OP == OP_JACOBI) {
+        const double u = pb - s;
+        const double v = omega * u;
+        const double w = v / dg;
+        out = px + w;
+    } else {
+        out = py + s;
+    }
+    if (in) y[i] = out;
+}
+
 // k_rows_pnc: the neighbour-coded prolongation (pamg::PncSet; round 5, the 512^3 P0). One row per
 // lane, about 8 workgroups per CU, each staging the two global tables (<= 1024 pattern words, <= 128
 // values) in LDS once and then walking 256-row blocks: at step t the workgroups of XCD j (block b
@@ -2307,6 +2379,14 @@ void launch_pnc(const pamg_mat& A, const double* x, const double* b, double* y, 
 }
 
 template <int OP>
+void launch_rpat(const pamg_mat& A, const double* x, const double* b, double* y, double omega, hipStream_t s) {
+    const RpatSet& R = A.rpat;
+    const int grid = (int)((R.ngroups + 7) / 8 * 8);
+    k_rows_rpat<OP><<<grid, kEllGroup, 0, s>>>((int)A.nrows, R.d_gorder, R.d_anc, R.d_pid, R.d_pmeta, R.npat,
+                                               R.d_pent, R.nent, R.d_vtab, R.nval, (int)R.ngroups, x, b, y, omega);
+}
+
+template <int OP>
 void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const double* b,
                     double* y, double omega, hipStream_t s) {
     if (ts.sym) launch_sym<OP>(A, x, b, y, omega, s);
@@ -2323,6 +2403,7 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
                                                                y, omega);
     }
     if (ts.pnc) launch_pnc<OP>(A, x, b, y, omega, s);
+    if (ts.rpat) launch_rpat<OP>(A, x, b, y, omega, s);
     if (ts.n_short > 0) {
         if (ts.tile_nnz == 1024) launch_tile<OP, 1024>(A, ts, x, b, y, omega, s);
         else if (ts.tile_nnz == 4096) launch_tile<OP, 4096>(A, ts, x, b, y, omega, s);

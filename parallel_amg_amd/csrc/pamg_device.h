@@ -102,6 +102,9 @@ struct TileSet {
     // neighbour-coded prolongation (pamg_mat::pnc; the whole set of a prolongation over a registered grid):
     // the rows run in k_rows_pnc instead of tiles
     bool pnc = false;
+    // pattern-dictionary rows (pamg_mat::rpat; the whole interior set of a restriction): the rows run in
+    // k_rows_rpat instead of tiles
+    bool rpat = false;
     int max_short_len = 0;    // longest row in a short tile
     int64_t rows_short = 0;   // rows covered by the short tiles
     int64_t nnz_short = 0, nnz_long = 0;  // nonzeros covered by the tiles / the long rows
@@ -147,6 +150,7 @@ struct Options {
     int ell_yblock = 16;       // restrictions over a grid: groups processed in (y-block of this many lines, z, y)
                                //    order within each XCD's eighth (0: row order; 512^3 R0 0.81 -> 0.745 ms for any
                                //    block of 2..64 lines, profiles/r05_r/); read at upload
+    int rpat = 1;              // 1: pattern-dictionary rows for restrictions whose rows repeat few patterns (RpatSet)
     int pnc = 1;               // 1: neighbour-coded prolongations over a grid registered on the context (PncSet)
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
@@ -226,6 +230,29 @@ struct PncSet {
     double* d_vtab = nullptr;
     int npat = 0, nval = 0;
     int grid = 0;               // workgroups of k_rows_pnc
+};
+
+// Pattern-dictionary rows (Options::rpat; round 6, the 512^3 R0): a restriction (fewer rows than columns)
+// whose rows, read as (column - the row's first column, value bits) sequences in storage order, are
+// copies of at most kRpatMax patterns of at most kRpatEnt entries in all. In smoothed aggregation a
+// row of R = P^T is one aggregate's dilated shape, so the patterns are the aggregate shapes: 58 of
+// them, 1,249 entries, for the 16.8M rows of the 512^3 R0 (the sliced ELL, 2 index bytes per padded
+// nonzero, streamed 59 B per row). Per row: its first column (4 B) and pattern id (1 B; kRpatSkip: a
+// row outside the set, several parts' boundary rows). Pattern p's entries at d_pent[start_p ..
+// start_p + len_p): column offset in bits 0-23, value index (into d_vtab, <= 256 bit patterns) in
+// bits 24-31. Rows keep their storage order (SPEC S3 sums); the groups of kEllGroup rows run in the
+// ELL's blocked order over the registered grid of the columns (d_gorder) where there is one.
+constexpr int kRpatMax = 255, kRpatEnt = 4096, kRpatMaxLen = 128;
+constexpr int kRpatSkip = 255;
+struct RpatSet {
+    int64_t ngroups = 0;
+    int* d_anc = nullptr;        // nrows (+ pad): the first column of each row
+    uint8_t* d_pid = nullptr;    // nrows (+ pad): the pattern id of each row
+    int2* d_pmeta = nullptr;     // per pattern: (first entry, entries)
+    uint32_t* d_pent = nullptr;  // the patterns' entries, concatenated
+    double* d_vtab = nullptr;    // the values' bit patterns
+    int* d_gorder = nullptr;     // the groups' processing order (as EllSet::d_gorder), or null
+    int npat = 0, nent = 0, nval = 0;
 };
 
 struct SymDia {
@@ -338,6 +365,7 @@ struct pamg_mat {
     pamg::TileSet boundary;  // rows with >= 1 ghost column
     pamg::EllSet ell;        // the interior set's sliced-ELL layout (TileSet::ell)
     pamg::PncSet pnc;        // the neighbour-coded prolongation layout (TileSet::pnc)
+    pamg::RpatSet rpat;      // the pattern-dictionary restriction layout (TileSet::rpat)
     int64_t stream_bytes = 0;  // matrix bytes one apply reads (values, columns, row pointers, tiles)
 };
 

@@ -1280,6 +1280,38 @@ int build_sym_dia(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double*
     return PAMG_OK;
 }
 
+// A restriction over a registered grid (Options::ell_yblock > 0; its columns are the grid's points):
+// the groups of kEllGroup rows of each XCD's eighth (kernels.hip k_rows_ell / k_rows_rpat) in
+// (y / yblock, z, y) order of their first row's anchor, so the window of groups in flight is a
+// compact (y, z) block of the grid, not whole planes. *d_order stays null otherwise.
+int blocked_group_order(pamg_ctx* ctx, const std::vector<int>& anc, int64_t ng, int64_t own_cols, int** d_order) {
+    using pamg::kEllGroup;
+    const int yb = pamg::options().ell_yblock;
+    for (const auto& gr : grids_of(ctx))
+        if (yb > 0 && gr[0] == own_cols) {
+            const int64_t gnx = gr[1], gny = gr[2], gM = gr[1] * gr[2];
+            std::vector<int64_t> key(ng);
+            par_for(ng, [&](int64_t a, int64_t b) {
+                for (int64_t g = a; g < b; ++g) {
+                    const int64_t c = anc[g * kEllGroup];
+                    const int64_t y = (c / gnx) % gny, z = c / gM;
+                    key[g] = ((y / yb) << 40) | (z << 20) | y;
+                }
+            });
+            const int64_t per = (ng + 7) / 8;
+            std::vector<int> order(ng);
+            for (int64_t g = 0; g < ng; ++g) order[g] = (int)g;
+            for (int64_t e = 0; e < 8; ++e) {
+                const int64_t lo = std::min(ng, e * per), hi = std::min(ng, (e + 1) * per);
+                std::stable_sort(order.begin() + lo, order.begin() + hi, [&](int p, int q) { return key[p] < key[q]; });
+            }
+            CHECK(dalloc(d_order, ng));
+            CHECK(h2d(ctx, *d_order, order.data(), sizeof(int) * ng));
+            break;
+        }
+    return PAMG_OK;
+}
+
 // Sliced ELL with per-group dictionaries (Options::ell, pamg::EllSet): a square operator whose
 // rows are all interior, in slices of kEllW rows padded to the slice's longest row, kEllGroup
 // rows sharing one table of column offsets (col - row) and one of values (bit patterns), each of
@@ -1428,34 +1460,7 @@ int build_ell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
         });
         CHECK(dalloc(&E.d_anc, n + kVecPad));
         CHECK(h2d(ctx, E.d_anc, anc.data(), sizeof(int) * anc.size()));
-        // a restriction over a registered grid (Options::ell_yblock > 0): the groups of each XCD's
-        // eighth (kernels.hip k_rows_ell) in (y / yblock, z, y) order of their first row's anchor, so
-        // the window of groups in flight is a compact (y, z) block of the grid, not whole planes
-        const int yb = pamg::options().ell_yblock;
-        const int64_t own_cols = A->plan ? A->plan->n_own : A->ncols;
-        for (const auto& gr : grids_of(ctx))
-            if (yb > 0 && gr[0] == own_cols) {
-                const int64_t gnx = gr[1], gny = gr[2], gM = gr[1] * gr[2];
-                std::vector<int64_t> key(ng);
-                par_for(ng, [&](int64_t a, int64_t b) {
-                    for (int64_t g = a; g < b; ++g) {
-                        const int64_t c = anc[g * kEllGroup];
-                        const int64_t y = (c / gnx) % gny, z = c / gM;
-                        key[g] = ((y / yb) << 40) | (z << 20) | y;
-                    }
-                });
-                const int64_t per = (ng + 7) / 8;
-                std::vector<int> order(ng);
-                for (int64_t g = 0; g < ng; ++g) order[g] = (int)g;
-                for (int64_t e = 0; e < 8; ++e) {
-                    const int64_t lo = std::min(ng, e * per), hi = std::min(ng, (e + 1) * per);
-                    std::stable_sort(order.begin() + lo, order.begin() + hi,
-                                     [&](int p, int q) { return key[p] < key[q]; });
-                }
-                CHECK(dalloc(&E.d_gorder, ng));
-                CHECK(h2d(ctx, E.d_gorder, order.data(), sizeof(int) * ng));
-                break;
-            }
+        CHECK(blocked_group_order(ctx, anc, ng, A->plan ? A->plan->n_own : A->ncols, &E.d_gorder));
     }
     A->interior.ell = true;
     return PAMG_OK;
@@ -1600,6 +1605,177 @@ int build_pnc(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
     CHECK(h2d(ctx, P.d_vtab, vtab.data(), sizeof(double) * vtab.size()));
     A->interior.pnc = true;
     return PAMG_OK;
+}
+
+// Pattern-dictionary rows (Options::rpat, pamg::RpatSet): a restriction whose rows, as (column - first
+// column, value bits) sequences, repeat at most kRpatMax patterns (<= kRpatEnt entries, <= 256 values,
+// offsets < 2^24, rows of 1 .. kRpatMaxLen entries). Declines (leaves ELL / tiles to the caller)
+// otherwise. The patterns are numbered in first-appearance order (chunks scanned in parallel, merged
+// in chunk order: the numbering one sequential pass gives).
+int build_rpat(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val, const std::vector<int>& inner) {
+    using pamg::kRpatEnt;
+    using pamg::kRpatMax;
+    using pamg::kRpatMaxLen;
+    using pamg::kRpatSkip;
+    const int64_t n = A->nrows;
+    if (n <= 0) return PAMG_OK;
+    std::vector<char> in_set;
+    if ((int64_t)inner.size() != n) {
+        in_set.assign(n, 0);
+        for (int i : inner) in_set[i] = 1;
+    }
+    auto member = [&](int64_t i) { return in_set.empty() || in_set[i]; };
+    // a row's pattern key: length, offsets, value bits
+    auto row_hash = [&](int64_t i) {
+        uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)(rp[i + 1] - rp[i]);
+        const int64_t c0 = ci[rp[i]];
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+            uint64_t u;
+            std::memcpy(&u, &val[k], 8);
+            h = (h ^ (uint64_t)(ci[k] - c0)) * 0x100000001B3ull;
+            h = (h ^ u) * 0x9E3779B97F4A7C15ull;
+            h ^= h >> 29;
+        }
+        return h;
+    };
+    auto same = [&](int64_t i, int64_t j) {
+        const int64_t L = rp[i + 1] - rp[i];
+        if (L != rp[j + 1] - rp[j]) return false;
+        const int64_t ci0 = ci[rp[i]], cj0 = ci[rp[j]];
+        for (int64_t k = 0; k < L; ++k) {
+            if (ci[rp[i] + k] - ci0 != ci[rp[j] + k] - cj0) return false;
+            if (std::memcmp(&val[rp[i] + k], &val[rp[j] + k], 8) != 0) return false;
+        }
+        return true;
+    };
+    // pass 1: each chunk's distinct patterns (hash, representative row) in first-appearance order
+    const int nch = std::max(1, std::min<int>(host_threads() * 4, (int)(n / 65536)));
+    std::vector<std::vector<std::pair<uint64_t, int64_t>>> firsts(nch);
+    std::atomic<bool> ok{true};
+    {
+        std::vector<std::thread> th;
+        const int nt = std::min(nch, host_threads());
+        std::atomic<int> next{0};
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&] {
+                for (int c; ok && (c = next.fetch_add(1)) < nch;) {
+                    auto& f = firsts[c];
+                    int last = -1;
+                    for (int64_t i = n * c / nch, e = n * (c + 1) / nch; i < e && ok; ++i) {
+                        if (!member(i)) continue;
+                        const int64_t L = rp[i + 1] - rp[i];
+                        if (L < 1 || L > kRpatMaxLen) {
+                            ok = false;
+                            break;
+                        }
+                        for (int64_t k = rp[i] + 1; k < rp[i + 1]; ++k)
+                            if (ci[k] <= ci[k - 1] || (int64_t)ci[k] - ci[rp[i]] >= (int64_t(1) << 24)) ok = false;
+                        const uint64_t h = row_hash(i);
+                        if (last >= 0 && f[last].first == h && same(f[last].second, i)) continue;
+                        last = -1;
+                        for (int q = 0; q < (int)f.size() && last < 0; ++q)
+                            if (f[q].first == h && same(f[q].second, i)) last = q;
+                        if (last >= 0) continue;
+                        if ((int)f.size() == kRpatMax) {
+                            ok = false;
+                            break;
+                        }
+                        f.emplace_back(h, i);
+                        last = (int)f.size() - 1;
+                    }
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    if (!ok) return PAMG_OK;
+    std::vector<std::pair<uint64_t, int64_t>> pats;  // (hash, representative row)
+    for (int c = 0; c < nch; ++c)
+        for (const auto& e : firsts[c]) {
+            bool seen = false;
+            for (const auto& q : pats) seen = seen || (q.first == e.first && same(q.second, e.second));
+            if (seen) continue;
+            if ((int)pats.size() == kRpatMax) return PAMG_OK;
+            pats.push_back(e);
+        }
+    if (pats.empty()) return PAMG_OK;
+    // the entries and the value table
+    std::vector<int2> pmeta(pats.size());
+    std::vector<uint32_t> pent;
+    std::vector<uint64_t> vals;
+    for (size_t p = 0; p < pats.size(); ++p) {
+        const int64_t r = pats[p].second;
+        pmeta[p] = make_int2((int)pent.size(), (int)(rp[r + 1] - rp[r]));
+        for (int64_t k = rp[r]; k < rp[r + 1]; ++k) {
+            uint64_t u;
+            std::memcpy(&u, &val[k], 8);
+            size_t vi = std::find(vals.begin(), vals.end(), u) - vals.begin();
+            if (vi == vals.size()) {
+                if (vals.size() == 256) return PAMG_OK;
+                vals.push_back(u);
+            }
+            pent.push_back((uint32_t)(ci[k] - ci[rp[r]]) | ((uint32_t)vi << 24));
+        }
+        if ((int)pent.size() > kRpatEnt) return PAMG_OK;
+    }
+    // pass 2: every row's pattern id (hash lookup, full compare) and first column
+    std::vector<std::pair<uint64_t, int>> byhash(pats.size());
+    for (size_t p = 0; p < pats.size(); ++p) byhash[p] = {pats[p].first, (int)p};
+    std::sort(byhash.begin(), byhash.end());
+    std::vector<uint8_t> pid(n + kVecPad, (uint8_t)kRpatSkip);
+    std::vector<int> anc(n + kVecPad, 0);
+    par_for(n, [&](int64_t a, int64_t b) {
+        int last = -1;
+        for (int64_t i = a; i < b; ++i) {
+            anc[i] = rp[i + 1] > rp[i] ? ci[rp[i]] : 0;
+            if (!member(i)) continue;
+            if (last >= 0 && same(pats[last].second, i)) {
+                pid[i] = (uint8_t)last;
+                continue;
+            }
+            const uint64_t h = row_hash(i);
+            last = -1;
+            for (auto it = std::lower_bound(byhash.begin(), byhash.end(), std::make_pair(h, -1));
+                 it != byhash.end() && it->first == h && last < 0; ++it)
+                if (same(pats[it->second].second, i)) last = it->second;
+            if (last < 0) {  // (cannot happen: every row's pattern was collected in pass 1)
+                ok = false;
+                return;
+            }
+            pid[i] = (uint8_t)last;
+        }
+    });
+    if (!ok) return PAMG_OK;
+    std::vector<double> vtab(vals.size());
+    for (size_t e = 0; e < vals.size(); ++e) std::memcpy(&vtab[e], &vals[e], 8);
+    pamg::RpatSet& R = A->rpat;
+    pamg_ctx* ctx = A->ctx;
+    R.ngroups = (n + pamg::kEllGroup - 1) / pamg::kEllGroup;
+    R.npat = (int)pats.size();
+    R.nent = (int)pent.size();
+    R.nval = (int)vals.size();
+    CHECK(dalloc(&R.d_anc, n + kVecPad));
+    CHECK(dalloc(&R.d_pid, n + kVecPad));
+    CHECK(dalloc(&R.d_pmeta, R.npat));
+    CHECK(dalloc(&R.d_pent, R.nent));
+    CHECK(dalloc(&R.d_vtab, R.nval));
+    CHECK(h2d(ctx, R.d_anc, anc.data(), sizeof(int) * anc.size()));
+    CHECK(h2d(ctx, R.d_pid, pid.data(), pid.size()));
+    CHECK(h2d(ctx, R.d_pmeta, pmeta.data(), sizeof(int2) * pmeta.size()));
+    CHECK(h2d(ctx, R.d_pent, pent.data(), sizeof(uint32_t) * pent.size()));
+    CHECK(h2d(ctx, R.d_vtab, vtab.data(), sizeof(double) * vtab.size()));
+    CHECK(blocked_group_order(ctx, anc, R.ngroups, A->plan ? A->plan->n_own : A->ncols, &R.d_gorder));
+    A->interior.rpat = true;
+    return PAMG_OK;
+}
+
+void free_rpat(pamg::RpatSet& R) {
+    dfree(R.d_anc);
+    dfree(R.d_pid);
+    dfree(R.d_pmeta);
+    dfree(R.d_pent);
+    dfree(R.d_vtab);
+    dfree(R.d_gorder);
+    R = pamg::RpatSet{};
 }
 
 void free_pnc(pamg::PncSet& P) {
@@ -2972,7 +3148,14 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     // square operators (offsets from the row) and restrictions (fewer rows than columns; offsets from
     // each row's first column)
     // (several parts: the interior rows, when they are >= 3/4 of the operator — a 512^3 z-slab part's level 1)
-    if (pamg::options().ell && !A->interior.sym && n_own_cols >= nrows && nrows > 0 &&
+    // restrictions whose rows repeat few patterns (an aggregate shape each): pattern-dictionary rows
+    if (pamg::options().rpat && !A->interior.sym && n_own_cols > nrows && nrows > 0 &&
+        (int64_t)inner.size() * 4 >= (int64_t)nrows * 3) {
+        CHECK(build_rpat(A.get(), rp, ci, val, inner));
+        if (A->interior.rpat) inner.clear();  // the rows run in k_rows_rpat, not in tiles
+        tr.mark("rpat");
+    }
+    if (pamg::options().ell && !A->interior.sym && !A->interior.rpat && n_own_cols >= nrows && nrows > 0 &&
         (int64_t)inner.size() * 4 >= (int64_t)nrows * 3 && nrows >= pamg::options().ell_min_rows &&
         (n_own_cols == nrows || pamg::options().ell_restrict)) {
         CHECK(build_ell(A.get(), rp, ci, val, n_own_cols != nrows, inner));
@@ -3056,8 +3239,10 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
                            8 * A->ell.vtab_n + (A->ell.d_anc ? 4 * nrows : 0);
     // neighbour-coded prolongation: the anchor and the record per row, the two tables
     if (A->interior.pnc) A->stream_bytes += 12 * nrows + 4 * A->pnc.npat + 8 * A->pnc.nval;
+    // pattern-dictionary rows: the first column and the pattern id per row, the tables
+    if (A->interior.rpat) A->stream_bytes += 5 * nrows + 8 * A->rpat.npat + 4 * A->rpat.nent + 8 * A->rpat.nval;
     for (const pamg::TileSet* t : {&A->interior, &A->boundary}) {
-        if (t->sym || t->ell || t->pnc) continue;  // counted above
+        if (t->sym || t->ell || t->pnc || t->rpat) continue;  // counted above
         const int64_t ns = t->n_short, nz = t->nnz_short;
         int64_t b = 8 * (int64_t)t->n_long + 12 * t->nnz_long;
         const bool base = t->c24 && !t->cd;
@@ -3177,6 +3362,7 @@ int pamg_mat_destroy(pamg_mat* A) {
     free_tiles(A->boundary);
     free_ell(A->ell);
     free_pnc(A->pnc);
+    free_rpat(A->rpat);
     pamg_ctx* owner = A->ctx;
     delete A;
     ctx_unref(owner);
@@ -3211,8 +3397,13 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
              (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0) |
-             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0) | (t.pnc ? 1024 : 0);
+             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0) | (t.pnc ? 1024 : 0) | (t.rpat ? 2048 : 0);
     if (t.ell) out[8] = (int)A->ell.ngroups;  // k_rows_ell's grid
+    if (t.rpat) {  // the pattern and value tables, k_rows_rpat's grid
+        out[3] = A->rpat.nval;
+        out[4] = A->rpat.npat;
+        out[8] = (int)A->rpat.ngroups;
+    }
     if (t.pnc) {  // the pattern and value tables, k_rows_pnc's grid
         out[3] = A->pnc.nval;
         out[4] = A->pnc.npat;
@@ -3888,6 +4079,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "ell" && (value == 0 || value == 1)) o.ell = (int)value;
     else if (k == "ell_restrict" && (value == 0 || value == 1)) o.ell_restrict = (int)value;
     else if (k == "pnc" && (value == 0 || value == 1)) o.pnc = (int)value;
+    else if (k == "rpat" && (value == 0 || value == 1)) o.rpat = (int)value;
     else if (k == "ell_yblock" && value >= 0 && value <= 65536) o.ell_yblock = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
@@ -3926,6 +4118,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "ell") *value = o.ell;
     else if (k == "ell_restrict") *value = o.ell_restrict;
     else if (k == "pnc") *value = o.pnc;
+    else if (k == "rpat") *value = o.rpat;
     else if (k == "ell_yblock") *value = o.ell_yblock;
     else if (k == "ell_min_rows") *value = o.ell_min_rows;
     else if (k == "zm_chunks") *value = o.zm_chunks;

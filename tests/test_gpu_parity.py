@@ -1128,27 +1128,105 @@ def test_ell_declines_what_does_not_fit(ctx):
         assert np.array_equal(bits(y.own_values()), bits(O.spmv(Mx, xh)))
 
 
-def test_ell_restriction_128(ctx):
+def test_restriction_layouts_128(ctx):
     """The 128^3 hierarchy's restriction R_0 (263,552 coarse rows reading the 2.1M-entry fine vector,
-    29 nonzeros per row) in the anchored sliced-ELL layout (offsets from each row's first column):
-    y = R r bit-exact with the oracle; declined with ell_restrict 0."""
+    29 nonzeros per row): in the pattern-dictionary layout (58 aggregate-shape patterns; round 6), in
+    the anchored sliced-ELL layout (rpat 0; offsets from each row's first column) and in tiles (rpat 0,
+    ell_restrict 0): y = R r and b - R r bit-exact with the oracle in all three."""
     from parallel_amg_amd._lib import layout_of
     be = pa.SequentialBackend(1)
     A, offs, xs = pa.generate_problem(be, "poisson3d", 128)
     H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=ctx)
     R0 = H.levels[0][0].R
     D = PSparseMatrix(ctx, R0)
-    assert layout_of(D)["ell"], layout_of(D)
-    with _with_option("ell_restrict", 0):
-        D2 = PSparseMatrix(ctx, R0)
-    assert not layout_of(D2)["ell"]
+    lay = layout_of(D)
+    assert lay["rpat"] and not lay["ell"] and lay["cd_offsets"] == 58, lay
+    with _with_option("rpat", 0):
+        D1 = PSparseMatrix(ctx, R0)
+        with _with_option("ell_restrict", 0):
+            D2 = PSparseMatrix(ctx, R0)
+    assert layout_of(D1)["ell"] and not layout_of(D1)["rpat"]
+    assert not layout_of(D2)["ell"] and not layout_of(D2)["rpat"]
     Mo = O.CSR(R0.rowptr.copy(), R0.col.astype(np.int64), R0.val.copy(), R0.ncols)
-    rh = np.random.default_rng(12).standard_normal(R0.ncols)
-    r = PVector(ctx, R0.ncols, 0, rh)
-    for M in (D, D2):
+    rng = np.random.default_rng(12)
+    rh, bh = rng.standard_normal(R0.ncols), rng.standard_normal(R0.nrows)
+    r, b = PVector(ctx, R0.ncols, 0, rh), PVector(ctx, R0.nrows, 0, bh)
+    for M in (D, D1, D2):
         y = PVector(ctx, R0.nrows)
         mul(y, M, r)
         assert np.array_equal(bits(y.own_values()), bits(O.spmv(Mo, rh)))
+        residual(y, M, r, b)
+        assert np.array_equal(bits(y.own_values()), bits(O.residual(Mo, rh, bh)))
+
+
+def _rpat_case(npat, seed, ragged=True, nrows=6000):
+    """A restriction-shaped matrix (nrows x 4 nrows + 64) whose rows copy npat patterns of
+    (offset, value) pairs from their first column: lengths 1..40 (ragged) or 29, values from a
+    12-entry palette, rows in runs of random length."""
+    rng = np.random.default_rng(seed)
+    pal = rng.standard_normal(12)
+    pats = []
+    for _ in range(npat):
+        L = int(rng.integers(1, 41)) if ragged else 29
+        offs = np.unique(np.concatenate([[0], rng.integers(1, 60, L - 1)]))
+        pats.append((offs, pal[rng.integers(0, 12, len(offs))]))
+    ncols = 4 * nrows + 64
+    rows, cols, vals = [], [], []
+    j = 0
+    while j < nrows:
+        p = int(rng.integers(0, npat))
+        for _ in range(int(rng.integers(1, 90))):
+            if j == nrows:
+                break
+            offs, v = pats[p]
+            rows += [j] * len(offs)
+            cols += (4 * j + offs).tolist()
+            vals += v.tolist()
+            j += 1
+    import scipy.sparse as sp
+    T = sp.csr_matrix((vals, (rows, cols)), shape=(nrows, ncols))
+    T.sort_indices()
+    return O.CSR(T.indptr.astype(np.int64), T.indices.astype(np.int64), T.data.copy(), ncols)
+
+
+@pytest.mark.parametrize("npat,ragged", [(1, False), (7, True), (255, True)])
+def test_rpat_bit_exact(ctx, npat, ragged):
+    """k_rows_rpat (round 6): restrictions whose rows repeat 1, 7 or up to 255 patterns (ragged
+    lengths 1..40): y = R r and b - R r bit-exact with the oracle, in this layout and in the tiles."""
+    from parallel_amg_amd._lib import layout_of
+    M = _rpat_case(npat, 20 + npat, ragged)
+    A, _h = upload(ctx, M)
+    with _with_option("rpat", 0):
+        B, _h2 = upload(ctx, M)
+    la = layout_of(A)
+    assert la["rpat"] and la["cd_offsets"] <= npat and not layout_of(B)["rpat"], (la, layout_of(B))
+    rng = np.random.default_rng(5)
+    xh, bh = rng.standard_normal(M.ncols), rng.standard_normal(M.nrows)
+    for D in (A, B):
+        x, b, y = PVector(ctx, M.ncols, 0, xh), PVector(ctx, M.nrows, 0, bh), PVector(ctx, M.nrows)
+        mul(y, D, x)
+        assert np.array_equal(bits(y.own_values()), bits(O.spmv(M, xh)))
+        residual(y, D, x, b)
+        assert np.array_equal(bits(y.own_values()), bits(O.residual(M, xh, bh)))
+
+
+def test_rpat_declines(ctx):
+    """More than 255 patterns (a restriction whose every row has its own values) or a row longer
+    than 128: ELL or the tiles, still bit-exact."""
+    from parallel_amg_amd._lib import layout_of
+    M = _rpat_case(7, 3)
+    many = O.CSR(M.rowptr.copy(), M.col.copy(), np.random.default_rng(1).standard_normal(M.nnz), M.ncols)
+    n, m = 50, 4000
+    long_rows = O.CSR(np.arange(0, n * 200 + 1, 200, dtype=np.int64),
+                      (np.arange(n)[:, None] * 40 + np.arange(200)[None, :]).ravel().astype(np.int64),
+                      np.ones(n * 200), m)
+    for Mx in (many, long_rows):
+        A, _h = upload(ctx, Mx)
+        assert not layout_of(A)["rpat"]
+        xh = np.random.default_rng(2).standard_normal(Mx.ncols)
+        x, y = PVector(ctx, Mx.ncols, 0, xh), PVector(ctx, Mx.nrows)
+        mul(y, A, x)
+        assert np.array_equal(bits(y.own_values()), bits(O.spmv(Mx, xh)))
 
 
 def test_ell_level1_operator_128(ctx):

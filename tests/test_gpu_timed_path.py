@@ -70,7 +70,7 @@ def test_timed_path_geometry(h512):
     lay = layout_of(S.A[0])
     assert lay["sym"] and lay["jr_fused"] and lay["cd_offsets"] == 3, lay
     assert S.L == 6
-    assert layout_of(S.A_dev[1])["ell"] and layout_of(S.R[0])["ell"], (layout_of(S.A_dev[1]), layout_of(S.R[0]))
+    assert layout_of(S.A_dev[1])["ell"] and layout_of(S.R[0])["rpat"], (layout_of(S.A_dev[1]), layout_of(S.R[0]))
 
 
 def test_pipelined_cycles_512_bit_exact(ctx, h512):
