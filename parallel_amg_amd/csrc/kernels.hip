@@ -1789,11 +1789,11 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __
 // k_rows_rpat: pattern-dictionary rows (pamg::RpatSet; round 6, the 512^3 R0). One row per lane, a
 // workgroup per kEllGroup rows (the groups in the ELL's blocked order where the columns are a
 // registered grid); every workgroup stages the entry, pattern and value tables (<= kRpatEnt + kRpatMax
-// + 256 words; 1,249 + 58 + 41 at 512^3) in LDS, then a lane walks its pattern's entries 4 per step —
+// + 256 words; 1,249 + 58 + 41 at 512^3) in LDS, then a lane walks its pattern's entries U per step —
 // their x gathers issued together, a step past the row's end re-reading its last entry — x at the
 // row's first column + offset, products rounded and summed left to right from +0.0 in storage order,
 // the entries past the end selected away (SPEC S3: the bits of every other row kernel).
-template <int OP>
+template <int OP, int U>
 __global__ __launch_bounds__(kEllGroup) void k_rows_rpat(int nrows, const int* __restrict__ gorder,
                                                          const int* __restrict__ anc, const uint8_t* __restrict__ pid,
                                                          const int2* __restrict__ pmeta, int npat,
@@ -1825,15 +1825,15 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_rpat(int nrows, const int* _
     const int2 m = in ? lm[p] : make_int2(0, 0);
     const int L = m.y;
     double s = 0.0, dg = 0.0;
-    for (int q = 0; q < L; q += 4) {
-        uint32_t w[4];
-        double xv[4];
+    for (int q = 0; q < L; q += U) {
+        uint32_t w[U];
+        double xv[U];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = le[m.x + min(q + e, L - 1)];
+        for (int e = 0; e < U; ++e) w[e] = le[m.x + min(q + e, L - 1)];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) xv[e] = x[a + (int)(w[e] & 0xffffffu)];
+        for (int e = 0; e < U; ++e) xv[e] = x[a + (int)(w[e] & 0xffffffu)];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < U; ++e) {
             const bool ok = q + e < L;
             const double v = lv[w[e] >> 24];
             const double pr = v * xv[e];
@@ -2382,8 +2382,12 @@ template <int OP>
 void launch_rpat(const pamg_mat& A, const double* x, const double* b, double* y, double omega, hipStream_t s) {
     const RpatSet& R = A.rpat;
     const int grid = (int)((R.ngroups + 7) / 8 * 8);
-    k_rows_rpat<OP><<<grid, kEllGroup, 0, s>>>((int)A.nrows, R.d_gorder, R.d_anc, R.d_pid, R.d_pmeta, R.npat,
-                                               R.d_pent, R.nent, R.d_vtab, R.nval, (int)R.ngroups, x, b, y, omega);
+    auto go = [&](auto kern) {
+        kern<<<grid, kEllGroup, 0, s>>>((int)A.nrows, R.d_gorder, R.d_anc, R.d_pid, R.d_pmeta, R.npat, R.d_pent, R.nent,
+                                        R.d_vtab, R.nval, (int)R.ngroups, x, b, y, omega);
+    };
+    // 8 entries per step (512^3 R0: 4 / 8 / 16 per step 0.552 / 0.544 / 0.539-0.548 ms, profiles/r06_m/)
+    go(k_rows_rpat<OP, 8>);
 }
 
 template <int OP>
