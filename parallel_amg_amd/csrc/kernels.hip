@@ -1871,17 +1871,19 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_rpat(int nrows, const int* _
 // the anchors of the in-plane neighbours, y / b / x; the z neighbours' anchors come from the
 // z-march's registers
 struct PncRow {
-    uint2 rec;
+    uint2 rec;   // the 64-bit record; compact records: rec.x = the 16-bit combination id
     int an[5];   // anchors of the points i, i-1, i+1, i-nx, i+nx (clamped to i off the plane)
     double p0;   // y (prolongate-add), b (residual, Jacobi)
     double p1;   // x_i (Jacobi)
 };
 
-template <int OP>
+template <int OP, bool CP>
 __device__ __forceinline__ void pnc_load(PncRow& r, int i, int nrows, int nx, const int* __restrict__ anc,
-                                         const uint2* __restrict__ rec, const double* __restrict__ x,
-                                         const double* __restrict__ b, const double* __restrict__ y) {
-    r.rec = rec[i];
+                                         const uint2* __restrict__ rec, const uint16_t* __restrict__ cid,
+                                         const double* __restrict__ x, const double* __restrict__ b,
+                                         const double* __restrict__ y) {
+    if constexpr (CP) r.rec = make_uint2((uint32_t)cid[i], 0u);
+    else r.rec = rec[i];
     r.an[0] = anc[i];
     r.an[1] = anc[i >= 1 ? i - 1 : i];
     r.an[2] = anc[i + 1 < nrows ? i + 1 : i];
@@ -1906,14 +1908,18 @@ __device__ __forceinline__ void pnc_load(PncRow& r, int i, int nrows, int nx, co
 // the other row kernels do. The next planes' records, anchors and y are loaded under this step's x
 // gathers; every gather is issued (a padded entry reloads the first entry's x), so the loads are
 // straight-line and the waits count exactly.
-template <int OP, int NS>
+// CP (compact records, PncSet::d_cid): a row holds a 16-bit combination id; the combination's pattern
+// word and value indices come from LDS (kPncCombMax entries each).
+template <int OP, int NS, bool CP>
 __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int nz, int zlen,
                                                   const int* __restrict__ anc, const uint2* __restrict__ rec,
+                                                  const uint16_t* __restrict__ cid, const uint64_t* __restrict__ pvals,
                                                   const uint32_t* __restrict__ ptab, int npat,
                                                   const double* __restrict__ vtab, int nval,
                                                   const double* __restrict__ x, const double* __restrict__ b,
                                                   double* __restrict__ y, double omega) {
-    __shared__ uint32_t lp[kPncPatMax];
+    __shared__ uint32_t lp[CP ? kPncCombMax : kPncPatMax];
+    __shared__ uint64_t lw[CP ? kPncCombMax : 1];
     __shared__ double lv[kPncValMax];
     const int nxb = M >> 8;                                    // 256-point blocks of a plane
     const int units = nxb * ((nz + zlen - 1) / zlen);
@@ -1921,6 +1927,8 @@ __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int 
     const int u = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // consecutive units on one XCD
     if (u >= units) return;  // the whole workgroup, before the barrier
     for (int t = threadIdx.x; t < npat; t += 256) lp[t] = ptab[t];
+    if constexpr (CP)
+        for (int t = threadIdx.x; t < npat; t += 256) lw[t] = pvals[t];
     for (int t = threadIdx.x; t < nval; t += 256) lv[t] = vtab[t];
     const int zc0 = (u / nxb) * zlen, zc1 = min(nz, zc0 + zlen);
     const int part = (zc1 - zc0 + NS - 1) / NS;  // planes per stream
@@ -1937,7 +1945,7 @@ __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int 
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
         const int z = min(zs[q], zl[q]);
-        pnc_load<OP>(cur[q], z * M + ixy, nrows, nx, anc, rec, x, b, y);
+        pnc_load<OP, CP>(cur[q], z * M + ixy, nrows, nx, anc, rec, cid, x, b, y);
         am[q] = anc[z > 0 ? (z - 1) * M + ixy : ixy];          // anchors of planes z - 1 and z + 1
         ap[q] = anc[z + 1 < nz ? (z + 1) * M + ixy : ixy];
     }
@@ -1948,8 +1956,8 @@ __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int 
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
             zq[q] = min(zs[q] + j, zl[q]);
-            const uint32_t pid = cur[q].rec.x & 1023u;
-            const uint32_t pw = pid < (uint32_t)npat ? lp[pid] : 0u;  // (kPncSkip: no entries, no store)
+            const uint32_t pid = CP ? cur[q].rec.x : cur[q].rec.x & 1023u;
+            const uint32_t pw = pid < (uint32_t)npat ? lp[pid] : 0u;  // (kPncSkip / kPncCombSkip: no entries, no store)
             L[q] = (int)(pw & 7u);
 #pragma unroll
             for (int k = 0; k < kPncMaxLen; ++k) {
@@ -1970,18 +1978,21 @@ __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int 
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
             const int zn = min(zq[q] + 1, zl[q]);
-            pnc_load<OP>(nxt[q], zn * M + ixy, nrows, nx, anc, rec, x, b, y);
+            pnc_load<OP, CP>(nxt[q], zn * M + ixy, nrows, nx, anc, rec, cid, x, b, y);
             ap2[q] = anc[zn + 1 < nz ? (zn + 1) * M + ixy : zn * M + ixy];
         }
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
             const int i = zq[q] * M + ixy;
-            const uint64_t rr = ((uint64_t)cur[q].rec.y << 32) | cur[q].rec.x;
+            // the value indices from bit 0 (compact: the combination's word; else the record's bits 10..)
+            uint64_t rr;
+            if constexpr (CP) rr = cur[q].rec.x < (uint32_t)npat ? lw[cur[q].rec.x] : 0ull;
+            else rr = (((uint64_t)cur[q].rec.y << 32) | cur[q].rec.x) >> 10;
             double s = 0.0, dg = 0.0;
 #pragma unroll
             for (int k = 0; k < kPncMaxLen; ++k) {
                 const bool ok = k < L[q];
-                const double v = lv[(uint32_t)(rr >> (10 + 7 * k)) & 127u];
+                const double v = lv[(uint32_t)(rr >> (7 * k)) & 127u];
                 const double p = v * xv[q][k];
                 const double t = s + p;
                 s = ok ? t : s;
@@ -2000,7 +2011,8 @@ __global__ __launch_bounds__(256) void k_rows_pnc(int nrows, int nx, int M, int 
             } else {
                 out = cur[q].p0 + s;
             }
-            if (zs[q] + j < ze[q] && (cur[q].rec.x & 1023u) != (uint32_t)kPncSkip) y[i] = out;
+            const bool in = CP ? cur[q].rec.x != (uint32_t)kPncCombSkip : (cur[q].rec.x & 1023u) != (uint32_t)kPncSkip;
+            if (zs[q] + j < ze[q] && in) y[i] = out;
             am[q] = cur[q].an[0];
             cur[q] = nxt[q];
             ap[q] = ap2[q];
@@ -2373,9 +2385,12 @@ void launch_pnc(const pamg_mat& A, const double* x, const double* b, double* y, 
     const PncSet& P = A.pnc;
     const int zlen = std::min(kPncZlen, P.nz);
     const int nxb = P.nx * P.ny / 256, units = nxb * ((P.nz + zlen - 1) / zlen);
-    k_rows_pnc<OP, kPncStreams><<<(units + 7) / 8 * 8, 256, 0, s>>>((int)A.nrows, P.nx, P.nx * P.ny, P.nz, zlen,
-                                                                    P.d_anc, P.d_rec, P.d_ptab, P.npat, P.d_vtab,
-                                                                    P.nval, x, b, y, omega);
+    auto go = [&](auto kern) {
+        kern<<<(units + 7) / 8 * 8, 256, 0, s>>>((int)A.nrows, P.nx, P.nx * P.ny, P.nz, zlen, P.d_anc, P.d_rec, P.d_cid,
+                                                P.d_pvals, P.d_ptab, P.npat, P.d_vtab, P.nval, x, b, y, omega);
+    };
+    if (P.d_cid) go(k_rows_pnc<OP, kPncStreams, true>);
+    else go(k_rows_pnc<OP, kPncStreams, false>);
 }
 
 template <int OP>

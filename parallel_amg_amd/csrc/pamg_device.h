@@ -151,6 +151,7 @@ struct Options {
                                //    order within each XCD's eighth (0: row order; 512^3 R0 0.81 -> 0.745 ms for any
                                //    block of 2..64 lines, profiles/r05_r/); read at upload
     int rpat = 1;              // 1: pattern-dictionary rows for restrictions whose rows repeat few patterns (RpatSet)
+    int pnc_compact = 1;       // 1: 16-bit combination ids instead of 64-bit records where <= kPncCombMax fit
     int pnc = 1;               // 1: neighbour-coded prolongations over a grid registered on the context (PncSet)
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
                                //    distinct (mask, diagonal, upper values) tuples (SymDia::vd_n)
@@ -222,10 +223,19 @@ struct EllSet {
 // keep their storage order (SPEC S3 sums).
 constexpr int kPncPatMax = 1024, kPncValMax = 128, kPncMaxLen = 7;
 constexpr int kPncSkip = kPncPatMax - 1;  // pattern id of a row outside the set (several parts: a boundary row)
+// Compact records (round 6): where the rows take at most kPncCombMax distinct (pattern word, value
+// indices) combinations — 428 for the 512^3 P0, whose aggregates are nearly all alike — a row stores
+// a 16-bit combination id (kPncCombSkip: outside the set) instead of the 64-bit record: 6 B per row
+// with the anchor instead of 12. Then d_ptab holds the combinations' pattern words and d_pvals their
+// value indices (7 bits per entry from bit 0), npat = the combinations, d_rec = null.
+constexpr int kPncCombMax = 1024;
+constexpr int kPncCombSkip = 0xffff;
 struct PncSet {
     int nx = 0, ny = 0, nz = 0;
     int* d_anc = nullptr;       // nrows (+ pad)
     uint2* d_rec = nullptr;     // nrows (+ pad): the 64-bit records as (low, high) dwords
+    uint16_t* d_cid = nullptr;  // compact records: nrows (+ pad) combination ids
+    uint64_t* d_pvals = nullptr;
     uint32_t* d_ptab = nullptr;
     double* d_vtab = nullptr;
     int npat = 0, nval = 0;

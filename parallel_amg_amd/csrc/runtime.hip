@@ -1582,6 +1582,32 @@ int build_pnc(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
     });
     std::vector<double> vtab(vals.size());
     for (size_t e = 0; e < vals.size(); ++e) std::memcpy(&vtab[e], &vals[e], 8);
+    // compact records: the distinct (pattern word, value indices) combinations, numbered in sorted order
+    std::vector<std::pair<uint32_t, uint64_t>> combs;
+    if (pamg::options().pnc_compact) {
+        std::atomic<bool> fits{true};
+        par_for(n, [&](int64_t a, int64_t b) {
+            std::vector<std::pair<uint32_t, uint64_t>> lc;
+            std::pair<uint32_t, uint64_t> last{0xffffffffu, 0};
+            for (int64_t i = a; i < b && fits; ++i) {
+                if (!member(i)) continue;
+                const uint64_t r = ((uint64_t)rec[i].y << 32) | rec[i].x;
+                const std::pair<uint32_t, uint64_t> c{pats[r & 1023u], r >> 10};
+                if (c == last) continue;
+                last = c;
+                if (std::find(lc.begin(), lc.end(), c) == lc.end()) {
+                    lc.push_back(c);
+                    if (lc.size() > (size_t)pamg::kPncCombMax) fits = false;
+                }
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            combs.insert(combs.end(), lc.begin(), lc.end());
+            std::sort(combs.begin(), combs.end());
+            combs.erase(std::unique(combs.begin(), combs.end()), combs.end());
+            if (combs.size() > (size_t)pamg::kPncCombMax) fits = false;
+        });
+        if (!fits) combs.clear();
+    }
     pamg::PncSet& P = A->pnc;
     pamg_ctx* ctx = A->ctx;
     P.nx = (int)nx;
@@ -1596,13 +1622,38 @@ int build_pnc(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
         P.grid = (int)((M / 256 * ((nz + zlen - 1) / zlen) + 7) / 8 * 8);
     }
     CHECK(dalloc(&P.d_anc, n + kVecPad));
-    CHECK(dalloc(&P.d_rec, n + kVecPad));
-    CHECK(dalloc(&P.d_ptab, (int64_t)pats.size()));
     CHECK(dalloc(&P.d_vtab, (int64_t)vals.size()));
     CHECK(h2d(ctx, P.d_anc, anc.data(), sizeof(int) * anc.size()));
-    CHECK(h2d(ctx, P.d_rec, rec.data(), sizeof(uint2) * rec.size()));
-    CHECK(h2d(ctx, P.d_ptab, pats.data(), sizeof(uint32_t) * pats.size()));
     CHECK(h2d(ctx, P.d_vtab, vtab.data(), sizeof(double) * vtab.size()));
+    if (!combs.empty()) {
+        std::vector<uint16_t> cid(n + kVecPad, (uint16_t)pamg::kPncCombSkip);
+        par_for(n, [&](int64_t a, int64_t b) {
+            for (int64_t i = a; i < b; ++i) {
+                if (!member(i)) continue;
+                const uint64_t r = ((uint64_t)rec[i].y << 32) | rec[i].x;
+                const std::pair<uint32_t, uint64_t> c{pats[r & 1023u], r >> 10};
+                cid[i] = (uint16_t)(std::lower_bound(combs.begin(), combs.end(), c) - combs.begin());
+            }
+        });
+        std::vector<uint32_t> cw(combs.size());
+        std::vector<uint64_t> cv(combs.size());
+        for (size_t e = 0; e < combs.size(); ++e) {
+            cw[e] = combs[e].first;
+            cv[e] = combs[e].second;
+        }
+        P.npat = (int)combs.size();
+        CHECK(dalloc(&P.d_cid, n + kVecPad));
+        CHECK(dalloc(&P.d_ptab, (int64_t)cw.size()));
+        CHECK(dalloc(&P.d_pvals, (int64_t)cv.size()));
+        CHECK(h2d(ctx, P.d_cid, cid.data(), sizeof(uint16_t) * cid.size()));
+        CHECK(h2d(ctx, P.d_ptab, cw.data(), sizeof(uint32_t) * cw.size()));
+        CHECK(h2d(ctx, P.d_pvals, cv.data(), sizeof(uint64_t) * cv.size()));
+    } else {
+        CHECK(dalloc(&P.d_rec, n + kVecPad));
+        CHECK(dalloc(&P.d_ptab, (int64_t)pats.size()));
+        CHECK(h2d(ctx, P.d_rec, rec.data(), sizeof(uint2) * rec.size()));
+        CHECK(h2d(ctx, P.d_ptab, pats.data(), sizeof(uint32_t) * pats.size()));
+    }
     A->interior.pnc = true;
     return PAMG_OK;
 }
@@ -1781,6 +1832,8 @@ void free_rpat(pamg::RpatSet& R) {
 void free_pnc(pamg::PncSet& P) {
     dfree(P.d_anc);
     dfree(P.d_rec);
+    dfree(P.d_cid);
+    dfree(P.d_pvals);
     dfree(P.d_ptab);
     dfree(P.d_vtab);
     P = pamg::PncSet{};
@@ -3238,7 +3291,8 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
         A->stream_bytes += 8 * A->ell.words + nrows + 8 * A->ell.nslices + 16 * A->ell.ngroups + 4 * A->ell.otab_n +
                            8 * A->ell.vtab_n + (A->ell.d_anc ? 4 * nrows : 0);
     // neighbour-coded prolongation: the anchor and the record per row, the two tables
-    if (A->interior.pnc) A->stream_bytes += 12 * nrows + 4 * A->pnc.npat + 8 * A->pnc.nval;
+    if (A->interior.pnc)
+        A->stream_bytes += (A->pnc.d_cid ? 6 : 12) * nrows + (A->pnc.d_cid ? 12 : 4) * A->pnc.npat + 8 * A->pnc.nval;
     // pattern-dictionary rows: the first column and the pattern id per row, the tables
     if (A->interior.rpat) A->stream_bytes += 5 * nrows + 8 * A->rpat.npat + 4 * A->rpat.nent + 8 * A->rpat.nval;
     for (const pamg::TileSet* t : {&A->interior, &A->boundary}) {
@@ -3397,7 +3451,8 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[8] = t.n_short;
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
              (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0) |
-             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0) | (t.pnc ? 1024 : 0) | (t.rpat ? 2048 : 0);
+             (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0) | (t.pnc ? 1024 : 0) | (t.rpat ? 2048 : 0) |
+             (t.pnc && A->pnc.d_cid ? 4096 : 0);
     if (t.ell) out[8] = (int)A->ell.ngroups;  // k_rows_ell's grid
     if (t.rpat) {  // the pattern and value tables, k_rows_rpat's grid
         out[3] = A->rpat.nval;
@@ -4080,6 +4135,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "ell_restrict" && (value == 0 || value == 1)) o.ell_restrict = (int)value;
     else if (k == "pnc" && (value == 0 || value == 1)) o.pnc = (int)value;
     else if (k == "rpat" && (value == 0 || value == 1)) o.rpat = (int)value;
+    else if (k == "pnc_compact" && (value == 0 || value == 1)) o.pnc_compact = (int)value;
     else if (k == "ell_yblock" && value >= 0 && value <= 65536) o.ell_yblock = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
@@ -4119,6 +4175,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "ell_restrict") *value = o.ell_restrict;
     else if (k == "pnc") *value = o.pnc;
     else if (k == "rpat") *value = o.rpat;
+    else if (k == "pnc_compact") *value = o.pnc_compact;
     else if (k == "ell_yblock") *value = o.ell_yblock;
     else if (k == "ell_min_rows") *value = o.ell_min_rows;
     else if (k == "zm_chunks") *value = o.zm_chunks;

@@ -1667,7 +1667,8 @@ def _grid_hierarchy_P0(nx, ny, nz):
 @pytest.mark.parametrize("shape", [(64, 16, 12), (128, 32, 20), (64, 64, 64)])
 def test_prolongation_neighbour_coded_bit_exact(ctx, shape):
     """k_rows_pnc (round 5: the prolongation's columns named by the grid neighbours whose anchors
-    they are — 12 B per row): a level-0 prolongation uploaded after its grid operator takes the
+    they are — 12 B per row; round 6: 6 B per row as 16-bit ids of the rows' (pattern, values)
+    combinations, pnc_compact): a level-0 prolongation uploaded after its grid operator takes the
     layout, and its SpMV, residual and prolongate-add are bit-exact with the oracle; with the
     option off the tile layouts give the same bits."""
     from parallel_amg_amd._lib import layout_of
@@ -1676,10 +1677,32 @@ def test_prolongation_neighbour_coded_bit_exact(ctx, shape):
     assert layout_of(Ad)["jr_fused"], layout_of(Ad)  # (the grid is registered on the context)
     D = _layout_ops_match_oracle(ctx, P, np.random.default_rng(sum(shape)))
     lay = layout_of(D)
-    assert lay["pnc"] and lay["cd"] <= 128 and lay["cd_offsets"] <= 1024, lay
+    # (compact records where the rows take <= 1024 (pattern, values) combinations: 128 x 32 x 20)
+    assert lay["pnc"] and lay["pnc_compact"] == (shape == (128, 32, 20)), lay
+    assert lay["cd"] <= 128 and lay["cd_offsets"] <= 1024, lay
+    with _with_option("pnc_compact", 0):
+        R = _layout_ops_match_oracle(ctx, P, np.random.default_rng(sum(shape)))
+    assert layout_of(R)["pnc"] and not layout_of(R)["pnc_compact"]
     with _with_option("pnc", 0):
         T = _layout_ops_match_oracle(ctx, P, np.random.default_rng(sum(shape)))
     assert not layout_of(T)["pnc"]
+    del Ad
+
+
+def test_prolongation_compact_records_128(ctx):
+    """The 128^3 level-0 prolongation (2.1M rows; its aggregates nearly all alike: 428 (pattern,
+    values) combinations) takes the compact records — a 16-bit combination id per row (round 6) —
+    and its SpMV, residual and prolongate-add are the oracle's bits, as with 64-bit records."""
+    from parallel_amg_amd._lib import layout_of
+    A0, P = _grid_hierarchy_P0(128, 128, 128)
+    Ad = PSparseMatrix(ctx, A0)
+    assert layout_of(Ad)["jr_fused"], layout_of(Ad)
+    D = _layout_ops_match_oracle(ctx, P, np.random.default_rng(7))
+    lay = layout_of(D)
+    assert lay["pnc"] and lay["pnc_compact"] and lay["cd_offsets"] == 428, lay
+    with _with_option("pnc_compact", 0):
+        E = _layout_ops_match_oracle(ctx, P, np.random.default_rng(7))
+    assert layout_of(E)["pnc"] and not layout_of(E)["pnc_compact"]
     del Ad
 
 
