@@ -77,9 +77,11 @@ def main():
         rep_next = l + 1 >= H.rep_level
         Rd = PSparseMatrix(ctx, lp.R, lp.planR)
         rec["ms"]["R_spmv"] = round(time_op(ctx, Rd, 0, a.reps), 4)
+        rec["R_layout"] = {k: v for k, v in layout_of(Rd).items() if k in ("rpat", "ell", "tm", "tile_nnz")}
         del Rd
         Pd = PSparseMatrix(ctx, lp.P, None if rep_next else lp.planP)
         rec["ms"]["P_prolong"] = round(time_op(ctx, Pd, 3, a.reps), 4)
+        rec["P_layout"] = {k: v for k, v in layout_of(Pd).items() if k in ("pnc", "pnc_compact", "tm", "tile_nnz")}
         del Pd
         out.append(rec)
         print(json.dumps(rec), file=sys.stderr, flush=True)
