@@ -213,7 +213,8 @@ int pamg_mat_stream_bytes(const pamg_mat* A, int64_t* bytes);
  * layout (rpat: a restriction whose rows repeat <= 255 (offset, value) patterns from their first
  * column; then out[3] = the value table's entries, out[4] = the pattern count, out[8] = the kernel's
  * grid); bit 12: with bit 10, the rows hold 16-bit combination ids instead of 64-bit records
- * (pnc_compact; out[4] = the combinations). */
+ * (pnc_compact; out[4] = the combinations); bit 13: with bit 9, one index byte per nonzero names an
+ * (offset, value) pair of the group (ell_pair). */
 int pamg_mat_layout(const pamg_mat* A, int set, int out[10]);
 
 /* mul!(y, A, x): exchanges x's ghosts (overlapped with the interior rows), then y = A x. */
@@ -309,7 +310,8 @@ int pamg_hier_bench_chain(pamg_hier* H, pamg_vec* x, const pamg_vec* b, int reps
  * blocked group order of a restriction over a grid), "pnc" (0 | 1: neighbour-coded
  * prolongations over a grid uploaded earlier on the context), "rpat" (0 | 1: pattern-dictionary
  * rows for restrictions whose rows repeat <= 255 patterns; tried before ELL), "pnc_compact" (0 | 1:
- * neighbour-coded rows as 16-bit ids of <= 1024 (pattern, values) combinations). Read at launch:
+ * neighbour-coded rows as 16-bit ids of <= 1024 (pattern, values) combinations), "ell_pair" (0 | 1:
+ * one ELL index byte per nonzero naming an (offset, value) pair where a group has <= 256). Read at launch:
  * "sym_zm" (0 | 1: z-marching single sweeps of the symmetric layout), "zm_chunks" (0 = auto |
  * z chunks per column of k_sym_zm), "tb_xfast" (0 | 1: x-fastest tile order of the chain),
  * "symd_chunks" (1 | 2 | 4), "chain_store_x" (0 | 1). Applied at every exchange:

@@ -195,7 +195,8 @@ def layout_of(M, part_set: int = 0) -> dict:
             "x_stage": bool(out[9] & 4), "sym": bool(out[9] & 8), "sym_rows": 2 if out[9] & 16 else 1,
             "jr_fused": bool(out[9] & 32), "tm_vd": bool(out[9] & 64), "sym_vd": bool(out[9] & 128),
             "ell": bool(out[9] & 512), "pnc": bool(out[9] & 1024),
-            "rpat": bool(out[9] & 2048), "pnc_compact": bool(out[9] & 4096)}
+            "rpat": bool(out[9] & 2048), "pnc_compact": bool(out[9] & 4096),
+            "ell_pair": bool(out[9] & 8192)}
 
 
 def last_error() -> str:

@@ -1707,7 +1707,8 @@ __global__ __launch_bounds__(kZmThreads) void k_sym_zm(int nrows, const uint8_t*
 // row (k >= its length) selected away: the bits of every other row kernel (SPEC §S3). Groups in
 // XCD-contiguous order: block b on XCD b % 8 takes the (b / 8)-th group of that XCD's eighth, so an
 // XCD's L2 holds the x window its consecutive rows reuse.
-template <int OP, bool ANC>
+// PAIR (EllSet::paired): one index byte per nonzero names an (offset, value) pair; no value stream.
+template <int OP, bool ANC, bool PAIR>
 __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __restrict__ gorder,
                                                         const int* __restrict__ anc, const int2* __restrict__ smeta,
                                                         const uint32_t* __restrict__ cw, const uint32_t* __restrict__ vw,
@@ -1732,9 +1733,9 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __
     const int L = in ? L8 : 0;
     const int base = ANC ? anc[ic] : ic;  // offsets from the row (square) or its first column (anchored)
     const uint32_t* __restrict__ cp = cw + sm.x + lane;
-    const uint32_t* __restrict__ vp = vw + sm.x + lane;
+    const uint32_t* __restrict__ vp = (PAIR ? cw : vw) + sm.x + lane;
     const int nq = (sm.y + 3) >> 2;
-    uint32_t c4 = nq > 0 ? cp[0] : 0u, v4 = nq > 0 ? vp[0] : 0u;
+    uint32_t c4 = nq > 0 ? cp[0] : 0u, v4 = PAIR ? 0u : (nq > 0 ? vp[0] : 0u);
     double pb = 0.0, px = 0.0, py = 0.0;
     if constexpr (OP == OP_RESID || OP == OP_JACOBI) pb = b[ic];
     if constexpr (OP == OP_JACOBI) px = x[ic];
@@ -1747,10 +1748,10 @@ __global__ __launch_bounds__(kEllGroup) void k_rows_ell(int nrows, const int* __
     __syncthreads();
     double s = 0.0, dg = 0.0;
     for (int q = 0; q < nq; ++q) {
-        const uint32_t cq = c4, vq = v4;
+        const uint32_t cq = c4, vq = PAIR ? c4 : v4;
         if (q + 1 < nq) {  // the next dword pair in flight while this one is used
             c4 = cp[(q + 1) * kEllW];
-            v4 = vp[(q + 1) * kEllW];
+            if constexpr (!PAIR) v4 = vp[(q + 1) * kEllW];
         }
         int of[4];
         double vv[4], xv[4];
@@ -2412,14 +2413,17 @@ void launch_rows_op(const pamg_mat& A, const TileSet& ts, const double* x, const
     if (ts.ell) {
         const EllSet& E = A.ell;
         const int grid = (int)((E.ngroups + 7) / 8 * 8);
-        if (E.d_anc)
-            k_rows_ell<OP, true><<<grid, kEllGroup, 0, s>>>((int)A.nrows, E.d_gorder, E.d_anc, E.d_smeta, E.d_ci, E.d_vi,
-                                                              E.d_len, E.d_gmeta, E.d_otab, E.d_vtab, (int)E.ngroups, x, b,
-                                                              y, omega);
-        else
-            k_rows_ell<OP, false><<<grid, kEllGroup, 0, s>>>((int)A.nrows, E.d_gorder, nullptr, E.d_smeta, E.d_ci, E.d_vi,
-                                                               E.d_len, E.d_gmeta, E.d_otab, E.d_vtab, (int)E.ngroups, x, b,
-                                                               y, omega);
+        auto go = [&](auto kern) {
+            kern<<<grid, kEllGroup, 0, s>>>((int)A.nrows, E.d_gorder, E.d_anc, E.d_smeta, E.d_ci, E.d_vi, E.d_len,
+                                            E.d_gmeta, E.d_otab, E.d_vtab, (int)E.ngroups, x, b, y, omega);
+        };
+        if (E.d_anc) {
+            if (E.paired) go(k_rows_ell<OP, true, true>);
+            else go(k_rows_ell<OP, true, false>);
+        } else {
+            if (E.paired) go(k_rows_ell<OP, false, true>);
+            else go(k_rows_ell<OP, false, false>);
+        }
     }
     if (ts.pnc) launch_pnc<OP>(A, x, b, y, omega, s);
     if (ts.rpat) launch_rpat<OP>(A, x, b, y, omega, s);

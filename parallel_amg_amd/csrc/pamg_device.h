@@ -151,6 +151,7 @@ struct Options {
                                //    order within each XCD's eighth (0: row order; 512^3 R0 0.81 -> 0.745 ms for any
                                //    block of 2..64 lines, profiles/r05_r/); read at upload
     int rpat = 1;              // 1: pattern-dictionary rows for restrictions whose rows repeat few patterns (RpatSet)
+    int ell_pair = 1;          // 1: one index byte per ELL nonzero naming an (offset, value) pair where they fit
     int pnc_compact = 1;       // 1: 16-bit combination ids instead of 64-bit records where <= kPncCombMax fit
     int pnc = 1;               // 1: neighbour-coded prolongations over a grid registered on the context (PncSet)
     int sym_vd = 1;            // 1: row-class dictionary for the symmetric layout where the rows take <= kSymVdMax
@@ -208,6 +209,9 @@ struct EllSet {
     // planes (Options::ell_yblock; kernels.hip k_rows_ell), null otherwise
     int* d_gorder = nullptr;
     int64_t words = 0, otab_n = 0, vtab_n = 0;
+    // paired dictionaries (Options::ell_pair): one index byte per nonzero names an (offset, value)
+    // pair of the group (d_otab / d_vtab entries in parallel, gmeta .x == .z, .y == .w); d_vi null
+    bool paired = false;
 };
 
 // Neighbour-coded prolongation (Options::pnc; round 5, the 512^3 P0): a prolongation (more rows than

@@ -1359,11 +1359,71 @@ int build_ell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
     // per group, one pass: an entry's offset and value take the index of their first appearance in
     // the group (open addressing over 512 slots, stamped per group instead of cleared), and the index
     // bytes go straight into the slice streams (a slice lies in one group: no two threads share a word)
+    // Paired dictionaries (Options::ell_pair, round 6): where every group has <= 256 distinct (offset,
+    // value) pairs — the 512^3 A1: a regular 27-point-like stencil over the aggregates — one index byte
+    // per nonzero names the pair (the offset and value tables then run in parallel); otherwise one byte
+    // each into separate offset and value tables.
     std::vector<std::vector<int>> goff(ng);
     std::vector<std::vector<uint64_t>> gval(ng);
-    std::vector<uint32_t> cw(words + 1, 0u), vw(words + 1, 0u);
+    std::vector<uint32_t> cw(words + 1, 0u), vw;
     std::vector<uint8_t> len(n + kVecPad, 0);
-    par_for(ng, [&](int64_t a, int64_t b) {
+    bool paired = pamg::options().ell_pair != 0;
+    if (paired) {
+        std::atomic<bool> fits{true};
+        par_for(ng, [&](int64_t a, int64_t b) {
+            constexpr int kSlots = 1024;
+            std::vector<int> pid(kSlots), pstamp(kSlots, -1), pkey_o(kSlots);
+            std::vector<uint64_t> pkey_v(kSlots);
+            std::vector<int> o;
+            std::vector<uint64_t> v;
+            for (int64_t g = a; g < b && fits; ++g) {
+                const int stamp = (int)(g - a);
+                o.clear();
+                v.clear();
+                const int64_t r1 = std::min(n, (g + 1) * kEllGroup);
+                for (int64_t i = g * kEllGroup; i < r1 && fits; ++i) {
+                    if (!member(i)) {
+                        len[i] = (uint8_t)kEllSkip;
+                        continue;
+                    }
+                    len[i] = (uint8_t)(rp[i + 1] - rp[i]);
+                    const int64_t q = i / kEllW, lane = i % kEllW;
+                    const int base = base_of(i);
+                    for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                        const int kk = (int)(k - rp[i]);
+                        const int off = ci[k] - base;
+                        uint64_t u;
+                        std::memcpy(&u, &val[k], 8);
+                        uint32_t h = (uint32_t)((((uint64_t)(uint32_t)off * 0x9E3779B1u) ^ u ^ (u >> 29)) *
+                                                0x9E3779B97F4A7C15ull >> 54);
+                        while (pstamp[h] == stamp && (pkey_o[h] != off || pkey_v[h] != u)) h = (h + 1) & (kSlots - 1);
+                        if (pstamp[h] != stamp) {
+                            pstamp[h] = stamp;
+                            pkey_o[h] = off;
+                            pkey_v[h] = u;
+                            pid[h] = (int)o.size();
+                            o.push_back(off);
+                            v.push_back(u);
+                            if (o.size() > 256) {
+                                fits = false;
+                                break;
+                            }
+                        }
+                        const int64_t w = smeta[q].x + (int64_t)(kk / 4) * kEllW + lane;
+                        cw[w] |= (uint32_t)pid[h] << (8 * (kk % 4));
+                    }
+                }
+                goff[g] = o;
+                gval[g] = v;
+            }
+        });
+        if (!fits) {  // back to separate tables: start over
+            paired = false;
+            std::fill(cw.begin(), cw.end(), 0u);
+        }
+    }
+    if (!paired) vw.assign(words + 1, 0u);
+    if (!paired) par_for(ng, [&](int64_t a, int64_t b) {
         constexpr int kSlots = 512;
         std::vector<int> okey(kSlots), oid(kSlots), ostamp(kSlots, -1), vid(kSlots), vstamp(kSlots, -1);
         std::vector<uint64_t> vkey(kSlots);
@@ -1439,16 +1499,17 @@ int build_ell(pamg_mat* A, const PtrVec& rp, const IdxVec& ci, const double* val
     E.words = words;
     E.otab_n = on;
     E.vtab_n = vn;
+    E.paired = paired;
     CHECK(dalloc(&E.d_smeta, ns));
     CHECK(dalloc(&E.d_ci, words + 1));
-    CHECK(dalloc(&E.d_vi, words + 1));
+    if (!paired) CHECK(dalloc(&E.d_vi, words + 1));
     CHECK(dalloc(&E.d_len, n + kVecPad));
     CHECK(dalloc(&E.d_gmeta, ng));
     CHECK(dalloc(&E.d_otab, on + 1));
     CHECK(dalloc(&E.d_vtab, vn + 1));
     CHECK(h2d(ctx, E.d_smeta, smeta.data(), sizeof(int2) * ns));
     CHECK(h2d(ctx, E.d_ci, cw.data(), sizeof(uint32_t) * (words + 1)));
-    CHECK(h2d(ctx, E.d_vi, vw.data(), sizeof(uint32_t) * (words + 1)));
+    if (!paired) CHECK(h2d(ctx, E.d_vi, vw.data(), sizeof(uint32_t) * (words + 1)));
     CHECK(h2d(ctx, E.d_len, len.data(), len.size()));
     CHECK(h2d(ctx, E.d_gmeta, gmeta.data(), sizeof(int4) * ng));
     CHECK(h2d(ctx, E.d_otab, otab.data(), sizeof(int) * (on + 1)));
@@ -3288,7 +3349,7 @@ int pamg_mat_upload(pamg_ctx* ctx, int64_t nrows, int64_t ncols, const int64_t* 
     // sliced ELL: two index bytes per padded nonzero, a length byte per row, the slice and group
     // descriptors and the group tables
     if (A->interior.ell)
-        A->stream_bytes += 8 * A->ell.words + nrows + 8 * A->ell.nslices + 16 * A->ell.ngroups + 4 * A->ell.otab_n +
+        A->stream_bytes += (A->ell.paired ? 4 : 8) * A->ell.words + nrows + 8 * A->ell.nslices + 16 * A->ell.ngroups + 4 * A->ell.otab_n +
                            8 * A->ell.vtab_n + (A->ell.d_anc ? 4 * nrows : 0);
     // neighbour-coded prolongation: the anchor and the record per row, the two tables
     if (A->interior.pnc)
@@ -3452,7 +3513,7 @@ int pamg_mat_layout(const pamg_mat* A, int set, int out[10]) {
     out[9] = (t.anc ? 1 : 0) | (t.pt ? 2 : 0) | (t.xs ? 4 : 0) | (t.sym ? 8 : 0) | (t.sym && A->sym.rpl == 2 ? 16 : 0) |
              (t.sym && (A->sym.tb_ok || A->sym.tb_part) ? 32 : 0) | (t.tm && t.tm_vt ? 64 : 0) |
              (t.sym && A->sym.vd_n ? 128 : 0) | (t.ell ? 512 : 0) | (t.pnc ? 1024 : 0) | (t.rpat ? 2048 : 0) |
-             (t.pnc && A->pnc.d_cid ? 4096 : 0);
+             (t.pnc && A->pnc.d_cid ? 4096 : 0) | (t.ell && A->ell.paired ? 8192 : 0);
     if (t.ell) out[8] = (int)A->ell.ngroups;  // k_rows_ell's grid
     if (t.rpat) {  // the pattern and value tables, k_rows_rpat's grid
         out[3] = A->rpat.nval;
@@ -4136,6 +4197,7 @@ int pamg_set_option(const char* key, int64_t value) {
     else if (k == "pnc" && (value == 0 || value == 1)) o.pnc = (int)value;
     else if (k == "rpat" && (value == 0 || value == 1)) o.rpat = (int)value;
     else if (k == "pnc_compact" && (value == 0 || value == 1)) o.pnc_compact = (int)value;
+    else if (k == "ell_pair" && (value == 0 || value == 1)) o.ell_pair = (int)value;
     else if (k == "ell_yblock" && value >= 0 && value <= 65536) o.ell_yblock = (int)value;
     else if (k == "ell_min_rows" && value >= 0 && value <= INT32_MAX) o.ell_min_rows = (int)value;
     else if (k == "zm_chunks" && value >= 0 && value <= 4096) o.zm_chunks = (int)value;
@@ -4176,6 +4238,7 @@ int pamg_get_option(const char* key, int64_t* value) {
     else if (k == "pnc") *value = o.pnc;
     else if (k == "rpat") *value = o.rpat;
     else if (k == "pnc_compact") *value = o.pnc_compact;
+    else if (k == "ell_pair") *value = o.ell_pair;
     else if (k == "ell_yblock") *value = o.ell_yblock;
     else if (k == "ell_min_rows") *value = o.ell_min_rows;
     else if (k == "zm_chunks") *value = o.zm_chunks;

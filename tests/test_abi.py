@@ -114,7 +114,7 @@ OPTION_DEFAULTS = {"tile_nnz": (1024, 4096), "tile_order": (1, 0), "col24": (1, 
                    "band_pct": (100, 50), "band_pct_restrict": (50, 100), "tile_major": (1, 2), "poison_ghosts": (0, 1),
                    "sym_dia": (1, 0), "sym_rows": (2, 1), "jr_fuse": (1, 0), "sym_vd": (1, 0),
                    "symd_chunks": (2, 4), "chain_store_x": (0, 1), "sym_zm": (1, 0), "zm_chunks": (0, 16),
-                   "tb_xfast": (1, 0), "ell": (1, 0), "ell_restrict": (1, 0), "ell_min_rows": (65536, 1024), "pnc": (1, 0), "rpat": (1, 0), "pnc_compact": (1, 0),
+                   "tb_xfast": (1, 0), "ell": (1, 0), "ell_restrict": (1, 0), "ell_min_rows": (65536, 1024), "pnc": (1, 0), "rpat": (1, 0), "pnc_compact": (1, 0), "ell_pair": (1, 0),
                    "ell_yblock": (16, 0)}
 
 

@@ -1083,18 +1083,22 @@ def _ell_cases(kind):
     return O.CSR(T.indptr.astype(np.int64), T.indices.astype(np.int64), T.data.copy(), n)
 
 
+@pytest.mark.parametrize("pair", [1, 0])
 @pytest.mark.parametrize("kind", ["grid3d", "grid2d", "random", "ragged"])
-def test_ell_bit_exact(ctx, kind):
-    """k_rows_ell (sliced ELL, per-group 8-bit offset and value dictionaries; round 5): SpMV and
-    residual bit-exact with the oracle, and two Jacobi sweeps where every row has its diagonal;
-    the same results as the tile layouts on the same matrix."""
+def test_ell_bit_exact(ctx, kind, pair):
+    """k_rows_ell (sliced ELL, per-group 8-bit offset and value dictionaries; round 5; round 6: one
+    byte per nonzero naming an (offset, value) pair where a group has <= 256 of them, ell_pair):
+    SpMV and residual bit-exact with the oracle, and two Jacobi sweeps where every row has its
+    diagonal; the same results as the tile layouts on the same matrix."""
     from parallel_amg_amd._lib import layout_of
     M = _ell_cases(kind)
-    with _with_option("ell_min_rows", 0), _with_option("sym_dia", 0):
+    with _with_option("ell_min_rows", 0), _with_option("sym_dia", 0), _with_option("ell_pair", pair):
         A, _h = upload(ctx, M)
         with _with_option("ell", 0):
             B, _h2 = upload(ctx, M)
     assert layout_of(A)["ell"] and not layout_of(B)["ell"], (layout_of(A), layout_of(B))
+    if kind != "ragged":  # (the ragged rows' groups hold more than 256 pairs: separate tables)
+        assert layout_of(A)["ell_pair"] == bool(pair), layout_of(A)
     rng = np.random.default_rng(3)
     xh, bh = rng.standard_normal(M.nrows), rng.standard_normal(M.nrows)
     for D in (A, B):
@@ -1239,7 +1243,7 @@ def test_ell_level1_operator_128(ctx):
     H = pa.build_hierarchy(be, A, offs, pa.SAParams(max_coarse=1000), device=ctx)
     M1 = H.levels[1][0].A
     D = PSparseMatrix(ctx, M1)
-    assert layout_of(D)["ell"], layout_of(D)
+    assert layout_of(D)["ell"] and layout_of(D)["ell_pair"], layout_of(D)
     Mo = O.CSR(M1.rowptr.copy(), M1.col.astype(np.int64), M1.val.copy(), M1.ncols)
     rng = np.random.default_rng(8)
     xh, bh = rng.standard_normal(M1.nrows), rng.standard_normal(M1.nrows)
