@@ -100,12 +100,14 @@ def main():
         P = H.smooth(A0, 0, T, AT, omega)
         del AT, T
         R = H.transpose(P, 0, 0, nc)
+        del A, A0
     else:
         Hh = pa.build_hierarchy(be, A, offs, pa.SAParams())
         lp = Hh.levels[0][0]
         P, R = lp.P, lp.R
         out["A1_pairs_per_group_max"], out["A1_pairs_per_group_mean"] = a1_pairs(Hh.levels[1][0].A)
     out["R0_patterns"], out["R0_pattern_entries"] = row_patterns(R.rowptr, R.col.astype(np.int64), R.val)
+    del R
     if a.kind != "aniso3d":
         out["P0_unmatched_entries"], out["P0_combinations"] = p0_combinations(P, a.n)
     print(json.dumps(out))
